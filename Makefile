@@ -1,0 +1,27 @@
+# Builds libleastereo_hip.so for gfx950 (MI355X) in-tree, plus the oracle's
+# nothing-to-build marker.  `make -j8` here; the GPU box uses the prebuilt .so.
+HIPCC    ?= /opt/rocm/bin/hipcc
+ARCH     ?= gfx950
+HIPFLAGS ?= -O3 -std=c++17 --offload-arch=$(ARCH) -fPIC -Wall -Wno-unused-function \
+            -Iinclude -Ileastereo_amd/csrc -munsafe-fp-atomics
+SRC      := $(wildcard leastereo_amd/csrc/*.hip)
+OBJ      := $(patsubst leastereo_amd/csrc/%.hip,build/obj/%.o,$(SRC))
+LIB      := leastereo_amd/libleastereo_hip.so
+
+all: $(LIB)
+
+build/obj/%.o: leastereo_amd/csrc/%.hip leastereo_amd/csrc/common.h include/leastereo_hip.h
+	@mkdir -p build/obj
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+$(LIB): $(OBJ)
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $(OBJ)
+
+resource-usage: $(SRC)
+	@mkdir -p build/ru
+	for f in $(SRC); do $(HIPCC) $(HIPFLAGS) -c $$f -o build/ru/$$(basename $$f).o -Rpass-analysis=kernel-resource-usage 2>&1 | grep -E "Function Name|VGPRs:|AGPRs|ScratchSize|Occupancy|LDS Size" ; done
+
+clean:
+	rm -rf build $(LIB)
+
+.PHONY: all clean resource-usage

@@ -1,0 +1,245 @@
+#!/usr/bin/env python3
+"""Benchmark: LEAStereo inference (feature net -> cost volume -> matching net ->
+disparity regression) on synthetic stereo pairs, one process per GPU.
+
+Contract (driver): ``python bench.py --gpus N --steps K --warmup W``; for N>1 it
+is launched by torch.distributed.run (one rank per GPU, RCCL).  A step is one
+forward of ``--batch`` pairs per rank with inputs already resident in HBM.
+Rank 0 prints one JSON line.
+
+Workload (BASELINE.json configs[1]): SceneFlow 576x960, maxdisp 192, fp32,
+batch 1 per GPU; random-init weights of the reference architecture
+(leastereo_amd.weights recipe; no checkpoints exist upstream) and synthetic
+N(0,1) images (the post-standardisation statistics of predict.py:162-184).
+
+Extras in the JSON line:
+  roofline      the dominant conv kernel instantiation timed with HIP events
+                inside the timed region (algorithmic FLOPs / event time)
+  cpu_baseline  the CPU oracle (oracle/torch_ref.py, a restatement of the
+                reference's exact aten op sequence) on the host cores, rank 0, N=1
+  epe_px        per rank: HIP disparity vs the reference's own fp32 output on the
+                golden e2e case, all-gathered over ranks (one RCCL all-gather)
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import platform
+import sys
+import time
+
+import torch
+import torch.distributed as dist
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+from leastereo_amd import kernels  # noqa: E402
+from leastereo_amd.config import LEAStereoArgs, default_arch_args  # noqa: E402
+from leastereo_amd.model import LEAStereo  # noqa: E402
+from leastereo_amd.weights import synthetic_state_dict  # noqa: E402
+
+METRIC = "stereo pairs/s at 576×960 D=192, 1/2/4/8 GPU; EPE vs reference"
+FP32_MFMA_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md, fp32 (vector = MFMA) dense
+HBM_PEAK_GBS = 8000.0           # MI355X_MICROARCH.md, spec
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=20)
+    p.add_argument("--warmup", type=int, default=5)
+    p.add_argument("--batch", type=int, default=1, help="pairs per GPU per step")
+    p.add_argument("--height", type=int, default=576)
+    p.add_argument("--width", type=int, default=960)
+    p.add_argument("--maxdisp", type=int, default=192)
+    p.add_argument("--cpu-baseline", type=int, default=1, help="time the CPU oracle (rank 0, N=1)")
+    p.add_argument("--cpu-steps", type=int, default=2)
+    p.add_argument("--epe", type=int, default=1, help="check EPE vs the reference golden disparity")
+    p.add_argument("--breakdown", type=int, default=0, help="print per-kernel conv times to stderr")
+    return p.parse_args()
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def build_model(maxdisp, device):
+    args = default_arch_args(LEAStereoArgs(maxdisp=maxdisp))
+    model = LEAStereo(args, device)
+    shapes = {k: tuple(v.shape) for k, v in model.state_dict().items()}
+    model.load_state_dict(synthetic_state_dict(shapes), strict=True)
+    return model.to(device).eval()
+
+
+def cpu_baseline(args, model, left0, right0, disp0):
+    """CPU leg: the oracle (oracle/torch_ref.py, the reference's aten op sequence
+    restated) on the host cores, on a bounded sample of the same workload: the
+    benchmark's own first pair, ``--cpu-steps`` times.  Its output doubles as
+    the parity check of the HIP disparity for that pair (EPE reported)."""
+    from oracle import torch_ref as ref
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
+    torch.set_num_threads(threads)
+    sd = {k: v.detach().cpu() for k, v in model.state_dict().items()}
+    a = arch_arrays()
+    left, right = left0.cpu(), right0.cpu()
+    with torch.no_grad():
+        ref.leastereo_forward(sd, left[..., :96, :192].contiguous(), right[..., :96, :192].contiguous(),
+                              48, a)  # warm the CPU kernels on a small case
+        t0 = time.perf_counter()
+        for _ in range(args.cpu_steps):
+            want = ref.leastereo_forward(sd, left, right, args.maxdisp, a)
+        dt = time.perf_counter() - t0
+    cpu_model = platform.processor() or platform.machine()
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    cpu_model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    return {"value": args.cpu_steps / dt, "unit": "pairs/s", "cores": threads, "kind": "port",
+            "sample": f"{args.cpu_steps} forward(s) of the benchmark's first pair at "
+                      f"{args.height}x{args.width} D={args.maxdisp} fp32 (oracle/torch_ref.py on "
+                      f"torch CPU, {cpu_model})",
+            "s_per_pair": dt / args.cpu_steps,
+            "epe_px_hip_vs_this": float((disp0.cpu().double() - want.double()).abs().mean())}
+
+
+def arch_arrays():
+    import numpy as np
+    from leastereo_amd.config import ARCH_DIR
+    return {k: np.load(os.path.join(ARCH_DIR, f)) for k, f in (
+        ("net_arch_fea", "feature_network_path.npy"), ("cell_arch_fea", "feature_genotype.npy"),
+        ("net_arch_mat", "matching_network_path.npy"), ("cell_arch_mat", "matching_genotype.npy"))}
+
+
+def golden_epe(device):
+    """HIP disparity vs the reference's own fp32 output (tests/golden/e2e.npz,
+    produced by tools/gen_golden.py from /root/reference) on its seeded input."""
+    import numpy as np
+    from leastereo_amd.weights import seeded_normal
+    gold = os.path.join(REPO, "tests", "golden")
+    with open(os.path.join(gold, "meta.json")) as f:
+        case = json.load(f)["cases"]["e2e/b1_h96_w192_md48"]
+    want = np.load(os.path.join(gold, "e2e.npz"))["b1_h96_w192_md48/disp32"]
+    m = build_model(case["maxdisp"], device)
+    shape = (1, 3, case["height"], case["width"])
+    left = torch.from_numpy(seeded_normal(case["seeds"][0], shape)).to(device)
+    right = torch.from_numpy(seeded_normal(case["seeds"][1], shape)).to(device)
+    with torch.no_grad():
+        got = m(left, right).cpu().double().numpy()
+    return float(np.abs(got - want).mean())
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    device = torch.device("cuda", local)
+    torch.backends.cudnn.benchmark = True
+    torch.backends.cudnn.allow_tf32 = False
+    torch.backends.cuda.matmul.allow_tf32 = False
+
+    model = build_model(args.maxdisp, device)
+    model.check_shape(args.height, args.width)
+    g = torch.Generator(device=device).manual_seed(1234 + rank)
+    left = torch.randn(args.batch, 3, args.height, args.width, device=device, generator=g)
+    right = torch.randn(args.batch, 3, args.height, args.width, device=device, generator=g)
+
+    def step():
+        return model(left, right)
+
+    with torch.no_grad():
+        for _ in range(max(args.warmup, 1)):
+            out = step()
+        # find the dominant conv kernel instantiation (untimed pass)
+        with kernels.KernelProbe() as probe:
+            step()
+        per_kernel = probe.summary()
+        dominant = max(per_kernel, key=lambda n: per_kernel[n]["ms"])
+        if args.breakdown and rank == 0:
+            for n, d in sorted(per_kernel.items(), key=lambda kv: -kv[1]["ms"]):
+                log(f"{n:40s} launches {d['launches']:3d}  {d['ms']:8.3f} ms  "
+                    f"{d['flops'] / d['ms'] / 1e9:8.1f} TFLOP/s  {d['bytes'] / d['ms'] / 1e6:8.1f} GB/s")
+
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        with kernels.KernelProbe([dominant]) as probe:
+            t0 = time.perf_counter()
+            for _ in range(args.steps):
+                out = step()
+            torch.cuda.synchronize()
+            if world > 1:
+                dist.barrier()
+            elapsed = time.perf_counter() - t0
+        dom = probe.summary()[dominant]
+
+    el = torch.tensor([elapsed], device=device, dtype=torch.float64)
+    if world > 1:
+        dist.all_reduce(el, op=dist.ReduceOp.MAX)
+    elapsed = float(el.item())
+
+    epe = None
+    if args.epe:
+        e = torch.tensor([golden_epe(device)], device=device, dtype=torch.float32)
+        if world > 1:
+            gathered = torch.empty(world, device=device, dtype=torch.float32)
+            dist.all_gather_into_tensor(gathered, e)  # the one RCCL all-gather (per-rank EPE)
+            e = gathered
+        epe = [float(v) for v in e.cpu()]
+
+    flops_per_launch = dom["flops"] / dom["launches"]
+    ms_per_launch = dom["ms"] / dom["launches"]
+    achieved = flops_per_launch / (ms_per_launch * 1e-3) / 1e12
+    traffic = None
+    tf_file = os.path.join(REPO, "profiles", "hbm_traffic.json")
+    if os.path.exists(tf_file):
+        with open(tf_file) as f:
+            traffic = json.load(f).get(dominant, {}).get("bytes_per_launch")
+
+    result = {
+        "metric": METRIC,
+        "value": world * args.batch * args.steps / elapsed,
+        "unit": "pairs/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": elapsed / args.steps * 1e3,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic N(0,1) stereo pairs generated on device; random-init weights of the "
+                "reference architecture (SceneFlow search result)",
+        "config": {"workload": f"SceneFlow {args.height}x{args.width} D={args.maxdisp} fp32, "
+                               f"batch {args.batch} per GPU (BASELINE configs[1])",
+                   "height": args.height, "width": args.width, "maxdisp": args.maxdisp,
+                   "global_batch": world * args.batch,
+                   "parallelism": f"dp{world} (independent pairs per rank, no collective in the step)"},
+        "roofline": {"bound": "mfma", "kernel": dominant, "achieved": achieved,
+                     "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
+                     "frac": achieved / FP32_MFMA_PEAK_TFLOPS, "traffic": traffic,
+                     "launches_per_step": dom["launches"] / args.steps,
+                     "flops_per_launch": flops_per_launch, "ms_per_launch": ms_per_launch},
+        "epe_px": None if epe is None else {
+            "vs": "reference LEAStereo fp32 disparity (tests/golden e2e b1_h96_w192_md48)",
+            "max_over_ranks": max(epe), "per_rank": epe},
+    }
+    if rank == 0 and world == 1 and args.cpu_baseline:
+        result["cpu_baseline"] = cpu_baseline(args, model, left[:1], right[:1], out[:1])
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,97 @@
+/*
+ * leastereo_hip.h — C ABI of libleastereo_hip.so, the MI355X (gfx950) kernels
+ * behind LEAStereo's inference hot path.
+ *
+ * The reference (devmentality/LEAStereo) is pure PyTorch and has no FFI; each
+ * entry point below replaces the aten op sequence at the cited reference line,
+ * and is what a ctypes/cffi binding of that path binds.
+ *
+ * Conventions
+ *   - All tensors are caller-owned device buffers, NCDHW (or NCHW) contiguous
+ *     in W, H, D order; channel stride is always D*H*W.  A per-batch stride
+ *     (in elements) lets an operand be a channel slice of a larger tensor, which
+ *     is how torch.cat (skip_model_3d.py:74,150,155) becomes free.
+ *   - `stream` is a hipStream_t (NULL = legacy default stream).  No call
+ *     allocates, synchronises or touches the host after argument checks, so every
+ *     call is hipGraph-capturable.
+ *   - Return 0 on success; LEA_E_INVALID / LEA_E_UNSUPPORTED on bad arguments
+ *     (nothing launched); otherwise a hipError_t from the launch.
+ *     lea_last_error() describes the last failure on the calling thread.
+ *   - dtype: LEA_F32 (the reference's arithmetic).  LEA_BF16 is reserved.
+ */
+#ifndef LEASTEREO_HIP_H
+#define LEASTEREO_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define LEA_ABI_VERSION 1
+
+#define LEA_F32 0
+#define LEA_BF16 1
+
+#define LEA_OK 0
+#define LEA_E_INVALID 1001
+#define LEA_E_UNSUPPORTED 1002
+
+/* conv epilogue flags */
+#define LEA_RELU 1u     /* ReLU after the BN affine (operations_3d.py:45-46)          */
+#define LEA_RESIDUAL 2u /* y = act(...) + residual: the cell's `sum(new_states)`
+                           (skip_model_3d.py:69); residual may alias y               */
+
+int lea_abi_version(void);
+const char* lea_last_error(void);
+
+/* Cost volume.  Replaces retrain/LEAStereo.py:34-48 (zero-init + 2*D3 strided copies).
+ *   cost[b, c,   i, h, w] = left [b, c, h, w]     for w >= i
+ *   cost[b, C+c, i, h, w] = right[b, c, h, w - i] for w >= i,   0 for w < i
+ * left/right: [B, C, H, W]; cost: [B, 2C, D3, H, W].  D3 = int(maxdisp / 3). */
+int lea_build_cost_volume(const void* left, const void* right, void* cost,
+                          int B, int C, int H, int W, int D3, int dtype, void* stream);
+
+/* Packed-weight size (in floats) for a ConvBR of the given shape; k in {1, 3}. */
+size_t lea_conv3d_packed_floats(int cout, int cin, int k);
+
+/* Re-lay an OIDHW fp32 weight ([cout, cin, k, k, k], device) into the kernel's
+ * packed layout (device).  Done once per load_state_dict. */
+int lea_conv3d_pack_weights(const float* w, float* packed, int cout, int cin, int k,
+                            void* stream);
+
+/* ConvBR3d.  Replaces models/operations_3d.py:41-47 (Conv3d no bias, stride 1,
+ * pad k/2 -> BatchNorm3d eval -> ReLU) with BN folded on the host into
+ *   scale = gamma / sqrt(var + eps),  shift = beta - mean * scale
+ * (both NULL = bn=False).  x: [B, cin, D, H, W] at batch stride x_bstride;
+ * y/residual: [B, cout, D, H, W] at their batch strides. */
+int lea_conv3d_bnrelu(const void* x, int64_t x_bstride, const float* w_packed,
+                      const float* scale, const float* shift,
+                      const void* residual, int64_t r_bstride,
+                      void* y, int64_t y_bstride,
+                      int B, int cin, int cout, int D, int H, int W, int k,
+                      unsigned flags, int dtype, void* stream);
+
+/* Name of the kernel instantiation lea_conv3d_bnrelu launches for this shape
+ * (matches the demangled name rocprofv3 reports); NULL if unsupported. */
+const char* lea_conv3d_kernel_name(int cout, int cin, int D, int H, int W, int k);
+
+/* Trilinear resample.  Replaces F.interpolate(mode='trilinear') at
+ * skip_model_3d.py:48,50 and nn.Upsample at :162-164 (align_corners=1), with
+ * PyTorch's source-index rule. */
+int lea_resample3d_trilinear(const void* x, int64_t x_bstride, void* y, int64_t y_bstride,
+                             int B, int C, int Di, int Hi, int Wi, int Do, int Ho, int Wo,
+                             int align_corners, int dtype, void* stream);
+
+/* Disparity regression.  Replaces models/build_model_2d.py:52-57 + :33-42:
+ *   U = trilinear(cost, [maxdisp, 3*H3, 3*W3], align_corners=False)
+ *   disp[b, h, w] = sum_d d * softmax(-U, dim=d)
+ * fused, U never materialised.  cost: [B, 1, D3, H3, W3]; disp: [B, 3H3, 3W3] fp32. */
+int lea_disparity_regression(const void* cost, float* disp, int B, int D3, int H3, int W3,
+                             int maxdisp, int dtype, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* LEASTEREO_HIP_H */

@@ -1,0 +1,71 @@
+"""ctypes binding of libleastereo_hip.so (include/leastereo_hip.h).
+
+Loading fails loudly: there is no CPU or eager fallback for the hot path.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+
+LIB_PATH = os.environ.get(
+    "LEASTEREO_HIP_LIB",
+    os.path.join(os.path.dirname(os.path.abspath(__file__)), "libleastereo_hip.so"))
+
+LEA_F32 = 0
+LEA_BF16 = 1
+LEA_RELU = 1
+LEA_RESIDUAL = 2
+
+_p = ctypes.c_void_p
+_i = ctypes.c_int
+_i64 = ctypes.c_int64
+_u = ctypes.c_uint
+
+# name -> (restype, argtypes); exactly the symbols include/leastereo_hip.h declares
+SIGNATURES = {
+    "lea_abi_version": (_i, []),
+    "lea_last_error": (ctypes.c_char_p, []),
+    "lea_build_cost_volume": (_i, [_p, _p, _p, _i, _i, _i, _i, _i, _i, _p]),
+    "lea_conv3d_packed_floats": (ctypes.c_size_t, [_i, _i, _i]),
+    "lea_conv3d_pack_weights": (_i, [_p, _p, _i, _i, _i, _p]),
+    "lea_conv3d_bnrelu": (_i, [_p, _i64, _p, _p, _p, _p, _i64, _p, _i64,
+                               _i, _i, _i, _i, _i, _i, _i, _u, _i, _p]),
+    "lea_conv3d_kernel_name": (ctypes.c_char_p, [_i, _i, _i, _i, _i, _i]),
+    "lea_resample3d_trilinear": (_i, [_p, _i64, _p, _i64, _i, _i, _i, _i, _i, _i, _i, _i,
+                                      _i, _i, _p]),
+    "lea_disparity_regression": (_i, [_p, _p, _i, _i, _i, _i, _i, _i, _p]),
+}
+
+_lib = None
+_lock = threading.Lock()
+
+
+class HipKernelError(RuntimeError):
+    pass
+
+
+def load():
+    """Load (once) and type the shared library; raise if it is missing."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    with _lock:
+        if _lib is None:
+            if not os.path.exists(LIB_PATH):
+                raise HipKernelError(
+                    f"{LIB_PATH} not found: build it with `make` (hipcc --offload-arch=gfx950); "
+                    "the LEAStereo hot path has no fallback")
+            lib = ctypes.CDLL(LIB_PATH)
+            for name, (res, args) in SIGNATURES.items():
+                fn = getattr(lib, name)
+                fn.restype = res
+                fn.argtypes = args
+            _lib = lib
+    return _lib
+
+
+def check(rc: int, what: str):
+    if rc != 0:
+        msg = load().lea_last_error().decode(errors="replace")
+        raise HipKernelError(f"{what} failed (rc={rc}): {msg}")

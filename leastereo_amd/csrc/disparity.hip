@@ -1,0 +1,123 @@
+// Fused disparity regression: trilinear (align_corners=False) upsample of the
+// matching-net output by 3 in D, H, W + softmin over D + sum_d d * p_d.
+// Replaces models/build_model_2d.py:52-57 (Disp.forward) and :33-42
+// (DisparityRegression.forward).  The [B, maxdisp, 3H3, 3W3] volume the reference
+// materialises (425 MB at 576x960 D192 fp32) never exists here.
+//
+// One thread per output pixel (b, oh, ow), 256 consecutive ow per workgroup.
+// The bilinear (h, w) weights and four source columns are fixed per pixel, so the
+// thread walks the D axis once: plane values v[dd] = bilerp(cost[dd]) are formed
+// on demand (each input plane at most once, d0(od) is monotone), the depth lerp
+// gives U[od], and an online softmin (running min m, s = sum e^(m-U), t = sum
+// od*e^(m-U), rescaled when m drops) produces disp = t / s.  Reads are the
+// 4*D3 cost values per pixel (cache-resident: 3x3 output pixels share them);
+// the kernel is bound by the exp/lerp issue, far below HBM time.
+#include "common.h"
+
+namespace lea {
+
+struct AxisW {
+  int i0, i1;
+  float l0, l1;
+};
+
+// aten area_pixel_compute_source_index, align_corners=False, clamped at 0.
+__device__ __forceinline__ AxisW src_axis(float ratio, int o, int in, int out) {
+#pragma clang fp contract(off)
+  AxisW a;
+  if (in == out) {
+    a.i0 = a.i1 = o;
+    a.l0 = 1.f;
+    a.l1 = 0.f;
+    return a;
+  }
+  float real = ratio * ((float)o + 0.5f) - 0.5f;
+  if (real < 0.f) real = 0.f;
+  int i = (int)floorf(real);
+  if (i > in - 1) i = in - 1;
+  float lam = fminf(fmaxf(real - (float)i, 0.f), 1.f);
+  a.i0 = i;
+  a.i1 = i + ((i < in - 1) ? 1 : 0);
+  a.l1 = lam;
+  a.l0 = 1.f - lam;
+  return a;
+}
+
+__global__ __launch_bounds__(256) void disparity_f32(const float* __restrict__ cost,
+                                                     float* __restrict__ disp, int D3, int H3,
+                                                     int W3, int maxdisp, float rd, float rh,
+                                                     float rw) {
+#pragma clang fp contract(off)
+  const int Ho = 3 * H3, Wo = 3 * W3;
+  const int ow = blockIdx.x * blockDim.x + threadIdx.x;
+  if (ow >= Wo) return;
+  const int oh = blockIdx.y;
+  const int b = blockIdx.z;
+  const AxisW ah = src_axis(rh, oh, H3, Ho);
+  const AxisW aw = src_axis(rw, ow, W3, Wo);
+  const long long HW = (long long)H3 * W3;
+  const float* base = cost + (long long)b * D3 * HW;
+  const float* r0 = base + (long long)ah.i0 * W3;
+  const float* r1 = base + (long long)ah.i1 * W3;
+
+  auto plane = [&](int dd) -> float {
+    const long long o = (long long)dd * HW;
+    return ah.l0 * (aw.l0 * r0[o + aw.i0] + aw.l1 * r0[o + aw.i1]) +
+           ah.l1 * (aw.l0 * r1[o + aw.i0] + aw.l1 * r1[o + aw.i1]);
+  };
+
+  int cur0 = -1, cur1 = -1;
+  float v0 = 0.f, v1 = 0.f;
+  float m = 0.f, s = 0.f, t = 0.f;
+  for (int od = 0; od < maxdisp; ++od) {
+    const AxisW ad = src_axis(rd, od, D3, maxdisp);
+    if (ad.i0 != cur0) {
+      v0 = (ad.i0 == cur1) ? v1 : plane(ad.i0);
+      cur0 = ad.i0;
+    }
+    if (ad.i1 != cur1) {
+      v1 = (ad.i1 == cur0) ? v0 : plane(ad.i1);
+      cur1 = ad.i1;
+    }
+    const float u = ad.l0 * v0 + ad.l1 * v1;
+    if (od == 0) {
+      m = u;
+      s = 1.f;
+      t = 0.f;
+    } else if (u < m) {
+      const float f = expf(u - m);  // < 1: rescale what was summed against the old min
+      s = s * f + 1.f;
+      t = t * f + (float)od;
+      m = u;
+    } else {
+      const float e = expf(m - u);
+      s += e;
+      t += (float)od * e;
+    }
+  }
+  disp[((long long)b * Ho + oh) * Wo + ow] = t / s;
+}
+
+}  // namespace lea
+
+extern "C" int lea_disparity_regression(const void* cost, float* disp, int B, int D3, int H3,
+                                        int W3, int maxdisp, int dtype, void* stream) {
+  using namespace lea;
+  clear_error();
+  LEA_CHECK_ARG(cost && disp, "lea_disparity_regression: null pointer");
+  LEA_CHECK_ARG(B > 0 && D3 > 0 && H3 > 0 && W3 > 0 && maxdisp > 0,
+                "lea_disparity_regression: bad shape B=%d D3=%d H3=%d W3=%d maxdisp=%d", B, D3, H3,
+                W3, maxdisp);
+  LEA_CHECK_ARG(3 * H3 <= 65535 && B <= 65535, "lea_disparity_regression: grid too large");
+  if (dtype != LEA_F32) {
+    set_error("lea_disparity_regression: dtype %d unsupported", dtype);
+    return LEA_E_UNSUPPORTED;
+  }
+  const int Wo = 3 * W3;
+  dim3 block(256);
+  dim3 grid((Wo + 255) / 256, 3 * H3, B);
+  disparity_f32<<<grid, block, 0, as_stream(stream)>>>(
+      (const float*)cost, disp, D3, H3, W3, maxdisp, (float)D3 / (float)maxdisp,
+      (float)H3 / (float)(3 * H3), (float)W3 / (float)(3 * W3));
+  return launch_status("lea_disparity_regression");
+}

@@ -1,0 +1,97 @@
+// Trilinear resample of an NCDHW volume with PyTorch's source-index rule.
+// Replaces F.interpolate(..., mode='trilinear', align_corners=True) at
+// retrain/skip_model_3d.py:48,50 and nn.Upsample at :162-164 (the level changes
+// between the 1x, 1/2x and 1/4x matching-net resolutions).
+//
+// One thread per output voxel along W (coalesced stores); the 8 taps come from
+// two input rows pairs that neighbouring threads share through L1/L2.  Pure
+// streaming: bound by (input + output) bytes.  Interpolation weights follow
+// aten's area_pixel_compute_scale / area_pixel_compute_source_index and the
+// nested lerp order t0*(h0*(w0*a + w1*b) + h1*(...)) + t1*(...).
+#include "common.h"
+
+namespace lea {
+
+struct Axis {
+  int i0, i1;
+  float l0, l1;
+};
+
+__device__ __forceinline__ Axis axis_index(float ratio, int o, int in, int out, int ac) {
+#pragma clang fp contract(off)
+  Axis a;
+  if (in == out) {
+    a.i0 = a.i1 = o;
+    a.l0 = 1.f;
+    a.l1 = 0.f;
+    return a;
+  }
+  float real = ac ? ratio * (float)o : ratio * ((float)o + 0.5f) - 0.5f;
+  if (!ac && real < 0.f) real = 0.f;
+  int i = (int)floorf(real);
+  if (i > in - 1) i = in - 1;
+  float lam = real - (float)i;
+  lam = fminf(fmaxf(lam, 0.f), 1.f);
+  a.i0 = i;
+  a.i1 = i + ((i < in - 1) ? 1 : 0);
+  a.l1 = lam;
+  a.l0 = 1.f - lam;
+  return a;
+}
+
+__host__ inline float axis_ratio(int in, int out, int ac) {
+  if (ac) return out > 1 ? (float)(in - 1) / (float)(out - 1) : 0.f;
+  return (float)in / (float)out;
+}
+
+__global__ __launch_bounds__(256) void resample3d_f32(const float* __restrict__ x, long long xbs,
+                                                      float* __restrict__ y, long long ybs, int C,
+                                                      int Di, int Hi, int Wi, int Do, int Ho, int Wo,
+                                                      float rd, float rh, float rw, int ac) {
+#pragma clang fp contract(off)
+  const int ow = blockIdx.x * blockDim.x + threadIdx.x;
+  if (ow >= Wo) return;
+  const int oh = blockIdx.y % Ho;
+  const int od = blockIdx.y / Ho;
+  const int bc = blockIdx.z;  // b * C + c
+  const int b = bc / C, c = bc - b * C;
+  const Axis ad = axis_index(rd, od, Di, Do, ac);
+  const Axis ah = axis_index(rh, oh, Hi, Ho, ac);
+  const Axis aw = axis_index(rw, ow, Wi, Wo, ac);
+  const long long HWi = (long long)Hi * Wi;
+  const float* xc = x + (long long)b * xbs + (long long)c * Di * HWi;
+  const float* p00 = xc + ad.i0 * HWi + (long long)ah.i0 * Wi;
+  const float* p01 = xc + ad.i0 * HWi + (long long)ah.i1 * Wi;
+  const float* p10 = xc + ad.i1 * HWi + (long long)ah.i0 * Wi;
+  const float* p11 = xc + ad.i1 * HWi + (long long)ah.i1 * Wi;
+  const float v = ad.l0 * (ah.l0 * (aw.l0 * p00[aw.i0] + aw.l1 * p00[aw.i1]) +
+                           ah.l1 * (aw.l0 * p01[aw.i0] + aw.l1 * p01[aw.i1])) +
+                  ad.l1 * (ah.l0 * (aw.l0 * p10[aw.i0] + aw.l1 * p10[aw.i1]) +
+                           ah.l1 * (aw.l0 * p11[aw.i0] + aw.l1 * p11[aw.i1]));
+  y[(long long)b * ybs + (long long)c * Do * Ho * Wo + ((long long)od * Ho + oh) * Wo + ow] = v;
+}
+
+}  // namespace lea
+
+extern "C" int lea_resample3d_trilinear(const void* x, int64_t x_bstride, void* y, int64_t y_bstride,
+                                        int B, int C, int Di, int Hi, int Wi, int Do, int Ho, int Wo,
+                                        int align_corners, int dtype, void* stream) {
+  using namespace lea;
+  clear_error();
+  LEA_CHECK_ARG(x && y && x != y, "lea_resample3d_trilinear: null or aliased pointer");
+  LEA_CHECK_ARG(B > 0 && C > 0 && Di > 0 && Hi > 0 && Wi > 0 && Do > 0 && Ho > 0 && Wo > 0,
+                "lea_resample3d_trilinear: bad shape");
+  LEA_CHECK_ARG((long long)Do * Ho <= 65535 && (long long)B * C <= 65535,
+                "lea_resample3d_trilinear: grid too large (Do*Ho=%d, B*C=%d)", Do * Ho, B * C);
+  if (dtype != LEA_F32) {
+    set_error("lea_resample3d_trilinear: dtype %d unsupported", dtype);
+    return LEA_E_UNSUPPORTED;
+  }
+  const int ac = align_corners ? 1 : 0;
+  dim3 block(Wo >= 256 ? 256 : ((Wo + 63) / 64) * 64);
+  dim3 grid((Wo + block.x - 1) / block.x, Do * Ho, B * C);
+  resample3d_f32<<<grid, block, 0, as_stream(stream)>>>(
+      (const float*)x, x_bstride, (float*)y, y_bstride, C, Di, Hi, Wi, Do, Ho, Wo,
+      axis_ratio(Di, Do, ac), axis_ratio(Hi, Ho, ac), axis_ratio(Wi, Wo, ac), ac);
+  return launch_status("lea_resample3d_trilinear");
+}

@@ -1,0 +1,125 @@
+"""Matching-net executor: runs retrain/skip_model_3d.py:140-174 on the HIP kernels.
+
+Prepared once per weight load (``NewMatching.executor()``): every 3D ConvBR's
+weight is re-laid out for the conv kernel and its BN folded into fp32
+scale/shift.  ``run`` then issues only C-ABI launches on the current stream
+(no host syncs), so a whole forward can be captured in a HIP graph.
+
+Memory plan per cell (skip_model_3d.py:41-75): the cell output
+``cat([s1, s2, s3, s4])`` is allocated once and every producer writes its
+channel slice directly (preprocess -> s1 slot, first DAG op -> s_k slot, second
+DAG op accumulates into the same slot through the conv epilogue), so neither the
+``cat`` nor the ``sum`` ever moves data.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+
+import torch
+
+from . import kernels
+from .arch import scale_dimension
+
+
+@dataclass
+class ConvParams:
+    packed: torch.Tensor
+    scale: torch.Tensor | None
+    shift: torch.Tensor | None
+    cin: int
+    cout: int
+    k: int
+    relu: bool
+
+
+class MatchingExecutor:
+    def __init__(self, matching):
+        from .model import ConvBR
+        self.m = matching
+        self.p = {}
+        with torch.no_grad():
+            for name, mod in matching.named_modules():
+                if isinstance(mod, ConvBR):
+                    w = mod.conv.weight
+                    if w.dim() != 5:
+                        continue
+                    scale, shift = mod.folded_bn()
+                    self.p[name] = ConvParams(kernels.pack_conv_weight(w), scale, shift,
+                                              w.shape[1], w.shape[0], w.shape[-1], mod.relu)
+
+    def conv(self, name, x, out=None, accumulate=False):
+        p = self.p[name]
+        if x.shape[1] != p.cin:
+            raise ValueError(f"{name}: expected {p.cin} input channels, got {x.shape[1]}")
+        return kernels.conv3d_bnrelu(x, p.packed, p.cout, p.k, p.scale, p.shift, p.relu, out,
+                                     accumulate)
+
+    def cell(self, i, s0, s1):
+        """Cell.forward (skip_model_3d.py:41-75)."""
+        cell = self.m.cells[i]
+        c = cell.c_out
+        prev_input = s1
+        if cell.downup_sample != 0:
+            sc = 0.5 if cell.downup_sample < 0 else 2
+            s1 = kernels.resample_trilinear(s1, [scale_dimension(n, sc) for n in s1.shape[2:]])
+        if s0.shape[2:] != s1.shape[2:]:
+            s0 = kernels.resample_trilinear(s0, s1.shape[2:])
+        b, _, d, h, w = s1.shape
+        bm = cell.block_multiplier
+        n_states = 2 + cell.steps
+        out = torch.empty((b, bm * c, d, h, w), device=s1.device, dtype=s1.dtype)
+        slot = {idx: out[:, k * c:(k + 1) * c] for k, idx in enumerate(range(n_states - bm, n_states))}
+        if s0.shape[1] != c:
+            s0 = self.conv(f"cells.{i}.pre_preprocess", s0, out=slot.get(0))
+        elif 0 in slot:
+            slot[0].copy_(s0)
+        s1 = self.conv(f"cells.{i}.preprocess", s1, out=slot.get(1))
+        states = [s0, s1]
+        for terms in cell.plan:
+            dst = slot.get(len(states))
+            if dst is None:
+                dst = torch.empty((b, c, d, h, w), device=s1.device, dtype=s1.dtype)
+            for n, (k, j) in enumerate(terms):
+                if cell.op_kinds[k] == "conv":
+                    self.conv(f"cells.{i}._ops.{k}", states[j], out=dst, accumulate=n > 0)
+                elif n == 0:
+                    dst.copy_(states[j])
+                else:
+                    dst.add_(states[j])
+            states.append(dst)
+        return prev_input, out
+
+    def run(self, x):
+        """newMatching.forward (skip_model_3d.py:140-174): [B,64,D3,H3,W3] -> [B,1,D3,H3,W3]."""
+        stem0 = self.conv("stem0", x)
+        stem1 = self.conv("stem1", stem0)
+        outs = []
+        prev = (stem0, stem1)
+        n = len(self.m.cells)
+        for i in range(n):
+            if i == 5 and n == 12:   # :150-151
+                fused = self.conv("conv1", torch.cat((outs[1][1], outs[4][1]), 1))
+                prev = (outs[4][0], fused)
+            elif i == 9 and n == 12:  # :155-156
+                fused = self.conv("conv2", torch.cat((outs[4][1], outs[8][1]), 1))
+                prev = (outs[8][0], fused)
+            o = self.cell(i, prev[0], prev[1])
+            outs.append(o)
+            prev = o
+        last = outs[-1][1]
+        d, h, w = x.shape[2:]
+        lh = last.shape[3]
+        if lh == h:
+            y = last
+        elif lh == h // 2:
+            y = kernels.resample_trilinear(self.conv("last_6", last), (d, h, w))
+        elif lh == h // 4:
+            y = kernels.resample_trilinear(self.conv("last_12", last), (d // 2, h // 2, w // 2))
+            y = kernels.resample_trilinear(self.conv("last_6", y), (d, h, w))
+        elif lh == h // 8:
+            y = kernels.resample_trilinear(self.conv("last_24", last), (d // 4, h // 4, w // 4))
+            y = kernels.resample_trilinear(self.conv("last_12", y), (d // 2, h // 2, w // 2))
+            y = kernels.resample_trilinear(self.conv("last_6", y), (d, h, w))
+        else:
+            raise ValueError(f"matching-net output size {tuple(last.shape[2:])} has no head")
+        return self.conv("last_3", y)

@@ -1,0 +1,178 @@
+"""Tensor-level wrappers over the C ABI: device tensors in, device tensors out.
+
+Each wrapper checks shapes/strides on the host, then launches on the current
+HIP stream (``torch.cuda.current_stream()``), so it composes with torch ops
+and is capturable by ``torch.cuda.graph``.  There is no fallback: a non-CUDA
+tensor or a missing library raises.
+"""
+from __future__ import annotations
+
+import torch
+
+from . import _lib
+from ._lib import LEA_F32, LEA_RELU, LEA_RESIDUAL, check
+
+
+def _stream():
+    return torch.cuda.current_stream().cuda_stream
+
+
+class KernelProbe:
+    """Times launches of conv kernel instantiations with HIP events recorded on
+    the stream the kernel is launched on (torch's current stream).
+
+    ``names=None`` records every conv launch.  Each record carries the launch's
+    algorithmic FLOPs and bytes (input + output + weights [+ residual read]).
+    """
+
+    def __init__(self, names=None):
+        self.names = None if names is None else set(names)
+        self.records = []  # (name, flops, bytes, start_event, end_event)
+
+    def __enter__(self):
+        global _probe
+        _probe = self
+        return self
+
+    def __exit__(self, *exc):
+        global _probe
+        _probe = None
+
+    def summary(self):
+        torch.cuda.synchronize()
+        out = {}
+        for name, flops, nbytes, e0, e1 in self.records:
+            d = out.setdefault(name, {"launches": 0, "flops": 0.0, "bytes": 0.0, "ms": 0.0})
+            d["launches"] += 1
+            d["flops"] += flops
+            d["bytes"] += nbytes
+            d["ms"] += e0.elapsed_time(e1)
+        return out
+
+
+_probe = None
+
+
+def conv_kernel_name(cout, cin, d, h, w, k):
+    name = _lib.load().lea_conv3d_kernel_name(cout, cin, d, h, w, k)
+    return name.decode() if name else None
+
+
+def _require_cuda(*ts):
+    for t in ts:
+        if t is not None and (not t.is_cuda or t.dtype != torch.float32):
+            raise _lib.HipKernelError(
+                f"HIP path needs float32 tensors on a ROCm device, got {t.dtype} on {t.device}")
+
+
+def _check_volume_view(t: torch.Tensor, name: str):
+    """NCDHW tensor whose (C, D, H, W) block is contiguous per batch (a channel
+    slice of a contiguous tensor qualifies); returns the batch stride."""
+    b, c, d, h, w = t.shape
+    if t.stride()[1:] != (d * h * w, h * w, w, 1):
+        raise ValueError(f"{name}: NCDHW slice with contiguous C,D,H,W required, strides {t.stride()}")
+    return t.stride(0)
+
+
+def build_cost_volume(fl: torch.Tensor, fr: torch.Tensor, maxdisp: int) -> torch.Tensor:
+    """retrain/LEAStereo.py:34-48 -> [B, 2C, int(maxdisp/3), H, W]."""
+    _require_cuda(fl, fr)
+    fl, fr = fl.contiguous(), fr.contiguous()
+    if fl.shape != fr.shape or fl.dim() != 4:
+        raise ValueError("left/right features must both be [B, C, H, W]")
+    b, c, h, w = fl.shape
+    d3 = int(maxdisp / 3)
+    cost = torch.empty((b, 2 * c, d3, h, w), device=fl.device, dtype=fl.dtype)
+    check(_lib.load().lea_build_cost_volume(fl.data_ptr(), fr.data_ptr(), cost.data_ptr(), b, c, h,
+                                            w, d3, LEA_F32, _stream()), "lea_build_cost_volume")
+    return cost
+
+
+def packed_floats(cout: int, cin: int, k: int) -> int:
+    n = _lib.load().lea_conv3d_packed_floats(cout, cin, k)
+    if n == 0:
+        raise ValueError(f"unsupported conv shape cout={cout} cin={cin} k={k}")
+    return n
+
+
+def pack_conv_weight(w: torch.Tensor) -> torch.Tensor:
+    """[cout, cin, k, k, k] fp32 device weight -> the kernel's packed layout."""
+    _require_cuda(w)
+    w = w.detach().contiguous()
+    cout, cin, k = w.shape[0], w.shape[1], w.shape[-1]
+    packed = torch.empty(packed_floats(cout, cin, k), device=w.device, dtype=torch.float32)
+    check(_lib.load().lea_conv3d_pack_weights(w.data_ptr(), packed.data_ptr(), cout, cin, k,
+                                              _stream()), "lea_conv3d_pack_weights")
+    return packed
+
+
+def conv3d_bnrelu(x: torch.Tensor, packed: torch.Tensor, cout: int, k: int,
+                  scale: torch.Tensor | None, shift: torch.Tensor | None, relu: bool = True,
+                  out: torch.Tensor | None = None, accumulate: bool = False) -> torch.Tensor:
+    """ConvBR3d (operations_3d.py:41-47).  ``out`` may be a channel slice of a
+    larger (cat) buffer; ``accumulate`` adds the activation to what ``out``
+    holds (the cell's pairwise sum, skip_model_3d.py:69)."""
+    _require_cuda(x, packed, scale, shift, out)
+    b, cin, d, h, w = x.shape
+    xbs = _check_volume_view(x, "x")
+    if out is None:
+        if accumulate:
+            raise ValueError("accumulate needs out")
+        out = torch.empty((b, cout, d, h, w), device=x.device, dtype=x.dtype)
+    if tuple(out.shape) != (b, cout, d, h, w):
+        raise ValueError(f"out shape {tuple(out.shape)} != {(b, cout, d, h, w)}")
+    ybs = _check_volume_view(out, "out")
+    flags = (LEA_RELU if relu else 0) | (LEA_RESIDUAL if accumulate else 0)
+    probe = _probe
+    if probe is not None:
+        name = conv_kernel_name(cout, cin, d, h, w, k)
+        if probe.names is None or name in probe.names:
+            vox = b * d * h * w
+            flops = 2.0 * vox * cout * cin * k ** 3
+            nbytes = 4.0 * (vox * (cin + cout * (2 if accumulate else 1)) + cout * cin * k ** 3)
+            e0 = torch.cuda.Event(enable_timing=True)
+            e1 = torch.cuda.Event(enable_timing=True)
+            e0.record()
+        else:
+            probe = None
+    check(_lib.load().lea_conv3d_bnrelu(
+        x.data_ptr(), xbs, packed.data_ptr(),
+        scale.data_ptr() if scale is not None else None,
+        shift.data_ptr() if shift is not None else None,
+        out.data_ptr() if accumulate else None, ybs if accumulate else 0,
+        out.data_ptr(), ybs, b, cin, cout, d, h, w, k, flags, LEA_F32, _stream()),
+        "lea_conv3d_bnrelu")
+    if probe is not None:
+        e1.record()
+        probe.records.append((name, flops, nbytes, e0, e1))
+    return out
+
+
+def resample_trilinear(x: torch.Tensor, size, align_corners: bool = True,
+                       out: torch.Tensor | None = None) -> torch.Tensor:
+    """F.interpolate(x, size, mode='trilinear', align_corners=...) for NCDHW."""
+    _require_cuda(x, out)
+    b, c, di, hi, wi = x.shape
+    do, ho, wo = (int(s) for s in size)
+    xbs = _check_volume_view(x, "x")
+    if out is None:
+        out = torch.empty((b, c, do, ho, wo), device=x.device, dtype=x.dtype)
+    ybs = _check_volume_view(out, "out")
+    check(_lib.load().lea_resample3d_trilinear(x.data_ptr(), xbs, out.data_ptr(), ybs, b, c, di, hi,
+                                               wi, do, ho, wo, 1 if align_corners else 0, LEA_F32,
+                                               _stream()), "lea_resample3d_trilinear")
+    return out
+
+
+def disparity_regression(cost: torch.Tensor, maxdisp: int) -> torch.Tensor:
+    """Disp + DisparityRegression (build_model_2d.py:52-57, 33-42): [B,1,D3,H3,W3] -> [B,3H3,3W3]."""
+    _require_cuda(cost)
+    if cost.dim() != 5 or cost.shape[1] != 1:
+        raise ValueError("cost must be [B, 1, D3, H3, W3]")
+    cost = cost.contiguous()
+    b, _, d3, h3, w3 = cost.shape
+    disp = torch.empty((b, 3 * h3, 3 * w3), device=cost.device, dtype=torch.float32)
+    check(_lib.load().lea_disparity_regression(cost.data_ptr(), disp.data_ptr(), b, d3, h3, w3,
+                                               maxdisp, LEA_F32, _stream()),
+          "lea_disparity_regression")
+    return disp

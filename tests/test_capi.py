@@ -1,0 +1,58 @@
+"""The C-ABI library loads and exports every symbol include/*.h declares (CPU:
+only argument-checking paths are called, nothing launches)."""
+import ctypes
+import glob
+import os
+import re
+
+import pytest
+
+from leastereo_amd import _lib
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def declared_symbols():
+    names = set()
+    for h in glob.glob(os.path.join(REPO, "include", "*.h")):
+        src = open(h).read()
+        src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+        names |= set(re.findall(r"\b(lea_\w+)\s*\(", src))
+    return names
+
+
+def test_header_and_binding_agree():
+    assert declared_symbols() == set(_lib.SIGNATURES)
+
+
+def test_library_exports_every_declared_symbol():
+    lib = _lib.load()
+    for name in declared_symbols():
+        assert hasattr(lib, name), name
+    assert lib.lea_abi_version() == 1
+
+
+def test_invalid_arguments_are_rejected_before_launch():
+    lib = _lib.load()
+    assert lib.lea_build_cost_volume(None, None, None, 1, 1, 1, 1, 1, 0, None) == 1001
+    assert b"null" in lib.lea_last_error()
+    assert lib.lea_conv3d_bnrelu(None, 0, None, None, None, None, 0, None, 0,
+                                 1, 1, 1, 1, 1, 1, 3, 1, 0, None) == 1001
+    x = ctypes.c_void_p(16)
+    # scale without shift
+    assert lib.lea_conv3d_bnrelu(x, 0, x, x, None, None, 0, ctypes.c_void_p(32), 0,
+                                 1, 1, 1, 1, 1, 1, 3, 1, 0, None) == 1001
+    # unsupported dtype is reported as such
+    assert lib.lea_disparity_regression(x, x, 1, 1, 1, 1, 1, 1, None) == 1002
+    assert lib.lea_resample3d_trilinear(x, 0, x, 0, 1, 1, 1, 1, 1, 1, 1, 1, 1, 0, None) == 1001
+
+
+@pytest.mark.parametrize("cout,cin,k", [(32, 64, 3), (64, 128, 3), (16, 16, 3), (8, 8, 3),
+                                        (1, 32, 3), (16, 64, 1), (32, 128, 1), (8, 64, 1)])
+def test_packed_sizes(cout, cin, k):
+    n = _lib.load().lea_conv3d_packed_floats(cout, cin, k)
+    cin_b = 4 if k == 3 else 32
+    mt = 1 if cout <= 16 else (2 if cout <= 32 else 4)
+    cops = mt * 16 + (16 if (mt * 16) % 32 == 0 else 0)
+    assert n == -(-cin // cin_b) * k ** 3 * cin_b * cops
+    assert _lib.load().lea_conv3d_packed_floats(65, 8, 3) == 0

@@ -1,0 +1,193 @@
+"""GPU parity: the HIP path (through the C ABI) against the golden vectors of the
+reference and against the CPU/torch oracle on the same seeded inputs.
+
+Tolerances (floating point, BASELINE.json north_star: disparity within 1e-3 px
+EPE of the PyTorch reference in fp32):
+  cost volume            bit-exact (pure copy)
+  ConvBR3d               |d| <= 1e-4 + 1e-4*|ref|  (fp32, K up to 3456, reassociated sums)
+  trilinear resample     |d| <= 2e-6
+  disparity regression   |d| <= 2e-5 px
+  end to end             EPE <= 1e-3 px vs reference fp32 and fp64 disparities
+"""
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+from leastereo_amd import kernels
+from leastereo_amd.config import LEAStereoArgs, default_arch_args
+from leastereo_amd.model import LEAStereo
+from oracle import torch_ref as ref
+from tests.golden_util import arch, golden, meta, normal, state_dict
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+CASES = meta()["cases"]
+
+
+def _cases(prefix):
+    return sorted(k.split("/", 1)[1] for k in CASES if k.startswith(prefix + "/"))
+
+
+@pytest.fixture(autouse=True, scope="module")
+def _no_tf32():
+    torch.backends.cudnn.allow_tf32 = False
+    torch.backends.cuda.matmul.allow_tf32 = False
+
+
+def _model(maxdisp):
+    m = LEAStereo(default_arch_args(LEAStereoArgs(maxdisp=maxdisp)), DEV)
+    m.load_state_dict(state_dict(), strict=True)
+    return m.to(DEV).eval()
+
+
+# ------------------------------------------------------------------ per-op golden
+@pytest.mark.parametrize("name", _cases("cost_volume"))
+def test_cost_volume_golden(name):
+    c = CASES["cost_volume/" + name]
+    fl = normal(c["seeds"][0], c["shape"]).to(DEV)
+    fr = normal(c["seeds"][1], c["shape"]).to(DEV)
+    out = kernels.build_cost_volume(fl, fr, c["maxdisp"]).cpu().numpy()
+    np.testing.assert_array_equal(out, golden("cost_volume")[name])
+
+
+def _conv_params(module):
+    sd = state_dict()
+    w = sd[module + ".conv.weight"].to(DEV)
+    packed = kernels.pack_conv_weight(w)
+    if module + ".bn.weight" in sd and not module.endswith("last_3"):
+        inv = 1.0 / torch.sqrt(sd[module + ".bn.running_var"] + 1e-5)
+        scale = (inv * sd[module + ".bn.weight"]).to(DEV)
+        shift = (sd[module + ".bn.bias"] - sd[module + ".bn.running_mean"] * inv * sd[module + ".bn.weight"]).to(DEV)
+    else:
+        scale = shift = None
+    return w, packed, scale, shift
+
+
+@pytest.mark.parametrize("name", _cases("convbr"))
+def test_convbr_golden(name):
+    c = CASES["convbr/" + name]
+    x = normal(c["seed"], c["input"]).to(DEV)
+    w, packed, scale, shift = _conv_params(c["module"])
+    if not c["bn"]:
+        scale = shift = None
+    y = kernels.conv3d_bnrelu(x, packed, c["cout"], c["k"], scale, shift, relu=c["relu"])
+    np.testing.assert_allclose(y.cpu().numpy(), golden("convbr")[name], rtol=1e-4, atol=1e-4)
+
+
+@pytest.mark.parametrize("name", _cases("resample"))
+def test_resample_golden(name):
+    c = CASES["resample/" + name]
+    y = kernels.resample_trilinear(normal(c["seed"], c["input"]).to(DEV), c["size"], True)
+    np.testing.assert_allclose(y.cpu().numpy(), golden("resample")[name], rtol=0, atol=2e-6)
+
+
+@pytest.mark.parametrize("name", _cases("disp"))
+def test_disparity_golden(name):
+    c = CASES["disp/" + name]
+    x = (normal(c["seed"], c["input"]) * c["gain"]).to(DEV)
+    y = kernels.disparity_regression(x, c["maxdisp"])
+    np.testing.assert_allclose(y.cpu().numpy(), golden("disp")[name], rtol=0, atol=2e-5)
+
+
+# ------------------------------------------------------------- randomized vs torch fp32
+@pytest.mark.parametrize("b,cin,cout,k,shape", [
+    (1, 64, 32, 3, (6, 20, 70)), (2, 128, 64, 3, (5, 9, 40)), (1, 16, 16, 3, (7, 33, 17)),
+    (1, 8, 8, 3, (3, 5, 100)), (1, 32, 1, 3, (4, 12, 64)), (1, 12, 20, 3, (3, 4, 5)),
+    (1, 64, 16, 1, (3, 7, 11)), (2, 128, 32, 1, (4, 6, 130)), (1, 40, 8, 1, (2, 3, 5)),
+    (1, 32, 64, 1, (1, 1, 1000))])
+def test_conv_random_vs_torch(b, cin, cout, k, shape):
+    g = torch.Generator().manual_seed(cin * 131 + cout)
+    x = torch.randn((b, cin) + shape, generator=g)
+    w = torch.randn(cout, cin, k, k, k, generator=g) / np.sqrt(cin * k ** 3)
+    scale = torch.rand(cout, generator=g) + 0.5
+    shift = torch.randn(cout, generator=g) * 0.1
+    res = torch.randn((b, cout) + shape, generator=g)
+    refy = F.conv3d(x.double(), w.double(), None, 1, k // 2)
+    refy = torch.relu(refy * scale.double().view(1, -1, 1, 1, 1) + shift.double().view(1, -1, 1, 1, 1))
+    refy = refy + res.double()
+    out = res.to(DEV).clone()
+    kernels.conv3d_bnrelu(x.to(DEV), kernels.pack_conv_weight(w.to(DEV)), cout, k, scale.to(DEV),
+                          shift.to(DEV), relu=True, out=out, accumulate=True)
+    np.testing.assert_allclose(out.cpu().double().numpy(), refy.numpy(), rtol=1e-4, atol=1e-4)
+
+
+def test_conv_channel_slices():
+    """Input and output as channel slices of larger tensors (the free cat)."""
+    g = torch.Generator().manual_seed(7)
+    big_in = torch.randn(2, 48, 4, 6, 70, generator=g).to(DEV)
+    x = big_in[:, 8:24]
+    w = (torch.randn(16, 16, 3, 3, 3, generator=g) / 10).to(DEV)
+    big_out = torch.zeros(2, 64, 4, 6, 70, device=DEV)
+    kernels.conv3d_bnrelu(x, kernels.pack_conv_weight(w), 16, 3, None, None, relu=False,
+                          out=big_out[:, 32:48])
+    refy = F.conv3d(x.cpu().double(), w.cpu().double(), None, 1, 1)
+    np.testing.assert_allclose(big_out[:, 32:48].cpu().double().numpy(), refy.numpy(), atol=1e-4, rtol=1e-4)
+    assert big_out[:, :32].abs().sum().item() == 0 and big_out[:, 48:].abs().sum().item() == 0
+
+
+def test_resample_vs_torch_random_sizes():
+    g = torch.Generator().manual_seed(3)
+    for src, dst in [((5, 9, 13), (3, 5, 7)), ((4, 6, 8), (8, 12, 16)), ((32, 96, 160), (64, 192, 320)),
+                     ((3, 3, 3), (1, 1, 1)), ((1, 4, 5), (2, 7, 9))]:
+        x = torch.randn((2, 3) + src, generator=g)
+        for ac in (True, False):
+            refy = F.interpolate(x, dst, mode="trilinear", align_corners=ac)
+            y = kernels.resample_trilinear(x.to(DEV), dst, ac).cpu()
+            np.testing.assert_allclose(y.numpy(), refy.numpy(), atol=3e-6, rtol=0)
+
+
+def test_disparity_vs_oracle_sizes():
+    g = torch.Generator().manual_seed(5)
+    for shape, md in [((1, 1, 64, 12, 20), 192), ((2, 1, 88, 5, 9), 264), ((1, 1, 16, 7, 4), 48)]:
+        x = torch.randn(shape, generator=g) * 3
+        refd = ref.disp_forward(x.double(), md)
+        y = kernels.disparity_regression(x.to(DEV), md).cpu()
+        assert torch.isfinite(y).all()
+        np.testing.assert_allclose(y.double().numpy(), refd.numpy(), atol=5e-5, rtol=0)
+
+
+# ----------------------------------------------------------------------- end to end
+@pytest.mark.parametrize("name", _cases("e2e"))
+def test_e2e_golden(name):
+    c = CASES["e2e/" + name]
+    shape = (c["batch"], 3, c["height"], c["width"])
+    left, right = normal(c["seeds"][0], shape).to(DEV), normal(c["seeds"][1], shape).to(DEV)
+    m = _model(c["maxdisp"])
+    g = golden("e2e")
+    with torch.no_grad():
+        if name + "/matching" in g:
+            fl, fr = m.feature(left), m.feature(right)
+            mat = m.matching(kernels.build_cost_volume(fl, fr, c["maxdisp"]))
+            np.testing.assert_allclose(mat.cpu().numpy(), g[name + "/matching"], rtol=1e-3, atol=1e-3)
+        disp = m(left, right).cpu()
+    assert disp.shape == g[name + "/disp32"].shape
+    e32 = ref.epe(disp, torch.from_numpy(g[name + "/disp32"]))
+    e64 = ref.epe(disp, torch.from_numpy(g[name + "/disp64"]))
+    assert e32 < 1e-3 and e64 < 1e-3, (e32, e64)
+
+
+def test_batch_rows_are_independent():
+    """B=2 result equals the two B=1 results bit for bit (no cross-pair mixing)."""
+    m = _model(48)
+    left = normal(901, (2, 3, 96, 192)).to(DEV)
+    right = normal(902, (2, 3, 96, 192)).to(DEV)
+    with torch.no_grad():
+        both = m(left, right)
+        one = torch.cat([m(left[i:i + 1], right[i:i + 1]) for i in range(2)])
+    assert torch.equal(both, one)
+
+
+def test_full_size_c2_vs_torch_oracle_on_gpu():
+    """576x960 D192 (the benchmark configuration): HIP vs the oracle's torch
+    restatement running fp32 on the same GPU (MIOpen), EPE <= 1e-3 px."""
+    m = _model(192)
+    left = normal(1234, (1, 3, 576, 960)).to(DEV)
+    right = normal(1235, (1, 3, 576, 960)).to(DEV)
+    sd = {k: v.to(DEV) for k, v in state_dict().items()}
+    with torch.no_grad():
+        disp = m(left, right)
+        want = ref.leastereo_forward(sd, left, right, 192, arch())
+    assert torch.isfinite(disp).all()
+    assert float(disp.min()) >= 0.0 and float(disp.max()) <= 191.0
+    assert ref.epe(disp.cpu(), want.cpu()) < 1e-3
