@@ -6,7 +6,7 @@
 //
 // GEMM view (per batch b, output plane d):
 //     Y[co][v] = sum_{ci, tap} Wt[co][ci][tap] * X[ci][v + off(tap)]
-// M = cout (<= 64, 16-row MFMA tiles), N = voxels (16-wide runs along W,
+// M = cout (blocks of <= 64 per workgroup, 16-row MFMA tiles), N = voxels (16-wide runs along W,
 // coalesced NCDHW), K = cin * k^3.  MFMA = v_mfma_f32_16x16x4_f32 (exact f32
 // products, f32 accumulate):
 //     A (lane l) = Wt[co = 16*mt + (l & 15)][k = l >> 4]
@@ -70,7 +70,7 @@ __global__ __launch_bounds__(kConvThreads, 2) void conv3d_f32_kernel(
     const float* __restrict__ x, long long xbs, const float* __restrict__ wp,
     const float* __restrict__ scale, const float* __restrict__ shift, const float* res,
     long long rbs, float* y, long long ybs, int cin, int cout, int D, int H, int W, int tiles_w,
-    unsigned flags) {
+    int ncob, unsigned flags) {
   using C = ConvCfg<KS, MT, NT, TW>;
   constexpr int CIN_B = C::CIN_B;
   __shared__ __attribute__((aligned(16))) float smem[C::XS + C::WS];
@@ -84,7 +84,11 @@ __global__ __launch_bounds__(kConvThreads, 2) void conv3d_f32_kernel(
   const int h0 = (tile / tiles_w) * C::TH;
   const int w0 = (tile % tiles_w) * TW;
   const int d0 = blockIdx.y;
-  const int b = blockIdx.z;
+  const int b = blockIdx.z / ncob;    // batch
+  const int cob = blockIdx.z - b * ncob;  // block of COP output channels
+  const int co0 = cob * C::COP;
+  const int nchunks = (cin + CIN_B - 1) / CIN_B;
+  wp += (long long)cob * nchunks * C::WS;
   const long long HW = (long long)H * W;
   const long long DHW = HW * D;
   const float* xb = x + (long long)b * xbs;
@@ -106,7 +110,6 @@ __global__ __launch_bounds__(kConvThreads, 2) void conv3d_f32_kernel(
 #pragma unroll
     for (int j = 0; j < NT; ++j) acc[m][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  const int nchunks = (cin + CIN_B - 1) / CIN_B;
   for (int ch = 0; ch < nchunks; ++ch) {
     const int c0 = ch * CIN_B;
     __syncthreads();  // previous chunk's reads are done
@@ -169,7 +172,7 @@ __global__ __launch_bounds__(kConvThreads, 2) void conv3d_f32_kernel(
   for (int m = 0; m < MT; ++m) {
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      const int co = m * 16 + kq * 4 + r;
+      const int co = co0 + m * 16 + kq * 4 + r;
       if (co >= cout) continue;
       const float sc = scale ? scale[co] : 1.f;
       const float sh = shift ? shift[co] : 0.f;
@@ -189,22 +192,24 @@ __global__ __launch_bounds__(kConvThreads, 2) void conv3d_f32_kernel(
   }
 }
 
-// Packed layout: [ceil(cin/CIN_B)][KS^3][CIN_B][COPS], zero outside (cin, cout).
+// Packed layout: [ceil(cout/COP)][ceil(cin/CIN_B)][KS^3][CIN_B][COPS], zero outside (cin, cout).
 template <int KS, int MT>
 __global__ void pack_weights_kernel(const float* __restrict__ w, float* __restrict__ packed,
-                                    int cout, int cin, long long total) {
+                                    int cout, int cin, int nchunks, long long total) {
   using P = PackCfg<KS, MT>;
   for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
        i += (long long)gridDim.x * blockDim.x) {
-    const int co = (int)(i % P::COPS);
+    const int col = (int)(i % P::COPS);
     long long r = i / P::COPS;
     const int cb = (int)(r % P::CIN_B);
     r /= P::CIN_B;
     const int tap = (int)(r % P::KT);
-    const int ch = (int)(r / P::KT);
+    r /= P::KT;
+    const int ch = (int)(r % nchunks);
+    const int co = (int)(r / nchunks) * P::COP + col;
     const int ci = ch * P::CIN_B + cb;
     float v = 0.f;
-    if (co < cout && ci < cin) v = w[((long long)co * cin + ci) * P::KT + tap];
+    if (col < P::COP && co < cout && ci < cin) v = w[((long long)co * cin + ci) * P::KT + tap];
     packed[i] = v;
   }
 }
@@ -212,15 +217,18 @@ __global__ void pack_weights_kernel(const float* __restrict__ w, float* __restri
 inline int mt_for(int cout) { return cout <= 16 ? 1 : (cout <= 32 ? 2 : 4); }
 
 template <int KS, int MT>
-size_t packed_floats_t(int cin) {
+size_t packed_floats_t(int cout, int cin) {
   using P = PackCfg<KS, MT>;
-  return (size_t)((cin + P::CIN_B - 1) / P::CIN_B) * P::CHUNK;
+  return (size_t)((cout + P::COP - 1) / P::COP) * ((cin + P::CIN_B - 1) / P::CIN_B) * P::CHUNK;
 }
 
 size_t packed_floats(int cout, int cin, int k) {
   const int mt = mt_for(cout);
-  if (k == 3) return mt == 1 ? packed_floats_t<3, 1>(cin) : mt == 2 ? packed_floats_t<3, 2>(cin) : packed_floats_t<3, 4>(cin);
-  return mt == 1 ? packed_floats_t<1, 1>(cin) : mt == 2 ? packed_floats_t<1, 2>(cin) : packed_floats_t<1, 4>(cin);
+  if (k == 3)
+    return mt == 1 ? packed_floats_t<3, 1>(cout, cin)
+                   : mt == 2 ? packed_floats_t<3, 2>(cout, cin) : packed_floats_t<3, 4>(cout, cin);
+  return mt == 1 ? packed_floats_t<1, 1>(cout, cin)
+                 : mt == 2 ? packed_floats_t<1, 2>(cout, cin) : packed_floats_t<1, 4>(cout, cin);
 }
 
 template <int KS, int MT, int NT, int TW>
@@ -231,10 +239,12 @@ int launch_conv(const float* x, long long xbs, const float* wp, const float* sca
   const int tiles_w = (W + TW - 1) / TW;
   const int tiles_h = (H + C::TH - 1) / C::TH;
   const long long nt = (long long)tiles_w * tiles_h;
-  LEA_CHECK_ARG(nt < (1LL << 31) && D <= 65535 && B <= 65535, "lea_conv3d_bnrelu: grid too large");
-  dim3 grid((unsigned)nt, D, B);
+  const int ncob = (cout + C::COP - 1) / C::COP;
+  LEA_CHECK_ARG(nt < (1LL << 31) && D <= 65535 && (long long)B * ncob <= 65535,
+                "lea_conv3d_bnrelu: grid too large");
+  dim3 grid((unsigned)nt, D, B * ncob);
   conv3d_f32_kernel<KS, MT, NT, TW><<<grid, kConvThreads, 0, st>>>(
-      x, xbs, wp, scale, shift, res, rbs, y, ybs, cin, cout, D, H, W, tiles_w, flags);
+      x, xbs, wp, scale, shift, res, rbs, y, ybs, cin, cout, D, H, W, tiles_w, ncob, flags);
   return launch_status("lea_conv3d_bnrelu");
 }
 
@@ -261,7 +271,7 @@ extern "C" const char* lea_conv3d_kernel_name(int cout, int cin, int D, int H, i
   (void)cin;
   (void)D;
   (void)H;
-  if (cout <= 0 || cout > 64 || (k != 1 && k != 3) || W <= 0) return nullptr;
+  if (cout <= 0 || (k != 1 && k != 3) || W <= 0) return nullptr;
   const int mt = lea::mt_for(cout);
   if (k == 1)
     return mt == 1 ? "conv3d_f32_kernel<1, 1, 8, 512>" : mt == 2 ? "conv3d_f32_kernel<1, 2, 4, 256>"
@@ -273,7 +283,7 @@ extern "C" const char* lea_conv3d_kernel_name(int cout, int cin, int D, int H, i
 }
 
 extern "C" size_t lea_conv3d_packed_floats(int cout, int cin, int k) {
-  if (cout <= 0 || cout > 64 || cin <= 0 || (k != 1 && k != 3)) return 0;
+  if (cout <= 0 || cin <= 0 || (k != 1 && k != 3)) return 0;
   return lea::packed_floats(cout, cin, k);
 }
 
@@ -282,14 +292,17 @@ extern "C" int lea_conv3d_pack_weights(const float* w, float* packed, int cout, 
   using namespace lea;
   clear_error();
   LEA_CHECK_ARG(w && packed, "lea_conv3d_pack_weights: null pointer");
-  LEA_CHECK_ARG(cout > 0 && cout <= 64 && cin > 0 && (k == 1 || k == 3),
+  LEA_CHECK_ARG(cout > 0 && cin > 0 && (k == 1 || k == 3),
                 "lea_conv3d_pack_weights: unsupported shape cout=%d cin=%d k=%d", cout, cin, k);
   const long long total = (long long)packed_floats(cout, cin, k);
   const int threads = 256;
   const int grid = (int)((total + threads - 1) / threads < 4096 ? (total + threads - 1) / threads : 4096);
   const int mt = mt_for(cout);
   hipStream_t st = as_stream(stream);
-#define LEA_PACK(KS, MT) pack_weights_kernel<KS, MT><<<grid, threads, 0, st>>>(w, packed, cout, cin, total)
+  const int nchunks = (cin + (k == 3 ? PackCfg<3, 1>::CIN_B : PackCfg<1, 1>::CIN_B) - 1) /
+                      (k == 3 ? PackCfg<3, 1>::CIN_B : PackCfg<1, 1>::CIN_B);
+#define LEA_PACK(KS, MT) \
+  pack_weights_kernel<KS, MT><<<grid, threads, 0, st>>>(w, packed, cout, cin, nchunks, total)
   if (k == 3) {
     if (mt == 1) LEA_PACK(3, 1); else if (mt == 2) LEA_PACK(3, 2); else LEA_PACK(3, 4);
   } else {
@@ -309,7 +322,7 @@ extern "C" int lea_conv3d_bnrelu(const void* x, int64_t x_bstride, const float* 
   LEA_CHECK_ARG(x && w_packed && y, "lea_conv3d_bnrelu: null pointer");
   LEA_CHECK_ARG((scale == nullptr) == (shift == nullptr), "lea_conv3d_bnrelu: scale/shift must both be set or both NULL");
   LEA_CHECK_ARG(!(flags & LEA_RESIDUAL) || residual, "lea_conv3d_bnrelu: LEA_RESIDUAL without residual");
-  LEA_CHECK_ARG(B > 0 && cin > 0 && cout > 0 && cout <= 64 && D > 0 && H > 0 && W > 0,
+  LEA_CHECK_ARG(B > 0 && cin > 0 && cout > 0 && D > 0 && H > 0 && W > 0,
                 "lea_conv3d_bnrelu: bad shape B=%d cin=%d cout=%d D=%d H=%d W=%d", B, cin, cout, D,
                 H, W);
   LEA_CHECK_ARG(k == 1 || k == 3, "lea_conv3d_bnrelu: k=%d unsupported", k);

@@ -48,11 +48,12 @@ def test_invalid_arguments_are_rejected_before_launch():
 
 
 @pytest.mark.parametrize("cout,cin,k", [(32, 64, 3), (64, 128, 3), (16, 16, 3), (8, 8, 3),
-                                        (1, 32, 3), (16, 64, 1), (32, 128, 1), (8, 64, 1)])
+                                        (1, 32, 3), (16, 64, 1), (32, 128, 1), (8, 64, 1),
+                                        (128, 256, 1), (80, 12, 3)])
 def test_packed_sizes(cout, cin, k):
     n = _lib.load().lea_conv3d_packed_floats(cout, cin, k)
     cin_b = 4 if k == 3 else 32
     mt = 1 if cout <= 16 else (2 if cout <= 32 else 4)
     cops = mt * 16 + (16 if (mt * 16) % 32 == 0 else 0)
-    assert n == -(-cin // cin_b) * k ** 3 * cin_b * cops
-    assert _lib.load().lea_conv3d_packed_floats(65, 8, 3) == 0
+    assert n == -(-cout // (mt * 16)) * -(-cin // cin_b) * k ** 3 * cin_b * cops
+    assert _lib.load().lea_conv3d_packed_floats(16, 8, 5) == 0

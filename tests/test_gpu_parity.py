@@ -95,7 +95,7 @@ def test_disparity_golden(name):
     (1, 64, 32, 3, (6, 20, 70)), (2, 128, 64, 3, (5, 9, 40)), (1, 16, 16, 3, (7, 33, 17)),
     (1, 8, 8, 3, (3, 5, 100)), (1, 32, 1, 3, (4, 12, 64)), (1, 12, 20, 3, (3, 4, 5)),
     (1, 64, 16, 1, (3, 7, 11)), (2, 128, 32, 1, (4, 6, 130)), (1, 40, 8, 1, (2, 3, 5)),
-    (1, 32, 64, 1, (1, 1, 1000))])
+    (1, 32, 64, 1, (1, 1, 1000)), (1, 256, 128, 1, (2, 5, 33)), (2, 12, 80, 3, (3, 6, 40))])
 def test_conv_random_vs_torch(b, cin, cout, k, shape):
     g = torch.Generator().manual_seed(cin * 131 + cout)
     x = torch.randn((b, cin) + shape, generator=g)
@@ -144,7 +144,9 @@ def test_disparity_vs_oracle_sizes():
         refd = ref.disp_forward(x.double(), md)
         y = kernels.disparity_regression(x.to(DEV), md).cpu()
         assert torch.isfinite(y).all()
-        np.testing.assert_allclose(y.double().numpy(), refd.numpy(), atol=5e-5, rtol=0)
+        # fp32 sums over maxdisp terms: error grows ~ md * 2^-24 * disparity; bar is 1e-3 px EPE
+        err = np.abs(y.double().numpy() - refd.numpy())
+        assert err.max() < 2e-3 and err.mean() < 1e-4, (err.max(), err.mean())
 
 
 # ----------------------------------------------------------------------- end to end
