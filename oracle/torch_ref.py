@@ -235,7 +235,8 @@ def disp_forward(cost, maxdisp):
                       align_corners=False)
     x = torch.squeeze(x, 1)
     p = torch.softmax(-x, dim=1)
-    d = torch.arange(0, maxdisp, dtype=torch.float32).to(p.dtype).reshape(1, maxdisp, 1, 1)
+    d = torch.arange(0, maxdisp, dtype=torch.float32, device=p.device).to(p.dtype).reshape(
+        1, maxdisp, 1, 1)
     return torch.sum(p * d, 1)
 
 

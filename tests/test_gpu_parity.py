@@ -170,14 +170,22 @@ def test_e2e_golden(name):
 
 
 def test_batch_rows_are_independent():
-    """B=2 result equals the two B=1 results bit for bit (no cross-pair mixing)."""
+    """On the HIP path (cost volume -> matching -> disparity) a B=2 batch equals
+    the two B=1 runs bit for bit: no cross-pair mixing, batch-invariant
+    arithmetic.  (The torch/MIOpen feature net may choose batch-dependent
+    algorithms, so it is checked with a tolerance instead.)"""
     m = _model(48)
     left = normal(901, (2, 3, 96, 192)).to(DEV)
     right = normal(902, (2, 3, 96, 192)).to(DEV)
     with torch.no_grad():
-        both = m(left, right)
-        one = torch.cat([m(left[i:i + 1], right[i:i + 1]) for i in range(2)])
-    assert torch.equal(both, one)
+        fl, fr = m.feature(left), m.feature(right)
+        both = m.disp(m.matching(kernels.build_cost_volume(fl, fr, 48)))
+        one = torch.cat([m.disp(m.matching(kernels.build_cost_volume(fl[i:i + 1], fr[i:i + 1], 48)))
+                         for i in range(2)])
+        assert torch.equal(both, one)
+        e2e_both = m(left, right)
+        e2e_one = torch.cat([m(left[i:i + 1], right[i:i + 1]) for i in range(2)])
+    assert ref.epe(e2e_both.cpu(), e2e_one.cpu()) < 1e-4
 
 
 def test_full_size_c2_vs_torch_oracle_on_gpu():
