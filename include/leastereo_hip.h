@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define LEA_ABI_VERSION 1
+#define LEA_ABI_VERSION 2
 
 #define LEA_F32 0
 #define LEA_BF16 1
@@ -64,18 +64,34 @@ int lea_conv3d_pack_weights(const float* w, float* packed, int cout, int cin, in
 /* ConvBR3d.  Replaces models/operations_3d.py:41-47 (Conv3d no bias, stride 1,
  * pad k/2 -> BatchNorm3d eval -> ReLU) with BN folded on the host into
  *   scale = gamma / sqrt(var + eps),  shift = beta - mean * scale
- * (both NULL = bn=False).  x: [B, cin, D, H, W] at batch stride x_bstride;
- * y/residual: [B, cout, D, H, W] at their batch strides. */
-int lea_conv3d_bnrelu(const void* x, int64_t x_bstride, const float* w_packed,
-                      const float* scale, const float* shift,
+ * (both NULL = bn=False).  Input channels [0, cin-cin2) come from x and
+ * [cin-cin2, cin) from x2 (cin2 = 0: single source), i.e. the conv reads
+ * torch.cat((x, x2), 1) without it existing (skip_model_3d.py:150,155).
+ * x: [B, cin-cin2, D, H, W], x2: [B, cin2, D, H, W], y/residual: [B, cout, D, H, W],
+ * each at its own batch stride. */
+int lea_conv3d_bnrelu(const void* x, int64_t x_bstride,
+                      const void* x2, int64_t x2_bstride, int cin2,
+                      const float* w_packed, const float* scale, const float* shift,
                       const void* residual, int64_t r_bstride,
                       void* y, int64_t y_bstride,
                       int B, int cin, int cout, int D, int H, int W, int k,
                       unsigned flags, int dtype, void* stream);
 
-/* Name of the kernel instantiation lea_conv3d_bnrelu launches for this shape
+/* ConvBR3d of a trilinearly resampled input: conv(interp(x, [D, H, W],
+ * align_corners=True)) with the interpolation done while staging, so the
+ * resampled volume never reaches HBM.  Replaces the F.interpolate + ConvBR pairs
+ * of Cell.forward (skip_model_3d.py:44-53) and the head's Upsample + last_3
+ * (:162-173).  x: [B, cin, Di, Hi, Wi]; y/residual: [B, cout, D, H, W]. */
+int lea_conv3d_bnrelu_resampled(const void* x, int64_t x_bstride, int Di, int Hi, int Wi,
+                                const float* w_packed, const float* scale, const float* shift,
+                                const void* residual, int64_t r_bstride,
+                                void* y, int64_t y_bstride,
+                                int B, int cin, int cout, int D, int H, int W, int k,
+                                unsigned flags, int dtype, void* stream);
+
+/* Name of the kernel instantiation a conv of this output shape launches
  * (matches the demangled name rocprofv3 reports); NULL if unsupported. */
-const char* lea_conv3d_kernel_name(int cout, int cin, int D, int H, int W, int k);
+const char* lea_conv3d_kernel_name(int B, int cout, int D, int H, int W, int k, int resampled);
 
 /* Trilinear resample.  Replaces F.interpolate(mode='trilinear') at
  * skip_model_3d.py:48,50 and nn.Upsample at :162-164 (align_corners=1), with

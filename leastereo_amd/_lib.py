@@ -12,6 +12,7 @@ LIB_PATH = os.environ.get(
     "LEASTEREO_HIP_LIB",
     os.path.join(os.path.dirname(os.path.abspath(__file__)), "libleastereo_hip.so"))
 
+ABI_VERSION = 2
 LEA_F32 = 0
 LEA_BF16 = 1
 LEA_RELU = 1
@@ -29,9 +30,11 @@ SIGNATURES = {
     "lea_build_cost_volume": (_i, [_p, _p, _p, _i, _i, _i, _i, _i, _i, _p]),
     "lea_conv3d_packed_floats": (ctypes.c_size_t, [_i, _i, _i]),
     "lea_conv3d_pack_weights": (_i, [_p, _p, _i, _i, _i, _p]),
-    "lea_conv3d_bnrelu": (_i, [_p, _i64, _p, _p, _p, _p, _i64, _p, _i64,
+    "lea_conv3d_bnrelu": (_i, [_p, _i64, _p, _i64, _i, _p, _p, _p, _p, _i64, _p, _i64,
                                _i, _i, _i, _i, _i, _i, _i, _u, _i, _p]),
-    "lea_conv3d_kernel_name": (ctypes.c_char_p, [_i, _i, _i, _i, _i, _i]),
+    "lea_conv3d_bnrelu_resampled": (_i, [_p, _i64, _i, _i, _i, _p, _p, _p, _p, _i64, _p, _i64,
+                                         _i, _i, _i, _i, _i, _i, _i, _u, _i, _p]),
+    "lea_conv3d_kernel_name": (ctypes.c_char_p, [_i, _i, _i, _i, _i, _i, _i]),
     "lea_resample3d_trilinear": (_i, [_p, _i64, _p, _i64, _i, _i, _i, _i, _i, _i, _i, _i,
                                       _i, _i, _p]),
     "lea_disparity_regression": (_i, [_p, _p, _i, _i, _i, _i, _i, _i, _p]),

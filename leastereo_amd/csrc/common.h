@@ -36,4 +36,51 @@ inline int launch_status(const char* what) {
 
 constexpr int kWave = 64;
 
+// ---- trilinear interpolation with aten's source-index rule (UpSample.h:
+// area_pixel_compute_scale / area_pixel_compute_source_index); shared by the
+// resample kernel and the conv's resampling stager so both round identically.
+struct Axis {
+  int i0, i1;
+  float l0, l1;
+};
+
+__host__ inline float axis_ratio(int in, int out, int ac) {
+  if (ac) return out > 1 ? (float)(in - 1) / (float)(out - 1) : 0.f;
+  return (float)in / (float)out;
+}
+
+__device__ __forceinline__ Axis axis_index(float ratio, int o, int in, int out, int ac) {
+#pragma clang fp contract(off)
+  Axis a;
+  if (in == out) {
+    a.i0 = a.i1 = o;
+    a.l0 = 1.f;
+    a.l1 = 0.f;
+    return a;
+  }
+  float real = ac ? ratio * (float)o : ratio * ((float)o + 0.5f) - 0.5f;
+  if (!ac && real < 0.f) real = 0.f;
+  int i = (int)floorf(real);
+  if (i > in - 1) i = in - 1;
+  float lam = real - (float)i;
+  lam = fminf(fmaxf(lam, 0.f), 1.f);
+  a.i0 = i;
+  a.i1 = i + ((i < in - 1) ? 1 : 0);
+  a.l1 = lam;
+  a.l0 = 1.f - lam;
+  return a;
+}
+
+// p{dz}{hy}: row pointers of source plane d_{dz}, row h_{hy}; nested-lerp order of
+// aten's upsample_trilinear3d: t0*(h0*(w0*a + w1*b) + h1*(...)) + t1*(...)
+__device__ __forceinline__ float trilerp(const Axis& ad, const Axis& ah, const Axis& aw,
+                                         const float* p00, const float* p01, const float* p10,
+                                         const float* p11) {
+#pragma clang fp contract(off)
+  return ad.l0 * (ah.l0 * (aw.l0 * p00[aw.i0] + aw.l1 * p00[aw.i1]) +
+                  ah.l1 * (aw.l0 * p01[aw.i0] + aw.l1 * p01[aw.i1])) +
+         ad.l1 * (ah.l0 * (aw.l0 * p10[aw.i0] + aw.l1 * p10[aw.i1]) +
+                  ah.l1 * (aw.l0 * p11[aw.i0] + aw.l1 * p11[aw.i1]));
+}
+
 }  // namespace lea

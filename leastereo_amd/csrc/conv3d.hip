@@ -1,28 +1,42 @@
 // ConvBR3d (Conv3d k in {1,3}, stride 1, pad k/2, no bias -> folded BN -> ReLU
 // [-> + residual]) as an implicit GEMM on the gfx950 fp32 matrix cores.
 // Replaces models/operations_3d.py:31-47 for every ConvBR of the matching net
-// (retrain/skip_model_3d.py) and, via LEA_RESIDUAL, the cell's pairwise sums
-// (skip_model_3d.py:69).
+// (retrain/skip_model_3d.py), the cell's pairwise sums (LEA_RESIDUAL,
+// skip_model_3d.py:69), the skip-fusion concat (two input sources,
+// skip_model_3d.py:150,155) and -- in the resampling variant -- the trilinear
+// level change that precedes every cell preprocess (skip_model_3d.py:44-53).
 //
 // GEMM view (per batch b, output plane d):
 //     Y[co][v] = sum_{ci, tap} Wt[co][ci][tap] * X[ci][v + off(tap)]
-// M = cout (blocks of <= 64 per workgroup, 16-row MFMA tiles), N = voxels (16-wide runs along W,
-// coalesced NCDHW), K = cin * k^3.  MFMA = v_mfma_f32_16x16x4_f32 (exact f32
-// products, f32 accumulate):
+// M = cout (blocks of <= 64 per workgroup, 16-row MFMA tiles), N = voxels
+// (16-wide runs along W, coalesced NCDHW), K = cin * k^3.
+// MFMA = v_mfma_f32_16x16x4_f32 (exact f32 products, f32 accumulate):
 //     A (lane l) = Wt[co = 16*mt + (l & 15)][k = l >> 4]
 //     B (lane l) = X [k = l >> 4][v = 16*nt + (l & 15)]
 //     D (lane l, reg r) = Y[co = 16*mt + 4*(l >> 4) + r][v = l & 15]
 // so the epilogue stores 16 consecutive w per cout row (64-B segments).
 //
-// Workgroup = 4 waves = one output plane tile of TH x TW voxels and all couts.
-// K is streamed in chunks of CIN_B input channels: per chunk the workgroup stages
-//   * X: CIN_B x KS x (TH+KS-1) x (TW+KS-1) input halo block (zero padded at the
-//     volume border = the conv's zero padding), and
-//   * W: KS^3 x CIN_B x COPS weights (a linear copy of the pre-packed layout),
-// into LDS, then every wave runs KS^3 * CIN_B/4 k-steps of MT x NT MFMAs whose
-// operands are single ds_read_b32 at per-lane base + compile-time offset.
-// LDS strides are chosen so each 32-lane read group hits 32 distinct banks
-// (the two k-rows of a half-wave sit 16 banks apart).
+// Workgroup = 4 waves = a TH x TW voxel tile of one output plane, all couts of
+// its block.  K is streamed in chunks of CIN_B input channels staged in LDS; every
+// wave then runs k^3 * CIN_B/4 k-steps of MT x NT MFMAs whose operands are single
+// ds_read_b32 at per-lane base + compile-time offset.  LDS strides keep each
+// 32-lane read group on 32 distinct banks (the two k-rows of a half-wave sit 16
+// banks apart: strides = 16 mod 32).
+//
+// Two staging engines:
+//  * conv3d_dma_kernel (k=3, the MFMA-bound layers): the input halo block is
+//    fetched by LDS-DMA (`buffer_load_dword ... lds`) through one buffer resource
+//    per input channel.  The per-lane source offsets are computed once per
+//    workgroup; voxels outside the volume get an offset beyond the resource's
+//    num_records, so the hardware range check returns 0 -- the conv's zero
+//    padding costs no VALU.  Weights arrive by `global_load_lds_dwordx4`.  Two
+//    LDS stages: chunk c+1's DMA is in flight while chunk c's MFMAs run; one
+//    vmcnt(0) + barrier per chunk.  (Register staging spent 2-7 VALU
+//    instructions per MFMA on index math and saturated VALU issue: r01 PMC.)
+//  * conv3d_reg_kernel (k=1, and the RESAMPLE variant for k in {1,3}): register
+//    staged; with RESAMPLE each staged value is the trilinear (align_corners=True)
+//    interpolation of the low/high-resolution input at the output voxel, so the
+//    resampled volume is never written to HBM.
 #include "common.h"
 
 namespace lea {
@@ -31,6 +45,7 @@ constexpr int kConvWaves = 4;
 constexpr int kConvThreads = kConvWaves * kWave;
 
 using f32x4 = __attribute__((__vector_size__(4 * sizeof(float)))) float;
+using lds_void = __attribute__((address_space(3))) void;
 
 // Row stride of the staged weight block / packed weights, congruent 16 mod 32
 // so lanes 0-15 and 16-31 of one ds_read_b32 fall on disjoint banks.
@@ -38,6 +53,26 @@ __host__ __device__ constexpr int cout_stride(int cop) { return (cop % 32 == 0) 
 __host__ __device__ constexpr int round_16mod32(int n) {
   return (n % 32 <= 16) ? n + (16 - n % 32) : n + (48 - n % 32);
 }
+
+struct ConvArgs {
+  const float* x;   // source 1: input channels [0, cin1)
+  long long xbs;
+  const float* x2;  // source 2: input channels [cin1, cin) (virtual concat)
+  long long x2bs;
+  int cin1;
+  const float* wp;
+  const float* scale;
+  const float* shift;
+  const float* res;
+  long long rbs;
+  float* y;
+  long long ybs;
+  int cin, cout, D, H, W;  // conv (= output) volume
+  int Di, Hi, Wi;          // stored input volume (RESAMPLE variant)
+  float rd, rh, rw;        // align_corners=True source ratios (RESAMPLE variant)
+  int tiles_w, ncob;
+  unsigned flags;
+};
 
 template <int KS, int MT>
 struct PackCfg {
@@ -49,7 +84,7 @@ struct PackCfg {
 };
 
 template <int KS, int MT, int NT, int TW>
-struct ConvCfg : PackCfg<KS, MT> {
+struct TileCfg : PackCfg<KS, MT> {
   using P = PackCfg<KS, MT>;
   static constexpr int PAD = KS / 2;
   static constexpr int NTILES = kConvWaves * NT;
@@ -59,21 +94,190 @@ struct ConvCfg : PackCfg<KS, MT> {
   static constexpr int RH = TH + KS - 1;
   static constexpr int RW = TW + KS - 1;
   static constexpr int PLANE = RH * RW;
-  static constexpr int CIS = round_16mod32(KS * PLANE);  // LDS stride between input channels
+  static constexpr int IMG = KS * PLANE;           // staged floats per input channel
+  static constexpr int CIS = round_16mod32(IMG);   // LDS stride between input channels
   static constexpr int XS = P::CIN_B * CIS;
   static constexpr int WS = P::CHUNK;
-  static constexpr int XELEMS = P::CIN_B * KS * PLANE;
+  static constexpr int STAGE = XS + WS;            // floats (multiple of 16: 64-B aligned)
+  static_assert(XS % 16 == 0 && WS % 16 == 0, "16-byte aligned LDS regions");
 };
 
+// ----------------------------------------------------------------- MFMA main loop
+// One K chunk from an LDS stage: KS^3 taps x CIN_B/4 k-steps x (MT x NT) MFMAs.
 template <int KS, int MT, int NT, int TW>
-__global__ __launch_bounds__(kConvThreads, 2) void conv3d_f32_kernel(
-    const float* __restrict__ x, long long xbs, const float* __restrict__ wp,
-    const float* __restrict__ scale, const float* __restrict__ shift, const float* res,
-    long long rbs, float* y, long long ybs, int cin, int cout, int D, int H, int W, int tiles_w,
-    int ncob, unsigned flags) {
-  using C = ConvCfg<KS, MT, NT, TW>;
+__device__ __forceinline__ void mfma_chunk(const float* xs, const float* ws, const int (&xoff)[NT],
+                                           int woff, f32x4 (&acc)[MT][NT]) {
+  using C = TileCfg<KS, MT, NT, TW>;
   constexpr int CIN_B = C::CIN_B;
-  __shared__ __attribute__((aligned(16))) float smem[C::XS + C::WS];
+#pragma unroll
+  for (int s = 0; s < CIN_B / 4; ++s) {
+#pragma unroll
+    for (int kd = 0; kd < KS; ++kd) {
+#pragma unroll
+      for (int kh = 0; kh < KS; ++kh) {
+#pragma unroll
+        for (int kw = 0; kw < KS; ++kw) {
+          const int tap = (kd * KS + kh) * KS + kw;
+          float av[MT], bv[NT];
+#pragma unroll
+          for (int m = 0; m < MT; ++m) av[m] = ws[woff + (tap * CIN_B + 4 * s) * C::COPS + m * 16];
+#pragma unroll
+          for (int j = 0; j < NT; ++j)
+            bv[j] = xs[xoff[j] + 4 * s * C::CIS + kd * C::PLANE + kh * C::RW + kw];
+#pragma unroll
+          for (int m = 0; m < MT; ++m)
+#pragma unroll
+            for (int j = 0; j < NT; ++j)
+              acc[m][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[m], bv[j], acc[m][j], 0, 0, 0);
+        }
+      }
+    }
+  }
+}
+
+// Folded-BN affine, ReLU, residual, masked store of the MT x NT accumulator tiles.
+template <int KS, int MT, int NT, int TW>
+__device__ __forceinline__ void epilogue(const ConvArgs& a, const f32x4 (&acc)[MT][NT], int b,
+                                         int co0, int d0, int h0, int w0, int wave, int lane) {
+  using C = TileCfg<KS, MT, NT, TW>;
+  const long long HW = (long long)a.H * a.W;
+  const long long DHW = HW * a.D;
+  const bool relu = a.flags & LEA_RELU;
+  const bool resid = a.flags & LEA_RESIDUAL;
+  const int kq = lane >> 4, n = lane & 15;
+#pragma unroll
+  for (int m = 0; m < MT; ++m) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int co = co0 + m * 16 + kq * 4 + r;
+      if (co >= a.cout) continue;
+      const float sc = a.scale ? a.scale[co] : 1.f;
+      const float sh = a.shift ? a.shift[co] : 0.f;
+#pragma unroll
+      for (int j = 0; j < NT; ++j) {
+        const int g = wave * NT + j;
+        const int h = h0 + g / C::TPR;
+        const int w = w0 + (g % C::TPR) * 16 + n;
+        if (h >= a.H || w >= a.W) continue;
+        const long long o = (long long)co * DHW + (long long)d0 * HW + (long long)h * a.W + w;
+        float v = acc[m][j][r] * sc + sh;
+        if (relu) v = fmaxf(v, 0.f);
+        if (resid) v += a.res[(long long)b * a.rbs + o];
+        a.y[(long long)b * a.ybs + o] = v;
+      }
+    }
+  }
+}
+
+// ------------------------------------------------------------- LDS-DMA engine (k=3)
+template <int MT, int NT, int TW>
+__global__ __launch_bounds__(kConvThreads, 2) void conv3d_dma_kernel(const ConvArgs a) {
+  using C = TileCfg<3, MT, NT, TW>;
+  constexpr int XSLOTS = (C::IMG + 63) / 64;  // 256-B DMA pieces per channel image
+  constexpr int XSLOTS_W = (XSLOTS + kConvWaves - 1) / kConvWaves;
+  constexpr int WSLOTS = (C::WS + 255) / 256;  // 1-KB DMA pieces of the weight chunk
+  constexpr int WSLOTS_W = (WSLOTS + kConvWaves - 1) / kConvWaves;
+  __shared__ __attribute__((aligned(16))) float smem[2 * C::STAGE];
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int tile = blockIdx.x;
+  const int h0 = (tile / a.tiles_w) * C::TH;
+  const int w0 = (tile % a.tiles_w) * TW;
+  const int d0 = blockIdx.y;
+  const int b = blockIdx.z / a.ncob;
+  const int co0 = (blockIdx.z - b * a.ncob) * C::COP;
+  const int nchunks = (a.cin + C::CIN_B - 1) / C::CIN_B;
+  const float* wp = a.wp + (long long)(co0 / C::COP) * nchunks * C::WS;
+  const int HW = a.H * a.W;  // host checks D*H*W*4 < 2^32
+  const unsigned nrec = (unsigned)(HW * a.D) * 4u;
+
+  // Per-lane byte offsets of this wave's DMA pieces inside one channel volume;
+  // identical for every channel and chunk.  Outside the volume -> beyond nrec -> 0.
+  unsigned voff[XSLOTS_W];
+#pragma unroll
+  for (int t = 0; t < XSLOTS_W; ++t) {
+    const int e = (wave + kConvWaves * t) * 64 + lane;
+    unsigned v = 0xFFFFFFF0u;
+    if (e < C::IMG) {
+      const int kd = e / C::PLANE;
+      const int r = e - kd * C::PLANE;
+      const int rr = r / C::RW;
+      const int cc = r - rr * C::RW;
+      const int d = d0 + kd - 1, h = h0 + rr - 1, w = w0 + cc - 1;
+      if ((unsigned)d < (unsigned)a.D && (unsigned)h < (unsigned)a.H && (unsigned)w < (unsigned)a.W)
+        v = (unsigned)(d * HW + h * a.W + w) * 4u;
+    }
+    voff[t] = v;
+  }
+
+  auto issue = [&](int ch, float* st) {
+    const float* wsrc = wp + (long long)ch * C::WS;
+    float* wdst = st + C::XS;
+#pragma unroll
+    for (int t = 0; t < WSLOTS_W; ++t) {
+      const int j = wave + kConvWaves * t;
+      if (j < WSLOTS && j * 256 + lane * 4 < C::WS)
+        __builtin_amdgcn_global_load_lds(wsrc + j * 256 + lane * 4, (lds_void*)(wdst + j * 256), 16, 0, 0);
+    }
+#pragma unroll
+    for (int ci = 0; ci < C::CIN_B; ++ci) {
+      const int c = ch * C::CIN_B + ci;
+      const float* base = a.x;
+      unsigned n = 0;
+      if (c < a.cin1) {
+        base = a.x + (long long)b * a.xbs + (long long)c * HW * a.D;
+        n = nrec;
+      } else if (c < a.cin) {
+        base = a.x2 + (long long)b * a.x2bs + (long long)(c - a.cin1) * HW * a.D;
+        n = nrec;
+      }
+      const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)base, 0, n, 0x00020000);
+#pragma unroll
+      for (int t = 0; t < XSLOTS_W; ++t) {
+        const int j = wave + kConvWaves * t;
+        if (j < XSLOTS && j * 64 + lane < C::IMG)
+          __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void*)(st + ci * C::CIS + j * 64), 4,
+                                                   voff[t], 0, 0, 0);
+      }
+    }
+  };
+
+  const int kq = lane >> 4;
+  const int n = lane & 15;
+  int xoff[NT];
+#pragma unroll
+  for (int j = 0; j < NT; ++j) {
+    const int g = wave * NT + j;
+    xoff[j] = kq * C::CIS + (g / C::TPR) * C::RW + (g % C::TPR) * 16 + n;
+  }
+  const int woff = kq * C::COPS + n;
+
+  f32x4 acc[MT][NT];
+#pragma unroll
+  for (int m = 0; m < MT; ++m)
+#pragma unroll
+    for (int j = 0; j < NT; ++j) acc[m][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  issue(0, smem);
+  for (int ch = 0; ch < nchunks; ++ch) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's pieces of chunk ch landed
+    __syncthreads();  // ... and everyone's; everyone is done reading chunk ch-1's stage
+    if (ch + 1 < nchunks) issue(ch + 1, smem + ((ch + 1) & 1) * C::STAGE);
+    const float* xs = smem + (ch & 1) * C::STAGE;
+    mfma_chunk<3, MT, NT, TW>(xs, xs + C::XS, xoff, woff, acc);
+  }
+  epilogue<3, MT, NT, TW>(a, acc, b, co0, d0, h0, w0, wave, lane);
+}
+
+// ------------------------------------------------- register-staged engine (+ resample)
+template <int KS, int MT, int NT, int TW, bool RS>
+__global__ __launch_bounds__(kConvThreads, 2) void conv3d_reg_kernel(const ConvArgs a) {
+  using C = TileCfg<KS, MT, NT, TW>;
+  constexpr int CIN_B = C::CIN_B;
+  __shared__ __attribute__((aligned(16))) float smem[C::STAGE];
+  __shared__ Axis tabs[RS ? (KS + C::RH + C::RW) : 1];
   float* xs = smem;
   float* ws = smem + C::XS;
 
@@ -81,21 +285,35 @@ __global__ __launch_bounds__(kConvThreads, 2) void conv3d_f32_kernel(
   const int lane = tid & 63;
   const int wave = tid >> 6;
   const int tile = blockIdx.x;
-  const int h0 = (tile / tiles_w) * C::TH;
-  const int w0 = (tile % tiles_w) * TW;
+  const int h0 = (tile / a.tiles_w) * C::TH;
+  const int w0 = (tile % a.tiles_w) * TW;
   const int d0 = blockIdx.y;
-  const int b = blockIdx.z / ncob;    // batch
-  const int cob = blockIdx.z - b * ncob;  // block of COP output channels
-  const int co0 = cob * C::COP;
-  const int nchunks = (cin + CIN_B - 1) / CIN_B;
-  wp += (long long)cob * nchunks * C::WS;
-  const long long HW = (long long)H * W;
-  const long long DHW = HW * D;
-  const float* xb = x + (long long)b * xbs;
+  const int b = blockIdx.z / a.ncob;
+  const int co0 = (blockIdx.z - b * a.ncob) * C::COP;
+  const int nchunks = (a.cin + CIN_B - 1) / CIN_B;
+  const float* wp = a.wp + (long long)(co0 / C::COP) * nchunks * C::WS;
+  const long long HW = (long long)a.H * a.W;
+  const long long DHW = HW * a.D;
+  const long long HWi = (long long)a.Hi * a.Wi;
+  const long long DHWi = HWi * a.Di;
 
-  const int kq = lane >> 4;  // k row of this lane inside an MFMA (0..3)
-  const int n = lane & 15;   // voxel column / cout row inside a 16 tile
+  if constexpr (RS) {  // source index/weights of every staged d, h, w (aten align_corners=True)
+    for (int i = tid; i < KS + C::RH + C::RW; i += kConvThreads) {
+      if (i < KS) {
+        const int d = d0 + i - C::PAD;
+        tabs[i] = axis_index(a.rd, (unsigned)d < (unsigned)a.D ? d : 0, a.Di, a.D, 1);
+      } else if (i < KS + C::RH) {
+        const int h = h0 + (i - KS) - C::PAD;
+        tabs[i] = axis_index(a.rh, (unsigned)h < (unsigned)a.H ? h : 0, a.Hi, a.H, 1);
+      } else {
+        const int w = w0 + (i - KS - C::RH) - C::PAD;
+        tabs[i] = axis_index(a.rw, (unsigned)w < (unsigned)a.W ? w : 0, a.Wi, a.W, 1);
+      }
+    }
+  }
 
+  const int kq = lane >> 4;
+  const int n = lane & 15;
   int xoff[NT];
 #pragma unroll
   for (int j = 0; j < NT; ++j) {
@@ -112,18 +330,17 @@ __global__ __launch_bounds__(kConvThreads, 2) void conv3d_f32_kernel(
 
   for (int ch = 0; ch < nchunks; ++ch) {
     const int c0 = ch * CIN_B;
-    __syncthreads();  // previous chunk's reads are done
-    {  // weights: linear 16-byte copy of the packed chunk
+    __syncthreads();  // previous chunk's reads are done (and the axis tables are ready)
+    {
       const float4* src = reinterpret_cast<const float4*>(wp + (long long)ch * C::WS);
       float4* dst = reinterpret_cast<float4*>(ws);
 #pragma unroll 4
       for (int i = tid; i < C::WS / 4; i += kConvThreads) dst[i] = src[i];
     }
-    // input halo block, zero outside the volume (= conv zero padding)
 #pragma unroll 4
-    for (int i = tid; i < C::XELEMS; i += kConvThreads) {
-      const int ci = i / (KS * C::PLANE);
-      int rem = i - ci * (KS * C::PLANE);
+    for (int i = tid; i < CIN_B * C::IMG; i += kConvThreads) {
+      const int ci = i / C::IMG;
+      int rem = i - ci * C::IMG;
       const int kd = rem / C::PLANE;
       rem -= kd * C::PLANE;
       const int rr = rem / C::RW;
@@ -131,67 +348,32 @@ __global__ __launch_bounds__(kConvThreads, 2) void conv3d_f32_kernel(
       const int d = d0 + kd - C::PAD;
       const int h = h0 + rr - C::PAD;
       const int w = w0 + cc - C::PAD;
+      const int c = c0 + ci;
       float v = 0.f;
-      if ((unsigned)d < (unsigned)D && (unsigned)h < (unsigned)H && (unsigned)w < (unsigned)W &&
-          c0 + ci < cin)
-        v = xb[(long long)(c0 + ci) * DHW + (long long)d * HW + (long long)h * W + w];
+      if ((unsigned)d < (unsigned)a.D && (unsigned)h < (unsigned)a.H && (unsigned)w < (unsigned)a.W &&
+          c < a.cin) {
+        const float* src = (c < a.cin1) ? a.x + (long long)b * a.xbs + (long long)c * (RS ? DHWi : DHW)
+                                        : a.x2 + (long long)b * a.x2bs + (long long)(c - a.cin1) * (RS ? DHWi : DHW);
+        if constexpr (RS) {
+          const Axis ad = tabs[kd], ah = tabs[KS + rr], aw = tabs[KS + C::RH + cc];
+          const float* p00 = src + ad.i0 * HWi + (long long)ah.i0 * a.Wi;
+          const float* p01 = src + ad.i0 * HWi + (long long)ah.i1 * a.Wi;
+          const float* p10 = src + ad.i1 * HWi + (long long)ah.i0 * a.Wi;
+          const float* p11 = src + ad.i1 * HWi + (long long)ah.i1 * a.Wi;
+          v = trilerp(ad, ah, aw, p00, p01, p10, p11);
+        } else {
+          v = src[(long long)d * HW + (long long)h * a.W + w];
+        }
+      }
       xs[ci * C::CIS + kd * C::PLANE + rr * C::RW + cc] = v;
     }
     __syncthreads();
-
-#pragma unroll
-    for (int s = 0; s < CIN_B / 4; ++s) {
-#pragma unroll
-      for (int kd = 0; kd < KS; ++kd) {
-#pragma unroll
-        for (int kh = 0; kh < KS; ++kh) {
-#pragma unroll
-          for (int kw = 0; kw < KS; ++kw) {
-            const int tap = (kd * KS + kh) * KS + kw;
-            float a[MT], bv[NT];
-#pragma unroll
-            for (int m = 0; m < MT; ++m) a[m] = ws[woff + (tap * CIN_B + 4 * s) * C::COPS + m * 16];
-#pragma unroll
-            for (int j = 0; j < NT; ++j)
-              bv[j] = xs[xoff[j] + 4 * s * C::CIS + kd * C::PLANE + kh * C::RW + kw];
-#pragma unroll
-            for (int m = 0; m < MT; ++m)
-#pragma unroll
-              for (int j = 0; j < NT; ++j)
-                acc[m][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[m], bv[j], acc[m][j], 0, 0, 0);
-          }
-        }
-      }
-    }
+    mfma_chunk<KS, MT, NT, TW>(xs, ws, xoff, woff, acc);
   }
-
-  // epilogue: folded BN affine, ReLU, residual, masked store
-  const bool relu = flags & LEA_RELU;
-  const bool resid = flags & LEA_RESIDUAL;
-#pragma unroll
-  for (int m = 0; m < MT; ++m) {
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int co = co0 + m * 16 + kq * 4 + r;
-      if (co >= cout) continue;
-      const float sc = scale ? scale[co] : 1.f;
-      const float sh = shift ? shift[co] : 0.f;
-#pragma unroll
-      for (int j = 0; j < NT; ++j) {
-        const int g = wave * NT + j;
-        const int h = h0 + g / C::TPR;
-        const int w = w0 + (g % C::TPR) * 16 + n;
-        if (h >= H || w >= W) continue;
-        const long long o = (long long)co * DHW + (long long)d0 * HW + (long long)h * W + w;
-        float v = acc[m][j][r] * sc + sh;
-        if (relu) v = fmaxf(v, 0.f);
-        if (resid) v += res[(long long)b * rbs + o];
-        y[(long long)b * ybs + o] = v;
-      }
-    }
-  }
+  epilogue<KS, MT, NT, TW>(a, acc, b, co0, d0, h0, w0, wave, lane);
 }
 
+// ------------------------------------------------------------------- weight packing
 // Packed layout: [ceil(cout/COP)][ceil(cin/CIN_B)][KS^3][CIN_B][COPS], zero outside (cin, cout).
 template <int KS, int MT>
 __global__ void pack_weights_kernel(const float* __restrict__ w, float* __restrict__ packed,
@@ -231,55 +413,132 @@ size_t packed_floats(int cout, int cin, int k) {
                  : mt == 2 ? packed_floats_t<1, 2>(cout, cin) : packed_floats_t<1, 4>(cout, cin);
 }
 
-template <int KS, int MT, int NT, int TW>
-int launch_conv(const float* x, long long xbs, const float* wp, const float* scale,
-                const float* shift, const float* res, long long rbs, float* y, long long ybs,
-                int B, int cin, int cout, int D, int H, int W, unsigned flags, hipStream_t st) {
-  using C = ConvCfg<KS, MT, NT, TW>;
-  const int tiles_w = (W + TW - 1) / TW;
-  const int tiles_h = (H + C::TH - 1) / C::TH;
-  const long long nt = (long long)tiles_w * tiles_h;
-  const int ncob = (cout + C::COP - 1) / C::COP;
-  LEA_CHECK_ARG(nt < (1LL << 31) && D <= 65535 && (long long)B * ncob <= 65535,
-                "lea_conv3d_bnrelu: grid too large");
-  dim3 grid((unsigned)nt, D, B * ncob);
-  conv3d_f32_kernel<KS, MT, NT, TW><<<grid, kConvThreads, 0, st>>>(
-      x, xbs, wp, scale, shift, res, rbs, y, ybs, cin, cout, D, H, W, tiles_w, ncob, flags);
-  return launch_status("lea_conv3d_bnrelu");
-}
+// ------------------------------------------------------------------------- dispatch
+// A launch plan: which instantiation runs a given shape (also reported by name).
+struct Plan {
+  int engine;  // 0 = dma (k3), 1 = reg flat (k1), 2 = reg resample
+  int mt, nt, tw;
+};
 
-// Pick the tile width with the least padding waste along W (ties -> wider).
 inline bool prefer_tw64(int W) {
   const int w64 = (W + 63) / 64 * 64, w32 = (W + 31) / 32 * 32;
   return (w64 - W) <= (w32 - W) || W >= 1024;
 }
 
+inline Plan make_plan(int B, int cout, int D, int H, int W, int k, bool resample) {
+  Plan p;
+  p.mt = mt_for(cout);
+  if (k == 1 && !resample) {
+    p.engine = 1;
+    p.nt = p.mt == 1 ? 8 : 4;
+    p.tw = p.nt * 64;
+    return p;
+  }
+  p.engine = resample ? 2 : 0;
+  p.tw = prefer_tw64(W) ? 64 : 32;
+  p.nt = p.mt == 1 ? 8 : 4;
+  if (!resample) {  // small volumes: halve the tile so the grid still fills 256 CUs twice
+    const int th = kConvWaves * p.nt * 16 / p.tw;
+    const long long wgs = (long long)((W + p.tw - 1) / p.tw) * ((H + th - 1) / th) * D * B *
+                          ((cout + p.mt * 16 - 1) / (p.mt * 16));
+    if (wgs < 512) p.nt /= 2;
+  }
+  return p;
+}
+
+template <typename K>
+int launch(K kernel, const ConvArgs& a0, int th, int tw, int B, hipStream_t st) {
+  ConvArgs a = a0;
+  const long long nt = (long long)((a.W + tw - 1) / tw) * ((a.H + th - 1) / th);
+  LEA_CHECK_ARG(nt < (1LL << 31) && a.D <= 65535 && (long long)B * a.ncob <= 65535,
+                "lea_conv3d: grid too large");
+  a.tiles_w = (a.W + tw - 1) / tw;
+  dim3 grid((unsigned)nt, a.D, B * a.ncob);
+  kernel<<<grid, kConvThreads, 0, st>>>(a);
+  return launch_status("lea_conv3d");
+}
+
+#define LEA_TILE_TH(KS, MT, NT, TW) (TileCfg<KS, MT, NT, TW>::TH)
+
 template <int MT, int NT>
-int dispatch_k3(const float* x, long long xbs, const float* wp, const float* scale,
-                const float* shift, const float* res, long long rbs, float* y, long long ybs,
-                int B, int cin, int cout, int D, int H, int W, unsigned flags, hipStream_t st) {
-  if (prefer_tw64(W))
-    return launch_conv<3, MT, NT, 64>(x, xbs, wp, scale, shift, res, rbs, y, ybs, B, cin, cout, D,
-                                      H, W, flags, st);
-  return launch_conv<3, MT, NT, 32>(x, xbs, wp, scale, shift, res, rbs, y, ybs, B, cin, cout, D, H,
-                                    W, flags, st);
+int run_dma(const ConvArgs& a, int tw, int B, hipStream_t st) {
+  if (tw == 64) return launch(conv3d_dma_kernel<MT, NT, 64>, a, LEA_TILE_TH(3, MT, NT, 64), 64, B, st);
+  return launch(conv3d_dma_kernel<MT, NT, 32>, a, LEA_TILE_TH(3, MT, NT, 32), 32, B, st);
+}
+
+template <int KS, int MT, int NT>
+int run_rs(const ConvArgs& a, int tw, int B, hipStream_t st) {
+  if (tw == 64) return launch(conv3d_reg_kernel<KS, MT, NT, 64, true>, a, LEA_TILE_TH(KS, MT, NT, 64), 64, B, st);
+  return launch(conv3d_reg_kernel<KS, MT, NT, 32, true>, a, LEA_TILE_TH(KS, MT, NT, 32), 32, B, st);
+}
+
+int run_plan(const Plan& p, ConvArgs a, int B, int k, hipStream_t st) {
+  a.ncob = (a.cout + p.mt * 16 - 1) / (p.mt * 16);
+  if (p.engine == 0) {
+    if (p.mt == 1) return p.nt == 8 ? run_dma<1, 8>(a, p.tw, B, st) : run_dma<1, 4>(a, p.tw, B, st);
+    if (p.mt == 2) return p.nt == 4 ? run_dma<2, 4>(a, p.tw, B, st) : run_dma<2, 2>(a, p.tw, B, st);
+    return p.nt == 4 ? run_dma<4, 4>(a, p.tw, B, st) : run_dma<4, 2>(a, p.tw, B, st);
+  }
+  if (p.engine == 2) {
+    if (k == 3) {
+      if (p.mt == 1) return run_rs<3, 1, 8>(a, p.tw, B, st);
+      if (p.mt == 2) return run_rs<3, 2, 4>(a, p.tw, B, st);
+      return run_rs<3, 4, 4>(a, p.tw, B, st);
+    }
+    if (p.mt == 1) return run_rs<1, 1, 8>(a, p.tw, B, st);
+    if (p.mt == 2) return run_rs<1, 2, 4>(a, p.tw, B, st);
+    return run_rs<1, 4, 4>(a, p.tw, B, st);
+  }
+  // 1x1x1 without resample: the volume is a flat run of D*H*W voxels (no halo)
+  a.W = a.D * a.H * a.W;
+  a.D = a.H = 1;
+  if (p.mt == 1) return launch(conv3d_reg_kernel<1, 1, 8, 512, false>, a, 1, 512, B, st);
+  if (p.mt == 2) return launch(conv3d_reg_kernel<1, 2, 4, 256, false>, a, 1, 256, B, st);
+  return launch(conv3d_reg_kernel<1, 4, 4, 256, false>, a, 1, 256, B, st);
+}
+
+thread_local char g_name[96];
+
+const char* plan_name(const Plan& p, int k) {
+  if (p.engine == 0)
+    snprintf(g_name, sizeof(g_name), "conv3d_dma_kernel<%d, %d, %d>", p.mt, p.nt, p.tw);
+  else if (p.engine == 2)
+    snprintf(g_name, sizeof(g_name), "conv3d_reg_kernel<%d, %d, %d, %d, true>", k, p.mt, p.nt, p.tw);
+  else
+    snprintf(g_name, sizeof(g_name), "conv3d_reg_kernel<1, %d, %d, %d, false>", p.mt, p.nt, p.tw);
+  return g_name;
+}
+
+int conv_common(ConvArgs& a, int B, int k, bool resample, int dtype, void* stream) {
+  clear_error();
+  LEA_CHECK_ARG(a.x && a.wp && a.y, "lea_conv3d: null pointer");
+  LEA_CHECK_ARG((a.scale == nullptr) == (a.shift == nullptr),
+                "lea_conv3d: scale/shift must both be set or both NULL");
+  LEA_CHECK_ARG(!(a.flags & LEA_RESIDUAL) || a.res, "lea_conv3d: LEA_RESIDUAL without residual");
+  LEA_CHECK_ARG(B > 0 && a.cin > 0 && a.cout > 0 && a.D > 0 && a.H > 0 && a.W > 0,
+                "lea_conv3d: bad shape B=%d cin=%d cout=%d D=%d H=%d W=%d", B, a.cin, a.cout, a.D,
+                a.H, a.W);
+  LEA_CHECK_ARG(a.cin1 >= 0 && a.cin1 <= a.cin && (a.cin1 == a.cin || a.x2),
+                "lea_conv3d: bad channel split %d/%d", a.cin1, a.cin);
+  LEA_CHECK_ARG(k == 1 || k == 3, "lea_conv3d: k=%d unsupported", k);
+  LEA_CHECK_ARG((long long)a.D * a.H * a.W * 4 < (1LL << 32), "lea_conv3d: volume too large");
+  LEA_CHECK_ARG(a.x != a.y && a.x2 != a.y, "lea_conv3d: input aliases output");
+  if (resample)
+    LEA_CHECK_ARG(a.Di > 0 && a.Hi > 0 && a.Wi > 0, "lea_conv3d: bad input volume");
+  if (dtype != LEA_F32) {
+    set_error("lea_conv3d: dtype %d unsupported", dtype);
+    return LEA_E_UNSUPPORTED;
+  }
+  const Plan p = make_plan(B, a.cout, a.D, a.H, a.W, k, resample);
+  return run_plan(p, a, B, k, as_stream(stream));
 }
 
 }  // namespace lea
 
-extern "C" const char* lea_conv3d_kernel_name(int cout, int cin, int D, int H, int W, int k) {
-  (void)cin;
-  (void)D;
-  (void)H;
-  if (cout <= 0 || (k != 1 && k != 3) || W <= 0) return nullptr;
-  const int mt = lea::mt_for(cout);
-  if (k == 1)
-    return mt == 1 ? "conv3d_f32_kernel<1, 1, 8, 512>" : mt == 2 ? "conv3d_f32_kernel<1, 2, 4, 256>"
-                                                               : "conv3d_f32_kernel<1, 4, 4, 256>";
-  const bool w64 = lea::prefer_tw64(W);
-  if (mt == 1) return w64 ? "conv3d_f32_kernel<3, 1, 8, 64>" : "conv3d_f32_kernel<3, 1, 8, 32>";
-  if (mt == 2) return w64 ? "conv3d_f32_kernel<3, 2, 4, 64>" : "conv3d_f32_kernel<3, 2, 4, 32>";
-  return w64 ? "conv3d_f32_kernel<3, 4, 4, 64>" : "conv3d_f32_kernel<3, 4, 4, 32>";
+extern "C" const char* lea_conv3d_kernel_name(int B, int cout, int D, int H, int W, int k,
+                                              int resample) {
+  if (B <= 0 || cout <= 0 || (k != 1 && k != 3) || D <= 0 || H <= 0 || W <= 0) return nullptr;
+  return lea::plan_name(lea::make_plan(B, cout, D, H, W, k, resample != 0), k);
 }
 
 extern "C" size_t lea_conv3d_packed_floats(int cout, int cin, int k) {
@@ -296,11 +555,12 @@ extern "C" int lea_conv3d_pack_weights(const float* w, float* packed, int cout, 
                 "lea_conv3d_pack_weights: unsupported shape cout=%d cin=%d k=%d", cout, cin, k);
   const long long total = (long long)packed_floats(cout, cin, k);
   const int threads = 256;
-  const int grid = (int)((total + threads - 1) / threads < 4096 ? (total + threads - 1) / threads : 4096);
+  const long long want = (total + threads - 1) / threads;
+  const int grid = (int)(want < 4096 ? want : 4096);
   const int mt = mt_for(cout);
   hipStream_t st = as_stream(stream);
-  const int nchunks = (cin + (k == 3 ? PackCfg<3, 1>::CIN_B : PackCfg<1, 1>::CIN_B) - 1) /
-                      (k == 3 ? PackCfg<3, 1>::CIN_B : PackCfg<1, 1>::CIN_B);
+  const int cin_b = k == 3 ? PackCfg<3, 1>::CIN_B : PackCfg<1, 1>::CIN_B;
+  const int nchunks = (cin + cin_b - 1) / cin_b;
 #define LEA_PACK(KS, MT) \
   pack_weights_kernel<KS, MT><<<grid, threads, 0, st>>>(w, packed, cout, cin, nchunks, total)
   if (k == 3) {
@@ -312,40 +572,62 @@ extern "C" int lea_conv3d_pack_weights(const float* w, float* packed, int cout, 
   return launch_status("lea_conv3d_pack_weights");
 }
 
-extern "C" int lea_conv3d_bnrelu(const void* x, int64_t x_bstride, const float* w_packed,
+extern "C" int lea_conv3d_bnrelu(const void* x, int64_t x_bstride, const void* x2,
+                                 int64_t x2_bstride, int cin2, const float* w_packed,
                                  const float* scale, const float* shift, const void* residual,
                                  int64_t r_bstride, void* y, int64_t y_bstride, int B, int cin,
                                  int cout, int D, int H, int W, int k, unsigned flags, int dtype,
                                  void* stream) {
-  using namespace lea;
-  clear_error();
-  LEA_CHECK_ARG(x && w_packed && y, "lea_conv3d_bnrelu: null pointer");
-  LEA_CHECK_ARG((scale == nullptr) == (shift == nullptr), "lea_conv3d_bnrelu: scale/shift must both be set or both NULL");
-  LEA_CHECK_ARG(!(flags & LEA_RESIDUAL) || residual, "lea_conv3d_bnrelu: LEA_RESIDUAL without residual");
-  LEA_CHECK_ARG(B > 0 && cin > 0 && cout > 0 && D > 0 && H > 0 && W > 0,
-                "lea_conv3d_bnrelu: bad shape B=%d cin=%d cout=%d D=%d H=%d W=%d", B, cin, cout, D,
-                H, W);
-  LEA_CHECK_ARG(k == 1 || k == 3, "lea_conv3d_bnrelu: k=%d unsupported", k);
-  if (dtype != LEA_F32) {
-    set_error("lea_conv3d_bnrelu: dtype %d unsupported", dtype);
-    return LEA_E_UNSUPPORTED;
-  }
-  // x must not alias y (the halo of other tiles would be overwritten mid-flight)
-  LEA_CHECK_ARG(x != y, "lea_conv3d_bnrelu: x aliases y");
-  const float* xf = (const float*)x;
-  const float* rf = (const float*)residual;
-  float* yf = (float*)y;
-  hipStream_t st = as_stream(stream);
-  const int mt = mt_for(cout);
-  if (k == 3) {
-    if (mt == 1) return dispatch_k3<1, 8>(xf, x_bstride, w_packed, scale, shift, rf, r_bstride, yf, y_bstride, B, cin, cout, D, H, W, flags, st);
-    if (mt == 2) return dispatch_k3<2, 4>(xf, x_bstride, w_packed, scale, shift, rf, r_bstride, yf, y_bstride, B, cin, cout, D, H, W, flags, st);
-    return dispatch_k3<4, 4>(xf, x_bstride, w_packed, scale, shift, rf, r_bstride, yf, y_bstride, B, cin, cout, D, H, W, flags, st);
-  }
-  // 1x1x1: the volume is a flat run of D*H*W voxels (no halo)
-  const long long dhw = (long long)D * H * W;
-  LEA_CHECK_ARG(dhw < (1LL << 31), "lea_conv3d_bnrelu: volume too large");
-  if (mt == 1) return launch_conv<1, 1, 8, 512>(xf, x_bstride, w_packed, scale, shift, rf, r_bstride, yf, y_bstride, B, cin, cout, 1, 1, (int)dhw, flags, st);
-  if (mt == 2) return launch_conv<1, 2, 4, 256>(xf, x_bstride, w_packed, scale, shift, rf, r_bstride, yf, y_bstride, B, cin, cout, 1, 1, (int)dhw, flags, st);
-  return launch_conv<1, 4, 4, 256>(xf, x_bstride, w_packed, scale, shift, rf, r_bstride, yf, y_bstride, B, cin, cout, 1, 1, (int)dhw, flags, st);
+  lea::ConvArgs a{};
+  a.x = (const float*)x;
+  a.xbs = x_bstride;
+  a.x2 = (const float*)x2;
+  a.x2bs = x2_bstride;
+  a.cin1 = cin - cin2;
+  a.wp = w_packed;
+  a.scale = scale;
+  a.shift = shift;
+  a.res = (const float*)residual;
+  a.rbs = r_bstride;
+  a.y = (float*)y;
+  a.ybs = y_bstride;
+  a.cin = cin;
+  a.cout = cout;
+  a.D = D;
+  a.H = H;
+  a.W = W;
+  a.flags = flags;
+  return lea::conv_common(a, B, k, false, dtype, stream);
+}
+
+extern "C" int lea_conv3d_bnrelu_resampled(const void* x, int64_t x_bstride, int Di, int Hi,
+                                           int Wi, const float* w_packed, const float* scale,
+                                           const float* shift, const void* residual,
+                                           int64_t r_bstride, void* y, int64_t y_bstride, int B,
+                                           int cin, int cout, int D, int H, int W, int k,
+                                           unsigned flags, int dtype, void* stream) {
+  lea::ConvArgs a{};
+  a.x = (const float*)x;
+  a.xbs = x_bstride;
+  a.cin1 = cin;
+  a.wp = w_packed;
+  a.scale = scale;
+  a.shift = shift;
+  a.res = (const float*)residual;
+  a.rbs = r_bstride;
+  a.y = (float*)y;
+  a.ybs = y_bstride;
+  a.cin = cin;
+  a.cout = cout;
+  a.D = D;
+  a.H = H;
+  a.W = W;
+  a.Di = Di;
+  a.Hi = Hi;
+  a.Wi = Wi;
+  a.rd = lea::axis_ratio(Di, D, 1);
+  a.rh = lea::axis_ratio(Hi, H, 1);
+  a.rw = lea::axis_ratio(Wi, W, 1);
+  a.flags = flags;
+  return lea::conv_common(a, B, k, true, dtype, stream);
 }

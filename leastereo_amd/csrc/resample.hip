@@ -12,38 +12,6 @@
 
 namespace lea {
 
-struct Axis {
-  int i0, i1;
-  float l0, l1;
-};
-
-__device__ __forceinline__ Axis axis_index(float ratio, int o, int in, int out, int ac) {
-#pragma clang fp contract(off)
-  Axis a;
-  if (in == out) {
-    a.i0 = a.i1 = o;
-    a.l0 = 1.f;
-    a.l1 = 0.f;
-    return a;
-  }
-  float real = ac ? ratio * (float)o : ratio * ((float)o + 0.5f) - 0.5f;
-  if (!ac && real < 0.f) real = 0.f;
-  int i = (int)floorf(real);
-  if (i > in - 1) i = in - 1;
-  float lam = real - (float)i;
-  lam = fminf(fmaxf(lam, 0.f), 1.f);
-  a.i0 = i;
-  a.i1 = i + ((i < in - 1) ? 1 : 0);
-  a.l1 = lam;
-  a.l0 = 1.f - lam;
-  return a;
-}
-
-__host__ inline float axis_ratio(int in, int out, int ac) {
-  if (ac) return out > 1 ? (float)(in - 1) / (float)(out - 1) : 0.f;
-  return (float)in / (float)out;
-}
-
 __global__ __launch_bounds__(256) void resample3d_f32(const float* __restrict__ x, long long xbs,
                                                       float* __restrict__ y, long long ybs, int C,
                                                       int Di, int Hi, int Wi, int Do, int Ho, int Wo,
@@ -64,10 +32,7 @@ __global__ __launch_bounds__(256) void resample3d_f32(const float* __restrict__ 
   const float* p01 = xc + ad.i0 * HWi + (long long)ah.i1 * Wi;
   const float* p10 = xc + ad.i1 * HWi + (long long)ah.i0 * Wi;
   const float* p11 = xc + ad.i1 * HWi + (long long)ah.i1 * Wi;
-  const float v = ad.l0 * (ah.l0 * (aw.l0 * p00[aw.i0] + aw.l1 * p00[aw.i1]) +
-                           ah.l1 * (aw.l0 * p01[aw.i0] + aw.l1 * p01[aw.i1])) +
-                  ad.l1 * (ah.l0 * (aw.l0 * p10[aw.i0] + aw.l1 * p10[aw.i1]) +
-                           ah.l1 * (aw.l0 * p11[aw.i0] + aw.l1 * p11[aw.i1]));
+  const float v = trilerp(ad, ah, aw, p00, p01, p10, p11);
   y[(long long)b * ybs + (long long)c * Do * Ho * Wo + ((long long)od * Ho + oh) * Wo + ow] = v;
 }
 

@@ -47,33 +47,46 @@ class MatchingExecutor:
                     self.p[name] = ConvParams(kernels.pack_conv_weight(w), scale, shift,
                                               w.shape[1], w.shape[0], w.shape[-1], mod.relu)
 
-    def conv(self, name, x, out=None, accumulate=False):
+    def conv(self, name, x, out=None, accumulate=False, x2=None, size=None):
+        """ConvBR3d ``name`` on x (or cat(x, x2)); with ``size`` != x's volume the
+        input is trilinearly resampled (align_corners=True) inside the conv."""
         p = self.p[name]
-        if x.shape[1] != p.cin:
-            raise ValueError(f"{name}: expected {p.cin} input channels, got {x.shape[1]}")
+        cin = x.shape[1] + (x2.shape[1] if x2 is not None else 0)
+        if cin != p.cin:
+            raise ValueError(f"{name}: expected {p.cin} input channels, got {cin}")
+        if size is not None and tuple(size) != tuple(x.shape[2:]):
+            if x2 is not None:
+                raise ValueError("resampled conv takes one input")
+            return kernels.conv3d_bnrelu_resampled(x, size, p.packed, p.cout, p.k, p.scale,
+                                                   p.shift, p.relu, out, accumulate)
         return kernels.conv3d_bnrelu(x, p.packed, p.cout, p.k, p.scale, p.shift, p.relu, out,
-                                     accumulate)
+                                     accumulate, x2)
 
     def cell(self, i, s0, s1):
-        """Cell.forward (skip_model_3d.py:41-75)."""
+        """Cell.forward (skip_model_3d.py:41-75).  The level change of s1 (:44-48)
+        and the size match of s0 (:49-51) are fused into the 1x1 preprocess convs
+        (:52-53) that consume them."""
         cell = self.m.cells[i]
         c = cell.c_out
         prev_input = s1
+        size = tuple(s1.shape[2:])
         if cell.downup_sample != 0:
             sc = 0.5 if cell.downup_sample < 0 else 2
-            s1 = kernels.resample_trilinear(s1, [scale_dimension(n, sc) for n in s1.shape[2:]])
-        if s0.shape[2:] != s1.shape[2:]:
-            s0 = kernels.resample_trilinear(s0, s1.shape[2:])
-        b, _, d, h, w = s1.shape
+            size = tuple(scale_dimension(n, sc) for n in size)
+        b = s1.shape[0]
+        d, h, w = size
         bm = cell.block_multiplier
         n_states = 2 + cell.steps
         out = torch.empty((b, bm * c, d, h, w), device=s1.device, dtype=s1.dtype)
         slot = {idx: out[:, k * c:(k + 1) * c] for k, idx in enumerate(range(n_states - bm, n_states))}
         if s0.shape[1] != c:
-            s0 = self.conv(f"cells.{i}.pre_preprocess", s0, out=slot.get(0))
-        elif 0 in slot:
-            slot[0].copy_(s0)
-        s1 = self.conv(f"cells.{i}.preprocess", s1, out=slot.get(1))
+            s0 = self.conv(f"cells.{i}.pre_preprocess", s0, out=slot.get(0), size=size)
+        else:
+            if tuple(s0.shape[2:]) != size:
+                s0 = kernels.resample_trilinear(s0, size)
+            if 0 in slot:
+                slot[0].copy_(s0)
+        s1 = self.conv(f"cells.{i}.preprocess", s1, out=slot.get(1), size=size)
         states = [s0, s1]
         for terms in cell.plan:
             dst = slot.get(len(states))
@@ -97,11 +110,11 @@ class MatchingExecutor:
         prev = (stem0, stem1)
         n = len(self.m.cells)
         for i in range(n):
-            if i == 5 and n == 12:   # :150-151
-                fused = self.conv("conv1", torch.cat((outs[1][1], outs[4][1]), 1))
+            if i == 5 and n == 12:   # :150-151, cat read in place by the conv
+                fused = self.conv("conv1", outs[1][1], x2=outs[4][1])
                 prev = (outs[4][0], fused)
             elif i == 9 and n == 12:  # :155-156
-                fused = self.conv("conv2", torch.cat((outs[4][1], outs[8][1]), 1))
+                fused = self.conv("conv2", outs[4][1], x2=outs[8][1])
                 prev = (outs[8][0], fused)
             o = self.cell(i, prev[0], prev[1])
             outs.append(o)
@@ -109,17 +122,17 @@ class MatchingExecutor:
         last = outs[-1][1]
         d, h, w = x.shape[2:]
         lh = last.shape[3]
+        full, half, quarter = (d, h, w), (d // 2, h // 2, w // 2), (d // 4, h // 4, w // 4)
+        # head (:161-173): each Upsample is fused into the conv that consumes it
         if lh == h:
-            y = last
-        elif lh == h // 2:
-            y = kernels.resample_trilinear(self.conv("last_6", last), (d, h, w))
+            return self.conv("last_3", last)
+        if lh == h // 2:
+            y = self.conv("last_6", last)
         elif lh == h // 4:
-            y = kernels.resample_trilinear(self.conv("last_12", last), (d // 2, h // 2, w // 2))
-            y = kernels.resample_trilinear(self.conv("last_6", y), (d, h, w))
+            y = self.conv("last_6", self.conv("last_12", last), size=half)
         elif lh == h // 8:
-            y = kernels.resample_trilinear(self.conv("last_24", last), (d // 4, h // 4, w // 4))
-            y = kernels.resample_trilinear(self.conv("last_12", y), (d // 2, h // 2, w // 2))
-            y = kernels.resample_trilinear(self.conv("last_6", y), (d, h, w))
+            y = self.conv("last_12", self.conv("last_24", last), size=quarter)
+            y = self.conv("last_6", y, size=half)
         else:
             raise ValueError(f"matching-net output size {tuple(last.shape[2:])} has no head")
-        return self.conv("last_3", y)
+        return self.conv("last_3", y, size=full)

@@ -53,8 +53,8 @@ class KernelProbe:
 _probe = None
 
 
-def conv_kernel_name(cout, cin, d, h, w, k):
-    name = _lib.load().lea_conv3d_kernel_name(cout, cin, d, h, w, k)
+def conv_kernel_name(b, cout, d, h, w, k, resampled=False):
+    name = _lib.load().lea_conv3d_kernel_name(b, cout, d, h, w, k, 1 if resampled else 0)
     return name.decode() if name else None
 
 
@@ -106,45 +106,95 @@ def pack_conv_weight(w: torch.Tensor) -> torch.Tensor:
     return packed
 
 
-def conv3d_bnrelu(x: torch.Tensor, packed: torch.Tensor, cout: int, k: int,
-                  scale: torch.Tensor | None, shift: torch.Tensor | None, relu: bool = True,
-                  out: torch.Tensor | None = None, accumulate: bool = False) -> torch.Tensor:
-    """ConvBR3d (operations_3d.py:41-47).  ``out`` may be a channel slice of a
-    larger (cat) buffer; ``accumulate`` adds the activation to what ``out``
-    holds (the cell's pairwise sum, skip_model_3d.py:69)."""
-    _require_cuda(x, packed, scale, shift, out)
-    b, cin, d, h, w = x.shape
-    xbs = _check_volume_view(x, "x")
+def _probe_begin(b, cin, cout, d, h, w, k, accumulate, in_vox, resampled):
+    """Start HIP-event timing of this launch if the active probe wants its kernel."""
+    probe = _probe
+    if probe is None:
+        return None
+    name = conv_kernel_name(b, cout, d, h, w, k, resampled)
+    if probe.names is not None and name not in probe.names:
+        return None
+    vox = b * d * h * w
+    flops = 2.0 * vox * cout * cin * k ** 3
+    nbytes = 4.0 * (in_vox * cin + vox * cout * (2 if accumulate else 1) + cout * cin * k ** 3)
+    e0 = torch.cuda.Event(enable_timing=True)
+    e0.record()
+    return probe, name, flops, nbytes, e0
+
+
+def _probe_end(rec):
+    if rec is not None:
+        probe, name, flops, nbytes, e0 = rec
+        e1 = torch.cuda.Event(enable_timing=True)
+        e1.record()
+        probe.records.append((name, flops, nbytes, e0, e1))
+
+
+def _conv_out(x_shape5, cout, spatial, out, accumulate, device, dtype):
+    b = x_shape5[0]
+    shape = (b, cout) + tuple(int(s) for s in spatial)
     if out is None:
         if accumulate:
             raise ValueError("accumulate needs out")
-        out = torch.empty((b, cout, d, h, w), device=x.device, dtype=x.dtype)
-    if tuple(out.shape) != (b, cout, d, h, w):
-        raise ValueError(f"out shape {tuple(out.shape)} != {(b, cout, d, h, w)}")
-    ybs = _check_volume_view(out, "out")
+        out = torch.empty(shape, device=device, dtype=dtype)
+    if tuple(out.shape) != shape:
+        raise ValueError(f"out shape {tuple(out.shape)} != {shape}")
+    return out, _check_volume_view(out, "out")
+
+
+def conv3d_bnrelu(x: torch.Tensor, packed: torch.Tensor, cout: int, k: int,
+                  scale: torch.Tensor | None, shift: torch.Tensor | None, relu: bool = True,
+                  out: torch.Tensor | None = None, accumulate: bool = False,
+                  x2: torch.Tensor | None = None) -> torch.Tensor:
+    """ConvBR3d (operations_3d.py:41-47) of ``torch.cat((x, x2), 1)`` (x2 optional,
+    never materialised).  ``out`` may be a channel slice of a larger (cat) buffer;
+    ``accumulate`` adds the activation to what ``out`` holds (the cell's pairwise
+    sum, skip_model_3d.py:69)."""
+    _require_cuda(x, x2, packed, scale, shift, out)
+    b, cin, d, h, w = x.shape
+    xbs = _check_volume_view(x, "x")
+    cin2, x2bs = 0, 0
+    if x2 is not None:
+        if x2.shape[0] != b or tuple(x2.shape[2:]) != (d, h, w):
+            raise ValueError("x2 must match x in batch and volume")
+        cin2 = x2.shape[1]
+        x2bs = _check_volume_view(x2, "x2")
+    out, ybs = _conv_out(x.shape, cout, (d, h, w), out, accumulate, x.device, x.dtype)
     flags = (LEA_RELU if relu else 0) | (LEA_RESIDUAL if accumulate else 0)
-    probe = _probe
-    if probe is not None:
-        name = conv_kernel_name(cout, cin, d, h, w, k)
-        if probe.names is None or name in probe.names:
-            vox = b * d * h * w
-            flops = 2.0 * vox * cout * cin * k ** 3
-            nbytes = 4.0 * (vox * (cin + cout * (2 if accumulate else 1)) + cout * cin * k ** 3)
-            e0 = torch.cuda.Event(enable_timing=True)
-            e1 = torch.cuda.Event(enable_timing=True)
-            e0.record()
-        else:
-            probe = None
+    rec = _probe_begin(b, cin + cin2, cout, d, h, w, k, accumulate, b * d * h * w, False)
     check(_lib.load().lea_conv3d_bnrelu(
-        x.data_ptr(), xbs, packed.data_ptr(),
+        x.data_ptr(), xbs, x2.data_ptr() if x2 is not None else None, x2bs, cin2,
+        packed.data_ptr(),
+        scale.data_ptr() if scale is not None else None,
+        shift.data_ptr() if shift is not None else None,
+        out.data_ptr() if accumulate else None, ybs if accumulate else 0,
+        out.data_ptr(), ybs, b, cin + cin2, cout, d, h, w, k, flags, LEA_F32, _stream()),
+        "lea_conv3d_bnrelu")
+    _probe_end(rec)
+    return out
+
+
+def conv3d_bnrelu_resampled(x: torch.Tensor, size, packed: torch.Tensor, cout: int, k: int,
+                            scale: torch.Tensor | None, shift: torch.Tensor | None,
+                            relu: bool = True, out: torch.Tensor | None = None,
+                            accumulate: bool = False) -> torch.Tensor:
+    """ConvBR3d(F.interpolate(x, size, mode='trilinear', align_corners=True)) with
+    the interpolation fused into the conv's input staging (skip_model_3d.py:44-53)."""
+    _require_cuda(x, packed, scale, shift, out)
+    b, cin, di, hi, wi = x.shape
+    d, h, w = (int(s) for s in size)
+    xbs = _check_volume_view(x, "x")
+    out, ybs = _conv_out(x.shape, cout, (d, h, w), out, accumulate, x.device, x.dtype)
+    flags = (LEA_RELU if relu else 0) | (LEA_RESIDUAL if accumulate else 0)
+    rec = _probe_begin(b, cin, cout, d, h, w, k, accumulate, b * di * hi * wi, True)
+    check(_lib.load().lea_conv3d_bnrelu_resampled(
+        x.data_ptr(), xbs, di, hi, wi, packed.data_ptr(),
         scale.data_ptr() if scale is not None else None,
         shift.data_ptr() if shift is not None else None,
         out.data_ptr() if accumulate else None, ybs if accumulate else 0,
         out.data_ptr(), ybs, b, cin, cout, d, h, w, k, flags, LEA_F32, _stream()),
-        "lea_conv3d_bnrelu")
-    if probe is not None:
-        e1.record()
-        probe.records.append((name, flops, nbytes, e0, e1))
+        "lea_conv3d_bnrelu_resampled")
+    _probe_end(rec)
     return out
 
 

@@ -29,19 +29,31 @@ def test_library_exports_every_declared_symbol():
     lib = _lib.load()
     for name in declared_symbols():
         assert hasattr(lib, name), name
-    assert lib.lea_abi_version() == 1
+    assert lib.lea_abi_version() == _lib.ABI_VERSION
 
 
 def test_invalid_arguments_are_rejected_before_launch():
     lib = _lib.load()
     assert lib.lea_build_cost_volume(None, None, None, 1, 1, 1, 1, 1, 0, None) == 1001
     assert b"null" in lib.lea_last_error()
-    assert lib.lea_conv3d_bnrelu(None, 0, None, None, None, None, 0, None, 0,
+    assert lib.lea_conv3d_bnrelu(None, 0, None, 0, 0, None, None, None, None, 0, None, 0,
                                  1, 1, 1, 1, 1, 1, 3, 1, 0, None) == 1001
     x = ctypes.c_void_p(16)
+    y = ctypes.c_void_p(32)
     # scale without shift
-    assert lib.lea_conv3d_bnrelu(x, 0, x, x, None, None, 0, ctypes.c_void_p(32), 0,
+    assert lib.lea_conv3d_bnrelu(x, 0, None, 0, 0, x, x, None, None, 0, y, 0,
                                  1, 1, 1, 1, 1, 1, 3, 1, 0, None) == 1001
+    # second source announced but missing
+    assert lib.lea_conv3d_bnrelu(x, 0, None, 0, 4, x, None, None, None, 0, y, 0,
+                                 1, 8, 1, 1, 1, 1, 3, 1, 0, None) == 1001
+    # output aliasing the input
+    assert lib.lea_conv3d_bnrelu(x, 0, None, 0, 0, x, None, None, None, 0, x, 0,
+                                 1, 1, 1, 1, 1, 1, 3, 1, 0, None) == 1001
+    assert lib.lea_conv3d_bnrelu_resampled(x, 0, 0, 1, 1, x, None, None, None, 0, y, 0,
+                                           1, 1, 1, 1, 1, 1, 1, 1, 0, None) == 1001
+    assert b"input volume" in lib.lea_last_error()
+    assert lib.lea_conv3d_kernel_name(1, 32, 64, 192, 320, 3, 0) == b"conv3d_dma_kernel<2, 4, 64>"
+    assert lib.lea_conv3d_kernel_name(1, 8, 64, 192, 320, 1, 1).startswith(b"conv3d_reg_kernel<1, 1")
     # unsupported dtype is reported as such
     assert lib.lea_disparity_regression(x, x, 1, 1, 1, 1, 1, 1, None) == 1002
     assert lib.lea_resample3d_trilinear(x, 0, x, 0, 1, 1, 1, 1, 1, 1, 1, 1, 1, 0, None) == 1001

@@ -112,6 +112,41 @@ def test_conv_random_vs_torch(b, cin, cout, k, shape):
     np.testing.assert_allclose(out.cpu().double().numpy(), refy.numpy(), rtol=1e-4, atol=1e-4)
 
 
+@pytest.mark.parametrize("c1,c2,cout,shape", [(64, 64, 64, (4, 10, 40)), (16, 12, 16, (3, 7, 33)),
+                                              (4, 4, 8, (2, 3, 5))])
+def test_conv_two_sources_is_cat(c1, c2, cout, shape):
+    """conv(cat(x, x2)) without the cat (skip_model_3d.py:150,155)."""
+    g = torch.Generator().manual_seed(c1 + c2)
+    x = torch.randn((2, c1) + shape, generator=g)
+    x2 = torch.randn((2, c2) + shape, generator=g)
+    w = torch.randn(cout, c1 + c2, 3, 3, 3, generator=g) / np.sqrt((c1 + c2) * 27)
+    refy = F.conv3d(torch.cat((x, x2), 1).double(), w.double(), None, 1, 1)
+    y = kernels.conv3d_bnrelu(x.to(DEV), kernels.pack_conv_weight(w.to(DEV)), cout, 3, None, None,
+                              relu=False, x2=x2.to(DEV))
+    np.testing.assert_allclose(y.cpu().double().numpy(), refy.numpy(), rtol=1e-4, atol=1e-4)
+
+
+@pytest.mark.parametrize("k,cin,cout,src,dst", [
+    (1, 64, 8, (4, 6, 10), (8, 12, 20)),      # L1 -> L0 (cell10)
+    (1, 32, 16, (8, 12, 20), (4, 6, 10)),     # L0 -> L1 (cell0/1/11)
+    (1, 128, 16, (3, 5, 9), (5, 9, 17)),      # odd sizes up (2n-1)
+    (1, 64, 32, (5, 9, 17), (3, 5, 9)),       # odd sizes down ((n+1)/2)
+    (3, 32, 1, (4, 6, 40), (8, 12, 80)),      # head: Upsample + last_3
+    (3, 16, 16, (5, 7, 9), (4, 5, 6))])       # generic size match
+def test_conv_resampled_vs_torch(k, cin, cout, src, dst):
+    g = torch.Generator().manual_seed(cin * 7 + k)
+    x = torch.randn((2, cin) + src, generator=g)
+    w = torch.randn(cout, cin, k, k, k, generator=g) / np.sqrt(cin * k ** 3)
+    scale = torch.rand(cout, generator=g) + 0.5
+    shift = torch.randn(cout, generator=g) * 0.1
+    xi = F.interpolate(x.double(), dst, mode="trilinear", align_corners=True)
+    refy = torch.relu(F.conv3d(xi, w.double(), None, 1, k // 2) * scale.double().view(1, -1, 1, 1, 1)
+                      + shift.double().view(1, -1, 1, 1, 1))
+    y = kernels.conv3d_bnrelu_resampled(x.to(DEV), dst, kernels.pack_conv_weight(w.to(DEV)), cout, k,
+                                        scale.to(DEV), shift.to(DEV), relu=True)
+    np.testing.assert_allclose(y.cpu().double().numpy(), refy.numpy(), rtol=1e-4, atol=1e-4)
+
+
 def test_conv_channel_slices():
     """Input and output as channel slices of larger tensors (the free cat)."""
     g = torch.Generator().manual_seed(7)
