@@ -95,10 +95,15 @@ const char* lea_conv3d_kernel_name(int B, int cout, int D, int H, int W, int k, 
 
 /* Trilinear resample.  Replaces F.interpolate(mode='trilinear') at
  * skip_model_3d.py:48,50 and nn.Upsample at :162-164 (align_corners=1), with
- * PyTorch's source-index rule. */
+ * PyTorch's source-index rule, then an optional epilogue
+ *   y = act(scale[c] * interp(x) + shift[c])      (scale/shift NULL: identity)
+ * with act = ReLU under LEA_RELU.  With the epilogue it completes an up-sampling
+ * ConvBR1x1 whose conv ran at the input resolution (the conv and the
+ * interpolation commute). */
 int lea_resample3d_trilinear(const void* x, int64_t x_bstride, void* y, int64_t y_bstride,
                              int B, int C, int Di, int Hi, int Wi, int Do, int Ho, int Wo,
-                             int align_corners, int dtype, void* stream);
+                             int align_corners, const float* scale, const float* shift,
+                             unsigned flags, int dtype, void* stream);
 
 /* Disparity regression.  Replaces models/build_model_2d.py:52-57 + :33-42:
  *   U = trilinear(cost, [maxdisp, 3*H3, 3*W3], align_corners=False)

@@ -373,6 +373,131 @@ __global__ __launch_bounds__(kConvThreads, 2) void conv3d_reg_kernel(const ConvA
   epilogue<KS, MT, NT, TW>(a, acc, b, co0, d0, h0, w0, wave, lane);
 }
 
+// ------------------------------------------------- VALU engine for cout <= 2 (k=3)
+// The head's last_3 (32 -> 1, skip_model_3d.py:132) would use 1/16 of each MFMA's
+// rows.  Here every thread owns 2 adjacent output voxels of a 8 x 64 plane tile
+// and runs plain FMAs; weights are wave-uniform (scalar loads from the packed
+// chunk), the input halo block comes by the same LDS-DMA pieces as the MFMA
+// engine (double-buffered), read back as ds_read_b64 pairs.
+template <int COUT>
+__global__ __launch_bounds__(kConvThreads) void conv3d_valu_kernel(const ConvArgs a) {
+  constexpr int TH = 8, TW = 64, RH = TH + 2, RW = TW + 2, PLANE = RH * RW, IMG = 3 * PLANE;
+  constexpr int CIN_B = PackCfg<3, 1>::CIN_B;
+  constexpr int CIS = (IMG + 15) / 16 * 16;
+  constexpr int STAGE = CIN_B * CIS;
+  constexpr int XSLOTS = (IMG + 63) / 64;
+  constexpr int XSLOTS_W = (XSLOTS + kConvWaves - 1) / kConvWaves;
+  constexpr int CHUNK = PackCfg<3, 1>::CHUNK;  // packed layout of mt=1: [tap][ci][16]
+  __shared__ __attribute__((aligned(16))) float smem[2 * STAGE];
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int h0 = (blockIdx.x / a.tiles_w) * TH;
+  const int w0 = (blockIdx.x % a.tiles_w) * TW;
+  const int d0 = blockIdx.y;
+  const int b = blockIdx.z;
+  const int nchunks = (a.cin + CIN_B - 1) / CIN_B;
+  const int HW = a.H * a.W;
+  const unsigned nrec = (unsigned)(HW * a.D) * 4u;
+
+  unsigned voff[XSLOTS_W];
+#pragma unroll
+  for (int t = 0; t < XSLOTS_W; ++t) {
+    const int e = (wave + kConvWaves * t) * 64 + lane;
+    unsigned v = 0xFFFFFFF0u;
+    if (e < IMG) {
+      const int kd = e / PLANE;
+      const int r = e - kd * PLANE;
+      const int rr = r / RW;
+      const int cc = r - rr * RW;
+      const int d = d0 + kd - 1, h = h0 + rr - 1, w = w0 + cc - 1;
+      if ((unsigned)d < (unsigned)a.D && (unsigned)h < (unsigned)a.H && (unsigned)w < (unsigned)a.W)
+        v = (unsigned)(d * HW + h * a.W + w) * 4u;
+    }
+    voff[t] = v;
+  }
+  auto issue = [&](int ch, float* st) {
+#pragma unroll
+    for (int ci = 0; ci < CIN_B; ++ci) {
+      const int c = ch * CIN_B + ci;
+      const float* base = a.x;
+      unsigned n = 0;
+      if (c < a.cin1) {
+        base = a.x + (long long)b * a.xbs + (long long)c * HW * a.D;
+        n = nrec;
+      } else if (c < a.cin) {
+        base = a.x2 + (long long)b * a.x2bs + (long long)(c - a.cin1) * HW * a.D;
+        n = nrec;
+      }
+      const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)base, 0, n, 0x00020000);
+#pragma unroll
+      for (int t = 0; t < XSLOTS_W; ++t) {
+        const int j = wave + kConvWaves * t;
+        if (j < XSLOTS && j * 64 + lane < IMG)
+          __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void*)(st + ci * CIS + j * 64), 4,
+                                                   voff[t], 0, 0, 0);
+      }
+    }
+  };
+
+  const int row = tid >> 5;        // 0..7
+  const int col = (tid & 31) * 2;  // 0..62
+  float acc[COUT][2];
+#pragma unroll
+  for (int co = 0; co < COUT; ++co) acc[co][0] = acc[co][1] = 0.f;
+
+  issue(0, smem);
+  for (int ch = 0; ch < nchunks; ++ch) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (ch + 1 < nchunks) issue(ch + 1, smem + ((ch + 1) & 1) * STAGE);
+    const float* xs = smem + (ch & 1) * STAGE;
+    const float* wc = a.wp + (long long)ch * CHUNK;
+#pragma unroll
+    for (int ci = 0; ci < CIN_B; ++ci) {
+#pragma unroll
+      for (int kd = 0; kd < 3; ++kd) {
+#pragma unroll
+        for (int kh = 0; kh < 3; ++kh) {
+          const float* p = xs + ci * CIS + kd * PLANE + (row + kh) * RW + col;
+          const float2 x01 = *reinterpret_cast<const float2*>(p);
+          const float2 x23 = *reinterpret_cast<const float2*>(p + 2);
+          const float xv[4] = {x01.x, x01.y, x23.x, x23.y};
+#pragma unroll
+          for (int kw = 0; kw < 3; ++kw) {
+            const int tap = (kd * 3 + kh) * 3 + kw;
+#pragma unroll
+            for (int co = 0; co < COUT; ++co) {
+              const float wv = wc[(tap * CIN_B + ci) * 16 + co];
+              acc[co][0] = fmaf(wv, xv[kw], acc[co][0]);
+              acc[co][1] = fmaf(wv, xv[kw + 1], acc[co][1]);
+            }
+          }
+        }
+      }
+    }
+  }
+  const long long HWl = HW, DHW = (long long)HW * a.D;
+  const int h = h0 + row;
+#pragma unroll
+  for (int co = 0; co < COUT; ++co) {
+    if (co >= a.cout) continue;
+    const float sc = a.scale ? a.scale[co] : 1.f;
+    const float sh = a.shift ? a.shift[co] : 0.f;
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+      const int w = w0 + col + e;
+      if (h >= a.H || w >= a.W) continue;
+      const long long o = (long long)co * DHW + (long long)d0 * HWl + (long long)h * a.W + w;
+      float v = acc[co][e] * sc + sh;
+      if (a.flags & LEA_RELU) v = fmaxf(v, 0.f);
+      if (a.flags & LEA_RESIDUAL) v += a.res[(long long)b * a.rbs + o];
+      a.y[(long long)b * a.ybs + o] = v;
+    }
+  }
+}
+
 // ------------------------------------------------------------------- weight packing
 // Packed layout: [ceil(cout/COP)][ceil(cin/CIN_B)][KS^3][CIN_B][COPS], zero outside (cin, cout).
 template <int KS, int MT>
@@ -416,7 +541,7 @@ size_t packed_floats(int cout, int cin, int k) {
 // ------------------------------------------------------------------------- dispatch
 // A launch plan: which instantiation runs a given shape (also reported by name).
 struct Plan {
-  int engine;  // 0 = dma (k3), 1 = reg flat (k1), 2 = reg resample
+  int engine;  // 0 = dma (k3), 1 = reg flat (k1), 2 = reg resample, 3 = valu (k3, cout <= 2)
   int mt, nt, tw;
 };
 
@@ -432,6 +557,12 @@ inline Plan make_plan(int B, int cout, int D, int H, int W, int k, bool resample
     p.engine = 1;
     p.nt = p.mt == 1 ? 8 : 4;
     p.tw = p.nt * 64;
+    return p;
+  }
+  if (k == 3 && cout <= 2 && !resample) {
+    p.engine = 3;
+    p.nt = 0;
+    p.tw = 64;
     return p;
   }
   p.engine = resample ? 2 : 0;
@@ -474,6 +605,10 @@ int run_rs(const ConvArgs& a, int tw, int B, hipStream_t st) {
 
 int run_plan(const Plan& p, ConvArgs a, int B, int k, hipStream_t st) {
   a.ncob = (a.cout + p.mt * 16 - 1) / (p.mt * 16);
+  if (p.engine == 3) {
+    if (a.cout == 1) return launch(conv3d_valu_kernel<1>, a, 8, 64, B, st);
+    return launch(conv3d_valu_kernel<2>, a, 8, 64, B, st);
+  }
   if (p.engine == 0) {
     if (p.mt == 1) return p.nt == 8 ? run_dma<1, 8>(a, p.tw, B, st) : run_dma<1, 4>(a, p.tw, B, st);
     if (p.mt == 2) return p.nt == 4 ? run_dma<2, 4>(a, p.tw, B, st) : run_dma<2, 2>(a, p.tw, B, st);
@@ -500,7 +635,9 @@ int run_plan(const Plan& p, ConvArgs a, int B, int k, hipStream_t st) {
 thread_local char g_name[96];
 
 const char* plan_name(const Plan& p, int k) {
-  if (p.engine == 0)
+  if (p.engine == 3)
+    snprintf(g_name, sizeof(g_name), "conv3d_valu_kernel<%d>", p.mt == 1 ? 1 : 2);
+  else if (p.engine == 0)
     snprintf(g_name, sizeof(g_name), "conv3d_dma_kernel<%d, %d, %d>", p.mt, p.nt, p.tw);
   else if (p.engine == 2)
     snprintf(g_name, sizeof(g_name), "conv3d_reg_kernel<%d, %d, %d, %d, true>", k, p.mt, p.nt, p.tw);

@@ -57,6 +57,12 @@ class MatchingExecutor:
         if size is not None and tuple(size) != tuple(x.shape[2:]):
             if x2 is not None:
                 raise ValueError("resampled conv takes one input")
+            up = all(int(o) >= int(i) for o, i in zip(size, x.shape[2:]))
+            if p.k == 1 and up and not accumulate:
+                # interp and the 1x1 conv commute: conv at the low resolution, then
+                # resample the narrow result with the BN/ReLU epilogue into `out`
+                z = kernels.conv3d_bnrelu(x, p.packed, p.cout, 1, None, None, relu=False)
+                return kernels.resample_trilinear(z, size, True, out, p.scale, p.shift, p.relu)
             return kernels.conv3d_bnrelu_resampled(x, size, p.packed, p.cout, p.k, p.scale,
                                                    p.shift, p.relu, out, accumulate)
         return kernels.conv3d_bnrelu(x, p.packed, p.cout, p.k, p.scale, p.shift, p.relu, out,
@@ -123,7 +129,8 @@ class MatchingExecutor:
         d, h, w = x.shape[2:]
         lh = last.shape[3]
         full, half, quarter = (d, h, w), (d // 2, h // 2, w // 2), (d // 4, h // 4, w // 4)
-        # head (:161-173): each Upsample is fused into the conv that consumes it
+        # head (:161-173): the 1x1 Upsample pairs run commuted (see conv()); the final
+        # Upsample is materialised once and read by the small-cout last_3 kernel
         if lh == h:
             return self.conv("last_3", last)
         if lh == h // 2:
@@ -135,4 +142,4 @@ class MatchingExecutor:
             y = self.conv("last_6", y, size=half)
         else:
             raise ValueError(f"matching-net output size {tuple(last.shape[2:])} has no head")
-        return self.conv("last_3", y, size=full)
+        return self.conv("last_3", kernels.resample_trilinear(y, full, True))

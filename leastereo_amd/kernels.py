@@ -199,18 +199,25 @@ def conv3d_bnrelu_resampled(x: torch.Tensor, size, packed: torch.Tensor, cout: i
 
 
 def resample_trilinear(x: torch.Tensor, size, align_corners: bool = True,
-                       out: torch.Tensor | None = None) -> torch.Tensor:
-    """F.interpolate(x, size, mode='trilinear', align_corners=...) for NCDHW."""
-    _require_cuda(x, out)
+                       out: torch.Tensor | None = None, scale: torch.Tensor | None = None,
+                       shift: torch.Tensor | None = None, relu: bool = False) -> torch.Tensor:
+    """F.interpolate(x, size, mode='trilinear', align_corners=...) for NCDHW, with
+    an optional per-channel ``relu(scale * . + shift)`` epilogue; ``out`` may be a
+    channel slice of a larger tensor."""
+    _require_cuda(x, out, scale, shift)
     b, c, di, hi, wi = x.shape
     do, ho, wo = (int(s) for s in size)
     xbs = _check_volume_view(x, "x")
     if out is None:
         out = torch.empty((b, c, do, ho, wo), device=x.device, dtype=x.dtype)
+    if tuple(out.shape) != (b, c, do, ho, wo):
+        raise ValueError(f"out shape {tuple(out.shape)} != {(b, c, do, ho, wo)}")
     ybs = _check_volume_view(out, "out")
-    check(_lib.load().lea_resample3d_trilinear(x.data_ptr(), xbs, out.data_ptr(), ybs, b, c, di, hi,
-                                               wi, do, ho, wo, 1 if align_corners else 0, LEA_F32,
-                                               _stream()), "lea_resample3d_trilinear")
+    check(_lib.load().lea_resample3d_trilinear(
+        x.data_ptr(), xbs, out.data_ptr(), ybs, b, c, di, hi, wi, do, ho, wo,
+        1 if align_corners else 0, scale.data_ptr() if scale is not None else None,
+        shift.data_ptr() if shift is not None else None, LEA_RELU if relu else 0, LEA_F32,
+        _stream()), "lea_resample3d_trilinear")
     return out
 
 

@@ -56,7 +56,10 @@ def test_invalid_arguments_are_rejected_before_launch():
     assert lib.lea_conv3d_kernel_name(1, 8, 64, 192, 320, 1, 1).startswith(b"conv3d_reg_kernel<1, 1")
     # unsupported dtype is reported as such
     assert lib.lea_disparity_regression(x, x, 1, 1, 1, 1, 1, 1, None) == 1002
-    assert lib.lea_resample3d_trilinear(x, 0, x, 0, 1, 1, 1, 1, 1, 1, 1, 1, 1, 0, None) == 1001
+    assert lib.lea_resample3d_trilinear(x, 0, x, 0, 1, 1, 1, 1, 1, 1, 1, 1, 1, None, None, 0, 0,
+                                        None) == 1001
+    assert lib.lea_resample3d_trilinear(x, 0, y, 0, 1, 1, 1, 1, 1, 1, 1, 1, 1, x, None, 0, 0,
+                                        None) == 1001
 
 
 @pytest.mark.parametrize("cout,cin,k", [(32, 64, 3), (64, 128, 3), (16, 16, 3), (8, 8, 3),

@@ -147,6 +147,34 @@ def test_conv_resampled_vs_torch(k, cin, cout, src, dst):
     np.testing.assert_allclose(y.cpu().double().numpy(), refy.numpy(), rtol=1e-4, atol=1e-4)
 
 
+@pytest.mark.parametrize("cout,cin,shape", [(1, 32, (6, 20, 130)), (2, 12, (3, 9, 64)),
+                                            (1, 5, (2, 3, 7))])
+def test_conv_small_cout_valu_engine(cout, cin, shape):
+    """last_3-like convs (cout <= 2) run on the VALU engine."""
+    g = torch.Generator().manual_seed(cout * 100 + cin)
+    x = torch.randn((2, cin) + shape, generator=g)
+    w = torch.randn(cout, cin, 3, 3, 3, generator=g) / np.sqrt(cin * 27)
+    assert kernels.conv_kernel_name(2, cout, *shape, 3).startswith("conv3d_valu_kernel")
+    refy = F.conv3d(x.double(), w.double(), None, 1, 1)
+    y = kernels.conv3d_bnrelu(x.to(DEV), kernels.pack_conv_weight(w.to(DEV)), cout, 3, None, None,
+                              relu=False)
+    np.testing.assert_allclose(y.cpu().double().numpy(), refy.numpy(), rtol=1e-4, atol=1e-4)
+
+
+def test_resample_affine_relu_epilogue_into_slice():
+    g = torch.Generator().manual_seed(11)
+    x = torch.randn(2, 8, 4, 6, 10, generator=g)
+    scale = torch.rand(8, generator=g) + 0.5
+    shift = torch.randn(8, generator=g)
+    big = torch.zeros(2, 24, 8, 12, 20, device=DEV)
+    kernels.resample_trilinear(x.to(DEV), (8, 12, 20), True, big[:, 8:16], scale.to(DEV),
+                               shift.to(DEV), relu=True)
+    refy = torch.relu(F.interpolate(x, (8, 12, 20), mode="trilinear", align_corners=True)
+                      * scale.view(1, -1, 1, 1, 1) + shift.view(1, -1, 1, 1, 1))
+    np.testing.assert_allclose(big[:, 8:16].cpu().numpy(), refy.numpy(), atol=1e-5, rtol=0)
+    assert big[:, :8].abs().sum().item() == 0 and big[:, 16:].abs().sum().item() == 0
+
+
 def test_conv_channel_slices():
     """Input and output as channel slices of larger tensors (the free cat)."""
     g = torch.Generator().manual_seed(7)
