@@ -373,6 +373,95 @@ __global__ __launch_bounds__(kConvThreads, 2) void conv3d_reg_kernel(const ConvA
   epilogue<KS, MT, NT, TW>(a, acc, b, co0, d0, h0, w0, wave, lane);
 }
 
+// ---------------------------------------------------------- 1x1x1 streaming engine
+// A 1x1 ConvBR is a [cout x cin] x [cin x voxels] GEMM that reads every input
+// element exactly once: HBM-bound.  No LDS for X: each lane's B fragment
+// (X[ci = 4s + kq][v = v0 + 16j + n]) is loaded straight from global memory
+// (16 consecutive floats per 16-lane group), all CIN_B/4 k-steps of a chunk
+// issued before its MFMAs so a chunk's loads are in flight together.  Weights of
+// the chunk (32 x COPS floats) are staged in LDS.  The volume is treated as a
+// flat run of D*H*W voxels.
+template <int MT, int NT>
+__global__ __launch_bounds__(kConvThreads) void conv1x1_kernel(const ConvArgs a) {
+  using P = PackCfg<1, MT>;
+  constexpr int CIN_B = P::CIN_B;
+  constexpr int KS = CIN_B / 4;
+  __shared__ __attribute__((aligned(16))) float ws[P::CHUNK];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int b = blockIdx.y / a.ncob;
+  const int co0 = (blockIdx.y - b * a.ncob) * P::COP;
+  const int nchunks = (a.cin + CIN_B - 1) / CIN_B;
+  const float* wp = a.wp + (long long)(co0 / P::COP) * nchunks * P::CHUNK;
+  const long long V = (long long)a.D * a.H * a.W;
+  const long long v0 = ((long long)blockIdx.x * kConvWaves + wave) * NT * 16;
+  const int kq = lane >> 4, n = lane & 15;
+
+  f32x4 acc[MT][NT];
+#pragma unroll
+  for (int m = 0; m < MT; ++m)
+#pragma unroll
+    for (int j = 0; j < NT; ++j) acc[m][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  for (int ch = 0; ch < nchunks; ++ch) {
+    float bv[KS][NT];
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+      const int c = ch * CIN_B + 4 * s + kq;
+      const float* src = (c < a.cin1) ? a.x + (long long)b * a.xbs + (long long)c * V
+                                      : a.x2 + (long long)b * a.x2bs + (long long)(c - a.cin1) * V;
+#pragma unroll
+      for (int j = 0; j < NT; ++j) {
+        const long long v = v0 + j * 16 + n;
+        bv[s][j] = (c < a.cin && v < V) ? src[v] : 0.f;
+      }
+    }
+    __syncthreads();  // previous chunk's weight reads are done
+    {
+      const float4* src = reinterpret_cast<const float4*>(wp + (long long)ch * P::CHUNK);
+      float4* dst = reinterpret_cast<float4*>(ws);
+#pragma unroll
+      for (int i = tid; i < P::CHUNK / 4; i += kConvThreads) dst[i] = src[i];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+      float av[MT];
+#pragma unroll
+      for (int m = 0; m < MT; ++m) av[m] = ws[(4 * s + kq) * P::COPS + m * 16 + n];
+#pragma unroll
+      for (int m = 0; m < MT; ++m)
+#pragma unroll
+        for (int j = 0; j < NT; ++j)
+          acc[m][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[m], bv[s][j], acc[m][j], 0, 0, 0);
+    }
+  }
+
+  const bool relu = a.flags & LEA_RELU;
+  const bool resid = a.flags & LEA_RESIDUAL;
+#pragma unroll
+  for (int m = 0; m < MT; ++m) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int co = co0 + m * 16 + kq * 4 + r;
+      if (co >= a.cout) continue;
+      const float sc = a.scale ? a.scale[co] : 1.f;
+      const float sh = a.shift ? a.shift[co] : 0.f;
+#pragma unroll
+      for (int j = 0; j < NT; ++j) {
+        const long long v = v0 + j * 16 + n;
+        if (v >= V) continue;
+        const long long o = (long long)co * V + v;
+        float val = acc[m][j][r] * sc + sh;
+        if (relu) val = fmaxf(val, 0.f);
+        if (resid) val += a.res[(long long)b * a.rbs + o];
+        a.y[(long long)b * a.ybs + o] = val;
+      }
+    }
+  }
+}
+
 // ------------------------------------------------- VALU engine for cout <= 2 (k=3)
 // The head's last_3 (32 -> 1, skip_model_3d.py:132) would use 1/16 of each MFMA's
 // rows.  Here every thread owns 2 adjacent output voxels of a 8 x 64 plane tile
@@ -555,8 +644,10 @@ inline Plan make_plan(int B, int cout, int D, int H, int W, int k, bool resample
   p.mt = mt_for(cout);
   if (k == 1 && !resample) {
     p.engine = 1;
-    p.nt = p.mt == 1 ? 8 : 4;
-    p.tw = p.nt * 64;
+    p.nt = 4;
+    p.tw = 0;
+    const long long vox = (long long)D * H * W;
+    if ((vox + kConvWaves * 64 - 1) / (kConvWaves * 64) * B < 512) p.nt = 2;
     return p;
   }
   if (k == 3 && cout <= 2 && !resample) {
@@ -603,6 +694,22 @@ int run_rs(const ConvArgs& a, int tw, int B, hipStream_t st) {
   return launch(conv3d_reg_kernel<KS, MT, NT, 32, true>, a, LEA_TILE_TH(KS, MT, NT, 32), 32, B, st);
 }
 
+template <int MT, int NT>
+int launch_1x1(const ConvArgs& a, int B, hipStream_t st) {
+  const long long vox = (long long)a.D * a.H * a.W;
+  const long long per = kConvWaves * NT * 16;
+  const long long gx = (vox + per - 1) / per;
+  LEA_CHECK_ARG(gx < (1LL << 31) && (long long)B * a.ncob <= 65535, "lea_conv3d: grid too large");
+  conv1x1_kernel<MT, NT><<<dim3((unsigned)gx, B * a.ncob), kConvThreads, 0, st>>>(a);
+  return launch_status("lea_conv3d");
+}
+
+int run_1x1(const Plan& p, const ConvArgs& a, int B, hipStream_t st) {
+  if (p.mt == 1) return p.nt == 4 ? launch_1x1<1, 4>(a, B, st) : launch_1x1<1, 2>(a, B, st);
+  if (p.mt == 2) return p.nt == 4 ? launch_1x1<2, 4>(a, B, st) : launch_1x1<2, 2>(a, B, st);
+  return p.nt == 4 ? launch_1x1<4, 4>(a, B, st) : launch_1x1<4, 2>(a, B, st);
+}
+
 int run_plan(const Plan& p, ConvArgs a, int B, int k, hipStream_t st) {
   a.ncob = (a.cout + p.mt * 16 - 1) / (p.mt * 16);
   if (p.engine == 3) {
@@ -624,12 +731,8 @@ int run_plan(const Plan& p, ConvArgs a, int B, int k, hipStream_t st) {
     if (p.mt == 2) return run_rs<1, 2, 4>(a, p.tw, B, st);
     return run_rs<1, 4, 4>(a, p.tw, B, st);
   }
-  // 1x1x1 without resample: the volume is a flat run of D*H*W voxels (no halo)
-  a.W = a.D * a.H * a.W;
-  a.D = a.H = 1;
-  if (p.mt == 1) return launch(conv3d_reg_kernel<1, 1, 8, 512, false>, a, 1, 512, B, st);
-  if (p.mt == 2) return launch(conv3d_reg_kernel<1, 2, 4, 256, false>, a, 1, 256, B, st);
-  return launch(conv3d_reg_kernel<1, 4, 4, 256, false>, a, 1, 256, B, st);
+  // 1x1x1 without resample: streaming engine over the flat voxel run
+  return run_1x1(p, a, B, st);
 }
 
 thread_local char g_name[96];
@@ -642,7 +745,7 @@ const char* plan_name(const Plan& p, int k) {
   else if (p.engine == 2)
     snprintf(g_name, sizeof(g_name), "conv3d_reg_kernel<%d, %d, %d, %d, true>", k, p.mt, p.nt, p.tw);
   else
-    snprintf(g_name, sizeof(g_name), "conv3d_reg_kernel<1, %d, %d, %d, false>", p.mt, p.nt, p.tw);
+    snprintf(g_name, sizeof(g_name), "conv1x1_kernel<%d, %d>", p.mt, p.nt);
   return g_name;
 }
 
