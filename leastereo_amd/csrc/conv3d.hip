@@ -610,7 +610,14 @@ __global__ void pack_weights_kernel(const float* __restrict__ w, float* __restri
   }
 }
 
-inline int mt_for(int cout) { return cout <= 16 ? 1 : (cout <= 32 ? 2 : 4); }
+// Rows (x16) of the output-channel block a workgroup owns: the smallest of
+// 16/32/48 that holds cout, else the 48- or 64-row blocking with less padding.
+inline int mt_for(int cout) {
+  if (cout <= 16) return 1;
+  if (cout <= 32) return 2;
+  if (cout <= 48) return 3;
+  return ((cout + 47) / 48) * 48 < ((cout + 63) / 64) * 64 ? 3 : 4;
+}
 
 template <int KS, int MT>
 size_t packed_floats_t(int cout, int cin) {
@@ -622,9 +629,11 @@ size_t packed_floats(int cout, int cin, int k) {
   const int mt = mt_for(cout);
   if (k == 3)
     return mt == 1 ? packed_floats_t<3, 1>(cout, cin)
-                   : mt == 2 ? packed_floats_t<3, 2>(cout, cin) : packed_floats_t<3, 4>(cout, cin);
+           : mt == 2 ? packed_floats_t<3, 2>(cout, cin)
+           : mt == 3 ? packed_floats_t<3, 3>(cout, cin) : packed_floats_t<3, 4>(cout, cin);
   return mt == 1 ? packed_floats_t<1, 1>(cout, cin)
-                 : mt == 2 ? packed_floats_t<1, 2>(cout, cin) : packed_floats_t<1, 4>(cout, cin);
+         : mt == 2 ? packed_floats_t<1, 2>(cout, cin)
+         : mt == 3 ? packed_floats_t<1, 3>(cout, cin) : packed_floats_t<1, 4>(cout, cin);
 }
 
 // ------------------------------------------------------------------------- dispatch
@@ -707,6 +716,7 @@ int launch_1x1(const ConvArgs& a, int B, hipStream_t st) {
 int run_1x1(const Plan& p, const ConvArgs& a, int B, hipStream_t st) {
   if (p.mt == 1) return p.nt == 4 ? launch_1x1<1, 4>(a, B, st) : launch_1x1<1, 2>(a, B, st);
   if (p.mt == 2) return p.nt == 4 ? launch_1x1<2, 4>(a, B, st) : launch_1x1<2, 2>(a, B, st);
+  if (p.mt == 3) return p.nt == 4 ? launch_1x1<3, 4>(a, B, st) : launch_1x1<3, 2>(a, B, st);
   return p.nt == 4 ? launch_1x1<4, 4>(a, B, st) : launch_1x1<4, 2>(a, B, st);
 }
 
@@ -719,16 +729,19 @@ int run_plan(const Plan& p, ConvArgs a, int B, int k, hipStream_t st) {
   if (p.engine == 0) {
     if (p.mt == 1) return p.nt == 8 ? run_dma<1, 8>(a, p.tw, B, st) : run_dma<1, 4>(a, p.tw, B, st);
     if (p.mt == 2) return p.nt == 4 ? run_dma<2, 4>(a, p.tw, B, st) : run_dma<2, 2>(a, p.tw, B, st);
+    if (p.mt == 3) return p.nt == 4 ? run_dma<3, 4>(a, p.tw, B, st) : run_dma<3, 2>(a, p.tw, B, st);
     return p.nt == 4 ? run_dma<4, 4>(a, p.tw, B, st) : run_dma<4, 2>(a, p.tw, B, st);
   }
   if (p.engine == 2) {
     if (k == 3) {
       if (p.mt == 1) return run_rs<3, 1, 8>(a, p.tw, B, st);
       if (p.mt == 2) return run_rs<3, 2, 4>(a, p.tw, B, st);
+      if (p.mt == 3) return run_rs<3, 3, 4>(a, p.tw, B, st);
       return run_rs<3, 4, 4>(a, p.tw, B, st);
     }
     if (p.mt == 1) return run_rs<1, 1, 8>(a, p.tw, B, st);
     if (p.mt == 2) return run_rs<1, 2, 4>(a, p.tw, B, st);
+    if (p.mt == 3) return run_rs<1, 3, 4>(a, p.tw, B, st);
     return run_rs<1, 4, 4>(a, p.tw, B, st);
   }
   // 1x1x1 without resample: streaming engine over the flat voxel run
@@ -804,9 +817,9 @@ extern "C" int lea_conv3d_pack_weights(const float* w, float* packed, int cout, 
 #define LEA_PACK(KS, MT) \
   pack_weights_kernel<KS, MT><<<grid, threads, 0, st>>>(w, packed, cout, cin, nchunks, total)
   if (k == 3) {
-    if (mt == 1) LEA_PACK(3, 1); else if (mt == 2) LEA_PACK(3, 2); else LEA_PACK(3, 4);
+    if (mt == 1) LEA_PACK(3, 1); else if (mt == 2) LEA_PACK(3, 2); else if (mt == 3) LEA_PACK(3, 3); else LEA_PACK(3, 4);
   } else {
-    if (mt == 1) LEA_PACK(1, 1); else if (mt == 2) LEA_PACK(1, 2); else LEA_PACK(1, 4);
+    if (mt == 1) LEA_PACK(1, 1); else if (mt == 2) LEA_PACK(1, 2); else if (mt == 3) LEA_PACK(1, 3); else LEA_PACK(1, 4);
   }
 #undef LEA_PACK
   return launch_status("lea_conv3d_pack_weights");

@@ -72,7 +72,8 @@ extern "C" int lea_build_cost_volume(const void* left, const void* right, void* 
   const bool vec = (W % 4) == 0;
   const int per_plane = H * (vec ? W / 4 : W);
   const int threads = 256;
-  const int gx = (per_plane + threads - 1) / threads;
+  // ~4 cells per thread (grid stride inside the plane): fewer, fatter workgroups
+  const int gx = (per_plane + threads * 4 - 1) / (threads * 4);
   dim3 grid(gx, planes < 65535 ? planes : 65535);
   if (vec)
     cost_volume_f32<true><<<grid, threads, 0, as_stream(stream)>>>(

@@ -10,13 +10,16 @@
 // conv then runs at the *input* resolution (8x fewer voxels for x2 up-sampling)
 // and only its narrow output is resampled -- straight into the cell's cat slot.
 //
-// One thread per output voxel along W (coalesced stores); the d and h source
-// rows are uniform per workgroup, the 8 taps come from two row pairs that
-// neighbouring threads share through L1/L2.  Streaming: bound by the output write.
+// Mapping: grid.y = output plane (b, c, od) -- its depth weights are uniform;
+// threads walk the plane's (oh, 4-wide ow quad) cells with a grid stride, so a
+// workgroup writes several KB (the first version launched one 256-thread group
+// per half row and was dispatch-bound at ~0.55 TB/s).  Output is stored as one
+// 16-byte vector per quad when Wo % 4 == 0.  Bound by the output write.
 #include "common.h"
 
 namespace lea {
 
+template <bool VEC>
 __global__ __launch_bounds__(256) void resample3d_f32(const float* __restrict__ x, long long xbs,
                                                       float* __restrict__ y, long long ybs, int C,
                                                       int Di, int Hi, int Wi, int Do, int Ho, int Wo,
@@ -25,25 +28,43 @@ __global__ __launch_bounds__(256) void resample3d_f32(const float* __restrict__ 
                                                       const float* __restrict__ shift,
                                                       unsigned flags) {
 #pragma clang fp contract(off)
-  const int ow = blockIdx.x * blockDim.x + threadIdx.x;
-  if (ow >= Wo) return;
-  const int oh = blockIdx.y % Ho;
-  const int od = blockIdx.y / Ho;
-  const int bc = blockIdx.z;  // b * C + c
+  const int plane = blockIdx.y;  // (b * C + c) * Do + od
+  const int od = plane % Do;
+  const int bc = plane / Do;
   const int b = bc / C, c = bc - b * C;
   const Axis ad = axis_index(rd, od, Di, Do, ac);
-  const Axis ah = axis_index(rh, oh, Hi, Ho, ac);
-  const Axis aw = axis_index(rw, ow, Wi, Wo, ac);
   const long long HWi = (long long)Hi * Wi;
   const float* xc = x + (long long)b * xbs + (long long)c * Di * HWi;
-  const float* p00 = xc + ad.i0 * HWi + (long long)ah.i0 * Wi;
-  const float* p01 = xc + ad.i0 * HWi + (long long)ah.i1 * Wi;
-  const float* p10 = xc + ad.i1 * HWi + (long long)ah.i0 * Wi;
-  const float* p11 = xc + ad.i1 * HWi + (long long)ah.i1 * Wi;
-  float v = trilerp(ad, ah, aw, p00, p01, p10, p11);
-  if (scale) v = v * scale[c] + shift[c];
-  if (flags & LEA_RELU) v = fmaxf(v, 0.f);
-  y[(long long)b * ybs + (long long)c * Do * Ho * Wo + ((long long)od * Ho + oh) * Wo + ow] = v;
+  const float* q0 = xc + ad.i0 * HWi;
+  const float* q1 = xc + ad.i1 * HWi;
+  float* yp = y + (long long)b * ybs + ((long long)c * Do + od) * Ho * Wo;
+  const float sc = scale ? scale[c] : 1.f;
+  const float sh = scale ? shift[c] : 0.f;
+  const bool relu = flags & LEA_RELU;
+  const int wq = VEC ? Wo / 4 : Wo;
+  const int cells = Ho * wq;
+  for (int t = blockIdx.x * blockDim.x + threadIdx.x; t < cells; t += gridDim.x * blockDim.x) {
+    const int oh = t / wq;
+    const int q = t - oh * wq;
+    const Axis ah = axis_index(rh, oh, Hi, Ho, ac);
+    const float* p00 = q0 + (long long)ah.i0 * Wi;
+    const float* p01 = q0 + (long long)ah.i1 * Wi;
+    const float* p10 = q1 + (long long)ah.i0 * Wi;
+    const float* p11 = q1 + (long long)ah.i1 * Wi;
+    float v[VEC ? 4 : 1];
+#pragma unroll
+    for (int e = 0; e < (VEC ? 4 : 1); ++e) {
+      const Axis aw = axis_index(rw, (VEC ? 4 * q : q) + e, Wi, Wo, ac);
+      float r = trilerp(ad, ah, aw, p00, p01, p10, p11);
+      if (scale) r = r * sc + sh;
+      if (relu) r = fmaxf(r, 0.f);
+      v[e] = r;
+    }
+    if constexpr (VEC)
+      *reinterpret_cast<float4*>(yp + (long long)oh * Wo + 4 * q) = make_float4(v[0], v[1], v[2], v[3]);
+    else
+      yp[(long long)oh * Wo + q] = v[0];
+  }
 }
 
 }  // namespace lea
@@ -59,18 +80,28 @@ extern "C" int lea_resample3d_trilinear(const void* x, int64_t x_bstride, void* 
                 "lea_resample3d_trilinear: scale/shift must both be set or both NULL");
   LEA_CHECK_ARG(B > 0 && C > 0 && Di > 0 && Hi > 0 && Wi > 0 && Do > 0 && Ho > 0 && Wo > 0,
                 "lea_resample3d_trilinear: bad shape");
-  LEA_CHECK_ARG((long long)Do * Ho <= 65535 && (long long)B * C <= 65535,
-                "lea_resample3d_trilinear: grid too large (Do*Ho=%d, B*C=%d)", Do * Ho, B * C);
+  LEA_CHECK_ARG((long long)B * C * Do <= 65535 && (long long)Ho * Wo < (1LL << 31),
+                "lea_resample3d_trilinear: grid too large (B*C*Do=%lld)", (long long)B * C * Do);
   if (dtype != LEA_F32) {
     set_error("lea_resample3d_trilinear: dtype %d unsupported", dtype);
     return LEA_E_UNSUPPORTED;
   }
+  // 16-byte stores need Wo % 4 == 0 and a 16-byte aligned output (y and its batch stride)
+  const bool vec = (Wo % 4) == 0 && ((uintptr_t)y % 16) == 0 && (y_bstride % 4) == 0;
   const int ac = align_corners ? 1 : 0;
-  dim3 block(Wo >= 256 ? 256 : ((Wo + 63) / 64) * 64);
-  dim3 grid((Wo + block.x - 1) / block.x, Do * Ho, B * C);
-  resample3d_f32<<<grid, block, 0, as_stream(stream)>>>(
-      (const float*)x, x_bstride, (float*)y, y_bstride, C, Di, Hi, Wi, Do, Ho, Wo,
-      axis_ratio(Di, Do, ac), axis_ratio(Hi, Ho, ac), axis_ratio(Wi, Wo, ac), ac, scale, shift,
-      flags);
+  const long long cells = (long long)Ho * (vec ? Wo / 4 : Wo);
+  const int threads = 256;
+  // ~8 cells per thread: a workgroup covers 2048 cells (8 KB written with quads)
+  const int gx = (int)((cells + threads * 8 - 1) / (threads * 8));
+  dim3 grid(gx, B * C * Do);
+  const float rd = axis_ratio(Di, Do, ac), rh = axis_ratio(Hi, Ho, ac), rw = axis_ratio(Wi, Wo, ac);
+  if (vec)
+    resample3d_f32<true><<<grid, threads, 0, as_stream(stream)>>>(
+        (const float*)x, x_bstride, (float*)y, y_bstride, C, Di, Hi, Wi, Do, Ho, Wo, rd, rh, rw, ac,
+        scale, shift, flags);
+  else
+    resample3d_f32<false><<<grid, threads, 0, as_stream(stream)>>>(
+        (const float*)x, x_bstride, (float*)y, y_bstride, C, Di, Hi, Wi, Do, Ho, Wo, rd, rh, rw, ac,
+        scale, shift, flags);
   return launch_status("lea_resample3d_trilinear");
 }

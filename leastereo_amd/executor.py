@@ -46,6 +46,31 @@ class MatchingExecutor:
                     scale, shift = mod.folded_bn()
                     self.p[name] = ConvParams(kernels.pack_conv_weight(w), scale, shift,
                                               w.shape[1], w.shape[0], w.shape[-1], mod.relu)
+            # Sibling ops: the DAG ops that read s1 (one per step here: ops 1, 2, 4 of
+            # the searched genotype) write consecutive cat slots, so they run as ONE
+            # conv with cout = n*C over channels [.., ..) of the cell output (their
+            # weights and folded BN stacked along cout).  The remaining ops accumulate.
+            self.s1_group = {}
+            for i, cell in enumerate(matching.cells):
+                group = []
+                for k, terms in enumerate(cell.plan):
+                    for op, j in terms:
+                        if j == 1 and cell.op_kinds[op] == "conv":
+                            group.append((k, op))
+                            break
+                first_cat_state = 2 + cell.steps - cell.block_multiplier
+                steps = [k for k, _ in group]
+                if (len(group) < 2 or steps != list(range(steps[0], steps[0] + len(steps)))
+                        or 2 + steps[0] < first_cat_state):
+                    continue
+                mods = [cell._ops[op] for _, op in group]
+                w = torch.cat([m.conv.weight for m in mods], 0)
+                folded = [m.folded_bn() for m in mods]
+                scale = torch.cat([f[0] for f in folded]).contiguous()
+                shift = torch.cat([f[1] for f in folded]).contiguous()
+                self.p[f"cells.{i}.s1_group"] = ConvParams(kernels.pack_conv_weight(w), scale, shift,
+                                                           w.shape[1], w.shape[0], 3, True)
+                self.s1_group[i] = group
 
     def conv(self, name, x, out=None, accumulate=False, x2=None, size=None):
         """ConvBR3d ``name`` on x (or cat(x, x2)); with ``size`` != x's volume the
@@ -94,17 +119,27 @@ class MatchingExecutor:
                 slot[0].copy_(s0)
         s1 = self.conv(f"cells.{i}.preprocess", s1, out=slot.get(1), size=size)
         states = [s0, s1]
-        for terms in cell.plan:
+        group = self.s1_group.get(i, [])
+        written = set()
+        if group:  # ops on s1 of every step, one launch, straight into their slots
+            k0 = 2 + group[0][0] - (n_states - bm)
+            self.conv(f"cells.{i}.s1_group", s1, out=out[:, k0 * c:(k0 + len(group)) * c])
+            written = {k for k, _ in group}
+        done = set(group)
+        for step, terms in enumerate(cell.plan):
             dst = slot.get(len(states))
             if dst is None:
                 dst = torch.empty((b, c, d, h, w), device=s1.device, dtype=s1.dtype)
-            for n, (k, j) in enumerate(terms):
+            for k, j in terms:
+                if (step, k) in done:
+                    continue
                 if cell.op_kinds[k] == "conv":
-                    self.conv(f"cells.{i}._ops.{k}", states[j], out=dst, accumulate=n > 0)
-                elif n == 0:
-                    dst.copy_(states[j])
-                else:
+                    self.conv(f"cells.{i}._ops.{k}", states[j], out=dst, accumulate=step in written)
+                elif step in written:
                     dst.add_(states[j])
+                else:
+                    dst.copy_(states[j])
+                written.add(step)
             states.append(dst)
         return prev_input, out
 

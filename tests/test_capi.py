@@ -69,7 +69,10 @@ def test_invalid_arguments_are_rejected_before_launch():
 def test_packed_sizes(cout, cin, k):
     n = _lib.load().lea_conv3d_packed_floats(cout, cin, k)
     cin_b = 4 if k == 3 else 32
-    mt = 1 if cout <= 16 else (2 if cout <= 32 else 4)
+    if cout <= 48:
+        mt = -(-cout // 16)
+    else:
+        mt = 3 if -(-cout // 48) * 48 < -(-cout // 64) * 64 else 4
     cops = mt * 16 + (16 if (mt * 16) % 32 == 0 else 0)
     assert n == -(-cout // (mt * 16)) * -(-cin // cin_b) * k ** 3 * cin_b * cops
     assert _lib.load().lea_conv3d_packed_floats(16, 8, 5) == 0

@@ -21,11 +21,14 @@ LAYERS = {
     "stem0_64to32_k3_L0": (64, 32, 3, L0, 1),
     "stem1_32to32_k3_L0": (32, 32, 3, L0, 1),
     "conv12_128to64_k3_L1": (128, 64, 3, L1, 2),
-    "cell_16to16_k3_L1": (16, 16, 3, L1, 36),
-    "cell_32to32_k3_L2": (32, 32, 3, L2, 30),
-    "cell_8to8_k3_L0": (8, 8, 3, L0, 6),
+    "cell_16to48_k3_L1_s1grp": (16, 48, 3, L1, 6),
+    "cell_16to16_k3_L1": (16, 16, 3, L1, 18),
+    "cell_32to96_k3_L2_s1grp": (32, 96, 3, L2, 5),
+    "cell_32to32_k3_L2": (32, 32, 3, L2, 15),
+    "cell_8to24_k3_L0_s1grp": (8, 24, 3, L0, 1),
+    "cell_8to8_k3_L0": (8, 8, 3, L0, 3),
     "last3_32to1_k3_L0": (32, 1, 3, L0, 1),
-    "pre_64to8_k1_L0": (64, 8, 1, L0, 2),
+    "pre_64to8_k1_L1": (64, 8, 1, L1, 2),
     "pre_32to16_k1_L1": (32, 16, 1, L1, 6),
     "pre_128to32_k1_L2": (128, 32, 1, L2, 8),
 }
@@ -64,7 +67,7 @@ def main():
         nbytes = 4.0 * vox * (cin + cout)
         res[name] = {"ms": ms, "tflops": flops / ms / 1e9, "gbs": nbytes / ms / 1e6,
                      "per_forward_ms": ms * count,
-                     "kernel": kernels.conv_kernel_name(cout, cin, d, h, w, k)}
+                     "kernel": kernels.conv_kernel_name(1, cout, d, h, w, k)}
         print(f"{name:24s} {ms * 1e3:9.1f} us  {flops / ms / 1e9:7.1f} TFLOP/s  "
               f"{nbytes / ms / 1e6:8.1f} GB/s  x{count:2d} = {ms * count:6.3f} ms/fwd  "
               f"{res[name]['kernel']}", flush=True)
