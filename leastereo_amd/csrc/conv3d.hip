@@ -79,11 +79,21 @@ struct PackCfg {
   static constexpr int KT = KS * KS * KS;
   static constexpr int CIN_B = (KS == 3) ? 4 : 32;
   static constexpr int COP = MT * 16;
-  static constexpr int COPS = cout_stride(COP);
+  static constexpr int COPS = COP;  // row stride of a staged weight row (floats)
+  // Rows 32 or 64 wide (stride = 0 mod 32 banks): odd input-channel rows are
+  // stored with 16-column halves swapped, so the two k-rows of a half-wave read
+  // disjoint banks without padding (16- and 48-wide rows are already 16 mod 32).
+  static constexpr bool SWZ = (COP % 32) == 0;
   static constexpr int CHUNK = KT * CIN_B * COPS;  // floats per K chunk
 };
 
-template <int KS, int MT, int NT, int TW>
+// Column of this lane's A element of m-tile m inside a staged weight row.
+template <int KS, int MT>
+__device__ __forceinline__ int a_col(int m, int kq, int n) {
+  return ((PackCfg<KS, MT>::SWZ ? (m ^ (kq & 1)) : m) * 16) + n;
+}
+
+template <int KS, int MT, int NT, int TW, int TD = 1>
 struct TileCfg : PackCfg<KS, MT> {
   using P = PackCfg<KS, MT>;
   static constexpr int PAD = KS / 2;
@@ -94,7 +104,8 @@ struct TileCfg : PackCfg<KS, MT> {
   static constexpr int RH = TH + KS - 1;
   static constexpr int RW = TW + KS - 1;
   static constexpr int PLANE = RH * RW;
-  static constexpr int IMG = KS * PLANE;           // staged floats per input channel
+  static constexpr int PLANES = KS + TD - 1;       // input planes feeding TD output planes
+  static constexpr int IMG = PLANES * PLANE;       // staged floats per input channel
   static constexpr int CIS = round_16mod32(IMG);   // LDS stride between input channels
   static constexpr int XS = P::CIN_B * CIS;
   static constexpr int WS = P::CHUNK;
@@ -104,10 +115,10 @@ struct TileCfg : PackCfg<KS, MT> {
 
 // ----------------------------------------------------------------- MFMA main loop
 // One K chunk from an LDS stage: KS^3 taps x CIN_B/4 k-steps x (MT x NT) MFMAs.
-template <int KS, int MT, int NT, int TW>
+template <int KS, int MT, int NT, int TW, int TD>
 __device__ __forceinline__ void mfma_chunk(const float* xs, const float* ws, const int (&xoff)[NT],
-                                           int woff, f32x4 (&acc)[MT][NT]) {
-  using C = TileCfg<KS, MT, NT, TW>;
+                                           const int (&woff)[MT], f32x4 (&acc)[TD][MT][NT]) {
+  using C = TileCfg<KS, MT, NT, TW, TD>;
   constexpr int CIN_B = C::CIN_B;
 #pragma unroll
   for (int s = 0; s < CIN_B / 4; ++s) {
@@ -118,17 +129,22 @@ __device__ __forceinline__ void mfma_chunk(const float* xs, const float* ws, con
 #pragma unroll
         for (int kw = 0; kw < KS; ++kw) {
           const int tap = (kd * KS + kh) * KS + kw;
-          float av[MT], bv[NT];
+          float av[MT], bv[TD][NT];
 #pragma unroll
-          for (int m = 0; m < MT; ++m) av[m] = ws[woff + (tap * CIN_B + 4 * s) * C::COPS + m * 16];
+          for (int m = 0; m < MT; ++m) av[m] = ws[woff[m] + (tap * CIN_B + 4 * s) * C::COPS];
 #pragma unroll
-          for (int j = 0; j < NT; ++j)
-            bv[j] = xs[xoff[j] + 4 * s * C::CIS + kd * C::PLANE + kh * C::RW + kw];
-#pragma unroll
-          for (int m = 0; m < MT; ++m)
+          for (int t = 0; t < TD; ++t)
 #pragma unroll
             for (int j = 0; j < NT; ++j)
-              acc[m][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[m], bv[j], acc[m][j], 0, 0, 0);
+              bv[t][j] = xs[xoff[j] + 4 * s * C::CIS + (t + kd) * C::PLANE + kh * C::RW + kw];
+#pragma unroll
+          for (int t = 0; t < TD; ++t)
+#pragma unroll
+            for (int m = 0; m < MT; ++m)
+#pragma unroll
+              for (int j = 0; j < NT; ++j)
+                acc[t][m][j] =
+                    __builtin_amdgcn_mfma_f32_16x16x4f32(av[m], bv[t][j], acc[t][m][j], 0, 0, 0);
         }
       }
     }
@@ -136,10 +152,10 @@ __device__ __forceinline__ void mfma_chunk(const float* xs, const float* ws, con
 }
 
 // Folded-BN affine, ReLU, residual, masked store of the MT x NT accumulator tiles.
-template <int KS, int MT, int NT, int TW>
-__device__ __forceinline__ void epilogue(const ConvArgs& a, const f32x4 (&acc)[MT][NT], int b,
+template <int KS, int MT, int NT, int TW, int TD>
+__device__ __forceinline__ void epilogue(const ConvArgs& a, const f32x4 (&acc)[TD][MT][NT], int b,
                                          int co0, int d0, int h0, int w0, int wave, int lane) {
-  using C = TileCfg<KS, MT, NT, TW>;
+  using C = TileCfg<KS, MT, NT, TW, TD>;
   const long long HW = (long long)a.H * a.W;
   const long long DHW = HW * a.D;
   const bool relu = a.flags & LEA_RELU;
@@ -154,25 +170,30 @@ __device__ __forceinline__ void epilogue(const ConvArgs& a, const f32x4 (&acc)[M
       const float sc = a.scale ? a.scale[co] : 1.f;
       const float sh = a.shift ? a.shift[co] : 0.f;
 #pragma unroll
-      for (int j = 0; j < NT; ++j) {
-        const int g = wave * NT + j;
-        const int h = h0 + g / C::TPR;
-        const int w = w0 + (g % C::TPR) * 16 + n;
-        if (h >= a.H || w >= a.W) continue;
-        const long long o = (long long)co * DHW + (long long)d0 * HW + (long long)h * a.W + w;
-        float v = acc[m][j][r] * sc + sh;
-        if (relu) v = fmaxf(v, 0.f);
-        if (resid) v += a.res[(long long)b * a.rbs + o];
-        a.y[(long long)b * a.ybs + o] = v;
+      for (int t = 0; t < TD; ++t) {
+        const int d = d0 + t;
+        if (d >= a.D) continue;
+#pragma unroll
+        for (int j = 0; j < NT; ++j) {
+          const int g = wave * NT + j;
+          const int h = h0 + g / C::TPR;
+          const int w = w0 + (g % C::TPR) * 16 + n;
+          if (h >= a.H || w >= a.W) continue;
+          const long long o = (long long)co * DHW + (long long)d * HW + (long long)h * a.W + w;
+          float v = acc[t][m][j][r] * sc + sh;
+          if (relu) v = fmaxf(v, 0.f);
+          if (resid) v += a.res[(long long)b * a.rbs + o];
+          a.y[(long long)b * a.ybs + o] = v;
+        }
       }
     }
   }
 }
 
 // ------------------------------------------------------------- LDS-DMA engine (k=3)
-template <int MT, int NT, int TW>
+template <int MT, int NT, int TW, int TD>
 __global__ __launch_bounds__(kConvThreads, 2) void conv3d_dma_kernel(const ConvArgs a) {
-  using C = TileCfg<3, MT, NT, TW>;
+  using C = TileCfg<3, MT, NT, TW, TD>;
   constexpr int XSLOTS = (C::IMG + 63) / 64;  // 256-B DMA pieces per channel image
   constexpr int XSLOTS_W = (XSLOTS + kConvWaves - 1) / kConvWaves;
   constexpr int WSLOTS = (C::WS + 255) / 256;  // 1-KB DMA pieces of the weight chunk
@@ -185,7 +206,7 @@ __global__ __launch_bounds__(kConvThreads, 2) void conv3d_dma_kernel(const ConvA
   const int tile = blockIdx.x;
   const int h0 = (tile / a.tiles_w) * C::TH;
   const int w0 = (tile % a.tiles_w) * TW;
-  const int d0 = blockIdx.y;
+  const int d0 = blockIdx.y * TD;
   const int b = blockIdx.z / a.ncob;
   const int co0 = (blockIdx.z - b * a.ncob) * C::COP;
   const int nchunks = (a.cin + C::CIN_B - 1) / C::CIN_B;
@@ -252,13 +273,17 @@ __global__ __launch_bounds__(kConvThreads, 2) void conv3d_dma_kernel(const ConvA
     const int g = wave * NT + j;
     xoff[j] = kq * C::CIS + (g / C::TPR) * C::RW + (g % C::TPR) * 16 + n;
   }
-  const int woff = kq * C::COPS + n;
+  int woff[MT];
+#pragma unroll
+  for (int m = 0; m < MT; ++m) woff[m] = kq * C::COPS + a_col<3, MT>(m, kq, n);
 
-  f32x4 acc[MT][NT];
+  f32x4 acc[TD][MT][NT];
 #pragma unroll
-  for (int m = 0; m < MT; ++m)
+  for (int t = 0; t < TD; ++t)
 #pragma unroll
-    for (int j = 0; j < NT; ++j) acc[m][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int m = 0; m < MT; ++m)
+#pragma unroll
+      for (int j = 0; j < NT; ++j) acc[t][m][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   issue(0, smem);
   for (int ch = 0; ch < nchunks; ++ch) {
@@ -266,9 +291,9 @@ __global__ __launch_bounds__(kConvThreads, 2) void conv3d_dma_kernel(const ConvA
     __syncthreads();  // ... and everyone's; everyone is done reading chunk ch-1's stage
     if (ch + 1 < nchunks) issue(ch + 1, smem + ((ch + 1) & 1) * C::STAGE);
     const float* xs = smem + (ch & 1) * C::STAGE;
-    mfma_chunk<3, MT, NT, TW>(xs, xs + C::XS, xoff, woff, acc);
+    mfma_chunk<3, MT, NT, TW, TD>(xs, xs + C::XS, xoff, woff, acc);
   }
-  epilogue<3, MT, NT, TW>(a, acc, b, co0, d0, h0, w0, wave, lane);
+  epilogue<3, MT, NT, TW, TD>(a, acc, b, co0, d0, h0, w0, wave, lane);
 }
 
 // ------------------------------------------------- register-staged engine (+ resample)
@@ -320,13 +345,15 @@ __global__ __launch_bounds__(kConvThreads, 2) void conv3d_reg_kernel(const ConvA
     const int g = wave * NT + j;
     xoff[j] = kq * C::CIS + (g / C::TPR) * C::RW + (g % C::TPR) * 16 + n;
   }
-  const int woff = kq * C::COPS + n;
+  int woff[MT];
+#pragma unroll
+  for (int m = 0; m < MT; ++m) woff[m] = kq * C::COPS + a_col<KS, MT>(m, kq, n);
 
-  f32x4 acc[MT][NT];
+  f32x4 acc[1][MT][NT];
 #pragma unroll
   for (int m = 0; m < MT; ++m)
 #pragma unroll
-    for (int j = 0; j < NT; ++j) acc[m][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < NT; ++j) acc[0][m][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   for (int ch = 0; ch < nchunks; ++ch) {
     const int c0 = ch * CIN_B;
@@ -368,9 +395,9 @@ __global__ __launch_bounds__(kConvThreads, 2) void conv3d_reg_kernel(const ConvA
       xs[ci * C::CIS + kd * C::PLANE + rr * C::RW + cc] = v;
     }
     __syncthreads();
-    mfma_chunk<KS, MT, NT, TW>(xs, ws, xoff, woff, acc);
+    mfma_chunk<KS, MT, NT, TW, 1>(xs, ws, xoff, woff, acc);
   }
-  epilogue<KS, MT, NT, TW>(a, acc, b, co0, d0, h0, w0, wave, lane);
+  epilogue<KS, MT, NT, TW, 1>(a, acc, b, co0, d0, h0, w0, wave, lane);
 }
 
 // ---------------------------------------------------------- 1x1x1 streaming engine
@@ -429,7 +456,7 @@ __global__ __launch_bounds__(kConvThreads) void conv1x1_kernel(const ConvArgs a)
     for (int s = 0; s < KS; ++s) {
       float av[MT];
 #pragma unroll
-      for (int m = 0; m < MT; ++m) av[m] = ws[(4 * s + kq) * P::COPS + m * 16 + n];
+      for (int m = 0; m < MT; ++m) av[m] = ws[(4 * s + kq) * P::COPS + a_col<1, MT>(m, kq, n)];
 #pragma unroll
       for (int m = 0; m < MT; ++m)
 #pragma unroll
@@ -588,7 +615,8 @@ __global__ __launch_bounds__(kConvThreads) void conv3d_valu_kernel(const ConvArg
 }
 
 // ------------------------------------------------------------------- weight packing
-// Packed layout: [ceil(cout/COP)][ceil(cin/CIN_B)][KS^3][CIN_B][COPS], zero outside (cin, cout).
+// Packed layout: [ceil(cout/COP)][ceil(cin/CIN_B)][KS^3][CIN_B][COP], zero outside (cin, cout);
+// rows of odd input channels swizzled (PackCfg::SWZ, a_col).
 template <int KS, int MT>
 __global__ void pack_weights_kernel(const float* __restrict__ w, float* __restrict__ packed,
                                     int cout, int cin, int nchunks, long long total) {
@@ -602,10 +630,10 @@ __global__ void pack_weights_kernel(const float* __restrict__ w, float* __restri
     const int tap = (int)(r % P::KT);
     r /= P::KT;
     const int ch = (int)(r % nchunks);
-    const int co = (int)(r / nchunks) * P::COP + col;
+    const int co = (int)(r / nchunks) * P::COP + ((P::SWZ && (cb & 1)) ? (col ^ 16) : col);
     const int ci = ch * P::CIN_B + cb;
     float v = 0.f;
-    if (col < P::COP && co < cout && ci < cin) v = w[((long long)co * cin + ci) * P::KT + tap];
+    if (co < cout && ci < cin) v = w[((long long)co * cin + ci) * P::KT + tap];
     packed[i] = v;
   }
 }
@@ -639,9 +667,23 @@ size_t packed_floats(int cout, int cin, int k) {
 // ------------------------------------------------------------------------- dispatch
 // A launch plan: which instantiation runs a given shape (also reported by name).
 struct Plan {
-  int engine;  // 0 = dma (k3), 1 = reg flat (k1), 2 = reg resample, 3 = valu (k3, cout <= 2)
-  int mt, nt, tw;
+  int engine;  // 0 = dma (k3), 1 = 1x1 streaming, 2 = reg resample, 3 = valu (k3, cout <= 2)
+  int mt, nt, tw, td;
 };
+
+// LDS bytes of a double-buffered DMA-engine workgroup (0 if not instantiated).
+inline int dma_lds_bytes(int mt, int nt, int tw, int td) {
+#define LEA_LDS(MT, NT, TW, TD) \
+  if (mt == MT && nt == NT && tw == TW && td == TD) return 2 * TileCfg<3, MT, NT, TW, TD>::STAGE * 4;
+#define LEA_LDS_TW(MT, NT, TD) LEA_LDS(MT, NT, 32, TD) LEA_LDS(MT, NT, 64, TD)
+#define LEA_LDS_TD(MT, NT) LEA_LDS_TW(MT, NT, 1) LEA_LDS_TW(MT, NT, 2)
+  LEA_LDS_TD(1, 8) LEA_LDS_TD(1, 4) LEA_LDS_TD(2, 4) LEA_LDS_TD(2, 2) LEA_LDS_TD(3, 4)
+  LEA_LDS_TD(3, 2) LEA_LDS_TD(4, 4) LEA_LDS_TD(4, 2)
+#undef LEA_LDS_TD
+#undef LEA_LDS_TW
+#undef LEA_LDS
+  return 0;
+}
 
 inline bool prefer_tw64(int W) {
   const int w64 = (W + 63) / 64 * 64, w32 = (W + 31) / 32 * 32;
@@ -650,6 +692,7 @@ inline bool prefer_tw64(int W) {
 
 inline Plan make_plan(int B, int cout, int D, int H, int W, int k, bool resample) {
   Plan p;
+  p.td = 1;
   p.mt = mt_for(cout);
   if (k == 1 && !resample) {
     p.engine = 1;
@@ -667,34 +710,54 @@ inline Plan make_plan(int B, int cout, int D, int H, int W, int k, bool resample
   }
   p.engine = resample ? 2 : 0;
   p.tw = prefer_tw64(W) ? 64 : 32;
-  p.nt = p.mt == 1 ? 8 : 4;
-  if (!resample) {  // small volumes: halve the tile so the grid still fills 256 CUs twice
-    const int th = kConvWaves * p.nt * 16 / p.tw;
-    const long long wgs = (long long)((W + p.tw - 1) / p.tw) * ((H + th - 1) / th) * D * B *
-                          ((cout + p.mt * 16 - 1) / (p.mt * 16));
-    if (wgs < 512) p.nt /= 2;
+  p.td = 1;
+  const int nt_full = p.mt == 1 ? 8 : 4;
+  p.nt = nt_full;
+  if (resample) return p;
+  const long long ncob = (cout + p.mt * 16 - 1) / (p.mt * 16);
+  auto wgs = [&](int nt, int td) {
+    const int th = kConvWaves * nt * 16 / p.tw;
+    return (long long)((W + p.tw - 1) / p.tw) * ((H + th - 1) / th) * ((D + td - 1) / td) * B * ncob;
+  };
+  // Preference: two output planes per workgroup (TD=2: 4 staged planes feed 2 outputs)
+  // while two workgroups still fit a CU's LDS and the grid keeps >= 4 per CU; else one
+  // plane, halving the tile when the grid would not fill 256 CUs twice.
+  const int cand[2] = {nt_full, nt_full / 2};
+  for (int nt : cand) {
+    if (dma_lds_bytes(p.mt, nt, p.tw, 2) <= 81920 && wgs(nt, 2) >= 1024) {
+      p.nt = nt;
+      p.td = 2;
+      return p;
+    }
   }
+  if (wgs(nt_full, 1) < 512) p.nt = nt_full / 2;
   return p;
 }
 
 template <typename K>
-int launch(K kernel, const ConvArgs& a0, int th, int tw, int B, hipStream_t st) {
+int launch(K kernel, const ConvArgs& a0, int th, int tw, int B, hipStream_t st, int td = 1) {
   ConvArgs a = a0;
   const long long nt = (long long)((a.W + tw - 1) / tw) * ((a.H + th - 1) / th);
   LEA_CHECK_ARG(nt < (1LL << 31) && a.D <= 65535 && (long long)B * a.ncob <= 65535,
                 "lea_conv3d: grid too large");
   a.tiles_w = (a.W + tw - 1) / tw;
-  dim3 grid((unsigned)nt, a.D, B * a.ncob);
+  dim3 grid((unsigned)nt, (a.D + td - 1) / td, B * a.ncob);
   kernel<<<grid, kConvThreads, 0, st>>>(a);
   return launch_status("lea_conv3d");
 }
 
 #define LEA_TILE_TH(KS, MT, NT, TW) (TileCfg<KS, MT, NT, TW>::TH)
 
+template <int MT, int NT, int TD>
+int run_dma_td(const ConvArgs& a, int tw, int B, hipStream_t st) {
+  if (tw == 64)
+    return launch(conv3d_dma_kernel<MT, NT, 64, TD>, a, LEA_TILE_TH(3, MT, NT, 64), 64, B, st, TD);
+  return launch(conv3d_dma_kernel<MT, NT, 32, TD>, a, LEA_TILE_TH(3, MT, NT, 32), 32, B, st, TD);
+}
+
 template <int MT, int NT>
-int run_dma(const ConvArgs& a, int tw, int B, hipStream_t st) {
-  if (tw == 64) return launch(conv3d_dma_kernel<MT, NT, 64>, a, LEA_TILE_TH(3, MT, NT, 64), 64, B, st);
-  return launch(conv3d_dma_kernel<MT, NT, 32>, a, LEA_TILE_TH(3, MT, NT, 32), 32, B, st);
+int run_dma(const ConvArgs& a, int tw, int td, int B, hipStream_t st) {
+  return td == 2 ? run_dma_td<MT, NT, 2>(a, tw, B, st) : run_dma_td<MT, NT, 1>(a, tw, B, st);
 }
 
 template <int KS, int MT, int NT>
@@ -727,10 +790,11 @@ int run_plan(const Plan& p, ConvArgs a, int B, int k, hipStream_t st) {
     return launch(conv3d_valu_kernel<2>, a, 8, 64, B, st);
   }
   if (p.engine == 0) {
-    if (p.mt == 1) return p.nt == 8 ? run_dma<1, 8>(a, p.tw, B, st) : run_dma<1, 4>(a, p.tw, B, st);
-    if (p.mt == 2) return p.nt == 4 ? run_dma<2, 4>(a, p.tw, B, st) : run_dma<2, 2>(a, p.tw, B, st);
-    if (p.mt == 3) return p.nt == 4 ? run_dma<3, 4>(a, p.tw, B, st) : run_dma<3, 2>(a, p.tw, B, st);
-    return p.nt == 4 ? run_dma<4, 4>(a, p.tw, B, st) : run_dma<4, 2>(a, p.tw, B, st);
+    const int tw = p.tw, td = p.td;
+    if (p.mt == 1) return p.nt == 8 ? run_dma<1, 8>(a, tw, td, B, st) : run_dma<1, 4>(a, tw, td, B, st);
+    if (p.mt == 2) return p.nt == 4 ? run_dma<2, 4>(a, tw, td, B, st) : run_dma<2, 2>(a, tw, td, B, st);
+    if (p.mt == 3) return p.nt == 4 ? run_dma<3, 4>(a, tw, td, B, st) : run_dma<3, 2>(a, tw, td, B, st);
+    return p.nt == 4 ? run_dma<4, 4>(a, tw, td, B, st) : run_dma<4, 2>(a, tw, td, B, st);
   }
   if (p.engine == 2) {
     if (k == 3) {
@@ -754,7 +818,7 @@ const char* plan_name(const Plan& p, int k) {
   if (p.engine == 3)
     snprintf(g_name, sizeof(g_name), "conv3d_valu_kernel<%d>", p.mt == 1 ? 1 : 2);
   else if (p.engine == 0)
-    snprintf(g_name, sizeof(g_name), "conv3d_dma_kernel<%d, %d, %d>", p.mt, p.nt, p.tw);
+    snprintf(g_name, sizeof(g_name), "conv3d_dma_kernel<%d, %d, %d, %d>", p.mt, p.nt, p.tw, p.td);
   else if (p.engine == 2)
     snprintf(g_name, sizeof(g_name), "conv3d_reg_kernel<%d, %d, %d, %d, true>", k, p.mt, p.nt, p.tw);
   else

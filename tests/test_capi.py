@@ -52,7 +52,7 @@ def test_invalid_arguments_are_rejected_before_launch():
     assert lib.lea_conv3d_bnrelu_resampled(x, 0, 0, 1, 1, x, None, None, None, 0, y, 0,
                                            1, 1, 1, 1, 1, 1, 1, 1, 0, None) == 1001
     assert b"input volume" in lib.lea_last_error()
-    assert lib.lea_conv3d_kernel_name(1, 32, 64, 192, 320, 3, 0) == b"conv3d_dma_kernel<2, 4, 64>"
+    assert lib.lea_conv3d_kernel_name(1, 32, 64, 192, 320, 3, 0) == b"conv3d_dma_kernel<2, 4, 64, 2>"
     assert lib.lea_conv3d_kernel_name(1, 8, 64, 192, 320, 1, 1).startswith(b"conv3d_reg_kernel<1, 1")
     assert lib.lea_conv3d_kernel_name(1, 8, 32, 96, 160, 1, 0) == b"conv1x1_kernel<1, 4>"
     # unsupported dtype is reported as such
@@ -73,6 +73,6 @@ def test_packed_sizes(cout, cin, k):
         mt = -(-cout // 16)
     else:
         mt = 3 if -(-cout // 48) * 48 < -(-cout // 64) * 64 else 4
-    cops = mt * 16 + (16 if (mt * 16) % 32 == 0 else 0)
+    cops = mt * 16  # no padding: 32/64-wide rows are XOR-swizzled instead
     assert n == -(-cout // (mt * 16)) * -(-cin // cin_b) * k ** 3 * cin_b * cops
     assert _lib.load().lea_conv3d_packed_floats(16, 8, 5) == 0

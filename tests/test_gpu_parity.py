@@ -112,6 +112,20 @@ def test_conv_random_vs_torch(b, cin, cout, k, shape):
     np.testing.assert_allclose(out.cpu().double().numpy(), refy.numpy(), rtol=1e-4, atol=1e-4)
 
 
+@pytest.mark.parametrize("cin,cout,shape", [(16, 16, (35, 96, 160)), (32, 48, (9, 100, 326))])
+def test_conv_two_plane_tiles_odd_depth(cin, cout, shape):
+    """Large volumes use 2 output planes per workgroup; odd D masks the last one."""
+    name = kernels.conv_kernel_name(1, cout, *shape, 3)
+    assert name.endswith(", 2>"), name
+    g = torch.Generator().manual_seed(cin + cout)
+    x = torch.randn((1, cin) + shape, generator=g)
+    w = torch.randn(cout, cin, 3, 3, 3, generator=g) / np.sqrt(cin * 27)
+    refy = F.conv3d(x.double(), w.double(), None, 1, 1)
+    y = kernels.conv3d_bnrelu(x.to(DEV), kernels.pack_conv_weight(w.to(DEV)), cout, 3, None, None,
+                              relu=False)
+    np.testing.assert_allclose(y.cpu().double().numpy(), refy.numpy(), rtol=1e-4, atol=1e-4)
+
+
 @pytest.mark.parametrize("c1,c2,cout,shape", [(64, 64, 64, (4, 10, 40)), (16, 12, 16, (3, 7, 33)),
                                               (4, 4, 8, (2, 3, 5))])
 def test_conv_two_sources_is_cat(c1, c2, cout, shape):
