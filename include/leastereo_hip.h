@@ -105,6 +105,18 @@ int lea_resample3d_trilinear(const void* x, int64_t x_bstride, void* y, int64_t 
                              int align_corners, const float* scale, const float* shift,
                              unsigned flags, int dtype, void* stream);
 
+/* Head conv of an upsampled tensor, from per-tap partial sums.  Replaces
+ * last_3(Upsample(y)) (skip_model_3d.py:161-173, 3x3x3 conv after a trilinear
+ * align_corners=True resize): with q[b][co*27 + tap] = sum_ci W[co][ci][tap]*y[ci]
+ * computed at the low resolution (lea_conv3d_bnrelu, k=1, 27*cout outputs),
+ *   y_out[b][co](v) = act(scale[co] * sum_tap interp(q[b][co*27+tap])(v + off(tap)) + shift[co])
+ * over the [Do, Ho, Wo] output, taps outside it contributing 0 (zero padding).
+ * q: [B, 27*cout, Di, Hi, Wi]; y_out: [B, cout, Do, Ho, Wo]. */
+int lea_tapsum_upsample(const void* q, int64_t q_bstride, void* y, int64_t y_bstride,
+                        int B, int cout, int Di, int Hi, int Wi, int Do, int Ho, int Wo,
+                        const float* scale, const float* shift, unsigned flags,
+                        int dtype, void* stream);
+
 /* Disparity regression.  Replaces models/build_model_2d.py:52-57 + :33-42:
  *   U = trilinear(cost, [maxdisp, 3*H3, 3*W3], align_corners=False)
  *   disp[b, h, w] = sum_d d * softmax(-U, dim=d)

@@ -37,6 +37,8 @@ SIGNATURES = {
     "lea_conv3d_kernel_name": (ctypes.c_char_p, [_i, _i, _i, _i, _i, _i, _i]),
     "lea_resample3d_trilinear": (_i, [_p, _i64, _p, _i64, _i, _i, _i, _i, _i, _i, _i, _i,
                                       _i, _p, _p, _u, _i, _p]),
+    "lea_tapsum_upsample": (_i, [_p, _i64, _p, _i64, _i, _i, _i, _i, _i, _i, _i, _i, _p, _p, _u,
+                                 _i, _p]),
     "lea_disparity_regression": (_i, [_p, _p, _i, _i, _i, _i, _i, _i, _p]),
 }
 

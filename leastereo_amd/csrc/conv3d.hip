@@ -720,11 +720,11 @@ inline Plan make_plan(int B, int cout, int D, int H, int W, int k, bool resample
     return (long long)((W + p.tw - 1) / p.tw) * ((H + th - 1) / th) * ((D + td - 1) / td) * B * ncob;
   };
   // Preference: two output planes per workgroup (TD=2: 4 staged planes feed 2 outputs)
-  // while two workgroups still fit a CU's LDS and the grid keeps >= 4 per CU; else one
+  // while two workgroups still fit a CU's LDS and the grid keeps >= 3 per CU; else one
   // plane, halving the tile when the grid would not fill 256 CUs twice.
   const int cand[2] = {nt_full, nt_full / 2};
   for (int nt : cand) {
-    if (dma_lds_bytes(p.mt, nt, p.tw, 2) <= 81920 && wgs(nt, 2) >= 1024) {
+    if (dma_lds_bytes(p.mt, nt, p.tw, 2) <= 81920 && wgs(nt, 2) >= 768) {
       p.nt = nt;
       p.td = 2;
       return p;

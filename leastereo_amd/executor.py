@@ -46,6 +46,13 @@ class MatchingExecutor:
                     scale, shift = mod.folded_bn()
                     self.p[name] = ConvParams(kernels.pack_conv_weight(w), scale, shift,
                                               w.shape[1], w.shape[0], w.shape[-1], mod.relu)
+            # Head: last_3(Upsample(y)) = sum over taps of upsampled per-tap partial
+            # sums (lea_tapsum_upsample); the taps run as a 1x1 conv with 27*cout outputs.
+            last3 = matching.last_3.conv.weight
+            co, ci = last3.shape[:2]
+            taps = last3.permute(0, 2, 3, 4, 1).reshape(co * 27, ci, 1, 1, 1)
+            self.p["last_3.taps"] = ConvParams(kernels.pack_conv_weight(taps), None, None,
+                                               ci, co * 27, 1, False)
             # Sibling ops: the DAG ops that read s1 (one per step here: ops 1, 2, 4 of
             # the searched genotype) write consecutive cat slots, so they run as ONE
             # conv with cout = n*C over channels [.., ..) of the cell output (their
@@ -165,7 +172,8 @@ class MatchingExecutor:
         lh = last.shape[3]
         full, half, quarter = (d, h, w), (d // 2, h // 2, w // 2), (d // 4, h // 4, w // 4)
         # head (:161-173): the 1x1 Upsample pairs run commuted (see conv()); the final
-        # Upsample is materialised once and read by the small-cout last_3 kernel
+        # Upsample + last_3 run as per-tap partial sums at the low resolution, then one
+        # 27-sample interpolating sum per output voxel (no full-resolution 32-ch tensor)
         if lh == h:
             return self.conv("last_3", last)
         if lh == h // 2:
@@ -177,4 +185,6 @@ class MatchingExecutor:
             y = self.conv("last_6", y, size=half)
         else:
             raise ValueError(f"matching-net output size {tuple(last.shape[2:])} has no head")
-        return self.conv("last_3", kernels.resample_trilinear(y, full, True))
+        p3 = self.p["last_3"]
+        q = self.conv("last_3.taps", y)
+        return kernels.tapsum_upsample(q, p3.cout, full, p3.scale, p3.shift, p3.relu)

@@ -221,6 +221,25 @@ def resample_trilinear(x: torch.Tensor, size, align_corners: bool = True,
     return out
 
 
+def tapsum_upsample(q: torch.Tensor, cout: int, size, scale: torch.Tensor | None = None,
+                    shift: torch.Tensor | None = None, relu: bool = False) -> torch.Tensor:
+    """conv3x3x3(upsample(y)) from q = per-tap partial sums of y (27*cout channels at
+    the low resolution): see include/leastereo_hip.h lea_tapsum_upsample."""
+    _require_cuda(q, scale, shift)
+    b, c27, di, hi, wi = q.shape
+    if c27 != 27 * cout:
+        raise ValueError(f"q has {c27} channels, expected 27*{cout}")
+    qbs = _check_volume_view(q, "q")
+    do, ho, wo = (int(s) for s in size)
+    out = torch.empty((b, cout, do, ho, wo), device=q.device, dtype=q.dtype)
+    check(_lib.load().lea_tapsum_upsample(
+        q.data_ptr(), qbs, out.data_ptr(), out.stride(0), b, cout, di, hi, wi, do, ho, wo,
+        scale.data_ptr() if scale is not None else None,
+        shift.data_ptr() if shift is not None else None, LEA_RELU if relu else 0, LEA_F32,
+        _stream()), "lea_tapsum_upsample")
+    return out
+
+
 def disparity_regression(cost: torch.Tensor, maxdisp: int) -> torch.Tensor:
     """Disp + DisparityRegression (build_model_2d.py:52-57, 33-42): [B,1,D3,H3,W3] -> [B,3H3,3W3]."""
     _require_cuda(cost)

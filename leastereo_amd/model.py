@@ -235,8 +235,11 @@ class LEAStereo(nn.Module):
         if not x.is_cuda:
             raise RuntimeError("leastereo_amd.LEAStereo runs the matching net on a ROCm device only")
         self.check_shape(x.shape[2], x.shape[3])
-        fx = self.feature(x)
-        fy = self.feature(y)
+        # LEAStereo.py:31-32 runs the feature net twice; in eval mode every layer is
+        # per-sample, so one call on the stacked pair halves the (launch-bound)
+        # torch/MIOpen kernel count.
+        f = self.feature(torch.cat((x, y), 0))
+        fx, fy = f[: x.shape[0]], f[x.shape[0]:]
         cost = kernels.build_cost_volume(fx, fy, self.maxdisp)
         cost = self.matching(cost)
         return self.disp(cost)

@@ -175,6 +175,24 @@ def test_conv_small_cout_valu_engine(cout, cin, shape):
     np.testing.assert_allclose(y.cpu().double().numpy(), refy.numpy(), rtol=1e-4, atol=1e-4)
 
 
+@pytest.mark.parametrize("cout,cin,src,dst", [(1, 32, (4, 6, 10), (8, 12, 20)),
+                                              (2, 8, (3, 5, 9), (5, 9, 17)),
+                                              (1, 32, (32, 96, 160), (64, 192, 320))])
+def test_head_tapsum_upsample_vs_torch(cout, cin, src, dst):
+    """last_3(Upsample(y)) via per-tap partial sums == conv3d(interpolate(y))."""
+    g = torch.Generator().manual_seed(cout * 31 + cin)
+    y = torch.randn((1, cin) + src, generator=g)
+    w = torch.randn(cout, cin, 3, 3, 3, generator=g) / np.sqrt(cin * 27)
+    taps = w.permute(0, 2, 3, 4, 1).reshape(cout * 27, cin, 1, 1, 1).contiguous()
+    q = kernels.conv3d_bnrelu(y.to(DEV), kernels.pack_conv_weight(taps.to(DEV)), cout * 27, 1,
+                              None, None, relu=False)
+    out = kernels.tapsum_upsample(q, cout, dst).cpu().double()
+    yd = y.to(DEV).double() if src[0] > 8 else y.double()
+    refy = F.conv3d(F.interpolate(yd, dst, mode="trilinear", align_corners=True),
+                    w.to(yd.device).double(), None, 1, 1).cpu()
+    np.testing.assert_allclose(out.numpy(), refy.numpy(), rtol=1e-4, atol=1e-4)
+
+
 def test_resample_affine_relu_epilogue_into_slice():
     g = torch.Generator().manual_seed(11)
     x = torch.randn(2, 8, 4, 6, 10, generator=g)
