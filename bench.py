@@ -30,12 +30,11 @@ import sys
 import time
 
 import torch
-import torch.distributed as dist
 
 REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)
 
-from leastereo_amd import kernels  # noqa: E402
+from leastereo_amd import kernels, parallel  # noqa: E402
 from leastereo_amd.config import LEAStereoArgs, default_arch_args  # noqa: E402
 from leastereo_amd.model import LEAStereo  # noqa: E402
 from leastereo_amd.weights import synthetic_state_dict  # noqa: E402
@@ -136,18 +135,19 @@ def golden_epe(device):
 
 def main():
     args = parse()
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    info = parallel.rank_info()
+    world, rank = info.world, info.rank
+    device = torch.device("cuda", info.local_rank)
     if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    device = torch.device("cuda", local)
+        torch.cuda.set_device(device)
+    parallel.init("nccl", info, device)  # nccl = RCCL over xGMI on ROCm
     torch.backends.cudnn.allow_tf32 = False
     torch.backends.cuda.matmul.allow_tf32 = False
 
     model = build_model(args.maxdisp, device)
     model.check_shape(args.height, args.width)
+    # weak scaling: every rank owns args.batch pairs of the global batch (shard of
+    # world*batch pairs), generated on its own device from a rank-seeded stream
     g = torch.Generator(device=device).manual_seed(1234 + rank)
     left = torch.randn(args.batch, 3, args.height, args.width, device=device, generator=g)
     right = torch.randn(args.batch, 3, args.height, args.width, device=device, generator=g)
@@ -163,37 +163,27 @@ def main():
             step()
         per_kernel = probe.summary()
         dominant = max(per_kernel, key=lambda n: per_kernel[n]["ms"])
-        if args.breakdown and rank == 0:
+        if args.breakdown and info.is_main:
             for n, d in sorted(per_kernel.items(), key=lambda kv: -kv[1]["ms"]):
                 log(f"{n:40s} launches {d['launches']:3d}  {d['ms']:8.3f} ms  "
                     f"{d['flops'] / d['ms'] / 1e9:8.1f} TFLOP/s  {d['bytes'] / d['ms'] / 1e6:8.1f} GB/s")
 
-        if world > 1:
-            dist.barrier()
+        parallel.barrier()
         torch.cuda.synchronize()
         with kernels.KernelProbe([dominant]) as probe:
             t0 = time.perf_counter()
             for _ in range(args.steps):
                 out = step()
             torch.cuda.synchronize()
-            if world > 1:
-                dist.barrier()
+            parallel.barrier()
             elapsed = time.perf_counter() - t0
         dom = probe.summary()[dominant]
-
-    el = torch.tensor([elapsed], device=device, dtype=torch.float64)
-    if world > 1:
-        dist.all_reduce(el, op=dist.ReduceOp.MAX)
-    elapsed = float(el.item())
+    elapsed = parallel.max_over_ranks(elapsed, device)
 
     epe = None
-    if args.epe:
+    if args.epe:  # after the timed region: one all-gather of the per-rank parity check
         e = torch.tensor([golden_epe(device)], device=device, dtype=torch.float32)
-        if world > 1:
-            gathered = torch.empty(world, device=device, dtype=torch.float32)
-            dist.all_gather_into_tensor(gathered, e)  # the one RCCL all-gather (per-rank EPE)
-            e = gathered
-        epe = [float(v) for v in e.cpu()]
+        epe = [float(v) for v in parallel.gather_per_pair(e).cpu()]
 
     flops_per_launch = dom["flops"] / dom["launches"]
     ms_per_launch = dom["ms"] / dom["launches"]
@@ -232,12 +222,11 @@ def main():
             "vs": "reference LEAStereo fp32 disparity (tests/golden e2e b1_h96_w192_md48)",
             "max_over_ranks": max(epe), "per_rank": epe},
     }
-    if rank == 0 and world == 1 and args.cpu_baseline:
+    if info.is_main and world == 1 and args.cpu_baseline:
         result["cpu_baseline"] = cpu_baseline(args, model, left[:1], right[:1], out[:1])
-    if rank == 0:
+    if info.is_main:
         print(json.dumps(result), flush=True)
-    if world > 1:
-        dist.destroy_process_group()
+    parallel.finalize()
 
 
 if __name__ == "__main__":
