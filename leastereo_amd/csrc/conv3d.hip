@@ -71,6 +71,7 @@ struct ConvArgs {
   int Di, Hi, Wi;          // stored input volume (RESAMPLE variant)
   float rd, rh, rw;        // align_corners=True source ratios (RESAMPLE variant)
   int tiles_w, ncob;
+  int ntiles, ndz, nblk;   // DMA engine's 1-D grid: tiles x depth groups x (B * ncob)
   unsigned flags;
 };
 
@@ -203,12 +204,23 @@ __global__ __launch_bounds__(kConvThreads, 2) void conv3d_dma_kernel(const ConvA
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int tile = blockIdx.x;
+  // XCD-aware order: blocks are dealt round-robin to the 8 XCDs, so block id i
+  // becomes position (i % 8) * ceil(N/8) + i / 8 of a (batch/cout-block, tile,
+  // depth group) walk with the depth group fastest -- every XCD then runs whole
+  // depth columns of neighbouring tiles, whose shared input planes and halo rows
+  // stay in its L2 (speed only: any placement is correct).
+  const int nblk = a.nblk;
+  const int xcd = blockIdx.x % 8, idx = blockIdx.x / 8;
+  const int q8 = nblk / 8, r8 = nblk % 8;
+  const int lin = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + idx;
+  const int dz = lin % a.ndz;
+  const int tile = (lin / a.ndz) % a.ntiles;
+  const int bc = lin / (a.ndz * a.ntiles);
   const int h0 = (tile / a.tiles_w) * C::TH;
   const int w0 = (tile % a.tiles_w) * TW;
-  const int d0 = blockIdx.y * TD;
-  const int b = blockIdx.z / a.ncob;
-  const int co0 = (blockIdx.z - b * a.ncob) * C::COP;
+  const int d0 = dz * TD;
+  const int b = bc / a.ncob;
+  const int co0 = (bc - b * a.ncob) * C::COP;
   const int nchunks = (a.cin + C::CIN_B - 1) / C::CIN_B;
   const float* wp = a.wp + (long long)(co0 / C::COP) * nchunks * C::WS;
   const int HW = a.H * a.W;  // host checks D*H*W*4 < 2^32
@@ -748,11 +760,25 @@ int launch(K kernel, const ConvArgs& a0, int th, int tw, int B, hipStream_t st, 
 
 #define LEA_TILE_TH(KS, MT, NT, TW) (TileCfg<KS, MT, NT, TW>::TH)
 
+// DMA engine: one-dimensional grid, decoded (XCD-aware) inside the kernel.
+template <typename K>
+int launch_dma(K kernel, const ConvArgs& a0, int th, int tw, int td, int B, hipStream_t st) {
+  ConvArgs a = a0;
+  a.tiles_w = (a.W + tw - 1) / tw;
+  a.ntiles = a.tiles_w * ((a.H + th - 1) / th);
+  a.ndz = (a.D + td - 1) / td;
+  const long long n = (long long)a.ntiles * a.ndz * B * a.ncob;
+  LEA_CHECK_ARG(n < (1LL << 31), "lea_conv3d: grid too large");
+  a.nblk = (int)n;
+  kernel<<<dim3((unsigned)n), kConvThreads, 0, st>>>(a);
+  return launch_status("lea_conv3d");
+}
+
 template <int MT, int NT, int TD>
 int run_dma_td(const ConvArgs& a, int tw, int B, hipStream_t st) {
   if (tw == 64)
-    return launch(conv3d_dma_kernel<MT, NT, 64, TD>, a, LEA_TILE_TH(3, MT, NT, 64), 64, B, st, TD);
-  return launch(conv3d_dma_kernel<MT, NT, 32, TD>, a, LEA_TILE_TH(3, MT, NT, 32), 32, B, st, TD);
+    return launch_dma(conv3d_dma_kernel<MT, NT, 64, TD>, a, LEA_TILE_TH(3, MT, NT, 64), 64, TD, B, st);
+  return launch_dma(conv3d_dma_kernel<MT, NT, 32, TD>, a, LEA_TILE_TH(3, MT, NT, 32), 32, TD, B, st);
 }
 
 template <int MT, int NT>
