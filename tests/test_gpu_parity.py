@@ -112,17 +112,28 @@ def test_conv_random_vs_torch(b, cin, cout, k, shape):
     np.testing.assert_allclose(out.cpu().double().numpy(), refy.numpy(), rtol=1e-4, atol=1e-4)
 
 
-@pytest.mark.parametrize("cin,cout,shape", [(16, 16, (35, 96, 160)), (32, 48, (9, 100, 326))])
-def test_conv_two_plane_tiles_odd_depth(cin, cout, shape):
-    """Large volumes use 2 output planes per workgroup; odd D masks the last one."""
+@pytest.mark.parametrize("cin,cout,shape,acc", [(16, 16, (35, 96, 160), False),
+                                                (16, 16, (35, 96, 160), True),
+                                                (8, 8, (33, 48, 320), True),
+                                                (32, 48, (9, 100, 326), False)])
+def test_conv_two_plane_tiles_odd_depth(cin, cout, shape, acc):
+    """Large volumes use 2 output planes per workgroup; odd D masks the last one.
+    With ``acc`` the residual is prefetched into registers at workgroup start."""
     name = kernels.conv_kernel_name(1, cout, *shape, 3)
     assert name.endswith(", 2>"), name
     g = torch.Generator().manual_seed(cin + cout)
     x = torch.randn((1, cin) + shape, generator=g)
     w = torch.randn(cout, cin, 3, 3, 3, generator=g) / np.sqrt(cin * 27)
+    res = torch.randn((1, cout) + shape, generator=g)
+    scale = torch.rand(cout, generator=g) + 0.5
+    shift = torch.randn(cout, generator=g) * 0.1
     refy = F.conv3d(x.double(), w.double(), None, 1, 1)
-    y = kernels.conv3d_bnrelu(x.to(DEV), kernels.pack_conv_weight(w.to(DEV)), cout, 3, None, None,
-                              relu=False)
+    refy = torch.relu(refy * scale.double().view(1, -1, 1, 1, 1) + shift.double().view(1, -1, 1, 1, 1))
+    out = res.to(DEV).clone() if acc else None
+    y = kernels.conv3d_bnrelu(x.to(DEV), kernels.pack_conv_weight(w.to(DEV)), cout, 3, scale.to(DEV),
+                              shift.to(DEV), relu=True, out=out, accumulate=acc)
+    if acc:
+        refy = refy + res.double()
     np.testing.assert_allclose(y.cpu().double().numpy(), refy.numpy(), rtol=1e-4, atol=1e-4)
 
 
@@ -224,7 +235,8 @@ def test_conv_channel_slices():
 def test_resample_vs_torch_random_sizes():
     g = torch.Generator().manual_seed(3)
     for src, dst in [((5, 9, 13), (3, 5, 7)), ((4, 6, 8), (8, 12, 16)), ((32, 96, 160), (64, 192, 320)),
-                     ((3, 3, 3), (1, 1, 1)), ((1, 4, 5), (2, 7, 9))]:
+                     ((3, 3, 3), (1, 1, 1)), ((1, 4, 5), (2, 7, 9)),
+                     ((2, 2000, 40), (3, 3, 40)), ((16, 48, 80), (32, 96, 160))]:
         x = torch.randn((2, 3) + src, generator=g)
         for ac in (True, False):
             refy = F.interpolate(x, dst, mode="trilinear", align_corners=ac)

@@ -16,17 +16,18 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from leastereo_amd import kernels  # noqa: E402
 
 L0, L1, L2 = (64, 192, 320), (32, 96, 160), (16, 48, 80)
-# name: (cin, cout, k, level, count per forward)
+# name: (cin, cout, k, level, count per forward[, accumulate: the cell's second op
+# of a step adds into the slot the first one wrote, LEA_RESIDUAL])
 LAYERS = {
     "stem0_64to32_k3_L0": (64, 32, 3, L0, 1),
     "stem1_32to32_k3_L0": (32, 32, 3, L0, 1),
     "conv12_128to64_k3_L1": (128, 64, 3, L1, 2),
     "cell_16to48_k3_L1_s1grp": (16, 48, 3, L1, 6),
-    "cell_16to16_k3_L1": (16, 16, 3, L1, 18),
+    "cell_16to16_k3_L1": (16, 16, 3, L1, 18, True),
     "cell_32to96_k3_L2_s1grp": (32, 96, 3, L2, 5),
-    "cell_32to32_k3_L2": (32, 32, 3, L2, 15),
+    "cell_32to32_k3_L2": (32, 32, 3, L2, 15, True),
     "cell_8to24_k3_L0_s1grp": (8, 24, 3, L0, 1),
-    "cell_8to8_k3_L0": (8, 8, 3, L0, 3),
+    "cell_8to8_k3_L0": (8, 8, 3, L0, 3, True),
     "last3_32to1_k3_L0": (32, 1, 3, L0, 1),
     "pre_64to8_k1_L1": (64, 8, 1, L1, 2),
     "pre_32to16_k1_L1": (32, 16, 1, L1, 6),
@@ -42,7 +43,8 @@ def main():
     dev = "cuda"
     only = set(a.only.split(",")) if a.only else None
     res = {}
-    for name, (cin, cout, k, (d, h, w), count) in LAYERS.items():
+    for name, (cin, cout, k, (d, h, w), count, *acc) in LAYERS.items():
+        acc = bool(acc and acc[0])
         if only and name not in only:
             continue
         g = torch.Generator(device=dev).manual_seed(0)
@@ -51,20 +53,20 @@ def main():
         packed = kernels.pack_conv_weight(wt)
         scale = torch.rand(cout, device=dev, generator=g) + 0.5
         shift = torch.randn(cout, device=dev, generator=g) * 0.1
-        out = torch.empty(1, cout, d, h, w, device=dev)
+        out = torch.zeros(1, cout, d, h, w, device=dev)
         for _ in range(3):
-            kernels.conv3d_bnrelu(x, packed, cout, k, scale, shift, True, out)
+            kernels.conv3d_bnrelu(x, packed, cout, k, scale, shift, True, out, acc)
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         torch.cuda.synchronize()
         e0.record()
         for _ in range(a.iters):
-            kernels.conv3d_bnrelu(x, packed, cout, k, scale, shift, True, out)
+            kernels.conv3d_bnrelu(x, packed, cout, k, scale, shift, True, out, acc)
         e1.record()
         torch.cuda.synchronize()
         ms = e0.elapsed_time(e1) / a.iters
         vox = d * h * w
         flops = 2.0 * vox * cin * cout * k ** 3
-        nbytes = 4.0 * vox * (cin + cout)
+        nbytes = 4.0 * vox * (cin + cout * (2 if acc else 1))
         res[name] = {"ms": ms, "tflops": flops / ms / 1e9, "gbs": nbytes / ms / 1e6,
                      "per_forward_ms": ms * count,
                      "kernel": kernels.conv_kernel_name(1, cout, d, h, w, k)}
