@@ -10,7 +10,7 @@ LIB      := leastereo_amd/libleastereo_hip.so
 
 all: $(LIB)
 
-build/obj/%.o: leastereo_amd/csrc/%.hip leastereo_amd/csrc/common.h include/leastereo_hip.h
+build/obj/%.o: leastereo_amd/csrc/%.hip $(wildcard leastereo_amd/csrc/*.h) include/leastereo_hip.h
 	@mkdir -p build/obj
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 

@@ -93,6 +93,12 @@ int lea_conv3d_bnrelu_resampled(const void* x, int64_t x_bstride, int Di, int Hi
  * (matches the demangled name rocprofv3 reports); NULL if unsupported. */
 const char* lea_conv3d_kernel_name(int B, int cout, int D, int H, int W, int k, int resampled);
 
+/* Tuning hook: force the (NT, TW, TD) tile of the k=3 DMA engine for later convs on
+ * the calling thread (nt <= 0 restores the built-in planner).  A tile that is not
+ * instantiated for the conv's cout block makes the conv return LEA_E_UNSUPPORTED.
+ * Used by tools/conv_sweep.py; callers never need it. */
+int lea_conv3d_set_tile_override(int nt, int tw, int td);
+
 /* Trilinear resample.  Replaces F.interpolate(mode='trilinear') at
  * skip_model_3d.py:48,50 and nn.Upsample at :162-164 (align_corners=1), with
  * PyTorch's source-index rule, then an optional epilogue

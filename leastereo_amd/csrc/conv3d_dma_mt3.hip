@@ -1,0 +1,7 @@
+// DMA-engine conv tiles with MT = 3 (see conv3d_impl.h); a translation unit
+// per MT keeps the ~60 instantiations compiling in parallel.
+#include "conv3d_impl.h"
+
+namespace lea {
+LEA_DMA_TU(3)
+}  // namespace lea
