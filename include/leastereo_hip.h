@@ -93,6 +93,33 @@ int lea_conv3d_bnrelu_resampled(const void* x, int64_t x_bstride, int Di, int Hi
  * (matches the demangled name rocprofv3 reports); NULL if unsupported. */
 const char* lea_conv3d_kernel_name(int B, int cout, int D, int H, int W, int k, int resampled);
 
+/* ---- 2D feature net (retrain/new_model_2d.py; models/operations_2d.py:31-47) ----
+ * 1x1 Conv2d and bilinear (align_corners) resizes of the feature net use the 3D
+ * entry points with D = Di = 1 (a bilinear resize is the trilinear one on a
+ * single plane, bit for bit).  The 3x3 convs have their own packing and entry. */
+
+/* Packed-weight size (floats) / packing of a Conv2d 3x3 weight [cout, cin, 3, 3]. */
+size_t lea_conv2d_packed_floats(int cout, int cin);
+int lea_conv2d_pack_weights(const float* w, float* packed, int cout, int cin, void* stream);
+
+/* ConvBR2d 3x3, stride 1, pad 1 (folded BN as in lea_conv3d_bnrelu, LEA_RELU,
+ * LEA_RESIDUAL -- the 2D cell's sum, including its skip_connect terms).
+ * x: [B, cin, H, W], y/residual: [B, cout, H, W], each at its own batch stride. */
+int lea_conv2d_bnrelu(const void* x, int64_t x_bstride, const float* w_packed,
+                      const float* scale, const float* shift, const void* residual,
+                      int64_t r_bstride, void* y, int64_t y_bstride, int B, int cin, int cout,
+                      int H, int W, unsigned flags, int dtype, void* stream);
+
+/* Kernel instantiation lea_conv2d_bnrelu launches for this shape. */
+const char* lea_conv2d_kernel_name(int B, int cout, int H, int W);
+
+/* Feature-net stem1: Conv2d 3x3, stride 3, pad 1 -> BN -> ReLU (new_model_2d.py:94).
+ * w: the raw [cout, cin, 3, 3] weight (no packing).  x: [B, cin, Hi, Wi];
+ * y: [B, cout, (Hi-1)/3+1, (Wi-1)/3+1]. */
+int lea_conv2d_s3_bnrelu(const void* x, int64_t x_bstride, const float* w, const float* scale,
+                         const float* shift, void* y, int64_t y_bstride, int B, int cin, int cout,
+                         int Hi, int Wi, unsigned flags, int dtype, void* stream);
+
 /* Tuning hook: force the (NT, TW, TD) tile of the k=3 DMA engine for later convs on
  * the calling thread (nt <= 0 restores the built-in planner).  A tile that is not
  * instantiated for the conv's cout block makes the conv return LEA_E_UNSUPPORTED.

@@ -326,10 +326,10 @@ __global__ __launch_bounds__(kConvThreads) void conv3d_valu_kernel(const ConvArg
 // ------------------------------------------------------------------- weight packing
 // Packed layout: [ceil(cout/COP)][ceil(cin/CIN_B)][KS^3][CIN_B][COP], zero outside (cin, cout);
 // rows of odd input channels swizzled (PackCfg::SWZ, a_col).
-template <int KS, int MT>
+template <int KS, int MT, int KD = KS>
 __global__ void pack_weights_kernel(const float* __restrict__ w, float* __restrict__ packed,
                                     int cout, int cin, int nchunks, long long total) {
-  using P = PackCfg<KS, MT>;
+  using P = PackCfg<KS, MT, KD>;
   for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
        i += (long long)gridDim.x * blockDim.x) {
     const int col = (int)(i % P::COPS);
@@ -356,9 +356,9 @@ inline int mt_for(int cout) {
   return ((cout + 47) / 48) * 48 < ((cout + 63) / 64) * 64 ? 3 : 4;
 }
 
-template <int KS, int MT>
+template <int KS, int MT, int KD = KS>
 size_t packed_floats_t(int cout, int cin) {
-  using P = PackCfg<KS, MT>;
+  using P = PackCfg<KS, MT, KD>;
   return (size_t)((cout + P::COP - 1) / P::COP) * ((cin + P::CIN_B - 1) / P::CIN_B) * P::CHUNK;
 }
 
@@ -510,12 +510,35 @@ const char* plan_name(const Plan& p, int k) {
   if (p.engine == 3)
     snprintf(g_name, sizeof(g_name), "conv3d_valu_kernel<%d>", p.mt == 1 ? 1 : 2);
   else if (p.engine == 0)
-    snprintf(g_name, sizeof(g_name), "conv3d_dma_kernel<%d, %d, %d, %d>", p.mt, p.nt, p.tw, p.td);
+    snprintf(g_name, sizeof(g_name), "conv3d_dma_kernel<%d, %d, %d, %d, %d>", p.mt, p.nt, p.tw, p.td,
+             k == 2 ? 1 : 3);
   else if (p.engine == 2)
     snprintf(g_name, sizeof(g_name), "conv3d_reg_kernel<%d, %d, %d, %d, true>", k, p.mt, p.nt, p.tw);
   else
     snprintf(g_name, sizeof(g_name), "conv1x1_kernel<%d, %d>", p.mt, p.nt);
   return g_name;
+}
+
+// ------------------------------------------------------------ 2D 3x3 (feature net)
+// The feature net's Conv2d 3x3 / stride 1 / pad 1 (models/operations_2d.py:31-47)
+// runs on the DMA engine as the D = 1 case of a (1, 3, 3) kernel.
+size_t packed_floats_2d(int cout, int cin) {
+  const int mt = mt_for(cout);
+  return mt == 1 ? packed_floats_t<3, 1, 1>(cout, cin)
+         : mt == 2 ? packed_floats_t<3, 2, 1>(cout, cin)
+         : mt == 3 ? packed_floats_t<3, 3, 1>(cout, cin) : packed_floats_t<3, 4, 1>(cout, cin);
+}
+
+inline Plan make_plan_2d(int B, int cout, int H, int W) {
+  Plan p;
+  p.engine = 0;
+  p.mt = mt_for(cout);
+  p.tw = 16;
+  p.td = 1;
+  const long long ncob = (cout + p.mt * 16 - 1) / (p.mt * 16);
+  const long long wgs8 = (long long)((W + 15) / 16) * ((H + 7) / 8) * B * ncob;
+  p.nt = wgs8 >= 512 ? 2 : 1;  // 8 x 16 tiles, or 4 x 16 on small maps
+  return p;
 }
 
 int conv_common(ConvArgs& a, int B, int k, bool resample, int dtype, void* stream) {
@@ -622,6 +645,83 @@ extern "C" int lea_conv3d_bnrelu(const void* x, int64_t x_bstride, const void* x
   a.W = W;
   a.flags = flags;
   return lea::conv_common(a, B, k, false, dtype, stream);
+}
+
+extern "C" size_t lea_conv2d_packed_floats(int cout, int cin) {
+  if (cout <= 0 || cin <= 0) return 0;
+  return lea::packed_floats_2d(cout, cin);
+}
+
+extern "C" int lea_conv2d_pack_weights(const float* w, float* packed, int cout, int cin,
+                                       void* stream) {
+  using namespace lea;
+  clear_error();
+  LEA_CHECK_ARG(w && packed, "lea_conv2d_pack_weights: null pointer");
+  LEA_CHECK_ARG(cout > 0 && cin > 0, "lea_conv2d_pack_weights: bad shape cout=%d cin=%d", cout, cin);
+  const long long total = (long long)packed_floats_2d(cout, cin);
+  const int threads = 256;
+  const long long want = (total + threads - 1) / threads;
+  const int grid = (int)(want < 4096 ? want : 4096);
+  const int nchunks = (cin + PackCfg<3, 1, 1>::CIN_B - 1) / PackCfg<3, 1, 1>::CIN_B;
+  hipStream_t st = as_stream(stream);
+  switch (mt_for(cout)) {
+    case 1: pack_weights_kernel<3, 1, 1><<<grid, threads, 0, st>>>(w, packed, cout, cin, nchunks, total); break;
+    case 2: pack_weights_kernel<3, 2, 1><<<grid, threads, 0, st>>>(w, packed, cout, cin, nchunks, total); break;
+    case 3: pack_weights_kernel<3, 3, 1><<<grid, threads, 0, st>>>(w, packed, cout, cin, nchunks, total); break;
+    default: pack_weights_kernel<3, 4, 1><<<grid, threads, 0, st>>>(w, packed, cout, cin, nchunks, total);
+  }
+  return launch_status("lea_conv2d_pack_weights");
+}
+
+extern "C" const char* lea_conv2d_kernel_name(int B, int cout, int H, int W) {
+  if (B <= 0 || cout <= 0 || H <= 0 || W <= 0) return nullptr;
+  return lea::plan_name(lea::make_plan_2d(B, cout, H, W), 2);
+}
+
+extern "C" int lea_conv2d_bnrelu(const void* x, int64_t x_bstride, const float* w_packed,
+                                 const float* scale, const float* shift, const void* residual,
+                                 int64_t r_bstride, void* y, int64_t y_bstride, int B, int cin,
+                                 int cout, int H, int W, unsigned flags, int dtype, void* stream) {
+  using namespace lea;
+  clear_error();
+  ConvArgs a{};
+  a.x = (const float*)x;
+  a.xbs = x_bstride;
+  a.cin1 = cin;
+  a.wp = w_packed;
+  a.scale = scale;
+  a.shift = shift;
+  a.res = (const float*)residual;
+  a.rbs = r_bstride;
+  a.y = (float*)y;
+  a.ybs = y_bstride;
+  a.cin = cin;
+  a.cout = cout;
+  a.D = 1;
+  a.H = H;
+  a.W = W;
+  a.flags = flags;
+  LEA_CHECK_ARG(a.x && a.wp && a.y, "lea_conv2d: null pointer");
+  LEA_CHECK_ARG((a.scale == nullptr) == (a.shift == nullptr),
+                "lea_conv2d: scale/shift must both be set or both NULL");
+  LEA_CHECK_ARG(!(flags & LEA_RESIDUAL) || a.res, "lea_conv2d: LEA_RESIDUAL without residual");
+  LEA_CHECK_ARG(B > 0 && cin > 0 && cout > 0 && H > 0 && W > 0,
+                "lea_conv2d: bad shape B=%d cin=%d cout=%d H=%d W=%d", B, cin, cout, H, W);
+  LEA_CHECK_ARG((long long)H * W * 4 < (1LL << 32), "lea_conv2d: plane too large");
+  LEA_CHECK_ARG(a.x != a.y, "lea_conv2d: input aliases output");
+  if (dtype != LEA_F32) {
+    set_error("lea_conv2d: dtype %d unsupported", dtype);
+    return LEA_E_UNSUPPORTED;
+  }
+  const Plan p = make_plan_2d(B, cout, H, W);
+  a.ncob = (cout + p.mt * 16 - 1) / (p.mt * 16);
+  hipStream_t st = as_stream(stream);
+  switch (p.mt) {
+    case 1: return run_dma2d_mt1(p, a, B, st);
+    case 2: return run_dma2d_mt2(p, a, B, st);
+    case 3: return run_dma2d_mt3(p, a, B, st);
+    default: return run_dma2d_mt4(p, a, B, st);
+  }
 }
 
 extern "C" int lea_conv3d_bnrelu_resampled(const void* x, int64_t x_bstride, int Di, int Hi,

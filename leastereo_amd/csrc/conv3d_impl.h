@@ -76,9 +76,11 @@ struct ConvArgs {
   unsigned flags;
 };
 
-template <int KS, int MT>
+// KD = kernel depth: KS for the 3D convs, 1 for the feature net's 2D 3x3 convs
+// (a 2D conv is the D = 1 case of a (1, 3, 3) kernel).
+template <int KS, int MT, int KD = KS>
 struct PackCfg {
-  static constexpr int KT = KS * KS * KS;
+  static constexpr int KT = KD * KS * KS;
   static constexpr int CIN_B = (KS == 3) ? 4 : 32;
   static constexpr int COP = MT * 16;
   static constexpr int COPS = COP;  // row stride of a staged weight row (floats)
@@ -95,9 +97,9 @@ __device__ __forceinline__ int a_col(int m, int kq, int n) {
   return ((PackCfg<KS, MT>::SWZ ? (m ^ (kq & 1)) : m) * 16) + n;
 }
 
-template <int KS, int MT, int NT, int TW, int TD = 1>
-struct TileCfg : PackCfg<KS, MT> {
-  using P = PackCfg<KS, MT>;
+template <int KS, int MT, int NT, int TW, int TD = 1, int KD = KS>
+struct TileCfg : PackCfg<KS, MT, KD> {
+  using P = PackCfg<KS, MT, KD>;
   static constexpr int PAD = KS / 2;
   static constexpr int NTILES = kConvWaves * NT;
   static constexpr int TPR = TW / 16;  // 16-voxel N tiles per row
@@ -106,7 +108,7 @@ struct TileCfg : PackCfg<KS, MT> {
   static constexpr int RH = TH + KS - 1;
   static constexpr int RW = TW + KS - 1;
   static constexpr int PLANE = RH * RW;
-  static constexpr int PLANES = KS + TD - 1;       // input planes feeding TD output planes
+  static constexpr int PLANES = KD + TD - 1;       // input planes feeding TD output planes
   static constexpr int IMG = PLANES * PLANE;       // staged floats per input channel
   static constexpr int CIS = round_16mod32(IMG);   // LDS stride between input channels
   static constexpr int XS = P::CIN_B * CIS;
@@ -117,15 +119,15 @@ struct TileCfg : PackCfg<KS, MT> {
 
 // ----------------------------------------------------------------- MFMA main loop
 // One K chunk from an LDS stage: KS^3 taps x CIN_B/4 k-steps x (MT x NT) MFMAs.
-template <int KS, int MT, int NT, int TW, int TD>
+template <int KS, int MT, int NT, int TW, int TD, int KD = KS>
 __device__ __forceinline__ void mfma_chunk(const float* xs, const float* ws, const int (&xoff)[NT],
                                            const int (&woff)[MT], f32x4 (&acc)[TD][MT][NT]) {
-  using C = TileCfg<KS, MT, NT, TW, TD>;
+  using C = TileCfg<KS, MT, NT, TW, TD, KD>;
   constexpr int CIN_B = C::CIN_B;
 #pragma unroll
   for (int s = 0; s < CIN_B / 4; ++s) {
 #pragma unroll
-    for (int kd = 0; kd < KS; ++kd) {
+    for (int kd = 0; kd < KD; ++kd) {
 #pragma unroll
       for (int kh = 0; kh < KS; ++kh) {
 #pragma unroll
@@ -274,9 +276,9 @@ __device__ __forceinline__ void epilogue_pre(const ConvArgs& a, const f32x4 (&ac
 }
 
 // ------------------------------------------------------------- LDS-DMA engine (k=3)
-template <int MT, int NT, int TW, int TD>
+template <int MT, int NT, int TW, int TD, int KD = 3>
 __global__ __launch_bounds__(kConvThreads, 2) void conv3d_dma_kernel(const ConvArgs a) {
-  using C = TileCfg<3, MT, NT, TW, TD>;
+  using C = TileCfg<3, MT, NT, TW, TD, KD>;
   constexpr int XSLOTS = (C::IMG + 63) / 64;  // 256-B DMA pieces per channel image
   constexpr int XSLOTS_W = (XSLOTS + kConvWaves - 1) / kConvWaves;
   constexpr int WSLOTS = (C::WS + 255) / 256;  // 1-KB DMA pieces of the weight chunk
@@ -320,7 +322,7 @@ __global__ __launch_bounds__(kConvThreads, 2) void conv3d_dma_kernel(const ConvA
       const int r = e - kd * C::PLANE;
       const int rr = r / C::RW;
       const int cc = r - rr * C::RW;
-      const int d = d0 + kd - 1, h = h0 + rr - 1, w = w0 + cc - 1;
+      const int d = d0 + kd - KD / 2, h = h0 + rr - 1, w = w0 + cc - 1;
       if ((unsigned)d < (unsigned)a.D && (unsigned)h < (unsigned)a.H && (unsigned)w < (unsigned)a.W)
         v = (unsigned)(d * HW + h * a.W + w) * 4u;
     }
@@ -390,7 +392,7 @@ __global__ __launch_bounds__(kConvThreads, 2) void conv3d_dma_kernel(const ConvA
     __syncthreads();  // ... and everyone's; everyone is done reading chunk ch-1's stage
     if (ch + 1 < nchunks) issue(ch + 1, smem + ((ch + 1) & 1) * C::STAGE);
     const float* xs = smem + (ch & 1) * C::STAGE;
-    mfma_chunk<3, MT, NT, TW, TD>(xs, xs + C::XS, xoff, woff, acc);
+    mfma_chunk<3, MT, NT, TW, TD, KD>(xs, xs + C::XS, xoff, woff, acc);
   }
   if constexpr (PRE)
     epilogue_pre<3, MT, NT, TW, TD>(a, acc, epi, b, co0, d0, h0, w0, wave, lane);
@@ -438,11 +440,15 @@ int launch_dma(K kernel, const ConvArgs& a0, int th, int tw, int td, int B, hipS
   LEA_DMA_TW_ALL(X, 4, 1, 1) LEA_DMA_TW_ALL(X, 4, 2, 1) LEA_DMA_TW_ALL(X, 4, 1, 2)      \
   X(4, 2, 16, 2) X(4, 2, 32, 2)
 
+// 2D (KD = 1) tiles for the feature net: one plane per workgroup.
+#define LEA_DMA2D_LIST(X, MT) X(MT, 1, 16, 1, 1) X(MT, 2, 16, 1, 1)
+
 // Per-MT entry points (defined by LEA_DMA_TU in conv3d_dma_mt*.hip).  lds_bytes
 // returns 0 for a tile that is not instantiated; run returns LEA_E_UNSUPPORTED.
 #define LEA_DMA_DECL(MT)                                                  \
   int dma_lds_bytes_mt##MT(int nt, int tw, int td);                       \
-  int run_dma_mt##MT(const Plan& p, const ConvArgs& a, int B, hipStream_t st);
+  int run_dma_mt##MT(const Plan& p, const ConvArgs& a, int B, hipStream_t st);   \
+  int run_dma2d_mt##MT(const Plan& p, const ConvArgs& a, int B, hipStream_t st);
 LEA_DMA_DECL(1)
 LEA_DMA_DECL(2)
 LEA_DMA_DECL(3)
@@ -455,6 +461,10 @@ LEA_DMA_DECL(4)
   if (p.nt == NT && p.tw == TW && p.td == TD)                                                 \
     return launch_dma(conv3d_dma_kernel<MT, NT, TW, TD>, a, TileCfg<3, MT, NT, TW, TD>::TH, TW, \
                       TD, B, st);
+#define LEA_DMA2D_RUN_CASE(MT, NT, TW, TD, KD)                                           \
+  if (p.nt == NT && p.tw == TW && p.td == TD)                                             \
+    return launch_dma(conv3d_dma_kernel<MT, NT, TW, TD, KD>,                              \
+                      a, TileCfg<3, MT, NT, TW, TD, KD>::TH, TW, TD, B, st);
 #define LEA_DMA_TU(MT)                                                            \
   int dma_lds_bytes_mt##MT(int nt, int tw, int td) {                              \
     LEA_DMA_LIST_##MT(LEA_DMA_LDS_CASE) return 0;                                 \
@@ -462,6 +472,11 @@ LEA_DMA_DECL(4)
   int run_dma_mt##MT(const Plan& p, const ConvArgs& a, int B, hipStream_t st) {   \
     LEA_DMA_LIST_##MT(LEA_DMA_RUN_CASE)                                           \
     set_error("lea_conv3d: no DMA tile <%d, %d, %d, %d>", MT, p.nt, p.tw, p.td);  \
+    return LEA_E_UNSUPPORTED;                                                     \
+  }                                                                               \
+  int run_dma2d_mt##MT(const Plan& p, const ConvArgs& a, int B, hipStream_t st) { \
+    LEA_DMA2D_LIST(LEA_DMA2D_RUN_CASE, MT)                                        \
+    set_error("lea_conv2d: no DMA tile <%d, %d, %d, 1, 1>", MT, p.nt, p.tw);     \
     return LEA_E_UNSUPPORTED;                                                     \
   }
 

@@ -1,15 +1,21 @@
-"""Matching-net executor: runs retrain/skip_model_3d.py:140-174 on the HIP kernels.
+"""Cell-graph executors: run the searched networks on the HIP kernels.
 
-Prepared once per weight load (``NewMatching.executor()``): every 3D ConvBR's
-weight is re-laid out for the conv kernel and its BN folded into fp32
-scale/shift.  ``run`` then issues only C-ABI launches on the current stream
-(no host syncs), so a whole forward can be captured in a HIP graph.
+``MatchingExecutor`` runs newMatching.forward (retrain/skip_model_3d.py:140-174),
+``FeatureExecutor`` runs newFeature.forward (retrain/new_model_2d.py:140-165).
+Both are prepared once per weight load (``NewMatching.executor()`` /
+``NewFeature.executor()``): every ConvBR's weight is re-laid out for its kernel
+and its BN folded into fp32 scale/shift.  ``run`` then issues only C-ABI launches
+on the current stream (no host syncs), so a whole forward can be captured in a
+HIP graph.
 
-Memory plan per cell (skip_model_3d.py:41-75): the cell output
-``cat([s1, s2, s3, s4])`` is allocated once and every producer writes its
+Memory plan per cell (skip_model_3d.py:41-75, new_model_2d.py:41-75): the cell
+output ``cat([s1, s2, s3, s4])`` is allocated once and every producer writes its
 channel slice directly (preprocess -> s1 slot, first DAG op -> s_k slot, second
-DAG op accumulates into the same slot through the conv epilogue), so neither the
-``cat`` nor the ``sum`` ever moves data.
+DAG op accumulates into the same slot through the conv epilogue; a skip_connect
+term enters as the epilogue's residual), so neither the ``cat`` nor the ``sum``
+moves data.  Feature-net activations are [B, C, 1, H, W] views: a 2D map is the
+one-plane case of the 3D kernels (1x1 convs, bilinear = trilinear on one plane),
+and the 3x3 convs run on the 2D entry of the same MFMA engine.
 """
 from __future__ import annotations
 
@@ -23,42 +29,50 @@ from .arch import scale_dimension
 
 @dataclass
 class ConvParams:
-    packed: torch.Tensor
+    packed: torch.Tensor      # packed weights ("s3": the raw [cout, cin, 3, 3] weight)
     scale: torch.Tensor | None
     shift: torch.Tensor | None
     cin: int
     cout: int
     k: int
     relu: bool
+    kind: str = "3d"          # "3d" (k 1/3), "2d" (3x3 s1), "s3" (3x3 stride 3)
 
 
-class MatchingExecutor:
-    def __init__(self, matching):
+def _conv_params(mod, w=None, folded=None):
+    """ConvParams of a ConvBR (weights/BN may be overridden by stacked ones)."""
+    w = mod.conv.weight if w is None else w
+    scale, shift = mod.folded_bn() if folded is None else folded
+    cout, cin, k = w.shape[0], w.shape[1], w.shape[-1]
+    if w.dim() == 5:
+        return ConvParams(kernels.pack_conv_weight(w), scale, shift, cin, cout, k, mod.relu)
+    if k == 1:  # 1x1 Conv2d = 1x1x1 Conv3d on one plane
+        return ConvParams(kernels.pack_conv_weight(w.reshape(cout, cin, 1, 1, 1)), scale, shift,
+                          cin, cout, 1, mod.relu)
+    if mod.stride == 3:
+        return ConvParams(w.detach().contiguous(), scale, shift, cin, cout, 3, mod.relu, "s3")
+    if mod.stride != 1 or mod.padding != 1:
+        raise ValueError(f"unsupported Conv2d stride={mod.stride} padding={mod.padding}")
+    return ConvParams(kernels.pack_conv2d_weight(w), scale, shift, cin, cout, 3, mod.relu, "2d")
+
+
+class CellGraphExecutor:
+    """Shared machinery: parameter packing, ConvBR dispatch, the searched cell."""
+
+    def __init__(self, net):
         from .model import ConvBR
-        self.m = matching
+        self.m = net
         self.p = {}
         with torch.no_grad():
-            for name, mod in matching.named_modules():
+            for name, mod in net.named_modules():
                 if isinstance(mod, ConvBR):
-                    w = mod.conv.weight
-                    if w.dim() != 5:
-                        continue
-                    scale, shift = mod.folded_bn()
-                    self.p[name] = ConvParams(kernels.pack_conv_weight(w), scale, shift,
-                                              w.shape[1], w.shape[0], w.shape[-1], mod.relu)
-            # Head: last_3(Upsample(y)) = sum over taps of upsampled per-tap partial
-            # sums (lea_tapsum_upsample); the taps run as a 1x1 conv with 27*cout outputs.
-            last3 = matching.last_3.conv.weight
-            co, ci = last3.shape[:2]
-            taps = last3.permute(0, 2, 3, 4, 1).reshape(co * 27, ci, 1, 1, 1)
-            self.p["last_3.taps"] = ConvParams(kernels.pack_conv_weight(taps), None, None,
-                                               ci, co * 27, 1, False)
-            # Sibling ops: the DAG ops that read s1 (one per step here: ops 1, 2, 4 of
-            # the searched genotype) write consecutive cat slots, so they run as ONE
-            # conv with cout = n*C over channels [.., ..) of the cell output (their
-            # weights and folded BN stacked along cout).  The remaining ops accumulate.
+                    self.p[name] = _conv_params(mod)
+            # Sibling ops: the DAG ops that read s1 (one per step: ops 1, 2, 4 of the
+            # matching genotype) write consecutive cat slots, so they run as ONE conv
+            # with cout = n*C over channels [.., ..) of the cell output (their weights
+            # and folded BN stacked along cout).  The remaining ops accumulate.
             self.s1_group = {}
-            for i, cell in enumerate(matching.cells):
+            for i, cell in enumerate(net.cells):
                 group = []
                 for k, terms in enumerate(cell.plan):
                     for op, j in terms:
@@ -75,20 +89,27 @@ class MatchingExecutor:
                 folded = [m.folded_bn() for m in mods]
                 scale = torch.cat([f[0] for f in folded]).contiguous()
                 shift = torch.cat([f[1] for f in folded]).contiguous()
-                self.p[f"cells.{i}.s1_group"] = ConvParams(kernels.pack_conv_weight(w), scale, shift,
-                                                           w.shape[1], w.shape[0], 3, True)
+                self.p[f"cells.{i}.s1_group"] = _conv_params(mods[0], w, (scale, shift))
                 self.s1_group[i] = group
 
-    def conv(self, name, x, out=None, accumulate=False, x2=None, size=None):
-        """ConvBR3d ``name`` on x (or cat(x, x2)); with ``size`` != x's volume the
-        input is trilinearly resampled (align_corners=True) inside the conv."""
+    def conv(self, name, x, out=None, accumulate=False, x2=None, size=None, residual=None):
+        """ConvBR ``name`` on x (or cat(x, x2)); with ``size`` != x's volume the input
+        is trilinearly resampled (align_corners=True) inside the conv."""
         p = self.p[name]
         cin = x.shape[1] + (x2.shape[1] if x2 is not None else 0)
         if cin != p.cin:
             raise ValueError(f"{name}: expected {p.cin} input channels, got {cin}")
-        if size is not None and tuple(size) != tuple(x.shape[2:]):
-            if x2 is not None:
-                raise ValueError("resampled conv takes one input")
+        resized = size is not None and tuple(size) != tuple(x.shape[2:])
+        if p.kind == "s3":
+            return kernels.conv2d_s3_bnrelu(x, p.packed, p.scale, p.shift, p.relu)
+        if p.kind == "2d":
+            if resized or x2 is not None:
+                raise ValueError(f"{name}: 2D 3x3 conv takes one input at its own size")
+            return kernels.conv2d_bnrelu(x, p.packed, p.cout, p.scale, p.shift, p.relu, out,
+                                         accumulate, residual)
+        if resized:
+            if x2 is not None or residual is not None:
+                raise ValueError("resampled conv takes one input and no residual")
             up = all(int(o) >= int(i) for o, i in zip(size, x.shape[2:]))
             if p.k == 1 and up and not accumulate:
                 # interp and the 1x1 conv commute: conv at the low resolution, then
@@ -98,19 +119,21 @@ class MatchingExecutor:
             return kernels.conv3d_bnrelu_resampled(x, size, p.packed, p.cout, p.k, p.scale,
                                                    p.shift, p.relu, out, accumulate)
         return kernels.conv3d_bnrelu(x, p.packed, p.cout, p.k, p.scale, p.shift, p.relu, out,
-                                     accumulate, x2)
+                                     accumulate, x2, residual)
 
     def cell(self, i, s0, s1):
-        """Cell.forward (skip_model_3d.py:41-75).  The level change of s1 (:44-48)
-        and the size match of s0 (:49-51) are fused into the 1x1 preprocess convs
-        (:52-53) that consume them."""
+        """Cell.forward (skip_model_3d.py:41-75 / new_model_2d.py:41-75).  The level
+        change of s1 (:44-48) and the size match of s0 (:49-51) are fused into the
+        1x1 preprocess convs (:52-53) that consume them."""
         cell = self.m.cells[i]
         c = cell.c_out
         prev_input = s1
         size = tuple(s1.shape[2:])
         if cell.downup_sample != 0:
             sc = 0.5 if cell.downup_sample < 0 else 2
-            size = tuple(scale_dimension(n, sc) for n in size)
+            # the D axis of a 2D map stays 1 (bilinear on H, W only)
+            size = tuple(n if (cell.dims == 2 and ax == 0) else scale_dimension(n, sc)
+                         for ax, n in enumerate(size))
         b = s1.shape[0]
         d, h, w = size
         bm = cell.block_multiplier
@@ -137,19 +160,27 @@ class MatchingExecutor:
             dst = slot.get(len(states))
             if dst is None:
                 dst = torch.empty((b, c, d, h, w), device=s1.device, dtype=s1.dtype)
+            skips = [states[j] for k, j in terms if cell.op_kinds[k] != "conv"]
             for k, j in terms:
-                if (step, k) in done:
+                if (step, k) in done or cell.op_kinds[k] != "conv":
                     continue
-                if cell.op_kinds[k] == "conv":
-                    self.conv(f"cells.{i}._ops.{k}", states[j], out=dst, accumulate=step in written)
-                elif step in written:
-                    dst.add_(states[j])
+                residual = None
+                if step not in written and skips:  # skip_connect term -> epilogue residual
+                    residual = skips.pop()
+                self.conv(f"cells.{i}._ops.{k}", states[j], out=dst, accumulate=step in written,
+                          residual=residual)
+                written.add(step)
+            for t in skips:
+                if step in written:
+                    dst.add_(t)
                 else:
-                    dst.copy_(states[j])
+                    dst.copy_(t)
                 written.add(step)
             states.append(dst)
         return prev_input, out
 
+
+class MatchingExecutor(CellGraphExecutor):
     def run(self, x):
         """newMatching.forward (skip_model_3d.py:140-174): [B,64,D3,H3,W3] -> [B,1,D3,H3,W3]."""
         stem0 = self.conv("stem0", x)
@@ -188,3 +219,45 @@ class MatchingExecutor:
         p3 = self.p["last_3"]
         q = self.conv("last_3.taps", y)
         return kernels.tapsum_upsample(q, p3.cout, full, p3.scale, p3.shift, p3.relu)
+
+    def __init__(self, matching):
+        super().__init__(matching)
+        with torch.no_grad():
+            # Head: last_3(Upsample(y)) = sum over taps of upsampled per-tap partial
+            # sums (lea_tapsum_upsample); the taps run as a 1x1 conv with 27*cout outputs.
+            last3 = matching.last_3.conv.weight
+            co, ci = last3.shape[:2]
+            taps = last3.permute(0, 2, 3, 4, 1).reshape(co * 27, ci, 1, 1, 1)
+            self.p["last_3.taps"] = ConvParams(kernels.pack_conv_weight(taps), None, None,
+                                               ci, co * 27, 1, False)
+
+
+class FeatureExecutor(CellGraphExecutor):
+    def run(self, x):
+        """newFeature.forward (new_model_2d.py:140-165): [N,3,H,W] -> [N,32,H/3,W/3]."""
+        x5 = x.unsqueeze(2)
+        stem1 = self.conv("stem1", self.conv("stem0", x5))
+        stem2 = self.conv("stem2", stem1)
+        out = (stem1, stem2)
+        for i in range(len(self.m.cells)):
+            out = self.cell(i, out[0], out[1])
+        last = out[-1]
+        h, w = stem2.shape[3:]
+        lh = last.shape[3]
+        full, half, quarter = (1, h, w), (1, h // 2, w // 2), (1, h // 4, w // 4)
+        # head (:156-163): ConvBR at the low level, then nn.Upsample; a ConvBR after an
+        # Upsample reads it through conv(size=...) (interpolation fused/commuted)
+        if lh == h:
+            y = last
+        elif lh == h // 2:
+            y = kernels.resample_trilinear(self.conv("last_6", last), full)
+        elif lh == h // 4:
+            y = self.conv("last_6", self.conv("last_12", last), size=half)
+            y = kernels.resample_trilinear(y, full)
+        elif lh == h // 8:
+            y = self.conv("last_12", self.conv("last_24", last), size=quarter)
+            y = kernels.resample_trilinear(self.conv("last_6", y, size=half), full)
+        else:
+            # the reference raises UnboundLocalError here (new_model_2d.py:156-165)
+            raise ValueError(f"feature size {tuple(x.shape[2:])} is not legal for the feature net")
+        return self.conv("last_3", y).squeeze(2)

@@ -142,10 +142,26 @@ def _conv_out(x_shape5, cout, spatial, out, accumulate, device, dtype):
     return out, _check_volume_view(out, "out")
 
 
+def _residual(out, accumulate, residual, ybs):
+    """(pointer, batch stride) of the epilogue's residual: ``out`` itself under
+    ``accumulate``, else an explicit tensor of out's shape (or none)."""
+    if accumulate:
+        if residual is not None:
+            raise ValueError("accumulate and residual are exclusive")
+        return out.data_ptr(), ybs
+    if residual is None:
+        return None, 0
+    _require_cuda(residual)
+    if tuple(residual.shape) != tuple(out.shape):
+        raise ValueError(f"residual shape {tuple(residual.shape)} != {tuple(out.shape)}")
+    return residual.data_ptr(), _check_volume_view(residual, "residual")
+
+
 def conv3d_bnrelu(x: torch.Tensor, packed: torch.Tensor, cout: int, k: int,
                   scale: torch.Tensor | None, shift: torch.Tensor | None, relu: bool = True,
                   out: torch.Tensor | None = None, accumulate: bool = False,
-                  x2: torch.Tensor | None = None) -> torch.Tensor:
+                  x2: torch.Tensor | None = None,
+                  residual: torch.Tensor | None = None) -> torch.Tensor:
     """ConvBR3d (operations_3d.py:41-47) of ``torch.cat((x, x2), 1)`` (x2 optional,
     never materialised).  ``out`` may be a channel slice of a larger (cat) buffer;
     ``accumulate`` adds the activation to what ``out`` holds (the cell's pairwise
@@ -160,15 +176,15 @@ def conv3d_bnrelu(x: torch.Tensor, packed: torch.Tensor, cout: int, k: int,
         cin2 = x2.shape[1]
         x2bs = _check_volume_view(x2, "x2")
     out, ybs = _conv_out(x.shape, cout, (d, h, w), out, accumulate, x.device, x.dtype)
-    flags = (LEA_RELU if relu else 0) | (LEA_RESIDUAL if accumulate else 0)
-    rec = _probe_begin(b, cin + cin2, cout, d, h, w, k, accumulate, b * d * h * w, False)
+    rptr, rbs = _residual(out, accumulate, residual, ybs)
+    flags = (LEA_RELU if relu else 0) | (LEA_RESIDUAL if rptr is not None else 0)
+    rec = _probe_begin(b, cin + cin2, cout, d, h, w, k, rptr is not None, b * d * h * w, False)
     check(_lib.load().lea_conv3d_bnrelu(
         x.data_ptr(), xbs, x2.data_ptr() if x2 is not None else None, x2bs, cin2,
         packed.data_ptr(),
         scale.data_ptr() if scale is not None else None,
         shift.data_ptr() if shift is not None else None,
-        out.data_ptr() if accumulate else None, ybs if accumulate else 0,
-        out.data_ptr(), ybs, b, cin + cin2, cout, d, h, w, k, flags, LEA_F32, _stream()),
+        rptr, rbs, out.data_ptr(), ybs, b, cin + cin2, cout, d, h, w, k, flags, LEA_F32, _stream()),
         "lea_conv3d_bnrelu")
     _probe_end(rec)
     return out
@@ -195,6 +211,73 @@ def conv3d_bnrelu_resampled(x: torch.Tensor, size, packed: torch.Tensor, cout: i
         out.data_ptr(), ybs, b, cin, cout, d, h, w, k, flags, LEA_F32, _stream()),
         "lea_conv3d_bnrelu_resampled")
     _probe_end(rec)
+    return out
+
+
+# ------------------------------------------------------------------- 2D feature net
+# Feature-net activations travel as NCDHW views with D = 1 ([B, C, 1, H, W]), so the
+# 1x1 convs and bilinear resizes are the 3D entry points on a single plane.
+
+def conv2d_kernel_name(b, cout, h, w):
+    name = _lib.load().lea_conv2d_kernel_name(b, cout, h, w)
+    return name.decode() if name else None
+
+
+def pack_conv2d_weight(w: torch.Tensor) -> torch.Tensor:
+    """[cout, cin, 3, 3] fp32 device weight -> packed layout of lea_conv2d_bnrelu."""
+    _require_cuda(w)
+    w = w.detach().contiguous()
+    if w.dim() != 4 or tuple(w.shape[2:]) != (3, 3):
+        raise ValueError(f"expected a [cout, cin, 3, 3] weight, got {tuple(w.shape)}")
+    cout, cin = w.shape[:2]
+    n = _lib.load().lea_conv2d_packed_floats(cout, cin)
+    packed = torch.empty(n, device=w.device, dtype=torch.float32)
+    check(_lib.load().lea_conv2d_pack_weights(w.data_ptr(), packed.data_ptr(), cout, cin, _stream()),
+          "lea_conv2d_pack_weights")
+    return packed
+
+
+def conv2d_bnrelu(x: torch.Tensor, packed: torch.Tensor, cout: int,
+                  scale: torch.Tensor | None, shift: torch.Tensor | None, relu: bool = True,
+                  out: torch.Tensor | None = None, accumulate: bool = False,
+                  residual: torch.Tensor | None = None) -> torch.Tensor:
+    """ConvBR2d 3x3/s1/p1 (operations_2d.py:31-47) on x [B, cin, 1, H, W]; ``residual``
+    (or ``accumulate`` into out) adds a cell-sum operand in the epilogue."""
+    _require_cuda(x, packed, scale, shift, out)
+    b, cin, d, h, w = x.shape
+    if d != 1:
+        raise ValueError("conv2d_bnrelu takes [B, C, 1, H, W] views")
+    xbs = _check_volume_view(x, "x")
+    out, ybs = _conv_out(x.shape, cout, (1, h, w), out, accumulate, x.device, x.dtype)
+    rptr, rbs = _residual(out, accumulate, residual, ybs)
+    flags = (LEA_RELU if relu else 0) | (LEA_RESIDUAL if rptr is not None else 0)
+    check(_lib.load().lea_conv2d_bnrelu(
+        x.data_ptr(), xbs, packed.data_ptr(),
+        scale.data_ptr() if scale is not None else None,
+        shift.data_ptr() if shift is not None else None,
+        rptr, rbs, out.data_ptr(), ybs, b, cin, cout, h, w, flags, LEA_F32, _stream()),
+        "lea_conv2d_bnrelu")
+    return out
+
+
+def conv2d_s3_bnrelu(x: torch.Tensor, w: torch.Tensor, scale: torch.Tensor | None,
+                     shift: torch.Tensor | None, relu: bool = True) -> torch.Tensor:
+    """ConvBR2d 3x3, stride 3, pad 1 (new_model_2d.py:94) on x [B, cin, 1, H, W]."""
+    _require_cuda(x, w, scale, shift)
+    b, cin, d, hi, wi = x.shape
+    if d != 1:
+        raise ValueError("conv2d_s3_bnrelu takes [B, C, 1, H, W] views")
+    w = w.detach().contiguous()
+    cout = w.shape[0]
+    if tuple(w.shape) != (cout, cin, 3, 3):
+        raise ValueError(f"weight {tuple(w.shape)} does not match cin={cin}")
+    xbs = _check_volume_view(x, "x")
+    out = torch.empty((b, cout, 1, (hi - 1) // 3 + 1, (wi - 1) // 3 + 1), device=x.device,
+                      dtype=x.dtype)
+    check(_lib.load().lea_conv2d_s3_bnrelu(
+        x.data_ptr(), xbs, w.data_ptr(), scale.data_ptr() if scale is not None else None,
+        shift.data_ptr() if shift is not None else None, out.data_ptr(), out.stride(0), b, cin,
+        cout, hi, wi, LEA_RELU if relu else 0, LEA_F32, _stream()), "lea_conv2d_s3_bnrelu")
     return out
 
 

@@ -4,18 +4,18 @@ Mirrors retrain/LEAStereo.py:12-52: same constructor arguments, same
 state_dict keys (918 tensors; ``load_state_dict(strict=True)`` of a reference
 checkpoint works), same ``forward(left, right) -> [B, H, W]`` disparity.
 
-Split (BASELINE.json north_star):
-  * 2D feature net (retrain/new_model_2d.py) -> PyTorch-ROCm modules (MIOpen);
-  * cost volume, matching net, disparity regression -> libleastereo_hip.so
-    (``kernels.py``), driven by ``MatchingExecutor``.
-There is no CPU path for the matching net: forward on a non-ROCm device raises.
+Everything runs on libleastereo_hip.so (``kernels.py``): the 2D feature net
+(retrain/new_model_2d.py, ``FeatureExecutor``; north_star allowed it to stay on
+PyTorch -- moved to HIP as SURVEY.md §8f rank 2), the cost volume, the matching net
+(``MatchingExecutor``) and the disparity regression.  The nn.Modules here are
+parameter containers with the reference's names; there is no torch/CPU compute
+path: forward on a non-ROCm device raises.
 """
 from __future__ import annotations
 
 import numpy as np
 import torch
 import torch.nn as nn
-import torch.nn.functional as F
 
 from . import kernels
 from .arch import (PRIMITIVES_2D, PRIMITIVES_3D, cell_specs, check_matching_shape,
@@ -42,14 +42,6 @@ class ConvBR(nn.Module):
             elif isinstance(m, (nn.BatchNorm2d, nn.BatchNorm3d)):
                 nn.init.constant_(m.weight, 1)
                 nn.init.constant_(m.bias, 0)
-
-    def forward(self, x):  # torch path: used by the 2D feature net only
-        x = self.conv(x)
-        if self.use_bn:
-            x = self.bn(x)
-        if self.relu:
-            x = F.relu(x, inplace=True)
-        return x
 
     @torch.no_grad()
     def folded_bn(self):
@@ -89,27 +81,6 @@ class Cell(nn.Module):
                 self.op_kinds.append("conv")
         self.plan = ops_in_iteration_order(np.asarray(cell_arch), steps)
 
-    def forward(self, s0, s1):
-        """2D (feature-net) forward in torch, new_model_2d.py:41-75."""
-        prev_input = s1
-        if self.downup_sample != 0:
-            sc = 0.5 if self.downup_sample < 0 else 2
-            s1 = F.interpolate(s1, [scale_dimension(n, sc) for n in s1.shape[2:]],
-                               mode="bilinear", align_corners=True)
-        if s0.shape[2:] != s1.shape[2:]:
-            s0 = F.interpolate(s0, s1.shape[2:], mode="bilinear", align_corners=True)
-        if s0.shape[1] != self.c_out:
-            s0 = self.pre_preprocess(s0)
-        s1 = self.preprocess(s1)
-        states = [s0, s1]
-        for terms in self.plan:
-            s = None
-            for k, j in terms:
-                t = self._ops[k](states[j])
-                s = t if s is None else s + t
-            states.append(s)
-        return prev_input, torch.cat(states[-self.block_multiplier:], dim=1)
-
 
 def _head_modules(mod, initial_fm, dims, last3_bn_relu):
     mod.last_3 = ConvBR(initial_fm, 1 if dims == 3 else initial_fm, 3 if dims == 3 else 1, 1,
@@ -119,8 +90,35 @@ def _head_modules(mod, initial_fm, dims, last3_bn_relu):
     mod.last_24 = ConvBR(initial_fm * 8, initial_fm * 4, 1, 1, 0, dims=dims)
 
 
-class NewFeature(nn.Module):
-    """2D feature net, retrain/new_model_2d.py:78-165 (stays on PyTorch-ROCm)."""
+class _ExecutorCache:
+    """Kernel-side parameters (packed weights, folded BN) built on first use and
+    dropped whenever the weights may have changed (load_state_dict, .to(), ...)."""
+
+    _executor_cls = None
+
+    def invalidate(self):
+        self._executor = None
+
+    def _apply(self, fn, *a, **kw):
+        self.invalidate()
+        return super()._apply(fn, *a, **kw)
+
+    def _load_from_state_dict(self, *a, **kw):
+        self.invalidate()
+        return super()._load_from_state_dict(*a, **kw)
+
+    def executor(self):
+        if self._executor is None:
+            from . import executor
+            self._executor = getattr(executor, self._executor_cls)(self)
+        return self._executor
+
+
+class NewFeature(_ExecutorCache, nn.Module):
+    """2D feature net, retrain/new_model_2d.py:78-165, on the HIP kernels
+    (``executor.FeatureExecutor``)."""
+
+    _executor_cls = "FeatureExecutor"
 
     def __init__(self, network_arch, cell_arch, args):
         super().__init__()
@@ -133,33 +131,18 @@ class NewFeature(nn.Module):
         specs = cell_specs(network_arch[: args.fea_num_layers], fm, bm)
         self.cells.extend(Cell(s, cell_arch, steps, bm, 2) for s in specs)
         _head_modules(self, initial_fm, 2, False)
+        self._executor = None
 
     def forward(self, x):
-        stem1 = self.stem1(self.stem0(x))
-        stem2 = self.stem2(stem1)
-        out = (stem1, stem2)
-        for cell in self.cells:
-            out = cell(out[0], out[1])
-        last = out[-1]
-        h, w = stem2.shape[2:]
-        up = lambda t, size: F.interpolate(t, size, mode="bilinear", align_corners=True)  # noqa: E731
-        if last.shape[2] == h:
-            fea = last
-        elif last.shape[2] == h // 2:
-            fea = up(self.last_6(last), [h, w])
-        elif last.shape[2] == h // 4:
-            fea = up(self.last_6(up(self.last_12(last), [h // 2, w // 2])), [h, w])
-        elif last.shape[2] == h // 8:
-            fea = up(self.last_6(up(self.last_12(up(self.last_24(last), [h // 4, w // 4])),
-                                    [h // 2, w // 2])), [h, w])
-        else:
-            # the reference raises UnboundLocalError here (new_model_2d.py:156-165)
-            raise ValueError(f"feature size {tuple(x.shape[2:])} is not legal for the feature net")
-        return self.last_3(fea)
+        if not x.is_cuda:
+            raise RuntimeError("leastereo_amd feature net runs on a ROCm device only")
+        return self.executor().run(x)
 
 
-class NewMatching(nn.Module):
+class NewMatching(_ExecutorCache, nn.Module):
     """Matching net parameters (retrain/skip_model_3d.py:78-138); forward on HIP."""
+
+    _executor_cls = "MatchingExecutor"
 
     def __init__(self, network_arch, cell_arch, args):
         super().__init__()
@@ -174,24 +157,6 @@ class NewMatching(nn.Module):
         self.conv1 = ConvBR(initial_fm * 4, initial_fm * 2, 3, 1, 1)
         self.conv2 = ConvBR(initial_fm * 4, initial_fm * 2, 3, 1, 1)
         self._executor = None
-
-    # parameter caches for the kernels are rebuilt whenever weights may have changed
-    def invalidate(self):
-        self._executor = None
-
-    def _apply(self, fn, *a, **kw):
-        self.invalidate()
-        return super()._apply(fn, *a, **kw)
-
-    def _load_from_state_dict(self, *a, **kw):
-        self.invalidate()
-        return super()._load_from_state_dict(*a, **kw)
-
-    def executor(self):
-        if self._executor is None:
-            from .executor import MatchingExecutor
-            self._executor = MatchingExecutor(self)
-        return self._executor
 
     def forward(self, cost):
         return self.executor().run(cost)
@@ -235,9 +200,8 @@ class LEAStereo(nn.Module):
         if not x.is_cuda:
             raise RuntimeError("leastereo_amd.LEAStereo runs the matching net on a ROCm device only")
         self.check_shape(x.shape[2], x.shape[3])
-        # LEAStereo.py:31-32 runs the feature net twice; in eval mode every layer is
-        # per-sample, so one call on the stacked pair halves the (launch-bound)
-        # torch/MIOpen kernel count.
+        # LEAStereo.py:31-32 runs the feature net twice; every layer is per-sample
+        # (eval-mode BN), so one call on the stacked pair halves the launch count.
         f = self.feature(torch.cat((x, y), 0))
         fx, fy = f[: x.shape[0]], f[x.shape[0]:]
         cost = kernels.build_cost_volume(fx, fy, self.maxdisp)

@@ -7,6 +7,7 @@ EPE of the PyTorch reference in fp32):
   ConvBR3d               |d| <= 1e-4 + 1e-4*|ref|  (fp32, K up to 3456, reassociated sums)
   trilinear resample     |d| <= 2e-6
   disparity regression   |d| <= 2e-5 px
+  ConvBR2d / feature net |d| <= 1e-4 + 1e-4*|ref| (per op), 1e-4 (whole net vs golden)
   end to end             EPE <= 1e-3 px vs reference fp32 and fp64 disparities
 """
 import numpy as np
@@ -120,7 +121,7 @@ def test_conv_two_plane_tiles_odd_depth(cin, cout, shape, acc):
     """Large volumes use 2 output planes per workgroup; odd D masks the last one.
     With ``acc`` the residual is prefetched into registers at workgroup start."""
     name = kernels.conv_kernel_name(1, cout, *shape, 3)
-    assert name.endswith(", 2>"), name
+    assert name.endswith(", 2, 3>"), name
     g = torch.Generator().manual_seed(cin + cout)
     x = torch.randn((1, cin) + shape, generator=g)
     w = torch.randn(cout, cin, 3, 3, 3, generator=g) / np.sqrt(cin * 27)
@@ -256,6 +257,68 @@ def test_disparity_vs_oracle_sizes():
         assert err.max() < 2e-3 and err.mean() < 1e-4, (err.max(), err.mean())
 
 
+# ------------------------------------------------------------------ 2D feature net
+@pytest.mark.parametrize("b,cin,cout,hw,res", [
+    (2, 3, 16, (96, 192), None), (1, 32, 32, (37, 53), "acc"), (2, 16, 48, (24, 40), "res"),
+    (1, 8, 8, (5, 3), "res"), (3, 12, 24, (17, 100), None), (1, 64, 64, (20, 33), "acc")])
+def test_conv2d_random_vs_torch(b, cin, cout, hw, res):
+    g = torch.Generator().manual_seed(cin * 7 + cout)
+    x = torch.randn((b, cin) + hw, generator=g)
+    w = torch.randn(cout, cin, 3, 3, generator=g) / np.sqrt(cin * 9)
+    scale = torch.rand(cout, generator=g) + 0.5
+    shift = torch.randn(cout, generator=g) * 0.1
+    r = torch.randn((b, cout) + hw, generator=g)
+    refy = F.conv2d(x.double(), w.double(), None, 1, 1)
+    refy = torch.relu(refy * scale.double().view(1, -1, 1, 1) + shift.double().view(1, -1, 1, 1))
+    if res:
+        refy = refy + r.double()
+    out = r.to(DEV).clone().unsqueeze(2) if res == "acc" else None
+    y = kernels.conv2d_bnrelu(x.to(DEV).unsqueeze(2), kernels.pack_conv2d_weight(w.to(DEV)), cout,
+                              scale.to(DEV), shift.to(DEV), relu=True, out=out,
+                              accumulate=res == "acc",
+                              residual=r.to(DEV).unsqueeze(2) if res == "res" else None)
+    np.testing.assert_allclose(y.squeeze(2).cpu().double().numpy(), refy.numpy(), rtol=1e-4, atol=1e-4)
+
+
+@pytest.mark.parametrize("b,cin,cout,hw", [(2, 16, 32, (96, 192)), (1, 5, 20, (31, 46)),
+                                           (1, 16, 32, (4, 3))])
+def test_conv2d_stride3_vs_torch(b, cin, cout, hw):
+    g = torch.Generator().manual_seed(cin + cout)
+    x = torch.randn((b, cin) + hw, generator=g)
+    w = torch.randn(cout, cin, 3, 3, generator=g) / np.sqrt(cin * 9)
+    scale = torch.rand(cout, generator=g) + 0.5
+    shift = torch.randn(cout, generator=g) * 0.1
+    refy = F.conv2d(x.double(), w.double(), None, 3, 1)
+    refy = torch.relu(refy * scale.double().view(1, -1, 1, 1) + shift.double().view(1, -1, 1, 1))
+    y = kernels.conv2d_s3_bnrelu(x.to(DEV).unsqueeze(2), w.to(DEV), scale.to(DEV), shift.to(DEV))
+    assert y.shape[3:] == refy.shape[2:]
+    np.testing.assert_allclose(y.squeeze(2).cpu().double().numpy(), refy.numpy(), rtol=1e-5, atol=1e-5)
+
+
+def test_feature_net_golden():
+    """HIP feature net vs the reference's own feature map (e2e fixture)."""
+    m = _model(48)
+    c = CASES["e2e/b1_h96_w192_md48"]
+    x = normal(c["seeds"][0], (1, 3, 96, 192)).to(DEV)
+    with torch.no_grad():
+        f = m.feature(x)
+    np.testing.assert_allclose(f.cpu().numpy(), golden("e2e")["b1_h96_w192_md48/fea_l"],
+                               rtol=1e-4, atol=1e-4)
+
+
+def test_feature_net_vs_oracle_c1_size():
+    """288x576 (config 1 crop), batch 2: HIP feature net vs the oracle on the GPU."""
+    m = _model(96)
+    x = normal(77, (2, 3, 288, 576)).to(DEV)
+    sd = {k: v.to(DEV) for k, v in state_dict().items()}
+    with torch.no_grad():
+        f = m.feature(x)
+        a = arch()
+        want = ref.feature_forward(sd, x, a["net_arch_fea"], a["cell_arch_fea"])
+    assert f.shape == want.shape
+    np.testing.assert_allclose(f.cpu().numpy(), want.cpu().numpy(), rtol=1e-3, atol=1e-3)
+
+
 # ----------------------------------------------------------------------- end to end
 @pytest.mark.parametrize("name", _cases("e2e"))
 def test_e2e_golden(name):
@@ -277,10 +340,8 @@ def test_e2e_golden(name):
 
 
 def test_batch_rows_are_independent():
-    """On the HIP path (cost volume -> matching -> disparity) a B=2 batch equals
-    the two B=1 runs bit for bit: no cross-pair mixing, batch-invariant
-    arithmetic.  (The torch/MIOpen feature net may choose batch-dependent
-    algorithms, so it is checked with a tolerance instead.)"""
+    """A B=2 batch equals the two B=1 runs bit for bit (feature net, cost volume,
+    matching, disparity): no cross-pair mixing, batch-invariant arithmetic."""
     m = _model(48)
     left = normal(901, (2, 3, 96, 192)).to(DEV)
     right = normal(902, (2, 3, 96, 192)).to(DEV)
@@ -292,7 +353,7 @@ def test_batch_rows_are_independent():
         assert torch.equal(both, one)
         e2e_both = m(left, right)
         e2e_one = torch.cat([m(left[i:i + 1], right[i:i + 1]) for i in range(2)])
-    assert ref.epe(e2e_both.cpu(), e2e_one.cpu()) < 1e-4
+    assert torch.equal(e2e_both, e2e_one)
 
 
 def test_full_size_c2_vs_torch_oracle_on_gpu():

@@ -63,17 +63,11 @@ def test_shape_legality_spatial():
         m.check_shape(540, 960)
 
 
-def test_feature_net_torch_path_matches_golden():
-    """The product keeps the 2D feature net on PyTorch; on CPU its math must
-    match the reference's feature outputs."""
+def test_feature_net_refuses_cpu():
+    """No torch fallback: the feature net runs on the HIP kernels only."""
     m = _model(48)
-    m.load_state_dict(state_dict(), strict=True)
-    m.eval()
-    c = meta()["cases"]["e2e/b1_h96_w192_md48"]
-    x = normal(c["seeds"][0], (1, 3, 96, 192))
-    with torch.no_grad():
-        f = m.feature(x)
-    np.testing.assert_allclose(f.numpy(), golden("e2e")["b1_h96_w192_md48/fea_l"], rtol=1e-4, atol=1e-4)
+    with pytest.raises(RuntimeError):
+        m.feature(torch.zeros(1, 3, 96, 192))
 
 
 def test_forward_refuses_cpu():
