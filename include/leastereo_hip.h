@@ -89,6 +89,18 @@ int lea_conv3d_bnrelu_resampled(const void* x, int64_t x_bstride, int Di, int Hi
                                 int B, int cin, int cout, int D, int H, int W, int k,
                                 unsigned flags, int dtype, void* stream);
 
+/* Matching-net stem0 on the cost volume without materialising it: the ConvBR3d
+ * (3x3x3) of cost = [B, 2C, D3, H, W] as built by lea_build_cost_volume
+ * (retrain/LEAStereo.py:34-48 then skip_model_3d.py:141), reading the feature maps
+ * left/right [B, C, H, W] (batch stride f_bstride) directly.  Bit-identical to
+ * lea_build_cost_volume + lea_conv3d_bnrelu; saves the 2*4*B*C*D3*H*W-byte volume's
+ * write and read.  C must be a multiple of 4.  y: [B, cout, D3, H, W]. */
+int lea_conv3d_bnrelu_costvolume(const void* left, const void* right, int64_t f_bstride,
+                                 const float* w_packed, const float* scale, const float* shift,
+                                 void* y, int64_t y_bstride, int B, int C, int cout, int D3,
+                                 int H, int W, unsigned flags, int dtype, void* stream);
+const char* lea_conv3d_costvolume_kernel_name(int B, int cout, int D3, int H, int W);
+
 /* Name of the kernel instantiation a conv of this output shape launches
  * (matches the demangled name rocprofv3 reports); NULL if unsupported. */
 const char* lea_conv3d_kernel_name(int B, int cout, int D, int H, int W, int k, int resampled);

@@ -36,6 +36,9 @@ SIGNATURES = {
                                          _i, _i, _i, _i, _i, _i, _i, _u, _i, _p]),
     "lea_conv3d_kernel_name": (ctypes.c_char_p, [_i, _i, _i, _i, _i, _i, _i]),
     "lea_conv3d_set_tile_override": (_i, [_i, _i, _i]),
+    "lea_conv3d_bnrelu_costvolume": (_i, [_p, _p, _i64, _p, _p, _p, _p, _i64, _i, _i, _i, _i, _i,
+                                          _i, _u, _i, _p]),
+    "lea_conv3d_costvolume_kernel_name": (ctypes.c_char_p, [_i, _i, _i, _i, _i]),
     "lea_conv2d_packed_floats": (ctypes.c_size_t, [_i, _i]),
     "lea_conv2d_pack_weights": (_i, [_p, _p, _i, _i, _p]),
     "lea_conv2d_bnrelu": (_i, [_p, _i64, _p, _p, _p, _p, _i64, _p, _i64, _i, _i, _i, _i, _i, _u,

@@ -724,6 +724,66 @@ extern "C" int lea_conv2d_bnrelu(const void* x, int64_t x_bstride, const float* 
   }
 }
 
+extern "C" const char* lea_conv3d_costvolume_kernel_name(int B, int cout, int D3, int H, int W) {
+  if (B <= 0 || cout <= 0 || D3 <= 0 || H <= 0 || W <= 0) return nullptr;
+  const lea::Plan p = lea::make_plan(B, cout, D3, H, W, 3, false);
+  if (p.engine != 0) return nullptr;
+  snprintf(lea::g_name, sizeof(lea::g_name), "conv3d_dma_kernel<%d, %d, %d, %d, 3, true>", p.mt, p.nt,
+           p.tw, p.td);
+  return lea::g_name;
+}
+
+extern "C" int lea_conv3d_bnrelu_costvolume(const void* left, const void* right, int64_t f_bstride,
+                                            const float* w_packed, const float* scale,
+                                            const float* shift, void* y, int64_t y_bstride, int B,
+                                            int C, int cout, int D3, int H, int W, unsigned flags,
+                                            int dtype, void* stream) {
+  using namespace lea;
+  clear_error();
+  ConvArgs a{};
+  a.x = (const float*)left;
+  a.xbs = f_bstride;
+  a.x2 = (const float*)right;
+  a.x2bs = f_bstride;
+  a.cin1 = C;
+  a.wp = w_packed;
+  a.scale = scale;
+  a.shift = shift;
+  a.y = (float*)y;
+  a.ybs = y_bstride;
+  a.cin = 2 * C;
+  a.cout = cout;
+  a.D = D3;
+  a.H = H;
+  a.W = W;
+  a.flags = flags & LEA_RELU;
+  LEA_CHECK_ARG(left && right && w_packed && y && y != left && y != right,
+                "lea_conv3d_bnrelu_costvolume: null or aliased pointer");
+  LEA_CHECK_ARG((scale == nullptr) == (shift == nullptr),
+                "lea_conv3d_bnrelu_costvolume: scale/shift must both be set or both NULL");
+  LEA_CHECK_ARG(B > 0 && C > 0 && cout > 0 && D3 > 0 && H > 0 && W > 0,
+                "lea_conv3d_bnrelu_costvolume: bad shape B=%d C=%d cout=%d D3=%d H=%d W=%d", B, C,
+                cout, D3, H, W);
+  constexpr int kCinB = PackCfg<3, 1>::CIN_B;  // chunks must not straddle left/right
+  LEA_CHECK_ARG(C % kCinB == 0, "lea_conv3d_bnrelu_costvolume: C=%d must be a multiple of %d", C,
+                kCinB);
+  LEA_CHECK_ARG((long long)D3 * H * W * 4 < (1LL << 32), "lea_conv3d_bnrelu_costvolume: volume too large");
+  if (dtype != LEA_F32) {
+    set_error("lea_conv3d_bnrelu_costvolume: dtype %d unsupported", dtype);
+    return LEA_E_UNSUPPORTED;
+  }
+  const Plan p = make_plan(B, cout, D3, H, W, 3, false);
+  LEA_CHECK_ARG(p.engine == 0, "lea_conv3d_bnrelu_costvolume: no DMA plan for cout=%d", cout);
+  a.ncob = (cout + p.mt * 16 - 1) / (p.mt * 16);
+  hipStream_t st = as_stream(stream);
+  switch (p.mt) {
+    case 1: return run_dma_cv_mt1(p, a, B, st);
+    case 2: return run_dma_cv_mt2(p, a, B, st);
+    case 3: return run_dma_cv_mt3(p, a, B, st);
+    default: return run_dma_cv_mt4(p, a, B, st);
+  }
+}
+
 extern "C" int lea_conv3d_bnrelu_resampled(const void* x, int64_t x_bstride, int Di, int Hi,
                                            int Wi, const float* w_packed, const float* scale,
                                            const float* shift, const void* residual,

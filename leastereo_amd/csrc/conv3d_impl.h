@@ -276,7 +276,12 @@ __device__ __forceinline__ void epilogue_pre(const ConvArgs& a, const f32x4 (&ac
 }
 
 // ------------------------------------------------------------- LDS-DMA engine (k=3)
-template <int MT, int NT, int TW, int TD, int KD = 3>
+// CV: the input is LEAStereo's cost volume (retrain/LEAStereo.py:34-48), never
+// materialised -- x / x2 are the left / right feature maps [B, cin1, H, W] and the
+// staged value of channel c < cin1 at (disparity d, h, w) is left[c][h][w], of
+// channel cin1 + c right[c][h][w - d], both 0 for w < d: per lane two offset sets
+// (left, right) whose out-of-range entries make the buffer load return the zero.
+template <int MT, int NT, int TW, int TD, int KD = 3, bool CV = false>
 __global__ __launch_bounds__(kConvThreads, 2) void conv3d_dma_kernel(const ConvArgs a) {
   using C = TileCfg<3, MT, NT, TW, TD, KD>;
   constexpr int XSLOTS = (C::IMG + 63) / 64;  // 256-B DMA pieces per channel image
@@ -312,21 +317,30 @@ __global__ __launch_bounds__(kConvThreads, 2) void conv3d_dma_kernel(const ConvA
 
   // Per-lane byte offsets of this wave's DMA pieces inside one channel volume;
   // identical for every channel and chunk.  Outside the volume -> beyond nrec -> 0.
-  unsigned voff[XSLOTS_W];
+  unsigned voff[XSLOTS_W], voffr[CV ? XSLOTS_W : 1];
 #pragma unroll
   for (int t = 0; t < XSLOTS_W; ++t) {
     const int e = (wave + kConvWaves * t) * 64 + lane;
-    unsigned v = 0xFFFFFFF0u;
+    unsigned v = 0xFFFFFFF0u, vr = 0xFFFFFFF0u;
     if (e < C::IMG) {
       const int kd = e / C::PLANE;
       const int r = e - kd * C::PLANE;
       const int rr = r / C::RW;
       const int cc = r - rr * C::RW;
       const int d = d0 + kd - KD / 2, h = h0 + rr - 1, w = w0 + cc - 1;
-      if ((unsigned)d < (unsigned)a.D && (unsigned)h < (unsigned)a.H && (unsigned)w < (unsigned)a.W)
-        v = (unsigned)(d * HW + h * a.W + w) * 4u;
+      if ((unsigned)d < (unsigned)a.D && (unsigned)h < (unsigned)a.H && (unsigned)w < (unsigned)a.W) {
+        if constexpr (CV) {
+          if (w >= d) {
+            v = (unsigned)(h * a.W + w) * 4u;
+            vr = (unsigned)(h * a.W + w - d) * 4u;
+          }
+        } else {
+          v = (unsigned)(d * HW + h * a.W + w) * 4u;
+        }
+      }
     }
     voff[t] = v;
+    if constexpr (CV) voffr[t] = vr;
   }
 
   auto issue = [&](int ch, float* st) {
@@ -343,20 +357,25 @@ __global__ __launch_bounds__(kConvThreads, 2) void conv3d_dma_kernel(const ConvA
       const int c = ch * C::CIN_B + ci;
       const float* base = a.x;
       unsigned n = 0;
+      const long long cvol = CV ? (long long)HW : (long long)HW * a.D;  // channel stride
+      const unsigned crec = CV ? (unsigned)HW * 4u : nrec;
       if (c < a.cin1) {
-        base = a.x + (long long)b * a.xbs + (long long)c * HW * a.D;
-        n = nrec;
+        base = a.x + (long long)b * a.xbs + (long long)c * cvol;
+        n = crec;
       } else if (c < a.cin) {
-        base = a.x2 + (long long)b * a.x2bs + (long long)(c - a.cin1) * HW * a.D;
-        n = nrec;
+        base = a.x2 + (long long)b * a.x2bs + (long long)(c - a.cin1) * cvol;
+        n = crec;
       }
       const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)base, 0, n, 0x00020000);
+      const bool right = CV && c >= a.cin1;  // uniform: chunks never straddle cin1 in CV
 #pragma unroll
       for (int t = 0; t < XSLOTS_W; ++t) {
         const int j = wave + kConvWaves * t;
+        unsigned vo = voff[t];
+        if constexpr (CV) vo = right ? voffr[t] : voff[t];
         if (j < XSLOTS && j * 64 + lane < C::IMG)
           __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void*)(st + ci * C::CIS + j * 64), 4,
-                                                   voff[t], 0, 0, 0);
+                                                   vo, 0, 0, 0);
       }
     }
   };
@@ -440,6 +459,10 @@ int launch_dma(K kernel, const ConvArgs& a0, int th, int tw, int td, int B, hipS
   LEA_DMA_TW_ALL(X, 4, 1, 1) LEA_DMA_TW_ALL(X, 4, 2, 1) LEA_DMA_TW_ALL(X, 4, 1, 2)      \
   X(4, 2, 16, 2) X(4, 2, 32, 2)
 
+// Cost-volume-input tiles (matching-net stem0): the planner's 8 x 16 / 4 x 16 tiles.
+#define LEA_DMA_CV_LIST(X, MT) \
+  X(MT, 1, 16, 1, 3) X(MT, 2, 16, 1, 3) X(MT, 1, 16, 2, 3) X(MT, 2, 16, 2, 3)
+
 // 2D (KD = 1) tiles for the feature net: one plane per workgroup.
 #define LEA_DMA2D_LIST(X, MT) X(MT, 1, 16, 1, 1) X(MT, 2, 16, 1, 1)
 
@@ -449,6 +472,13 @@ int launch_dma(K kernel, const ConvArgs& a0, int th, int tw, int td, int B, hipS
   int dma_lds_bytes_mt##MT(int nt, int tw, int td);                       \
   int run_dma_mt##MT(const Plan& p, const ConvArgs& a, int B, hipStream_t st);   \
   int run_dma2d_mt##MT(const Plan& p, const ConvArgs& a, int B, hipStream_t st);
+#define LEA_DMA_DECL_CV(MT) \
+  int run_dma_cv_mt##MT(const Plan& p, const ConvArgs& a, int B, hipStream_t st);
+LEA_DMA_DECL_CV(1)
+LEA_DMA_DECL_CV(2)
+LEA_DMA_DECL_CV(3)
+LEA_DMA_DECL_CV(4)
+#undef LEA_DMA_DECL_CV
 LEA_DMA_DECL(1)
 LEA_DMA_DECL(2)
 LEA_DMA_DECL(3)
@@ -465,6 +495,10 @@ LEA_DMA_DECL(4)
   if (p.nt == NT && p.tw == TW && p.td == TD)                                             \
     return launch_dma(conv3d_dma_kernel<MT, NT, TW, TD, KD>,                              \
                       a, TileCfg<3, MT, NT, TW, TD, KD>::TH, TW, TD, B, st);
+#define LEA_DMA_CV_RUN_CASE(MT, NT, TW, TD, KD)                                          \
+  if (p.nt == NT && p.tw == TW && p.td == TD)                                             \
+    return launch_dma(conv3d_dma_kernel<MT, NT, TW, TD, KD, true>,                        \
+                      a, TileCfg<3, MT, NT, TW, TD, KD>::TH, TW, TD, B, st);
 #define LEA_DMA_TU(MT)                                                            \
   int dma_lds_bytes_mt##MT(int nt, int tw, int td) {                              \
     LEA_DMA_LIST_##MT(LEA_DMA_LDS_CASE) return 0;                                 \
@@ -477,6 +511,11 @@ LEA_DMA_DECL(4)
   int run_dma2d_mt##MT(const Plan& p, const ConvArgs& a, int B, hipStream_t st) { \
     LEA_DMA2D_LIST(LEA_DMA2D_RUN_CASE, MT)                                        \
     set_error("lea_conv2d: no DMA tile <%d, %d, %d, 1, 1>", MT, p.nt, p.tw);     \
+    return LEA_E_UNSUPPORTED;                                                     \
+  }                                                                               \
+  int run_dma_cv_mt##MT(const Plan& p, const ConvArgs& a, int B, hipStream_t st) { \
+    LEA_DMA_CV_LIST(LEA_DMA_CV_RUN_CASE, MT)                                      \
+    set_error("lea_conv3d_costvolume: no tile <%d, %d, %d, %d>", MT, p.nt, p.tw, p.td); \
     return LEA_E_UNSUPPORTED;                                                     \
   }
 

@@ -183,7 +183,20 @@ class CellGraphExecutor:
 class MatchingExecutor(CellGraphExecutor):
     def run(self, x):
         """newMatching.forward (skip_model_3d.py:140-174): [B,64,D3,H3,W3] -> [B,1,D3,H3,W3]."""
-        stem0 = self.conv("stem0", x)
+        return self._from_stem0(self.conv("stem0", x))
+
+    def run_features(self, fl, fr, maxdisp):
+        """build_cost_volume + newMatching.forward (LEAStereo.py:34-50) with the cost
+        volume read in place by stem0's conv (never materialised)."""
+        p = self.p["stem0"]
+        if fl.shape[1] * 2 != p.cin:
+            raise ValueError(f"stem0 expects {p.cin} cost-volume channels, got 2*{fl.shape[1]}")
+        stem0 = kernels.conv3d_bnrelu_costvolume(fl, fr, maxdisp, p.packed, p.cout, p.scale,
+                                                 p.shift, p.relu)
+        return self._from_stem0(stem0)
+
+    def _from_stem0(self, stem0):
+        d, h, w = stem0.shape[2:]
         stem1 = self.conv("stem1", stem0)
         outs = []
         prev = (stem0, stem1)
@@ -199,7 +212,6 @@ class MatchingExecutor(CellGraphExecutor):
             outs.append(o)
             prev = o
         last = outs[-1][1]
-        d, h, w = x.shape[2:]
         lh = last.shape[3]
         full, half, quarter = (d, h, w), (d // 2, h // 2, w // 2), (d // 4, h // 4, w // 4)
         # head (:161-173): the 1x1 Upsample pairs run commuted (see conv()); the final

@@ -106,12 +106,13 @@ def pack_conv_weight(w: torch.Tensor) -> torch.Tensor:
     return packed
 
 
-def _probe_begin(b, cin, cout, d, h, w, k, accumulate, in_vox, resampled):
+def _probe_begin(b, cin, cout, d, h, w, k, accumulate, in_vox, resampled, name=None):
     """Start HIP-event timing of this launch if the active probe wants its kernel."""
     probe = _probe
     if probe is None:
         return None
-    name = conv_kernel_name(b, cout, d, h, w, k, resampled)
+    if name is None:
+        name = conv_kernel_name(b, cout, d, h, w, k, resampled)
     if probe.names is not None and name not in probe.names:
         return None
     vox = b * d * h * w
@@ -186,6 +187,36 @@ def conv3d_bnrelu(x: torch.Tensor, packed: torch.Tensor, cout: int, k: int,
         shift.data_ptr() if shift is not None else None,
         rptr, rbs, out.data_ptr(), ybs, b, cin + cin2, cout, d, h, w, k, flags, LEA_F32, _stream()),
         "lea_conv3d_bnrelu")
+    _probe_end(rec)
+    return out
+
+
+def costvolume_kernel_name(b, cout, d3, h, w):
+    name = _lib.load().lea_conv3d_costvolume_kernel_name(b, cout, d3, h, w)
+    return name.decode() if name else None
+
+
+def conv3d_bnrelu_costvolume(fl: torch.Tensor, fr: torch.Tensor, maxdisp: int, packed: torch.Tensor,
+                             cout: int, scale: torch.Tensor | None, shift: torch.Tensor | None,
+                             relu: bool = True) -> torch.Tensor:
+    """ConvBR3d 3x3x3 of the cost volume of (fl, fr) (LEAStereo.py:34-48 then
+    skip_model_3d.py:141) without materialising the volume; bit-identical to
+    ``conv3d_bnrelu(build_cost_volume(fl, fr, maxdisp), ...)``."""
+    _require_cuda(fl, fr, packed, scale, shift)
+    if fl.shape != fr.shape or fl.dim() != 4:
+        raise ValueError("left/right features must both be [B, C, H, W]")
+    if fl.stride() != fr.stride() or fl.stride()[1:] != (fl.shape[2] * fl.shape[3], fl.shape[3], 1):
+        raise ValueError("left/right features need contiguous C,H,W and equal strides")
+    b, c, h, w = fl.shape
+    d3 = int(maxdisp / 3)
+    out = torch.empty((b, cout, d3, h, w), device=fl.device, dtype=fl.dtype)
+    rec = _probe_begin(b, 2 * c, cout, d3, h, w, 3, False, 0, False,
+                       name=costvolume_kernel_name(b, cout, d3, h, w))
+    check(_lib.load().lea_conv3d_bnrelu_costvolume(
+        fl.data_ptr(), fr.data_ptr(), fl.stride(0), packed.data_ptr(),
+        scale.data_ptr() if scale is not None else None,
+        shift.data_ptr() if shift is not None else None, out.data_ptr(), out.stride(0), b, c, cout,
+        d3, h, w, LEA_RELU if relu else 0, LEA_F32, _stream()), "lea_conv3d_bnrelu_costvolume")
     _probe_end(rec)
     return out
 

@@ -204,6 +204,6 @@ class LEAStereo(nn.Module):
         # (eval-mode BN), so one call on the stacked pair halves the launch count.
         f = self.feature(torch.cat((x, y), 0))
         fx, fy = f[: x.shape[0]], f[x.shape[0]:]
-        cost = kernels.build_cost_volume(fx, fy, self.maxdisp)
-        cost = self.matching(cost)
+        # cost volume (:34-48) + matching (:50): stem0 reads the volume in place
+        cost = self.matching.executor().run_features(fx, fy, self.maxdisp)
         return self.disp(cost)

@@ -257,6 +257,28 @@ def test_disparity_vs_oracle_sizes():
         assert err.max() < 2e-3 and err.mean() < 1e-4, (err.max(), err.mean())
 
 
+@pytest.mark.parametrize("b,c,cout,maxdisp,hw", [(2, 32, 32, 48, (12, 40)), (1, 4, 16, 27, (5, 7)),
+                                                  (1, 32, 32, 192, (30, 100)), (1, 8, 48, 9, (9, 18))])
+def test_costvolume_stem0_is_bit_identical(b, c, cout, maxdisp, hw):
+    """stem0 reading the cost volume in place == building it, then convolving."""
+    g = torch.Generator().manual_seed(c + cout + maxdisp)
+    fl = torch.randn((b, c) + hw, generator=g).to(DEV)
+    fr = torch.randn((b, c) + hw, generator=g).to(DEV)
+    w = (torch.randn(cout, 2 * c, 3, 3, 3, generator=g) / np.sqrt(2 * c * 27)).to(DEV)
+    scale = (torch.rand(cout, generator=g) + 0.5).to(DEV)
+    shift = (torch.randn(cout, generator=g) * 0.1).to(DEV)
+    packed = kernels.pack_conv_weight(w)
+    want = kernels.conv3d_bnrelu(kernels.build_cost_volume(fl, fr, maxdisp), packed, cout, 3, scale,
+                                 shift, relu=True)
+    got = kernels.conv3d_bnrelu_costvolume(fl, fr, maxdisp, packed, cout, scale, shift, relu=True)
+    assert torch.equal(got, want)
+    refy = F.conv3d(ref.build_cost_volume(fl.cpu().double(), fr.cpu().double(), maxdisp),
+                    w.cpu().double(), None, 1, 1)
+    refy = torch.relu(refy * scale.cpu().double().view(1, -1, 1, 1, 1)
+                      + shift.cpu().double().view(1, -1, 1, 1, 1))
+    np.testing.assert_allclose(got.cpu().double().numpy(), refy.numpy(), rtol=1e-4, atol=1e-4)
+
+
 # ------------------------------------------------------------------ 2D feature net
 @pytest.mark.parametrize("b,cin,cout,hw,res", [
     (2, 3, 16, (96, 192), None), (1, 32, 32, (37, 53), "acc"), (2, 16, 48, (24, 40), "res"),
