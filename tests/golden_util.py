@@ -44,3 +44,15 @@ def arch():
 
 def normal(seed, shape):
     return torch.from_numpy(seeded_normal(seed, shape))
+
+
+def c1_inputs():
+    """Config-1 fixture -> (left, right) [1, 3, 288, 576] float32 exactly as
+    predict.py's load_data + test_transform make them (whole-image statistics)."""
+    g = golden("c1_sceneflow")
+    planes = []
+    for i, img in enumerate((g["left_u8"], g["right_u8"])):
+        for c in range(3):
+            planes.append(((img[:, :, c] - g["mean"][3 * i + c]) / g["std"][3 * i + c]).astype(np.float32))
+    x = np.stack(planes)
+    return torch.from_numpy(x[None, 0:3].copy()), torch.from_numpy(x[None, 3:6].copy())

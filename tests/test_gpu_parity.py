@@ -19,7 +19,7 @@ from leastereo_amd import kernels
 from leastereo_amd.config import LEAStereoArgs, default_arch_args
 from leastereo_amd.model import LEAStereo
 from oracle import torch_ref as ref
-from tests.golden_util import arch, golden, meta, normal, state_dict
+from tests.golden_util import arch, c1_inputs, golden, meta, normal, state_dict
 
 pytestmark = pytest.mark.gpu
 DEV = "cuda"
@@ -361,6 +361,40 @@ def test_e2e_golden(name):
     assert e32 < 1e-3 and e64 < 1e-3, (e32, e64)
 
 
+def test_c1_sceneflow_pair_vs_reference():
+    """Config 1 (SceneFlow 0001, predict.py preprocessing, 288x576 D96) on the HIP
+    model vs the reference model's disparity for the same inputs."""
+    from leastereo_amd import predict as P
+    c = meta()["c1"]
+    left, right = c1_inputs()
+    m = _model(c["maxdisp"])
+    with torch.no_grad():
+        d = m(left.to(DEV), right.to(DEV)).cpu().numpy()
+    disp = P.crop_output(d, *c["full_hw"], *c["crop_hw"])
+    assert ref.epe(torch.from_numpy(disp), torch.from_numpy(golden("c1_sceneflow")["disp"])) < 1e-3
+
+
+def test_predict_cli_runs_on_a_list(tmp_path):
+    """predict.py's list loop end to end on PNG files (sceneflow layout)."""
+    from PIL import Image
+    from leastereo_amd import predict as P
+    g = golden("c1_sceneflow")
+    for side in ("left", "right"):
+        d = tmp_path / "frames_finalpass" / "S" / side
+        d.mkdir(parents=True)
+        Image.fromarray(g[side + "_u8"][:96, :192]).save(d / "0001.png")
+    (tmp_path / "list.txt").write_text("S/left/0001.png\n")
+    # a DataParallel-style checkpoint ('module.' keys), as predict.py:55-65 loads
+    torch.save({"state_dict": {"module." + k: v for k, v in state_dict().items()}},
+               tmp_path / "ckpt.pth")
+    rc = P.main(["--sceneflow=1", "--maxdisp=48", "--crop_height=96", "--crop_width=192",
+                 f"--data_path={tmp_path}/", f"--test_list={tmp_path}/list.txt",
+                 f"--save_path={tmp_path}/out/", f"--resume={tmp_path}/ckpt.pth"])
+    assert rc == 0
+    out = np.load(tmp_path / "out" / "0.npy")
+    assert out.shape == (96, 192) and np.isfinite(out).all()
+
+
 def test_batch_rows_are_independent():
     """A B=2 batch equals the two B=1 runs bit for bit (feature net, cost volume,
     matching, disparity): no cross-pair mixing, batch-invariant arithmetic."""
@@ -376,6 +410,26 @@ def test_batch_rows_are_independent():
         e2e_both = m(left, right)
         e2e_one = torch.cat([m(left[i:i + 1], right[i:i + 1]) for i in range(2)])
     assert torch.equal(e2e_both, e2e_one)
+
+
+@pytest.mark.parametrize("b,h,w,maxdisp,oracle_dev", [(1, 1008, 1512, 264, "cpu"),
+                                                      (2, 384, 1248, 192, DEV)])
+def test_large_configs_vs_torch_oracle(b, h, w, maxdisp, oracle_dev):
+    """Config 5 (Middlebury 1008x1512, D264 -- D256 is illegal in the reference) and
+    config 3's KITTI shape (384x1248 D192, here fp32, batch 2): HIP vs the oracle,
+    EPE <= 1e-3 px per pair.  (At config 5 MIOpen falls back to naive 3D convs, so
+    that oracle runs on the host CPU.)"""
+    m = _model(maxdisp)
+    left = normal(4321 + h, (b, 3, h, w))
+    right = normal(4322 + h, (b, 3, h, w))
+    sd = {k: v.to(oracle_dev) for k, v in state_dict().items()}
+    with torch.no_grad():
+        disp = m(left.to(DEV), right.to(DEV)).cpu()
+        want = ref.leastereo_forward(sd, left.to(oracle_dev), right.to(oracle_dev), maxdisp,
+                                     arch()).cpu()
+    assert disp.shape == (b, h, w) and torch.isfinite(disp).all()
+    for i in range(b):
+        assert ref.epe(disp[i], want[i]) < 1e-3
 
 
 def test_full_size_c2_vs_torch_oracle_on_gpu():
