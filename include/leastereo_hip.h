@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define LEA_ABI_VERSION 2
+#define LEA_ABI_VERSION 3
 
 #define LEA_F32 0
 #define LEA_BF16 1
@@ -156,11 +156,14 @@ int lea_resample3d_trilinear(const void* x, int64_t x_bstride, void* y, int64_t 
  * computed at the low resolution (lea_conv3d_bnrelu, k=1, 27*cout outputs),
  *   y_out[b][co](v) = act(scale[co] * sum_tap interp(q[b][co*27+tap])(v + off(tap)) + shift[co])
  * over the [Do, Ho, Wo] output, taps outside it contributing 0 (zero padding).
- * q: [B, 27*cout, Di, Hi, Wi]; y_out: [B, cout, Do, Ho, Wo]. */
+ * q: [B, 27*cout, Di, Hi, Wi]; y_out: [B, cout, Do, Ho, Wo].  workspace: device
+ * scratch of lea_tapsum_workspace_bytes(B, cout, Hi, Wi, Do) bytes, 16-B aligned
+ * (the d-interpolated partial sums; the caller owns it, as every buffer here). */
+size_t lea_tapsum_workspace_bytes(int B, int cout, int Hi, int Wi, int Do);
 int lea_tapsum_upsample(const void* q, int64_t q_bstride, void* y, int64_t y_bstride,
                         int B, int cout, int Di, int Hi, int Wi, int Do, int Ho, int Wo,
                         const float* scale, const float* shift, unsigned flags,
-                        int dtype, void* stream);
+                        void* workspace, int dtype, void* stream);
 
 /* Disparity regression.  Replaces models/build_model_2d.py:52-57 + :33-42:
  *   U = trilinear(cost, [maxdisp, 3*H3, 3*W3], align_corners=False)

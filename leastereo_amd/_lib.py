@@ -12,7 +12,7 @@ LIB_PATH = os.environ.get(
     "LEASTEREO_HIP_LIB",
     os.path.join(os.path.dirname(os.path.abspath(__file__)), "libleastereo_hip.so"))
 
-ABI_VERSION = 2
+ABI_VERSION = 3
 LEA_F32 = 0
 LEA_BF16 = 1
 LEA_RELU = 1
@@ -47,8 +47,9 @@ SIGNATURES = {
     "lea_conv2d_s3_bnrelu": (_i, [_p, _i64, _p, _p, _p, _p, _i64, _i, _i, _i, _i, _i, _u, _i, _p]),
     "lea_resample3d_trilinear": (_i, [_p, _i64, _p, _i64, _i, _i, _i, _i, _i, _i, _i, _i,
                                       _i, _p, _p, _u, _i, _p]),
+    "lea_tapsum_workspace_bytes": (ctypes.c_size_t, [_i, _i, _i, _i, _i]),
     "lea_tapsum_upsample": (_i, [_p, _i64, _p, _i64, _i, _i, _i, _i, _i, _i, _i, _i, _p, _p, _u,
-                                 _i, _p]),
+                                 _p, _i, _p]),
     "lea_disparity_regression": (_i, [_p, _p, _i, _i, _i, _i, _i, _i, _p]),
 }
 

@@ -73,7 +73,9 @@ __global__ __launch_bounds__(kConvThreads, 2) void conv3d_reg_kernel(const ConvA
 #pragma unroll 4
       for (int i = tid; i < C::WS / 4; i += kConvThreads) dst[i] = src[i];
     }
-#pragma unroll 4
+    // RESAMPLE: 8 gathered loads per staged value; unroll deep enough that a
+    // thread keeps ~64 loads in flight (the loop is latency-bound otherwise)
+#pragma unroll 8
     for (int i = tid; i < CIN_B * C::IMG; i += kConvThreads) {
       const int ci = i / C::IMG;
       int rem = i - ci * C::IMG;

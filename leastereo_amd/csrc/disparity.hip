@@ -43,14 +43,24 @@ __device__ __forceinline__ AxisW src_axis(float ratio, int o, int in, int out) {
   return a;
 }
 
-__global__ __launch_bounds__(256) void disparity_f32(const float* __restrict__ cost,
-                                                     float* __restrict__ disp, int D3, int H3,
-                                                     int W3, int maxdisp, float rd, float rh,
-                                                     float rw) {
+constexpr int kDispThreads = 256;
+constexpr int kDispChunk = 16;  // cost planes fetched per batch of loads
+
+// LDS: the depth axis table (identical for every pixel) and, per thread, one
+// batch of bilinearly interpolated cost planes (own column: conflict-free).
+__global__ __launch_bounds__(kDispThreads) void disparity_f32(const float* __restrict__ cost,
+                                                              float* __restrict__ disp, int D3,
+                                                              int H3, int W3, int maxdisp,
+                                                              float rd, float rh, float rw) {
 #pragma clang fp contract(off)
+  extern __shared__ float lds[];
+  AxisW* tab = reinterpret_cast<AxisW*>(lds);                      // [maxdisp]
+  float* pv = lds + 4 * maxdisp;                                   // [kDispChunk + 1][threads]
+  for (int od = threadIdx.x; od < maxdisp; od += blockDim.x) tab[od] = src_axis(rd, od, D3, maxdisp);
+  __syncthreads();
   const int Ho = 3 * H3, Wo = 3 * W3;
   const int ow = blockIdx.x * blockDim.x + threadIdx.x;
-  if (ow >= Wo) return;
+  if (ow >= Wo) return;  // no barrier below
   const int oh = blockIdx.y;
   const int b = blockIdx.z;
   const AxisW ah = src_axis(rh, oh, H3, Ho);
@@ -59,40 +69,37 @@ __global__ __launch_bounds__(256) void disparity_f32(const float* __restrict__ c
   const float* base = cost + (long long)b * D3 * HW;
   const float* r0 = base + (long long)ah.i0 * W3;
   const float* r1 = base + (long long)ah.i1 * W3;
+  float* col = pv + threadIdx.x;
 
-  auto plane = [&](int dd) -> float {
-    const long long o = (long long)dd * HW;
-    return ah.l0 * (aw.l0 * r0[o + aw.i0] + aw.l1 * r0[o + aw.i1]) +
-           ah.l1 * (aw.l0 * r1[o + aw.i0] + aw.l1 * r1[o + aw.i1]);
-  };
-
-  int cur0 = -1, cur1 = -1;
-  float v0 = 0.f, v1 = 0.f;
   float m = 0.f, s = 0.f, t = 0.f;
-  for (int od = 0; od < maxdisp; ++od) {
-    const AxisW ad = src_axis(rd, od, D3, maxdisp);
-    if (ad.i0 != cur0) {
-      v0 = (ad.i0 == cur1) ? v1 : plane(ad.i0);
-      cur0 = ad.i0;
+  int od = 0;
+  for (int p0 = 0; p0 < D3; p0 += kDispChunk) {
+    // planes p0 .. p0 + kDispChunk (one past: the upper lerp source of the last
+    // depth in this batch), all loads issued before the first use
+#pragma unroll
+    for (int k = 0; k <= kDispChunk; ++k) {
+      const int dd = min(p0 + k, D3 - 1);
+      const long long o = (long long)dd * HW;
+      col[k * kDispThreads] = ah.l0 * (aw.l0 * r0[o + aw.i0] + aw.l1 * r0[o + aw.i1]) +
+                              ah.l1 * (aw.l0 * r1[o + aw.i0] + aw.l1 * r1[o + aw.i1]);
     }
-    if (ad.i1 != cur1) {
-      v1 = (ad.i1 == cur0) ? v0 : plane(ad.i1);
-      cur1 = ad.i1;
-    }
-    const float u = ad.l0 * v0 + ad.l1 * v1;
-    if (od == 0) {
-      m = u;
-      s = 1.f;
-      t = 0.f;
-    } else if (u < m) {
-      const float f = expf(u - m);  // < 1: rescale what was summed against the old min
-      s = s * f + 1.f;
-      t = t * f + (float)od;
-      m = u;
-    } else {
-      const float e = expf(m - u);
-      s += e;
-      t += (float)od * e;
+    for (; od < maxdisp && tab[od].i0 < p0 + kDispChunk; ++od) {
+      const AxisW ad = tab[od];
+      const float u = ad.l0 * col[(ad.i0 - p0) * kDispThreads] + ad.l1 * col[(ad.i1 - p0) * kDispThreads];
+      if (od == 0) {
+        m = u;
+        s = 1.f;
+        t = 0.f;
+      } else if (u < m) {
+        const float f = expf(u - m);  // < 1: rescale what was summed against the old min
+        s = s * f + 1.f;
+        t = t * f + (float)od;
+        m = u;
+      } else {
+        const float e = expf(m - u);
+        s += e;
+        t += (float)od * e;
+      }
     }
   }
   disp[((long long)b * Ho + oh) * Wo + ow] = t / s;
@@ -114,9 +121,11 @@ extern "C" int lea_disparity_regression(const void* cost, float* disp, int B, in
     return LEA_E_UNSUPPORTED;
   }
   const int Wo = 3 * W3;
-  dim3 block(256);
-  dim3 grid((Wo + 255) / 256, 3 * H3, B);
-  disparity_f32<<<grid, block, 0, as_stream(stream)>>>(
+  const size_t lds = (size_t)4 * maxdisp * sizeof(float) + (size_t)(kDispChunk + 1) * kDispThreads * sizeof(float);
+  LEA_CHECK_ARG(lds <= 65536, "lea_disparity_regression: maxdisp %d too large", maxdisp);
+  dim3 block(kDispThreads);
+  dim3 grid((Wo + kDispThreads - 1) / kDispThreads, 3 * H3, B);
+  disparity_f32<<<grid, block, lds, as_stream(stream)>>>(
       (const float*)cost, disp, D3, H3, W3, maxdisp, (float)D3 / (float)maxdisp,
       (float)H3 / (float)(3 * H3), (float)W3 / (float)(3 * W3));
   return launch_status("lea_disparity_regression");

@@ -12,59 +12,99 @@
 // as the reference up to fp32 reassociation; the 32-channel full-resolution
 // tensor (503 MB at 576x960 D192) is never written or read.
 //
-// Mapping: one thread per output voxel; workgroup = a row segment of one
-// (b, co, d, h), so the d/h source rows of each tap are uniform and only the
-// w-axis weights are per lane.  27 trilinear samples per voxel from the
-// cache-resident Q (53 MB at 576x960 D192).
+// Separable evaluation, two launches (r01: one 27-tap trilinear gather per voxel
+// issued 216 loads per output and ran at 0.4 TB/s):
+//   pass 1  Y[d][kh,kw](hi, wi) = sum_kd  lerp_d(Q[kd,kh,kw])(d + kd - 1)   low-res h, w
+//   pass 2  out(d, h, w)        = sum_kh,kw  bilerp(Y[d][kh,kw])(h + kh - 1, w + kw - 1)
+// (taps outside the output volume skipped), i.e. 6 loads per Y element and 36 per
+// output voxel.  Y (B*cout*Do*9*Hi*Wi floats) lives in a caller-provided workspace
+// (lea_tapsum_workspace_bytes).  Same sums in a different association order.
 #include "common.h"
 
 namespace lea {
 
-__global__ __launch_bounds__(512) void tapsum_upsample_f32(
-    const float* __restrict__ q, long long qbs, float* __restrict__ y, long long ybs, int cout,
-    int Di, int Hi, int Wi, int Do, int Ho, int Wo, float rd, float rh, float rw,
-    const float* __restrict__ scale, const float* __restrict__ shift, unsigned flags) {
+// pass 1: grid (quads of one low-res plane, (b, co, d, kh*3+kw)); float4 when Wi % 4 == 0
+template <bool VEC>
+__global__ __launch_bounds__(256) void tapsum_dpass_f32(const float* __restrict__ q, long long qbs,
+                                                        float* __restrict__ ws, int cout, int Di,
+                                                        int Hi, int Wi, int Do, float rd) {
 #pragma clang fp contract(off)
-  const int row = blockIdx.x;  // ((b * cout + co) * Do + d) * Ho + h
-  const int h = row % Ho;
-  int r = row / Ho;
+  int r = blockIdx.y;  // ((b * cout + co) * Do + d) * 9 + khw
+  const int khw = r % 9;
+  r /= 9;
   const int d = r % Do;
   r /= Do;
   const int co = r % cout;
   const int b = r / cout;
   const long long HWi = (long long)Hi * Wi;
   const long long vol = HWi * Di;
-  const float* qb = q + (long long)b * qbs + (long long)co * 27 * vol;
-  Axis aws[3];
-  bool wok[3];
-  for (int w = threadIdx.x; w < Wo; w += blockDim.x) {
-#pragma unroll
-    for (int kw = 0; kw < 3; ++kw) {
-      const int p = w + kw - 1;
-      wok[kw] = (unsigned)p < (unsigned)Wo;
-      aws[kw] = axis_index(rw, wok[kw] ? p : 0, Wi, Wo, 1);
-    }
-    float acc = 0.f;
+  const float* qb = q + (long long)b * qbs + ((long long)co * 27 + khw) * vol;
+  float* yo = ws + (long long)blockIdx.y * HWi;
+  const int n = VEC ? (int)(HWi / 4) : (int)HWi;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    float acc[VEC ? 4 : 1] = {};
 #pragma unroll
     for (int kd = 0; kd < 3; ++kd) {
       const int pd = d + kd - 1;
       if ((unsigned)pd >= (unsigned)Do) continue;
       const Axis ad = axis_index(rd, pd, Di, Do, 1);
+      const float* q0 = qb + (long long)kd * 9 * vol + ad.i0 * HWi;
+      const float* q1 = qb + (long long)kd * 9 * vol + ad.i1 * HWi;
+      if constexpr (VEC) {
+        const float4 a = reinterpret_cast<const float4*>(q0)[i];
+        const float4 c = reinterpret_cast<const float4*>(q1)[i];
+        acc[0] += ad.l0 * a.x + ad.l1 * c.x;
+        acc[1] += ad.l0 * a.y + ad.l1 * c.y;
+        acc[2] += ad.l0 * a.z + ad.l1 * c.z;
+        acc[3] += ad.l0 * a.w + ad.l1 * c.w;
+      } else {
+        acc[0] += ad.l0 * q0[i] + ad.l1 * q1[i];
+      }
+    }
+    if constexpr (VEC)
+      reinterpret_cast<float4*>(yo)[i] = make_float4(acc[0], acc[1], acc[2], acc[3]);
+    else
+      yo[i] = acc[0];
+  }
+}
+
+// pass 2: one workgroup per output row (b, co, d, h); lanes along w
+__global__ __launch_bounds__(512) void tapsum_hwpass_f32(
+    const float* __restrict__ ws, float* __restrict__ y, long long ybs, int cout, int Hi, int Wi,
+    int Do, int Ho, int Wo, float rh, float rw, const float* __restrict__ scale,
+    const float* __restrict__ shift, unsigned flags) {
+#pragma clang fp contract(off)
+  const int row = blockIdx.x;  // ((b * cout + co) * Do + d) * Ho + h
+  const int h = row % Ho;
+  const int plane = row / Ho;  // (b * cout + co) * Do + d
+  const int co = (plane / Do) % cout;
+  const int b = plane / (Do * cout);
+  const int d = plane % Do;
+  const long long HWi = (long long)Hi * Wi;
+  const float* yp = ws + (long long)plane * 9 * HWi;
+  Axis ah[3];
+  bool hok[3];
+#pragma unroll
+  for (int kh = 0; kh < 3; ++kh) {
+    const int p = h + kh - 1;
+    hok[kh] = (unsigned)p < (unsigned)Ho;
+    ah[kh] = axis_index(rh, hok[kh] ? p : 0, Hi, Ho, 1);
+  }
+  for (int w = threadIdx.x; w < Wo; w += blockDim.x) {
+    float acc = 0.f;
+#pragma unroll
+    for (int kw = 0; kw < 3; ++kw) {
+      const int p = w + kw - 1;
+      if ((unsigned)p >= (unsigned)Wo) continue;
+      const Axis aw = axis_index(rw, p, Wi, Wo, 1);
 #pragma unroll
       for (int kh = 0; kh < 3; ++kh) {
-        const int ph = h + kh - 1;
-        if ((unsigned)ph >= (unsigned)Ho) continue;
-        const Axis ah = axis_index(rh, ph, Hi, Ho, 1);
-#pragma unroll
-        for (int kw = 0; kw < 3; ++kw) {
-          const float* qt = qb + (long long)((kd * 3 + kh) * 3 + kw) * vol;
-          const float* p00 = qt + ad.i0 * HWi + (long long)ah.i0 * Wi;
-          const float* p01 = qt + ad.i0 * HWi + (long long)ah.i1 * Wi;
-          const float* p10 = qt + ad.i1 * HWi + (long long)ah.i0 * Wi;
-          const float* p11 = qt + ad.i1 * HWi + (long long)ah.i1 * Wi;
-          const float v = trilerp(ad, ah, aws[kw], p00, p01, p10, p11);
-          acc += wok[kw] ? v : 0.f;
-        }
+        if (!hok[kh]) continue;
+        const float* t = yp + (long long)(kh * 3 + kw) * HWi;
+        const float* r0 = t + (long long)ah[kh].i0 * Wi;
+        const float* r1 = t + (long long)ah[kh].i1 * Wi;
+        acc += ah[kh].l0 * (aw.l0 * r0[aw.i0] + aw.l1 * r0[aw.i1]) +
+               ah[kh].l1 * (aw.l0 * r1[aw.i0] + aw.l1 * r1[aw.i1]);
       }
     }
     if (scale) acc = acc * scale[co] + shift[co];
@@ -75,26 +115,46 @@ __global__ __launch_bounds__(512) void tapsum_upsample_f32(
 
 }  // namespace lea
 
+extern "C" size_t lea_tapsum_workspace_bytes(int B, int cout, int Hi, int Wi, int Do) {
+  if (B <= 0 || cout <= 0 || Hi <= 0 || Wi <= 0 || Do <= 0) return 0;
+  return (size_t)B * cout * Do * 9 * Hi * Wi * sizeof(float);
+}
+
 extern "C" int lea_tapsum_upsample(const void* q, int64_t q_bstride, void* y, int64_t y_bstride,
                                    int B, int cout, int Di, int Hi, int Wi, int Do, int Ho, int Wo,
                                    const float* scale, const float* shift, unsigned flags,
-                                   int dtype, void* stream) {
+                                   void* workspace, int dtype, void* stream) {
   using namespace lea;
   clear_error();
-  LEA_CHECK_ARG(q && y && q != y, "lea_tapsum_upsample: null or aliased pointer");
+  LEA_CHECK_ARG(q && y && q != y && workspace, "lea_tapsum_upsample: null or aliased pointer");
   LEA_CHECK_ARG((scale == nullptr) == (shift == nullptr),
                 "lea_tapsum_upsample: scale/shift must both be set or both NULL");
   LEA_CHECK_ARG(B > 0 && cout > 0 && Di > 0 && Hi > 0 && Wi > 0 && Do > 0 && Ho > 0 && Wo > 0,
                 "lea_tapsum_upsample: bad shape");
-  LEA_CHECK_ARG((long long)B * cout * Do * Ho < (1LL << 31), "lea_tapsum_upsample: grid too large");
+  LEA_CHECK_ARG((long long)B * cout * Do * Ho < (1LL << 31) && (long long)B * cout * Do * 9 <= 65535,
+                "lea_tapsum_upsample: grid too large");
   if (dtype != LEA_F32) {
     set_error("lea_tapsum_upsample: dtype %d unsupported", dtype);
     return LEA_E_UNSUPPORTED;
   }
+  hipStream_t st = as_stream(stream);
+  float* ws = (float*)workspace;
+  const long long HWi = (long long)Hi * Wi;
+  const bool vec = (HWi % 4) == 0 && ((uintptr_t)q % 16) == 0 && (q_bstride % 4) == 0 &&
+                   ((long long)Di * HWi) % 4 == 0 && ((uintptr_t)ws % 16) == 0;
+  const long long n = vec ? HWi / 4 : HWi;
+  dim3 g1((unsigned)((n + 255) / 256), (unsigned)(B * cout * Do * 9));
+  const float rd = axis_ratio(Di, Do, 1);
+  if (vec)
+    tapsum_dpass_f32<true><<<g1, 256, 0, st>>>((const float*)q, q_bstride, ws, cout, Di, Hi, Wi, Do, rd);
+  else
+    tapsum_dpass_f32<false><<<g1, 256, 0, st>>>((const float*)q, q_bstride, ws, cout, Di, Hi, Wi, Do, rd);
+  const int rc = launch_status("lea_tapsum_upsample");
+  if (rc) return rc;
   const int threads = Wo >= 512 ? 512 : ((Wo + 63) / 64) * 64;  // one row per workgroup
-  dim3 grid((unsigned)((long long)B * cout * Do * Ho));
-  tapsum_upsample_f32<<<grid, threads, 0, as_stream(stream)>>>(
-      (const float*)q, q_bstride, (float*)y, y_bstride, cout, Di, Hi, Wi, Do, Ho, Wo,
-      axis_ratio(Di, Do, 1), axis_ratio(Hi, Ho, 1), axis_ratio(Wi, Wo, 1), scale, shift, flags);
+  dim3 g2((unsigned)((long long)B * cout * Do * Ho));
+  tapsum_hwpass_f32<<<g2, threads, 0, st>>>(ws, (float*)y, y_bstride, cout, Hi, Wi, Do, Ho, Wo,
+                                            axis_ratio(Hi, Ho, 1), axis_ratio(Wi, Wo, 1), scale,
+                                            shift, flags);
   return launch_status("lea_tapsum_upsample");
 }

@@ -346,11 +346,14 @@ def tapsum_upsample(q: torch.Tensor, cout: int, size, scale: torch.Tensor | None
     qbs = _check_volume_view(q, "q")
     do, ho, wo = (int(s) for s in size)
     out = torch.empty((b, cout, do, ho, wo), device=q.device, dtype=q.dtype)
-    check(_lib.load().lea_tapsum_upsample(
+    lib = _lib.load()
+    ws = torch.empty(lib.lea_tapsum_workspace_bytes(b, cout, hi, wi, do) // 4, device=q.device,
+                     dtype=torch.float32)
+    check(lib.lea_tapsum_upsample(
         q.data_ptr(), qbs, out.data_ptr(), out.stride(0), b, cout, di, hi, wi, do, ho, wo,
         scale.data_ptr() if scale is not None else None,
-        shift.data_ptr() if shift is not None else None, LEA_RELU if relu else 0, LEA_F32,
-        _stream()), "lea_tapsum_upsample")
+        shift.data_ptr() if shift is not None else None, LEA_RELU if relu else 0,
+        ws.data_ptr(), LEA_F32, _stream()), "lea_tapsum_upsample")
     return out
 
 

@@ -413,12 +413,12 @@ def test_batch_rows_are_independent():
 
 
 @pytest.mark.parametrize("b,h,w,maxdisp,oracle_dev", [(1, 1008, 1512, 264, "cpu"),
-                                                      (2, 384, 1248, 192, DEV)])
+                                                      (2, 384, 1248, 192, "cpu")])
 def test_large_configs_vs_torch_oracle(b, h, w, maxdisp, oracle_dev):
     """Config 5 (Middlebury 1008x1512, D264 -- D256 is illegal in the reference) and
     config 3's KITTI shape (384x1248 D192, here fp32, batch 2): HIP vs the oracle,
-    EPE <= 1e-3 px per pair.  (At config 5 MIOpen falls back to naive 3D convs, so
-    that oracle runs on the host CPU.)"""
+    EPE <= 1e-3 px per pair.  (MIOpen's 3D convs at these sizes take minutes, so
+    the oracle runs on the host CPU.)"""
     m = _model(maxdisp)
     left = normal(4321 + h, (b, 3, h, w))
     right = normal(4322 + h, (b, 3, h, w))
@@ -432,16 +432,16 @@ def test_large_configs_vs_torch_oracle(b, h, w, maxdisp, oracle_dev):
         assert ref.epe(disp[i], want[i]) < 1e-3
 
 
-def test_full_size_c2_vs_torch_oracle_on_gpu():
+def test_full_size_c2_vs_torch_oracle():
     """576x960 D192 (the benchmark configuration): HIP vs the oracle's torch
-    restatement running fp32 on the same GPU (MIOpen), EPE <= 1e-3 px."""
+    restatement in fp32 on the host CPU (MIOpen's 3D convs at this size take
+    minutes), EPE <= 1e-3 px."""
     m = _model(192)
-    left = normal(1234, (1, 3, 576, 960)).to(DEV)
-    right = normal(1235, (1, 3, 576, 960)).to(DEV)
-    sd = {k: v.to(DEV) for k, v in state_dict().items()}
+    left = normal(1234, (1, 3, 576, 960))
+    right = normal(1235, (1, 3, 576, 960))
     with torch.no_grad():
-        disp = m(left, right)
-        want = ref.leastereo_forward(sd, left, right, 192, arch())
+        disp = m(left.to(DEV), right.to(DEV)).cpu()
+        want = ref.leastereo_forward(state_dict(), left, right, 192, arch())
     assert torch.isfinite(disp).all()
     assert float(disp.min()) >= 0.0 and float(disp.max()) <= 191.0
     assert ref.epe(disp.cpu(), want.cpu()) < 1e-3

@@ -35,6 +35,13 @@ LAYERS = {
 }
 
 
+# name: (cin, cout, input volume, output volume, count per forward)
+RESAMPLED = {
+    "down_32to16_k1_L0toL1": (32, 16, L0, L1, 4),
+    "down_64to32_k1_L1toL2": (64, 32, L1, L2, 5),
+}
+
+
 def main():
     p = argparse.ArgumentParser()
     p.add_argument("--iters", type=int, default=20)
@@ -73,6 +80,31 @@ def main():
         print(f"{name:24s} {ms * 1e3:9.1f} us  {flops / ms / 1e9:7.1f} TFLOP/s  "
               f"{nbytes / ms / 1e6:8.1f} GB/s  x{count:2d} = {ms * count:6.3f} ms/fwd  "
               f"{res[name]['kernel']}", flush=True)
+    # resampled 1x1 preprocess (trilinear align_corners down by 2 fused into the conv)
+    for name, (cin, cout, src, dst, count) in RESAMPLED.items():
+        if only and name not in only:
+            continue
+        g = torch.Generator(device=dev).manual_seed(1)
+        x = torch.randn((1, cin) + src, device=dev, generator=g)
+        wt = torch.randn(cout, cin, 1, 1, 1, device=dev, generator=g) * 0.1
+        packed = kernels.pack_conv_weight(wt)
+        scale = torch.rand(cout, device=dev, generator=g) + 0.5
+        shift = torch.randn(cout, device=dev, generator=g) * 0.1
+        for _ in range(3):
+            y = kernels.conv3d_bnrelu_resampled(x, dst, packed, cout, 1, scale, shift, True)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        torch.cuda.synchronize()
+        e0.record()
+        for _ in range(a.iters):
+            y = kernels.conv3d_bnrelu_resampled(x, dst, packed, cout, 1, scale, shift, True)
+        e1.record()
+        torch.cuda.synchronize()
+        ms = e0.elapsed_time(e1) / a.iters
+        nbytes = 4.0 * (cin * src[0] * src[1] * src[2] + cout * dst[0] * dst[1] * dst[2])
+        res[name] = {"ms": ms, "tflops": 0.0, "gbs": nbytes / ms / 1e6, "per_forward_ms": ms * count,
+                     "kernel": kernels.conv_kernel_name(1, cout, *dst, 1, True)}
+        print(f"{name:24s} {ms * 1e3:9.1f} us  {'':15s}  {nbytes / ms / 1e6:8.1f} GB/s  "
+              f"x{count:2d} = {ms * count:6.3f} ms/fwd  {res[name]['kernel']}", flush=True)
     print("total ms/forward", sum(v["per_forward_ms"] for v in res.values()))
     print(json.dumps(res))
 
