@@ -512,8 +512,8 @@ const char* plan_name(const Plan& p, int k) {
   if (p.engine == 3)
     snprintf(g_name, sizeof(g_name), "conv3d_valu_kernel<%d>", p.mt == 1 ? 1 : 2);
   else if (p.engine == 0)
-    snprintf(g_name, sizeof(g_name), "conv3d_dma_kernel<%d, %d, %d, %d, %d>", p.mt, p.nt, p.tw, p.td,
-             k == 2 ? 1 : 3);
+    snprintf(g_name, sizeof(g_name), "conv3d_dma_kernel<%d, %d, %d, %d, %d, false>", p.mt, p.nt,
+             p.tw, p.td, k == 2 ? 1 : 3);
   else if (p.engine == 2)
     snprintf(g_name, sizeof(g_name), "conv3d_reg_kernel<%d, %d, %d, %d, true>", k, p.mt, p.nt, p.tw);
   else
@@ -555,7 +555,9 @@ int conv_common(ConvArgs& a, int B, int k, bool resample, int dtype, void* strea
   LEA_CHECK_ARG(a.cin1 >= 0 && a.cin1 <= a.cin && (a.cin1 == a.cin || a.x2),
                 "lea_conv3d: bad channel split %d/%d", a.cin1, a.cin);
   LEA_CHECK_ARG(k == 1 || k == 3, "lea_conv3d: k=%d unsupported", k);
-  LEA_CHECK_ARG((long long)a.D * a.H * a.W * 4 < (1LL << 32), "lea_conv3d: volume too large");
+  LEA_CHECK_ARG((long long)a.D * a.H * a.W * 4 < (1LL << 32) &&
+                    (long long)(a.cout + 63) * a.D * a.H * a.W < (1LL << 31),
+                "lea_conv3d: volume too large");
   LEA_CHECK_ARG(a.x != a.y && a.x2 != a.y, "lea_conv3d: input aliases output");
   if (resample)
     LEA_CHECK_ARG(a.Di > 0 && a.Hi > 0 && a.Wi > 0, "lea_conv3d: bad input volume");
@@ -709,7 +711,7 @@ extern "C" int lea_conv2d_bnrelu(const void* x, int64_t x_bstride, const float* 
   LEA_CHECK_ARG(!(flags & LEA_RESIDUAL) || a.res, "lea_conv2d: LEA_RESIDUAL without residual");
   LEA_CHECK_ARG(B > 0 && cin > 0 && cout > 0 && H > 0 && W > 0,
                 "lea_conv2d: bad shape B=%d cin=%d cout=%d H=%d W=%d", B, cin, cout, H, W);
-  LEA_CHECK_ARG((long long)H * W * 4 < (1LL << 32), "lea_conv2d: plane too large");
+  LEA_CHECK_ARG((long long)(cout + 63) * H * W < (1LL << 31), "lea_conv2d: plane too large");
   LEA_CHECK_ARG(a.x != a.y, "lea_conv2d: input aliases output");
   if (dtype != LEA_F32) {
     set_error("lea_conv2d: dtype %d unsupported", dtype);
@@ -769,7 +771,8 @@ extern "C" int lea_conv3d_bnrelu_costvolume(const void* left, const void* right,
   constexpr int kCinB = PackCfg<3, 1>::CIN_B;  // chunks must not straddle left/right
   LEA_CHECK_ARG(C % kCinB == 0, "lea_conv3d_bnrelu_costvolume: C=%d must be a multiple of %d", C,
                 kCinB);
-  LEA_CHECK_ARG((long long)D3 * H * W * 4 < (1LL << 32), "lea_conv3d_bnrelu_costvolume: volume too large");
+  LEA_CHECK_ARG((long long)(cout + 63) * D3 * H * W < (1LL << 31),
+                "lea_conv3d_bnrelu_costvolume: volume too large");
   if (dtype != LEA_F32) {
     set_error("lea_conv3d_bnrelu_costvolume: dtype %d unsupported", dtype);
     return LEA_E_UNSUPPORTED;

@@ -194,84 +194,120 @@ __device__ __forceinline__ void epilogue(const ConvArgs& a, const f32x4 (&acc)[T
   }
 }
 
-// Epilogue operands fetched into registers at the start of a workgroup (folded BN
-// of this lane's couts and, under LEA_RESIDUAL, the residual of every voxel it
-// stores), so their latency hides under the main loop instead of stalling the
-// store phase -- the cell's accumulating ops were ~25% slower than plain ones.
-template <int MT, int NT, int TD>
+// DMA-engine epilogue.  Output addressing is one per-lane 32-bit element offset
+// (host checks cout*D*H*W < 2^31) plus per-element offsets that are uniform across
+// the wave, and tiles that lie wholly inside the volume and the cout block skip
+// the per-element masks: on the small-K cell layers the r01 epilogue (64-bit
+// index math and four compares per stored value) was ~1 VALU op per MFMA.
+// Epilogue operands -- folded BN of this lane's couts and, under LEA_RESIDUAL with
+// RES, the residual of every voxel it stores -- are loaded at the start of the
+// workgroup so their latency hides under the main loop (accumulating cell ops were
+// ~25% slower when the residual was read in the store phase).
+template <int MT, int NT, int TD, bool RES>
 struct EpiRegs {
   float sc[MT][4], sh[MT][4];
-  float rv[TD][MT][NT][4];
+  float rv[RES ? TD : 1][RES ? MT : 1][RES ? NT : 1][4];
 };
 
 template <int KS, int MT, int NT, int TW, int TD>
-__device__ __forceinline__ void epi_prefetch(const ConvArgs& a, EpiRegs<MT, NT, TD>& e, int b,
-                                             int co0, int d0, int h0, int w0, int wave, int lane) {
+struct EpiGeom {
   using C = TileCfg<KS, MT, NT, TW, TD>;
-  const long long HW = (long long)a.H * a.W;
-  const long long DHW = HW * a.D;
-  const bool resid = a.flags & LEA_RESIDUAL;
-  const int kq = lane >> 4, n = lane & 15;
+  int HW, DHW, W;
+  int base;       // element offset (in one batch) of this lane's (m, r, t, j) = 0 output
+  int wave;
+  bool interior;  // the whole tile is inside the volume and the cout block
+  int co0, d0, h0, w0, kq, n;
+  __device__ EpiGeom(const ConvArgs& a, int co0_, int d0_, int h0_, int w0_, int wave_, int lane)
+      : co0(co0_), d0(d0_), h0(h0_), w0(w0_) {
+    HW = a.H * a.W;
+    DHW = HW * a.D;
+    W = a.W;
+    wave = wave_;
+    kq = lane >> 4;
+    n = lane & 15;
+    const int g0 = wave * NT;
+    base = (co0 + kq * 4) * DHW + d0 * HW + (h0 + g0 / C::TPR) * a.W + w0 + (g0 % C::TPR) * 16 + n;
+    interior = co0 + C::COP <= a.cout && d0 + TD <= a.D && h0 + C::TH <= a.H && w0 + TW <= a.W;
+  }
+  // offset of element (m, r, t, j) relative to base: uniform across the wave
+  __device__ int rel(int m, int r, int t, int j) const {
+    const int g0 = wave * NT, g = g0 + j;
+    return (m * 16 + r) * DHW + t * HW + (g / C::TPR - g0 / C::TPR) * W +
+           ((g % C::TPR) - (g0 % C::TPR)) * 16;
+  }
+  __device__ bool inside(const ConvArgs& a, int m, int r, int t, int j) const {
+    const int g = wave * NT + j;
+    return co0 + m * 16 + kq * 4 + r < a.cout && d0 + t < a.D && h0 + g / C::TPR < a.H &&
+           w0 + (g % C::TPR) * 16 + n < a.W;
+  }
+};
+
+template <int KS, int MT, int NT, int TW, int TD, bool RES>
+__device__ __forceinline__ void epi_prefetch(const ConvArgs& a, EpiRegs<MT, NT, TD, RES>& e,
+                                             const EpiGeom<KS, MT, NT, TW, TD>& g, int b) {
 #pragma unroll
-  for (int m = 0; m < MT; ++m) {
+  for (int m = 0; m < MT; ++m)
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      const int co = co0 + m * 16 + kq * 4 + r;
+      const int co = g.co0 + m * 16 + g.kq * 4 + r;
       const bool cv = co < a.cout;
       e.sc[m][r] = (cv && a.scale) ? a.scale[co] : 1.f;
       e.sh[m][r] = (cv && a.shift) ? a.shift[co] : 0.f;
-#pragma unroll
-      for (int t = 0; t < TD; ++t)
-#pragma unroll
-        for (int j = 0; j < NT; ++j) {
-          const int g = wave * NT + j;
-          const int d = d0 + t;
-          const int h = h0 + g / C::TPR;
-          const int w = w0 + (g % C::TPR) * 16 + n;
-          float v = 0.f;
-          if (resid && cv && d < a.D && h < a.H && w < a.W)
-            v = a.res[(long long)b * a.rbs + (long long)co * DHW + (long long)d * HW +
-                      (long long)h * a.W + w];
-          e.rv[t][m][j][r] = v;
-        }
     }
+  if constexpr (RES) {
+    const bool resid = a.flags & LEA_RESIDUAL;
+    const float* rb = a.res + (long long)b * a.rbs + g.base;
+#pragma unroll
+    for (int t = 0; t < TD; ++t)
+#pragma unroll
+      for (int m = 0; m < MT; ++m)
+#pragma unroll
+        for (int j = 0; j < NT; ++j)
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            e.rv[t][m][j][r] =
+                (resid && (g.interior || g.inside(a, m, r, t, j))) ? rb[g.rel(m, r, t, j)] : 0.f;
   }
 }
 
-template <int KS, int MT, int NT, int TW, int TD>
-__device__ __forceinline__ void epilogue_pre(const ConvArgs& a, const f32x4 (&acc)[TD][MT][NT],
-                                             const EpiRegs<MT, NT, TD>& e, int b, int co0, int d0,
-                                             int h0, int w0, int wave, int lane) {
-  using C = TileCfg<KS, MT, NT, TW, TD>;
-  const long long HW = (long long)a.H * a.W;
-  const long long DHW = HW * a.D;
+template <int KS, int MT, int NT, int TW, int TD, bool RES>
+__device__ __forceinline__ void epilogue_dma(const ConvArgs& a, const f32x4 (&acc)[TD][MT][NT],
+                                             const EpiRegs<MT, NT, TD, RES>& e,
+                                             const EpiGeom<KS, MT, NT, TW, TD>& g, int b) {
   const bool relu = a.flags & LEA_RELU;
   const bool resid = a.flags & LEA_RESIDUAL;
-  const int kq = lane >> 4, n = lane & 15;
-#pragma unroll
-  for (int m = 0; m < MT; ++m) {
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int co = co0 + m * 16 + kq * 4 + r;
-      if (co >= a.cout) continue;
-#pragma unroll
-      for (int t = 0; t < TD; ++t) {
-        const int d = d0 + t;
-        if (d >= a.D) continue;
-#pragma unroll
-        for (int j = 0; j < NT; ++j) {
-          const int g = wave * NT + j;
-          const int h = h0 + g / C::TPR;
-          const int w = w0 + (g % C::TPR) * 16 + n;
-          if (h >= a.H || w >= a.W) continue;
-          const long long o = (long long)co * DHW + (long long)d * HW + (long long)h * a.W + w;
-          float v = acc[t][m][j][r] * e.sc[m][r] + e.sh[m][r];
-          if (relu) v = fmaxf(v, 0.f);
-          if (resid) v += e.rv[t][m][j][r];
-          a.y[(long long)b * a.ybs + o] = v;
-        }
-      }
+  float* yb = a.y + (long long)b * a.ybs + g.base;
+  const float* rb = a.res + (long long)b * a.rbs + g.base;
+  auto value = [&](int m, int r, int t, int j) {
+    float v = acc[t][m][j][r] * e.sc[m][r] + e.sh[m][r];
+    if (relu) v = fmaxf(v, 0.f);
+    if (resid) {
+      if constexpr (RES)
+        v += e.rv[t][m][j][r];
+      else
+        v += rb[g.rel(m, r, t, j)];
     }
+    return v;
+  };
+  if (g.interior) {
+#pragma unroll
+    for (int t = 0; t < TD; ++t)
+#pragma unroll
+      for (int m = 0; m < MT; ++m)
+#pragma unroll
+        for (int j = 0; j < NT; ++j)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) yb[g.rel(m, r, t, j)] = value(m, r, t, j);
+  } else {
+#pragma unroll
+    for (int t = 0; t < TD; ++t)
+#pragma unroll
+      for (int m = 0; m < MT; ++m)
+#pragma unroll
+        for (int j = 0; j < NT; ++j)
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            if (g.inside(a, m, r, t, j)) yb[g.rel(m, r, t, j)] = value(m, r, t, j);
   }
 }
 
@@ -402,10 +438,11 @@ __global__ __launch_bounds__(kConvThreads, 2) void conv3d_dma_kernel(const ConvA
 
   issue(0, smem);
   // small accumulator tiles (the cell ops, which accumulate) have registers to
-  // spare for the prefetched epilogue operands; big tiles keep 2 WGs/CU without
-  constexpr bool PRE = TD * MT * NT <= 8;
-  EpiRegs<PRE ? MT : 1, PRE ? NT : 1, PRE ? TD : 1> epi;
-  if constexpr (PRE) epi_prefetch<3, MT, NT, TW, TD>(a, epi, b, co0, d0, h0, w0, wave, lane);
+  // spare for a prefetched residual; big tiles keep 2 WGs/CU without
+  constexpr bool RES = TD * MT * NT <= 8;
+  const EpiGeom<3, MT, NT, TW, TD> geo(a, co0, d0, h0, w0, wave, lane);
+  EpiRegs<MT, NT, TD, RES> epi;
+  epi_prefetch<3, MT, NT, TW, TD, RES>(a, epi, geo, b);
   for (int ch = 0; ch < nchunks; ++ch) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's pieces of chunk ch landed
     __syncthreads();  // ... and everyone's; everyone is done reading chunk ch-1's stage
@@ -413,10 +450,7 @@ __global__ __launch_bounds__(kConvThreads, 2) void conv3d_dma_kernel(const ConvA
     const float* xs = smem + (ch & 1) * C::STAGE;
     mfma_chunk<3, MT, NT, TW, TD, KD>(xs, xs + C::XS, xoff, woff, acc);
   }
-  if constexpr (PRE)
-    epilogue_pre<3, MT, NT, TW, TD>(a, acc, epi, b, co0, d0, h0, w0, wave, lane);
-  else
-    epilogue<3, MT, NT, TW, TD>(a, acc, b, co0, d0, h0, w0, wave, lane);
+  epilogue_dma<3, MT, NT, TW, TD, RES>(a, acc, epi, geo, b);
 }
 
 // A launch plan: which instantiation runs a given shape (also reported by name).

@@ -52,13 +52,13 @@ def test_invalid_arguments_are_rejected_before_launch():
     assert lib.lea_conv3d_bnrelu_resampled(x, 0, 0, 1, 1, x, None, None, None, 0, y, 0,
                                            1, 1, 1, 1, 1, 1, 1, 1, 0, None) == 1001
     assert b"input volume" in lib.lea_last_error()
-    assert lib.lea_conv3d_kernel_name(1, 32, 64, 192, 320, 3, 0) == b"conv3d_dma_kernel<2, 2, 16, 2, 3>"
-    assert lib.lea_conv3d_kernel_name(1, 32, 16, 48, 80, 3, 0) == b"conv3d_dma_kernel<2, 2, 16, 1, 3>"
+    assert lib.lea_conv3d_kernel_name(1, 32, 64, 192, 320, 3, 0) == b"conv3d_dma_kernel<2, 2, 16, 2, 3, false>"
+    assert lib.lea_conv3d_kernel_name(1, 32, 16, 48, 80, 3, 0) == b"conv3d_dma_kernel<2, 2, 16, 1, 3, false>"
     # tuning override: forced tile, then back to the planner; bad tiles rejected
     assert lib.lea_conv3d_set_tile_override(4, 64, 2) == 0
-    assert lib.lea_conv3d_kernel_name(1, 32, 64, 192, 320, 3, 0) == b"conv3d_dma_kernel<2, 4, 64, 2, 3>"
+    assert lib.lea_conv3d_kernel_name(1, 32, 64, 192, 320, 3, 0) == b"conv3d_dma_kernel<2, 4, 64, 2, 3, false>"
     assert lib.lea_conv3d_set_tile_override(0, 0, 0) == 0
-    assert lib.lea_conv3d_kernel_name(1, 32, 64, 192, 320, 3, 0) == b"conv3d_dma_kernel<2, 2, 16, 2, 3>"
+    assert lib.lea_conv3d_kernel_name(1, 32, 64, 192, 320, 3, 0) == b"conv3d_dma_kernel<2, 2, 16, 2, 3, false>"
     assert lib.lea_conv3d_set_tile_override(3, 16, 2) == 1001
     assert lib.lea_conv3d_kernel_name(1, 8, 64, 192, 320, 1, 1).startswith(b"conv3d_reg_kernel<1, 1")
     assert lib.lea_conv3d_kernel_name(1, 8, 32, 96, 160, 1, 0) == b"conv1x1_kernel<1, 4>"

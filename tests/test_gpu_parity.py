@@ -121,7 +121,7 @@ def test_conv_two_plane_tiles_odd_depth(cin, cout, shape, acc):
     """Large volumes use 2 output planes per workgroup; odd D masks the last one.
     With ``acc`` the residual is prefetched into registers at workgroup start."""
     name = kernels.conv_kernel_name(1, cout, *shape, 3)
-    assert name.endswith(", 2, 3>"), name
+    assert name.endswith(", 2, 3, false>"), name
     g = torch.Generator().manual_seed(cin + cout)
     x = torch.randn((1, cin) + shape, generator=g)
     w = torch.randn(cout, cin, 3, 3, 3, generator=g) / np.sqrt(cin * 27)
