@@ -415,9 +415,13 @@ inline Plan make_plan(int B, int cout, int D, int H, int W, int k, bool resample
   p.engine = resample ? 2 : 0;
   p.tw = prefer_tw64(W) ? 64 : 32;
   p.td = 1;
-  const int nt_full = p.mt == 1 ? 8 : (p.mt == 4 ? 2 : 4);
-  p.nt = nt_full;
-  if (resample) return p;
+  if (resample) {
+    // register-staged resampling engine; for k = 1 (the level-change preprocess,
+    // HBM-bound gathers) half-height tiles halve the LDS stage so 4 workgroups
+    // share a CU and keep more loads in flight
+    p.nt = (k == 1) ? (p.mt == 1 ? 4 : 2) : (p.mt == 1 ? 8 : 4);
+    return p;
+  }
   const long long ncob = (cout + p.mt * 16 - 1) / (p.mt * 16);
   if (g_tile_override[0] > 0) {  // lea_conv3d_set_tile_override (tuning tools)
     p.nt = g_tile_override[0];
@@ -497,10 +501,10 @@ int run_plan(const Plan& p, ConvArgs a, int B, int k, hipStream_t st) {
       if (p.mt == 3) return run_rs<3, 3, 4>(a, p.tw, B, st);
       return run_rs<3, 4, 4>(a, p.tw, B, st);
     }
-    if (p.mt == 1) return run_rs<1, 1, 8>(a, p.tw, B, st);
-    if (p.mt == 2) return run_rs<1, 2, 4>(a, p.tw, B, st);
-    if (p.mt == 3) return run_rs<1, 3, 4>(a, p.tw, B, st);
-    return run_rs<1, 4, 4>(a, p.tw, B, st);
+    if (p.mt == 1) return run_rs<1, 1, 4>(a, p.tw, B, st);
+    if (p.mt == 2) return run_rs<1, 2, 2>(a, p.tw, B, st);
+    if (p.mt == 3) return run_rs<1, 3, 2>(a, p.tw, B, st);
+    return run_rs<1, 4, 2>(a, p.tw, B, st);
   }
   // 1x1x1 without resample: streaming engine over the flat voxel run
   return run_1x1(p, a, B, st);
