@@ -349,6 +349,29 @@ __global__ void pack_weights_kernel(const float* __restrict__ w, float* __restri
   }
 }
 
+// Depth-paired packing (couts <= 8): [chunk][p = 0..3][kh][kw][CIN_B][16] with
+// column 8t + c = W[c][ci][kd = p - t][kh][kw] (zero when kd is outside 0..2).
+__global__ void pack_weights_dp_kernel(const float* __restrict__ w, float* __restrict__ packed,
+                                       int cout, int cin, int nchunks, long long total) {
+  using P = PackCfg<3, 1, 4>;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
+       i += (long long)gridDim.x * blockDim.x) {
+    const int col = (int)(i % P::COPS);
+    long long r = i / P::COPS;
+    const int cb = (int)(r % P::CIN_B);
+    r /= P::CIN_B;
+    const int tap = (int)(r % P::KT);  // p * 9 + kh * 3 + kw
+    const int ch = (int)(r / P::KT);
+    const int t = col / 8, co = col % 8;
+    const int kd = tap / 9 - t, khw = tap % 9;
+    const int ci = ch * P::CIN_B + cb;
+    float v = 0.f;
+    if (kd >= 0 && kd < 3 && co < cout && ci < cin && ch < nchunks)
+      v = w[((long long)co * cin + ci) * 27 + kd * 9 + khw];
+    packed[i] = v;
+  }
+}
+
 // Rows (x16) of the output-channel block a workgroup owns: the smallest of
 // 16/32/48 that holds cout, else the 48- or 64-row blocking with less padding.
 inline int mt_for(int cout) {
@@ -364,8 +387,12 @@ size_t packed_floats_t(int cout, int cin) {
   return (size_t)((cout + P::COP - 1) / P::COP) * ((cin + P::CIN_B - 1) / P::CIN_B) * P::CHUNK;
 }
 
+// k = 3 convs with 3..8 output channels run depth-paired (conv3d_dma_kernel, KD = 4)
+inline bool depth_paired(int cout, int k) { return k == 3 && cout > 2 && cout <= 8; }
+
 size_t packed_floats(int cout, int cin, int k) {
   const int mt = mt_for(cout);
+  if (depth_paired(cout, k)) return packed_floats_t<3, 1, 4>(cout, cin);
   if (k == 3)
     return mt == 1 ? packed_floats_t<3, 1>(cout, cin)
            : mt == 2 ? packed_floats_t<3, 2>(cout, cin)
@@ -410,6 +437,15 @@ inline Plan make_plan(int B, int cout, int D, int H, int W, int k, bool resample
     p.engine = 3;
     p.nt = 0;
     p.tw = 64;
+    return p;
+  }
+  if (depth_paired(cout, k) && !resample) {  // engine 4: two planes x 8 couts per tile
+    p.engine = 4;
+    p.mt = 1;
+    p.tw = 16;
+    p.td = 1;
+    const long long wgs8 = (long long)((W + 15) / 16) * ((H + 7) / 8) * ((D + 1) / 2) * B;
+    p.nt = wgs8 >= 512 ? 2 : 1;
     return p;
   }
   p.engine = resample ? 2 : 0;
@@ -488,6 +524,7 @@ int run_plan(const Plan& p, ConvArgs a, int B, int k, hipStream_t st) {
     if (a.cout == 1) return launch(conv3d_valu_kernel<1>, a, 8, 64, B, st);
     return launch(conv3d_valu_kernel<2>, a, 8, 64, B, st);
   }
+  if (p.engine == 4) return run_dma_dp(p, a, B, st);
   if (p.engine == 0) {
     if (p.mt == 1) return run_dma_mt1(p, a, B, st);
     if (p.mt == 2) return run_dma_mt2(p, a, B, st);
@@ -518,6 +555,8 @@ const char* plan_name(const Plan& p, int k) {
   else if (p.engine == 0)
     snprintf(g_name, sizeof(g_name), "conv3d_dma_kernel<%d, %d, %d, %d, %d, false>", p.mt, p.nt,
              p.tw, p.td, k == 2 ? 1 : 3);
+  else if (p.engine == 4)
+    snprintf(g_name, sizeof(g_name), "conv3d_dma_kernel<1, %d, %d, 1, 4, false>", p.nt, p.tw);
   else if (p.engine == 2)
     snprintf(g_name, sizeof(g_name), "conv3d_reg_kernel<%d, %d, %d, %d, true>", k, p.mt, p.nt, p.tw);
   else
@@ -563,8 +602,14 @@ int conv_common(ConvArgs& a, int B, int k, bool resample, int dtype, void* strea
                     (long long)(a.cout + 63) * a.D * a.H * a.W < (1LL << 31),
                 "lea_conv3d: volume too large");
   LEA_CHECK_ARG(a.x != a.y && a.x2 != a.y, "lea_conv3d: input aliases output");
-  if (resample)
+  if (resample) {
     LEA_CHECK_ARG(a.Di > 0 && a.Hi > 0 && a.Wi > 0, "lea_conv3d: bad input volume");
+    if (depth_paired(a.cout, k)) {
+      set_error("lea_conv3d_bnrelu_resampled: k=3 with %d output channels (depth-paired packing) "
+                "is not supported", a.cout);
+      return LEA_E_UNSUPPORTED;
+    }
+  }
   if (dtype != LEA_F32) {
     set_error("lea_conv3d: dtype %d unsupported", dtype);
     return LEA_E_UNSUPPORTED;
@@ -618,7 +663,9 @@ extern "C" int lea_conv3d_pack_weights(const float* w, float* packed, int cout, 
   const int nchunks = (cin + cin_b - 1) / cin_b;
 #define LEA_PACK(KS, MT) \
   pack_weights_kernel<KS, MT><<<grid, threads, 0, st>>>(w, packed, cout, cin, nchunks, total)
-  if (k == 3) {
+  if (depth_paired(cout, k)) {
+    pack_weights_dp_kernel<<<grid, threads, 0, st>>>(w, packed, cout, cin, nchunks, total);
+  } else if (k == 3) {
     if (mt == 1) LEA_PACK(3, 1); else if (mt == 2) LEA_PACK(3, 2); else if (mt == 3) LEA_PACK(3, 3); else LEA_PACK(3, 4);
   } else {
     if (mt == 1) LEA_PACK(1, 1); else if (mt == 2) LEA_PACK(1, 2); else if (mt == 3) LEA_PACK(1, 3); else LEA_PACK(1, 4);

@@ -209,9 +209,12 @@ struct EpiRegs {
   float rv[RES ? TD : 1][RES ? MT : 1][RES ? NT : 1][4];
 };
 
-template <int KS, int MT, int NT, int TW, int TD>
+// KD = 4 marks the depth-paired layout (couts <= 8): accumulator row 8t + c is
+// output channel c of plane d0 + t (see conv3d_dma_kernel).
+template <int KS, int MT, int NT, int TW, int TD, int KD = KS>
 struct EpiGeom {
   using C = TileCfg<KS, MT, NT, TW, TD>;
+  static constexpr bool DP = KD == 4;
   int HW, DHW, W;
   int base;       // element offset (in one batch) of this lane's (m, r, t, j) = 0 output
   int wave;
@@ -226,8 +229,13 @@ struct EpiGeom {
     kq = lane >> 4;
     n = lane & 15;
     const int g0 = wave * NT;
-    base = (co0 + kq * 4) * DHW + d0 * HW + (h0 + g0 / C::TPR) * a.W + w0 + (g0 % C::TPR) * 16 + n;
-    interior = co0 + C::COP <= a.cout && d0 + TD <= a.D && h0 + C::TH <= a.H && w0 + TW <= a.W;
+    const int cq = DP ? (kq & 1) * 4 : kq * 4, dq = DP ? (kq >> 1) : 0;
+    base = (co0 + cq) * DHW + (d0 + dq) * HW + (h0 + g0 / C::TPR) * a.W + w0 + (g0 % C::TPR) * 16 + n;
+    interior = co0 + (DP ? 8 : C::COP) <= a.cout && d0 + (DP ? 2 : TD) <= a.D && h0 + C::TH <= a.H &&
+               w0 + TW <= a.W;
+  }
+  __device__ int cout_of(int m, int r) const {  // output channel of accumulator row (m, r)
+    return co0 + m * 16 + (DP ? (kq & 1) * 4 : kq * 4) + r;
   }
   // offset of element (m, r, t, j) relative to base: uniform across the wave
   __device__ int rel(int m, int r, int t, int j) const {
@@ -237,19 +245,19 @@ struct EpiGeom {
   }
   __device__ bool inside(const ConvArgs& a, int m, int r, int t, int j) const {
     const int g = wave * NT + j;
-    return co0 + m * 16 + kq * 4 + r < a.cout && d0 + t < a.D && h0 + g / C::TPR < a.H &&
+    return cout_of(m, r) < a.cout && d0 + t + (DP ? (kq >> 1) : 0) < a.D && h0 + g / C::TPR < a.H &&
            w0 + (g % C::TPR) * 16 + n < a.W;
   }
 };
 
-template <int KS, int MT, int NT, int TW, int TD, bool RES>
+template <int KS, int MT, int NT, int TW, int TD, bool RES, int KD>
 __device__ __forceinline__ void epi_prefetch(const ConvArgs& a, EpiRegs<MT, NT, TD, RES>& e,
-                                             const EpiGeom<KS, MT, NT, TW, TD>& g, int b) {
+                                             const EpiGeom<KS, MT, NT, TW, TD, KD>& g, int b) {
 #pragma unroll
   for (int m = 0; m < MT; ++m)
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      const int co = g.co0 + m * 16 + g.kq * 4 + r;
+      const int co = g.cout_of(m, r);
       const bool cv = co < a.cout;
       e.sc[m][r] = (cv && a.scale) ? a.scale[co] : 1.f;
       e.sh[m][r] = (cv && a.shift) ? a.shift[co] : 0.f;
@@ -270,10 +278,10 @@ __device__ __forceinline__ void epi_prefetch(const ConvArgs& a, EpiRegs<MT, NT, 
   }
 }
 
-template <int KS, int MT, int NT, int TW, int TD, bool RES>
+template <int KS, int MT, int NT, int TW, int TD, bool RES, int KD>
 __device__ __forceinline__ void epilogue_dma(const ConvArgs& a, const f32x4 (&acc)[TD][MT][NT],
                                              const EpiRegs<MT, NT, TD, RES>& e,
-                                             const EpiGeom<KS, MT, NT, TW, TD>& g, int b) {
+                                             const EpiGeom<KS, MT, NT, TW, TD, KD>& g, int b) {
   const bool relu = a.flags & LEA_RELU;
   const bool resid = a.flags & LEA_RESIDUAL;
   float* yb = a.y + (long long)b * a.ybs + g.base;
@@ -317,9 +325,18 @@ __device__ __forceinline__ void epilogue_dma(const ConvArgs& a, const f32x4 (&ac
 // staged value of channel c < cin1 at (disparity d, h, w) is left[c][h][w], of
 // channel cin1 + c right[c][h][w - d], both 0 for w < d: per lane two offset sets
 // (left, right) whose out-of-range entries make the buffer load return the zero.
+// KD = 4 (MT = 1, TD = 1): depth-paired tile for convs with <= 8 output channels.
+// The 16 MFMA rows hold output channels 0..7 of TWO planes d0, d0+1; the four
+// staged input planes p = 0..3 each feed both, through paired weight rows
+// W'[p][8t + c] = W[c][kd = p - t] (zero outside 0..2), packed by
+// pack_weights_dp_kernel.  36 k-steps per plane pair instead of 2 x 27 on
+// half-empty 16-row tiles: 1.5x fewer MFMAs for the 8->8 cell ops.
 template <int MT, int NT, int TW, int TD, int KD = 3, bool CV = false>
 __global__ __launch_bounds__(kConvThreads, 2) void conv3d_dma_kernel(const ConvArgs a) {
   using C = TileCfg<3, MT, NT, TW, TD, KD>;
+  static_assert(KD != 4 || (MT == 1 && TD == 1), "depth pairing is an MT=1, TD=1 tile");
+  constexpr int DSTEP = KD == 4 ? 2 : TD;      // output planes per workgroup
+  constexpr int DOFF = KD == 4 ? 1 : KD / 2;   // staged plane 0 = output plane d0 - DOFF
   constexpr int XSLOTS = (C::IMG + 63) / 64;  // 256-B DMA pieces per channel image
   constexpr int XSLOTS_W = (XSLOTS + kConvWaves - 1) / kConvWaves;
   constexpr int WSLOTS = (C::WS + 255) / 256;  // 1-KB DMA pieces of the weight chunk
@@ -343,7 +360,7 @@ __global__ __launch_bounds__(kConvThreads, 2) void conv3d_dma_kernel(const ConvA
   const int bc = lin / (a.ndz * a.ntiles);
   const int h0 = (tile / a.tiles_w) * C::TH;
   const int w0 = (tile % a.tiles_w) * TW;
-  const int d0 = dz * TD;
+  const int d0 = dz * DSTEP;
   const int b = bc / a.ncob;
   const int co0 = (bc - b * a.ncob) * C::COP;
   const int nchunks = (a.cin + C::CIN_B - 1) / C::CIN_B;
@@ -363,7 +380,7 @@ __global__ __launch_bounds__(kConvThreads, 2) void conv3d_dma_kernel(const ConvA
       const int r = e - kd * C::PLANE;
       const int rr = r / C::RW;
       const int cc = r - rr * C::RW;
-      const int d = d0 + kd - KD / 2, h = h0 + rr - 1, w = w0 + cc - 1;
+      const int d = d0 + kd - DOFF, h = h0 + rr - 1, w = w0 + cc - 1;
       if ((unsigned)d < (unsigned)a.D && (unsigned)h < (unsigned)a.H && (unsigned)w < (unsigned)a.W) {
         if constexpr (CV) {
           if (w >= d) {
@@ -440,9 +457,9 @@ __global__ __launch_bounds__(kConvThreads, 2) void conv3d_dma_kernel(const ConvA
   // small accumulator tiles (the cell ops, which accumulate) have registers to
   // spare for a prefetched residual; big tiles keep 2 WGs/CU without
   constexpr bool RES = TD * MT * NT <= 8;
-  const EpiGeom<3, MT, NT, TW, TD> geo(a, co0, d0, h0, w0, wave, lane);
+  const EpiGeom<3, MT, NT, TW, TD, KD> geo(a, co0, d0, h0, w0, wave, lane);
   EpiRegs<MT, NT, TD, RES> epi;
-  epi_prefetch<3, MT, NT, TW, TD, RES>(a, epi, geo, b);
+  epi_prefetch<3, MT, NT, TW, TD, RES, KD>(a, epi, geo, b);
   for (int ch = 0; ch < nchunks; ++ch) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's pieces of chunk ch landed
     __syncthreads();  // ... and everyone's; everyone is done reading chunk ch-1's stage
@@ -450,7 +467,7 @@ __global__ __launch_bounds__(kConvThreads, 2) void conv3d_dma_kernel(const ConvA
     const float* xs = smem + (ch & 1) * C::STAGE;
     mfma_chunk<3, MT, NT, TW, TD, KD>(xs, xs + C::XS, xoff, woff, acc);
   }
-  epilogue_dma<3, MT, NT, TW, TD, RES>(a, acc, epi, geo, b);
+  epilogue_dma<3, MT, NT, TW, TD, RES, KD>(a, acc, epi, geo, b);
 }
 
 // A launch plan: which instantiation runs a given shape (also reported by name).
@@ -499,6 +516,8 @@ int launch_dma(K kernel, const ConvArgs& a0, int th, int tw, int td, int B, hipS
 
 // 2D (KD = 1) tiles for the feature net: one plane per workgroup.
 #define LEA_DMA2D_LIST(X, MT) X(MT, 1, 16, 1, 1) X(MT, 2, 16, 1, 1)
+// Depth-paired tiles (KD = 4, couts <= 8; grid steps two planes per workgroup).
+#define LEA_DMA_DP_LIST(X) X(1, 1, 16, 1, 4) X(1, 2, 16, 1, 4)
 
 // Per-MT entry points (defined by LEA_DMA_TU in conv3d_dma_mt*.hip).  lds_bytes
 // returns 0 for a tile that is not instantiated; run returns LEA_E_UNSUPPORTED.
@@ -513,6 +532,7 @@ LEA_DMA_DECL_CV(2)
 LEA_DMA_DECL_CV(3)
 LEA_DMA_DECL_CV(4)
 #undef LEA_DMA_DECL_CV
+int run_dma_dp(const Plan& p, const ConvArgs& a, int B, hipStream_t st);  // conv3d_dma_mt1.hip
 LEA_DMA_DECL(1)
 LEA_DMA_DECL(2)
 LEA_DMA_DECL(3)
@@ -529,6 +549,10 @@ LEA_DMA_DECL(4)
   if (p.nt == NT && p.tw == TW && p.td == TD)                                             \
     return launch_dma(conv3d_dma_kernel<MT, NT, TW, TD, KD>,                              \
                       a, TileCfg<3, MT, NT, TW, TD, KD>::TH, TW, TD, B, st);
+#define LEA_DMA_DP_RUN_CASE(MT, NT, TW, TD, KD)                                          \
+  if (p.nt == NT && p.tw == TW)                                                           \
+    return launch_dma(conv3d_dma_kernel<MT, NT, TW, TD, KD>,                              \
+                      a, TileCfg<3, MT, NT, TW, TD, KD>::TH, TW, 2, B, st);
 #define LEA_DMA_CV_RUN_CASE(MT, NT, TW, TD, KD)                                          \
   if (p.nt == NT && p.tw == TW && p.td == TD)                                             \
     return launch_dma(conv3d_dma_kernel<MT, NT, TW, TD, KD, true>,                        \

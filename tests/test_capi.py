@@ -70,7 +70,7 @@ def test_invalid_arguments_are_rejected_before_launch():
                                         None) == 1001
 
 
-@pytest.mark.parametrize("cout,cin,k", [(32, 64, 3), (64, 128, 3), (16, 16, 3), (8, 8, 3),
+@pytest.mark.parametrize("cout,cin,k", [(32, 64, 3), (64, 128, 3), (16, 16, 3), (8, 8, 3), (3, 5, 3),
                                         (1, 32, 3), (16, 64, 1), (32, 128, 1), (8, 64, 1),
                                         (128, 256, 1), (80, 12, 3)])
 def test_packed_sizes(cout, cin, k):
@@ -81,5 +81,8 @@ def test_packed_sizes(cout, cin, k):
     else:
         mt = 3 if -(-cout // 48) * 48 < -(-cout // 64) * 64 else 4
     cops = mt * 16  # no padding: 32/64-wide rows are XOR-swizzled instead
-    assert n == -(-cout // (mt * 16)) * -(-cin // cin_b) * k ** 3 * cin_b * cops
+    if k == 3 and 2 < cout <= 8:  # depth-paired: 4 input planes x 9 taps, 16 = 2 planes x 8
+        assert n == -(-cin // cin_b) * 36 * cin_b * 16
+    else:
+        assert n == -(-cout // (mt * 16)) * -(-cin // cin_b) * k ** 3 * cin_b * cops
     assert _lib.load().lea_conv3d_packed_floats(16, 8, 5) == 0
