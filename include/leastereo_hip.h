@@ -17,7 +17,8 @@
  *   - Return 0 on success; LEA_E_INVALID / LEA_E_UNSUPPORTED on bad arguments
  *     (nothing launched); otherwise a hipError_t from the launch.
  *     lea_last_error() describes the last failure on the calling thread.
- *   - dtype: LEA_F32 (the reference's arithmetic).  LEA_BF16 is reserved.
+ *   - dtype: LEA_F32 (the reference's arithmetic) for the entries below that take
+ *     one; the bf16 path (configs 3/4) has its own *_bf16 entries at the end.
  */
 #ifndef LEASTEREO_HIP_H
 #define LEASTEREO_HIP_H
@@ -171,6 +172,51 @@ int lea_tapsum_upsample(const void* q, int64_t q_bstride, void* y, int64_t y_bst
  * fused, U never materialised.  cost: [B, 1, D3, H3, W3]; disp: [B, 3H3, 3W3] fp32. */
 int lea_disparity_regression(const void* cost, float* disp, int B, int D3, int H3, int W3,
                              int maxdisp, int dtype, void* stream);
+
+/* ---- bf16 path (BASELINE configs 3 and 4) ----
+ * Activations are bf16 in the "c8" layout: NCDHW with channels blocked by 8
+ * innermost, x[b][c/8][d][h][w][c%8] (one voxel's 8 channels = one 16-byte word;
+ * channel counts multiples of 8; a channel slice on a multiple of 8 is a block
+ * slice, so the free-cat trick carries over).  Convs run on the bf16 matrix cores
+ * (v_mfma_f32_16x16x32_bf16) with f32 accumulation and the f32 BN epilogue;
+ * outputs are rounded to bf16.  Batch strides are in elements. */
+
+/* Packed bf16 weights for a ConvBR of this shape (elements; 0 = unsupported), and
+ * the packing of an f32 OIDHW weight into them (k in {1, 3}, cin % 8 == 0). */
+size_t lea_conv3d_packed_elems_bf16(int cout, int cin, int k);
+int lea_conv3d_pack_weights_bf16(const float* w, void* packed, int cout, int cin, int k,
+                                 void* stream);
+
+/* lea_conv3d_bnrelu on c8 tensors (cout, cin, cin2 multiples of 8). */
+int lea_conv3d_bnrelu_bf16(const void* x, int64_t x_bstride, const void* x2, int64_t x2_bstride,
+                           int cin2, const void* w_packed, const float* scale, const float* shift,
+                           const void* residual, int64_t r_bstride, void* y, int64_t y_bstride,
+                           int B, int cin, int cout, int D, int H, int W, int k, unsigned flags,
+                           void* stream);
+
+/* lea_conv3d_bnrelu_costvolume on c8 feature maps [B, C/8, H, W, 8] (C % 16 == 0). */
+int lea_conv3d_bnrelu_costvolume_bf16(const void* left, const void* right, int64_t f_bstride,
+                                      const void* w_packed, const float* scale, const float* shift,
+                                      void* y, int64_t y_bstride, int B, int C, int cout, int D3,
+                                      int H, int W, unsigned flags, void* stream);
+
+/* Kernel instantiation the bf16 conv of this shape launches. */
+const char* lea_conv3d_kernel_name_bf16(int B, int cout, int cin, int D, int H, int W, int k,
+                                        int costvolume);
+
+/* lea_resample3d_trilinear on c8 tensors (same source-index rule and epilogue). */
+int lea_resample3d_trilinear_bf16(const void* x, int64_t x_bstride, void* y, int64_t y_bstride,
+                                  int B, int C, int Di, int Hi, int Wi, int Do, int Ho, int Wo,
+                                  int align_corners, const float* scale, const float* shift,
+                                  unsigned flags, void* stream);
+
+/* Layout converters: f32 NC[D]HW (vol = D*H*W voxels per channel) <-> bf16 c8. */
+int lea_to_c8_bf16(const float* x, int64_t x_bstride, void* y, int64_t y_bstride, int B, int C,
+                   int64_t vol, void* stream);
+int lea_from_c8_bf16(const void* x, int64_t x_bstride, float* y, int64_t y_bstride, int B, int C,
+                     int64_t vol, void* stream);
+
+/* lea_tapsum_upsample also takes dtype LEA_BF16: q in the c8 layout, output f32. */
 
 #ifdef __cplusplus
 }

@@ -51,6 +51,18 @@ SIGNATURES = {
     "lea_tapsum_upsample": (_i, [_p, _i64, _p, _i64, _i, _i, _i, _i, _i, _i, _i, _i, _p, _p, _u,
                                  _p, _i, _p]),
     "lea_disparity_regression": (_i, [_p, _p, _i, _i, _i, _i, _i, _i, _p]),
+    # bf16 path (c8 layout)
+    "lea_conv3d_packed_elems_bf16": (ctypes.c_size_t, [_i, _i, _i]),
+    "lea_conv3d_pack_weights_bf16": (_i, [_p, _p, _i, _i, _i, _p]),
+    "lea_conv3d_bnrelu_bf16": (_i, [_p, _i64, _p, _i64, _i, _p, _p, _p, _p, _i64, _p, _i64,
+                                    _i, _i, _i, _i, _i, _i, _i, _u, _p]),
+    "lea_conv3d_bnrelu_costvolume_bf16": (_i, [_p, _p, _i64, _p, _p, _p, _p, _i64, _i, _i, _i, _i,
+                                               _i, _i, _u, _p]),
+    "lea_conv3d_kernel_name_bf16": (ctypes.c_char_p, [_i, _i, _i, _i, _i, _i, _i, _i]),
+    "lea_resample3d_trilinear_bf16": (_i, [_p, _i64, _p, _i64, _i, _i, _i, _i, _i, _i, _i, _i,
+                                           _i, _p, _p, _u, _p]),
+    "lea_to_c8_bf16": (_i, [_p, _i64, _p, _i64, _i, _i, _i64, _p]),
+    "lea_from_c8_bf16": (_i, [_p, _i64, _p, _i64, _i, _i, _i64, _p]),
 }
 
 _lib = None

@@ -1,0 +1,555 @@
+// bf16 path (BASELINE configs 3 and 4): ConvBR3d on bf16 activations with the
+// gfx950 bf16 matrix cores, v_mfma_f32_16x16x32_bf16 (f32 accumulate).
+// Replaces models/operations_3d.py:31-47 like conv3d.hip, at dtype LEA_BF16.
+//
+// Layout "c8": bf16 NCDHW with channels blocked by 8 innermost,
+//     x[b][c / 8][d][h][w][c % 8]
+// so one voxel's 8 channels are one 16-byte word.  The MFMA wants, per lane, 8
+// consecutive K values (lane l holds A[row l&15][k = 8(l>>4) + j] and
+// B[k = 8(l>>4) + j][col l&15]); with K ordered (tap, channel block) a B fragment
+// is one such word: ds_read_b128 from the staged halo.  K slot 4s + g of k-step s
+// (lane group g = l >> 4) is tap (4s+g) / NB, channel block (4s+g) % NB of the
+// chunk, NB in {1, 2} blocks per K chunk (4 for 1x1).
+//
+// Workgroup = 4 waves over a TH x 16 voxel x TD plane tile and COB = WC*MT*16
+// output channels: WC waves split the couts (MT 16-row tiles each), WV = 4/WC
+// split the voxel rows (NV 16-voxel rows each), so every wave reuses each B
+// fragment for MT MFMAs and each A fragment for NV.  A fragments (weights) come
+// straight from global memory (L2-resident, packed in fragment order) into
+// registers at the start of each chunk; the input halo is staged by LDS-DMA
+// (buffer_load_dwordx4 ... lds: one voxel-block per lane, out-of-range offsets
+// return zeros = the conv's padding), double-buffered.
+#include "common.h"
+
+namespace lea {
+namespace bf {
+
+using bf16x8 = __attribute__((ext_vector_type(8))) __bf16;
+using bf16x4 = __attribute__((ext_vector_type(4))) __bf16;
+using f32x4 = __attribute__((__vector_size__(4 * sizeof(float)))) float;
+using lds_void = __attribute__((address_space(3))) void;
+constexpr int kThreads = 256;
+
+struct Args {
+  const __bf16* x;   // blocks [0, cb1)
+  long long xbs;
+  const __bf16* x2;  // blocks [cb1, cin/8): the virtual concat
+  long long x2bs;
+  int cb1;
+  const __bf16* wp;
+  const float* scale;
+  const float* shift;
+  const __bf16* res;
+  long long rbs;
+  __bf16* y;
+  long long ybs;
+  int cin, cout, D, H, W;
+  int tiles_w, ntiles, ndz, nblk, ncob, nchunks;
+  unsigned flags;
+};
+
+// packing geometry shared by host and device
+__host__ __device__ constexpr int cob_of(int cout) { return cout <= 16 ? 16 : (cout <= 32 ? 32 : 64); }
+__host__ __device__ constexpr int nb_of(int cin, int ks) { return ks == 1 ? 4 : (cin <= 8 ? 1 : 2); }
+__host__ __device__ constexpr int ksteps(int ks, int nb) { return (ks * ks * ks * nb + 3) / 4; }
+
+template <int KS, int MT, int WC, int TH, int TD, int NB, bool CV>
+struct Cfg {
+  static constexpr int WV = 4 / WC;
+  static constexpr int VT = TH * TD;        // 16-voxel rows in the tile
+  static constexpr int NV = VT / WV;        // per wave
+  static_assert(VT % WV == 0, "rows per wave");
+  static constexpr int T = KS * KS * KS;
+  static constexpr int S = (T * NB + 3) / 4;
+  static constexpr int COB = WC * MT * 16;
+  static constexpr int PLANES = KS + TD - 1;
+  static constexpr int RH = TH + KS - 1, RW = 16 + KS - 1;
+  static constexpr int PLANE = RH * RW;
+  static constexpr int IMG = PLANES * PLANE;  // 16-B voxel-blocks per channel block
+  static constexpr int STAGE = NB * IMG;      // 16-B slots per stage
+  static constexpr int PIECES = (IMG + 63) / 64;
+  static constexpr int PIECES_W = (PIECES + 3) / 4;
+};
+
+template <int KS, int MT, int WC, int TH, int TD, int NB, bool CV>
+__global__ __launch_bounds__(kThreads, 2) void conv_bf16_kernel(const Args a) {
+  using C = Cfg<KS, MT, WC, TH, TD, NB, CV>;
+  __shared__ __attribute__((aligned(16))) bf16x8 smem[2 * C::STAGE];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wc = wave % WC, wv = wave / WC;
+  const int g = lane >> 4, n = lane & 15;
+
+  // XCD-aware 1-D order as the f32 engine (conv3d_impl.h)
+  const int xcd = blockIdx.x % 8, idx = blockIdx.x / 8;
+  const int q8 = a.nblk / 8, r8 = a.nblk % 8;
+  const int lin = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + idx;
+  const int dz = lin % a.ndz;
+  const int tile = (lin / a.ndz) % a.ntiles;
+  const int bc = lin / (a.ndz * a.ntiles);
+  const int b = bc / a.ncob, cob = bc - b * a.ncob;
+  const int h0 = (tile / a.tiles_w) * TH, w0 = (tile % a.tiles_w) * 16, d0 = dz * TD;
+  const int HW = a.H * a.W;
+  const int DHW = HW * a.D;
+
+  // per-lane byte offsets (within one channel block) of this wave's DMA pieces
+  unsigned voff[C::PIECES_W], voffr[CV ? C::PIECES_W : 1];
+#pragma unroll
+  for (int t = 0; t < C::PIECES_W; ++t) {
+    const int e = (wave + 4 * t) * 64 + lane;
+    unsigned v = 0xFFFFFFF0u, vr = 0xFFFFFFF0u;
+    if (e < C::IMG) {
+      const int p = e / C::PLANE, r = e % C::PLANE;
+      const int rr = r / C::RW, cc = r % C::RW;
+      const int d = d0 + p - KS / 2, h = h0 + rr - KS / 2, w = w0 + cc - KS / 2;
+      if ((unsigned)d < (unsigned)a.D && (unsigned)h < (unsigned)a.H && (unsigned)w < (unsigned)a.W) {
+        if constexpr (CV) {
+          if (w >= d) {
+            v = (unsigned)(h * a.W + w) * 16u;
+            vr = (unsigned)(h * a.W + w - d) * 16u;
+          }
+        } else {
+          v = (unsigned)(d * HW + h * a.W + w) * 16u;
+        }
+      }
+    }
+    voff[t] = v;
+    if constexpr (CV) voffr[t] = vr;
+  }
+  // plain locals: a lambda capturing the kernel-argument struct makes the
+  // compiler copy it to scratch
+  const int nblocks = a.cin / 8, cb1 = a.cb1;
+  const __bf16* const xb1 = a.x + (long long)b * a.xbs;
+  const __bf16* const xb2 = a.x2 + (long long)b * a.x2bs;
+  const unsigned brec = (unsigned)(CV ? HW : DHW) * 16u;
+  const long long bstride = (long long)(CV ? HW : DHW) * 8;
+  auto issue = [&](int ch, bf16x8* st) {
+#pragma unroll
+    for (int k = 0; k < NB; ++k) {
+      const int blk = ch * NB + k;
+      const __bf16* base = xb1;
+      unsigned nrec = 0;
+      if (blk < cb1) {
+        base = xb1 + blk * bstride;
+        nrec = brec;
+      } else if (blk < nblocks) {
+        base = xb2 + (blk - cb1) * bstride;
+        nrec = brec;
+      }
+      const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)base, 0, nrec, 0x00020000);
+      // right-image chunk: arithmetic select (a ?: between two register arrays
+      // becomes a pointer select and sends both arrays to scratch)
+      const unsigned rmask = (CV && blk >= cb1) ? 0xFFFFFFFFu : 0u;
+#pragma unroll
+      for (int t = 0; t < C::PIECES_W; ++t) {
+        const int j = wave + 4 * t;
+        unsigned vo = voff[t];
+        if constexpr (CV) vo = voff[t] ^ ((voff[t] ^ voffr[t]) & rmask);
+        if (j < C::PIECES && j * 64 + lane < C::IMG)
+          __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void*)(st + k * C::IMG + j * 64), 16, vo, 0, 0, 0);
+      }
+    }
+  };
+
+  // B fragment slot offset (in 16-B units) of k-step s for this lane
+  auto boff = [&](int s) -> int {
+    const int slot = 4 * s + g;
+    const int tap = min(slot / NB, C::T - 1);  // slots past the last tap carry zero weights
+    const int blk = slot % NB;
+    const int kd = tap / (KS * KS), kh = (tap / KS) % KS, kw = tap % KS;
+    return blk * C::IMG + kd * C::PLANE + kh * C::RW + kw;
+  };
+  int vrow[C::NV];  // staged-halo slot of this wave's rows (output plane t, row r), column n
+#pragma unroll
+  for (int i = 0; i < C::NV; ++i) {
+    const int q = wv * C::NV + i;
+    const int t = q / TH, r = q % TH;
+    vrow[i] = t * C::PLANE + r * C::RW + n;
+  }
+
+  const int mtile0 = wc * MT;
+  const bf16x8* wpv = reinterpret_cast<const bf16x8*>(a.wp);
+  f32x4 acc[MT][C::NV];
+#pragma unroll
+  for (int m = 0; m < MT; ++m)
+#pragma unroll
+    for (int i = 0; i < C::NV; ++i) acc[m][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // A fragments: a window of PF k-steps ahead in registers (the first PF issued
+  // before the chunk's barrier so their L2 latency overlaps the halo DMA)
+  constexpr int PF = C::S < 4 ? C::S : 4;
+  issue(0, smem);
+  for (int ch = 0; ch < a.nchunks; ++ch) {
+    const long long wbase = ((long long)cob * a.nchunks + ch) * C::S * (WC * MT);
+    auto wload = [&](int s, int m) {
+      return wpv[((wbase + (long long)s * (WC * MT) + mtile0 + m) * 4 + g) * 16 + n];
+    };
+    bf16x8 av[C::S][MT];
+#pragma unroll
+    for (int s = 0; s < PF; ++s)
+#pragma unroll
+      for (int m = 0; m < MT; ++m) av[s][m] = wload(s, m);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (ch + 1 < a.nchunks) issue(ch + 1, smem + ((ch + 1) & 1) * C::STAGE);
+    const bf16x8* xs = smem + (ch & 1) * C::STAGE;
+#pragma unroll
+    for (int s = 0; s < C::S; ++s) {
+      if (s + PF < C::S)
+#pragma unroll
+        for (int m = 0; m < MT; ++m) av[s + PF][m] = wload(s + PF, m);
+      const int bo = boff(s);
+#pragma unroll
+      for (int i = 0; i < C::NV; ++i) {
+        const bf16x8 bv = xs[bo + vrow[i]];
+#pragma unroll
+        for (int m = 0; m < MT; ++m)
+          acc[m][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[s][m], bv, acc[m][i], 0, 0, 0);
+      }
+    }
+  }
+
+  // epilogue: lane holds couts 4g..4g+3 of each 16-row tile at voxel column n
+  const bool relu = a.flags & LEA_RELU, resid = a.flags & LEA_RESIDUAL;
+#pragma unroll
+  for (int m = 0; m < MT; ++m) {
+    const int co = cob * C::COB + (mtile0 + m) * 16 + 4 * g;  // first of 4
+    if (co >= a.cout) continue;                                // cout % 4 == 0 (host)
+    float sc[4], sh[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      sc[r] = a.scale ? a.scale[co + r] : 1.f;
+      sh[r] = a.shift ? a.shift[co + r] : 0.f;
+    }
+    const long long cofs = (long long)(co / 8) * DHW * 8 + (co % 8);
+#pragma unroll
+    for (int i = 0; i < C::NV; ++i) {
+      const int q = wv * C::NV + i;
+      const int d = d0 + q / TH, h = h0 + q % TH, w = w0 + n;
+      if (d >= a.D || h >= a.H || w >= a.W) continue;
+      const long long o = cofs + ((long long)d * HW + h * a.W + w) * 8;
+      float v[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        v[r] = acc[m][i][r] * sc[r] + sh[r];
+        if (relu) v[r] = fmaxf(v[r], 0.f);
+      }
+      if (resid) {
+        const bf16x4 rv = *reinterpret_cast<const bf16x4*>(a.res + (long long)b * a.rbs + o);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] += (float)rv[r];
+      }
+      bf16x4 out;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) out[r] = (__bf16)v[r];
+      *reinterpret_cast<bf16x4*>(a.y + (long long)b * a.ybs + o) = out;
+    }
+  }
+}
+
+// weights [cout][cin][k^3] f32 -> [cob][chunk][s][mtile][g][16][8] bf16
+__global__ void pack_bf16_kernel(const float* __restrict__ w, __bf16* __restrict__ packed, int cout,
+                                 int cin, int ks, int nb, int S, int mtiles, int nchunks,
+                                 long long total) {
+  const int T = ks * ks * ks;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
+       i += (long long)gridDim.x * blockDim.x) {
+    long long r = i;
+    const int j = (int)(r % 8); r /= 8;
+    const int n = (int)(r % 16); r /= 16;
+    const int g = (int)(r % 4); r /= 4;
+    const int mt = (int)(r % mtiles); r /= mtiles;
+    const int s = (int)(r % S); r /= S;
+    const int ch = (int)(r % nchunks);
+    const int cob = (int)(r / nchunks);
+    const int slot = 4 * s + g;
+    const int tap = slot / nb, blk = slot % nb;
+    const int co = cob * mtiles * 16 + mt * 16 + n;
+    const int ci = (ch * nb + blk) * 8 + j;
+    float v = 0.f;
+    if (tap < T && co < cout && ci < cin) v = w[((long long)co * cin + ci) * T + tap];
+    packed[i] = (__bf16)v;
+  }
+}
+
+// f32 NCDHW (batch stride xbs) <-> bf16 c8 layout converters
+__global__ void to_c8_kernel(const float* __restrict__ x, long long xbs, __bf16* __restrict__ y,
+                             long long ybs, int C, long long vol) {
+  const int b = blockIdx.y;
+  const long long nvox = vol * (C / 8);
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < nvox;
+       i += (long long)gridDim.x * blockDim.x) {
+    const long long cb = i / vol, v = i % vol;
+    bf16x8 o;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] = (__bf16)x[(long long)b * xbs + (cb * 8 + j) * vol + v];
+    reinterpret_cast<bf16x8*>(y + (long long)b * ybs)[i] = o;
+  }
+}
+
+__global__ void from_c8_kernel(const __bf16* __restrict__ x, long long xbs, float* __restrict__ y,
+                               long long ybs, int C, long long vol) {
+  const int b = blockIdx.y;
+  const long long nvox = vol * (C / 8);
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < nvox;
+       i += (long long)gridDim.x * blockDim.x) {
+    const long long cb = i / vol, v = i % vol;
+    const bf16x8 o = reinterpret_cast<const bf16x8*>(x + (long long)b * xbs)[i];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) y[(long long)b * ybs + (cb * 8 + j) * vol + v] = (float)o[j];
+  }
+}
+
+// Trilinear resample (aten source-index rule, common.h Axis) of a c8 volume with
+// the optional per-channel relu(scale * . + shift) epilogue; one 16-byte voxel
+// block (8 channels) per thread: 8 corner words, interpolated in f32.
+__global__ __launch_bounds__(256) void resample_c8_kernel(
+    const __bf16* __restrict__ x, long long xbs, __bf16* __restrict__ y, long long ybs, int CB,
+    int Di, int Hi, int Wi, int Do, int Ho, int Wo, float rd, float rh, float rw, int ac,
+    const float* __restrict__ scale, const float* __restrict__ shift, unsigned flags) {
+#pragma clang fp contract(off)
+  const int plane = blockIdx.y;  // (b * CB + cb) * Do + od
+  const int od = plane % Do;
+  const int bcb = plane / Do;
+  const int b = bcb / CB, cb = bcb % CB;
+  const Axis ad = axis_index(rd, od, Di, Do, ac);
+  const long long HWi = (long long)Hi * Wi;
+  const bf16x8* xc = reinterpret_cast<const bf16x8*>(x + (long long)b * xbs) + (long long)cb * Di * HWi;
+  bf16x8* yp = reinterpret_cast<bf16x8*>(y + (long long)b * ybs) + ((long long)cb * Do + od) * Ho * Wo;
+  const bool relu = flags & LEA_RELU;
+  for (int t = blockIdx.x * blockDim.x + threadIdx.x; t < Ho * Wo; t += gridDim.x * blockDim.x) {
+    const int oh = t / Wo, ow = t % Wo;
+    const Axis ah = axis_index(rh, oh, Hi, Ho, ac);
+    const Axis aw = axis_index(rw, ow, Wi, Wo, ac);
+    const bf16x8* p0 = xc + ad.i0 * HWi;
+    const bf16x8* p1 = xc + ad.i1 * HWi;
+    const bf16x8 c000 = p0[(long long)ah.i0 * Wi + aw.i0], c001 = p0[(long long)ah.i0 * Wi + aw.i1];
+    const bf16x8 c010 = p0[(long long)ah.i1 * Wi + aw.i0], c011 = p0[(long long)ah.i1 * Wi + aw.i1];
+    const bf16x8 c100 = p1[(long long)ah.i0 * Wi + aw.i0], c101 = p1[(long long)ah.i0 * Wi + aw.i1];
+    const bf16x8 c110 = p1[(long long)ah.i1 * Wi + aw.i0], c111 = p1[(long long)ah.i1 * Wi + aw.i1];
+    bf16x8 o;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      float r = ad.l0 * (ah.l0 * (aw.l0 * (float)c000[j] + aw.l1 * (float)c001[j]) +
+                         ah.l1 * (aw.l0 * (float)c010[j] + aw.l1 * (float)c011[j])) +
+                ad.l1 * (ah.l0 * (aw.l0 * (float)c100[j] + aw.l1 * (float)c101[j]) +
+                         ah.l1 * (aw.l0 * (float)c110[j] + aw.l1 * (float)c111[j]));
+      if (scale) r = r * scale[cb * 8 + j] + shift[cb * 8 + j];
+      if (relu) r = fmaxf(r, 0.f);
+      o[j] = (__bf16)r;
+    }
+    yp[t] = o;
+  }
+}
+
+struct Plan {
+  int ks, mt, wc, th, td, nb;
+};
+
+inline Plan plan(int B, int cout, int D, int H, int W, int ks, int cin) {
+  Plan p;
+  p.ks = ks;
+  const int cobv = cob_of(cout);
+  p.wc = cobv == 64 ? 2 : 1;
+  p.mt = cobv == 16 ? 1 : 2;
+  p.nb = nb_of(cin, ks);
+  p.th = 8;
+  p.td = (ks == 3) ? 2 : 1;
+  const long long ncob = (cout + cobv - 1) / cobv;
+  const long long wgs = (long long)((W + 15) / 16) * ((H + p.th - 1) / p.th) * ((D + p.td - 1) / p.td) * B * ncob;
+  if (wgs < 512) p.th = 4;
+  return p;
+}
+
+#define LEA_BF_CASE(KS, MT, WC, TH, TD, NB, CV)                                       \
+  if (p.ks == KS && p.mt == MT && p.wc == WC && p.th == TH && p.td == TD && p.nb == NB) { \
+    a.tiles_w = (a.W + 15) / 16;                                                      \
+    a.ntiles = a.tiles_w * ((a.H + TH - 1) / TH);                                     \
+    a.ndz = (a.D + TD - 1) / TD;                                                      \
+    const long long nb_ = (long long)a.ntiles * a.ndz * B * a.ncob;                   \
+    LEA_CHECK_ARG(nb_ < (1LL << 31), "lea_conv3d(bf16): grid too large");             \
+    a.nblk = (int)nb_;                                                                \
+    conv_bf16_kernel<KS, MT, WC, TH, TD, NB, CV><<<dim3((unsigned)nb_), kThreads, 0, st>>>(a); \
+    return launch_status("lea_conv3d(bf16)");                                         \
+  }
+#define LEA_BF_TH(KS, MT, WC, TD, NB, CV) \
+  LEA_BF_CASE(KS, MT, WC, 8, TD, NB, CV) LEA_BF_CASE(KS, MT, WC, 4, TD, NB, CV)
+#define LEA_BF_MT(KS, TD, NB, CV) \
+  LEA_BF_TH(KS, 1, 1, TD, NB, CV) LEA_BF_TH(KS, 2, 1, TD, NB, CV) LEA_BF_TH(KS, 2, 2, TD, NB, CV)
+
+int run(const Plan& p, Args a, int B, hipStream_t st, bool cv) {
+  if (cv) {
+    LEA_BF_MT(3, 2, 2, true)
+  } else {
+    LEA_BF_MT(3, 2, 1, false)
+    LEA_BF_MT(3, 2, 2, false)
+    LEA_BF_MT(1, 1, 4, false)
+  }
+  set_error("lea_conv3d(bf16): no tile ks=%d mt=%d wc=%d th=%d td=%d nb=%d cv=%d", p.ks, p.mt, p.wc,
+            p.th, p.td, p.nb, (int)cv);
+  return LEA_E_UNSUPPORTED;
+}
+
+thread_local char g_bf_name[96];
+
+}  // namespace bf
+}  // namespace lea
+
+using namespace lea;
+
+extern "C" size_t lea_conv3d_packed_elems_bf16(int cout, int cin, int k) {
+  if (cout <= 0 || cin <= 0 || cin % 8 != 0 || (k != 1 && k != 3)) return 0;
+  const int cobv = bf::cob_of(cout), nb = bf::nb_of(cin, k);
+  const int nch = (cin / 8 + nb - 1) / nb;
+  return (size_t)((cout + cobv - 1) / cobv) * nch * bf::ksteps(k, nb) * (cobv / 16) * 4 * 16 * 8;
+}
+
+extern "C" int lea_conv3d_pack_weights_bf16(const float* w, void* packed, int cout, int cin, int k,
+                                            void* stream) {
+  clear_error();
+  LEA_CHECK_ARG(w && packed, "lea_conv3d_pack_weights_bf16: null pointer");
+  LEA_CHECK_ARG(cout > 0 && cin > 0 && cin % 8 == 0 && cout % 4 == 0 && (k == 1 || k == 3),
+                "lea_conv3d_pack_weights_bf16: unsupported shape cout=%d cin=%d k=%d", cout, cin, k);
+  const int cobv = bf::cob_of(cout), nb = bf::nb_of(cin, k);
+  const int nch = (cin / 8 + nb - 1) / nb;
+  const long long total = (long long)lea_conv3d_packed_elems_bf16(cout, cin, k);
+  const int grid = (int)std::min<long long>((total + 255) / 256, 4096);
+  bf::pack_bf16_kernel<<<grid, 256, 0, as_stream(stream)>>>(w, (__bf16*)packed, cout, cin, k, nb,
+                                                            bf::ksteps(k, nb), cobv / 16, nch, total);
+  return launch_status("lea_conv3d_pack_weights_bf16");
+}
+
+extern "C" const char* lea_conv3d_kernel_name_bf16(int B, int cout, int cin, int D, int H, int W,
+                                                   int k, int costvolume) {
+  if (B <= 0 || cout <= 0 || cin <= 0 || (k != 1 && k != 3) || D <= 0 || H <= 0 || W <= 0) return nullptr;
+  const bf::Plan p = bf::plan(B, cout, D, H, W, k, cin);
+  snprintf(bf::g_bf_name, sizeof(bf::g_bf_name), "conv_bf16_kernel<%d, %d, %d, %d, %d, %d, %s>",
+           p.ks, p.mt, p.wc, p.th, p.td, p.nb, costvolume ? "true" : "false");
+  return bf::g_bf_name;
+}
+
+static int bf16_conv_common(bf::Args& a, int B, int k, bool cv, void* stream) {
+  clear_error();
+  LEA_CHECK_ARG(a.x && a.wp && a.y, "lea_conv3d(bf16): null pointer");
+  LEA_CHECK_ARG((a.scale == nullptr) == (a.shift == nullptr),
+                "lea_conv3d(bf16): scale/shift must both be set or both NULL");
+  LEA_CHECK_ARG(!(a.flags & LEA_RESIDUAL) || a.res, "lea_conv3d(bf16): LEA_RESIDUAL without residual");
+  LEA_CHECK_ARG(B > 0 && a.cin > 0 && a.cout > 0 && a.D > 0 && a.H > 0 && a.W > 0,
+                "lea_conv3d(bf16): bad shape");
+  LEA_CHECK_ARG(a.cin % 8 == 0 && a.cout % 8 == 0 && a.cb1 * 8 <= a.cin,
+                "lea_conv3d(bf16): channels must be multiples of 8 (cin=%d cout=%d)", a.cin, a.cout);
+  LEA_CHECK_ARG((long long)a.D * a.H * a.W * 16 < (1LL << 32), "lea_conv3d(bf16): volume too large");
+  LEA_CHECK_ARG(a.x != (const __bf16*)a.y && a.x2 != (const __bf16*)a.y,
+                "lea_conv3d(bf16): input aliases output");
+  const bf::Plan p = bf::plan(B, a.cout, a.D, a.H, a.W, k, a.cin);
+  const int cobv = bf::cob_of(a.cout);
+  a.ncob = (a.cout + cobv - 1) / cobv;
+  a.nchunks = (a.cin / 8 + p.nb - 1) / p.nb;
+  return bf::run(p, a, B, as_stream(stream), cv);
+}
+
+// dtype LEA_BF16 counterparts of lea_conv3d_bnrelu / lea_conv3d_bnrelu_costvolume
+// (tensors in the c8 layout; batch strides in elements)
+extern "C" int lea_conv3d_bnrelu_bf16(const void* x, int64_t x_bstride, const void* x2,
+                                      int64_t x2_bstride, int cin2, const void* w_packed,
+                                      const float* scale, const float* shift, const void* residual,
+                                      int64_t r_bstride, void* y, int64_t y_bstride, int B, int cin,
+                                      int cout, int D, int H, int W, int k, unsigned flags,
+                                      void* stream) {
+  bf::Args a{};
+  a.x = (const __bf16*)x;
+  a.xbs = x_bstride;
+  a.x2 = (const __bf16*)x2;
+  a.x2bs = x2_bstride;
+  a.cb1 = (cin - cin2) / 8;
+  a.wp = (const __bf16*)w_packed;
+  a.scale = scale;
+  a.shift = shift;
+  a.res = (const __bf16*)residual;
+  a.rbs = r_bstride;
+  a.y = (__bf16*)y;
+  a.ybs = y_bstride;
+  a.cin = cin;
+  a.cout = cout;
+  a.D = D;
+  a.H = H;
+  a.W = W;
+  a.flags = flags;
+  if (cin2 % 8 != 0 || (cin2 > 0 && !x2)) {
+    set_error("lea_conv3d_bnrelu_bf16: bad second source");
+    return LEA_E_INVALID;
+  }
+  return bf16_conv_common(a, B, k, false, stream);
+}
+
+extern "C" int lea_conv3d_bnrelu_costvolume_bf16(const void* left, const void* right,
+                                                 int64_t f_bstride, const void* w_packed,
+                                                 const float* scale, const float* shift, void* y,
+                                                 int64_t y_bstride, int B, int C, int cout, int D3,
+                                                 int H, int W, unsigned flags, void* stream) {
+  bf::Args a{};
+  a.x = (const __bf16*)left;
+  a.xbs = f_bstride;
+  a.x2 = (const __bf16*)right;
+  a.x2bs = f_bstride;
+  a.cb1 = C / 8;
+  a.wp = (const __bf16*)w_packed;
+  a.scale = scale;
+  a.shift = shift;
+  a.y = (__bf16*)y;
+  a.ybs = y_bstride;
+  a.cin = 2 * C;
+  a.cout = cout;
+  a.D = D3;
+  a.H = H;
+  a.W = W;
+  a.flags = flags & LEA_RELU;
+  if (C % 16 != 0) {  // chunks of 2 blocks must not straddle left/right
+    set_error("lea_conv3d_bnrelu_costvolume_bf16: C=%d must be a multiple of 16", C);
+    return LEA_E_INVALID;
+  }
+  return bf16_conv_common(a, B, 3, true, stream);
+}
+
+extern "C" int lea_to_c8_bf16(const float* x, int64_t x_bstride, void* y, int64_t y_bstride, int B,
+                              int C, int64_t vol, void* stream) {
+  clear_error();
+  LEA_CHECK_ARG(x && y && B > 0 && C > 0 && C % 8 == 0 && vol > 0 && B <= 65535,
+                "lea_to_c8_bf16: bad arguments");
+  const long long n = vol * (C / 8);
+  dim3 grid((unsigned)std::min<long long>((n + 255) / 256, 65535), B);
+  bf::to_c8_kernel<<<grid, 256, 0, as_stream(stream)>>>(x, x_bstride, (__bf16*)y, y_bstride, C, vol);
+  return launch_status("lea_to_c8_bf16");
+}
+
+extern "C" int lea_from_c8_bf16(const void* x, int64_t x_bstride, float* y, int64_t y_bstride, int B,
+                                int C, int64_t vol, void* stream) {
+  clear_error();
+  LEA_CHECK_ARG(x && y && B > 0 && C > 0 && C % 8 == 0 && vol > 0 && B <= 65535,
+                "lea_from_c8_bf16: bad arguments");
+  const long long n = vol * (C / 8);
+  dim3 grid((unsigned)std::min<long long>((n + 255) / 256, 65535), B);
+  bf::from_c8_kernel<<<grid, 256, 0, as_stream(stream)>>>((const __bf16*)x, x_bstride, y, y_bstride, C, vol);
+  return launch_status("lea_from_c8_bf16");
+}
+
+extern "C" int lea_resample3d_trilinear_bf16(const void* x, int64_t x_bstride, void* y,
+                                             int64_t y_bstride, int B, int C, int Di, int Hi,
+                                             int Wi, int Do, int Ho, int Wo, int align_corners,
+                                             const float* scale, const float* shift,
+                                             unsigned flags, void* stream) {
+  clear_error();
+  LEA_CHECK_ARG(x && y && x != y, "lea_resample3d_trilinear_bf16: null or aliased pointer");
+  LEA_CHECK_ARG((scale == nullptr) == (shift == nullptr),
+                "lea_resample3d_trilinear_bf16: scale/shift must both be set or both NULL");
+  LEA_CHECK_ARG(B > 0 && C > 0 && C % 8 == 0 && Di > 0 && Hi > 0 && Wi > 0 && Do > 0 && Ho > 0 &&
+                    Wo > 0 && (long long)B * (C / 8) * Do <= 65535,
+                "lea_resample3d_trilinear_bf16: bad shape");
+  const int ac = align_corners ? 1 : 0;
+  const long long cells = (long long)Ho * Wo;
+  dim3 grid((unsigned)std::min<long long>((cells + 255) / 256, 64), B * (C / 8) * Do);
+  bf::resample_c8_kernel<<<grid, 256, 0, as_stream(stream)>>>(
+      (const __bf16*)x, x_bstride, (__bf16*)y, y_bstride, C / 8, Di, Hi, Wi, Do, Ho, Wo,
+      axis_ratio(Di, Do, ac), axis_ratio(Hi, Ho, ac), axis_ratio(Wi, Wo, ac), ac, scale, shift, flags);
+  return launch_status("lea_resample3d_trilinear_bf16");
+}

@@ -420,12 +420,14 @@ __global__ __launch_bounds__(kConvThreads, 2) void conv3d_dma_kernel(const ConvA
         n = crec;
       }
       const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)base, 0, n, 0x00020000);
-      const bool right = CV && c >= a.cin1;  // uniform: chunks never straddle cin1 in CV
+      // uniform (chunks never straddle cin1 in CV); an arithmetic select -- a ?:
+      // between two register arrays becomes a pointer select into scratch
+      const unsigned rmask = (CV && c >= a.cin1) ? 0xFFFFFFFFu : 0u;
 #pragma unroll
       for (int t = 0; t < XSLOTS_W; ++t) {
         const int j = wave + kConvWaves * t;
         unsigned vo = voff[t];
-        if constexpr (CV) vo = right ? voffr[t] : voff[t];
+        if constexpr (CV) vo = voff[t] ^ ((voff[t] ^ voffr[t]) & rmask);
         if (j < XSLOTS && j * 64 + lane < C::IMG)
           __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void*)(st + ci * C::CIS + j * 64), 4,
                                                    vo, 0, 0, 0);

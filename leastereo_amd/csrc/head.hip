@@ -68,6 +68,39 @@ __global__ __launch_bounds__(256) void tapsum_dpass_f32(const float* __restrict_
   }
 }
 
+// pass 1 with q in the bf16 c8 layout (dtype LEA_BF16): channel co*27 + tap at
+// block (co*27 + tap) / 8, lane (co*27 + tap) % 8
+__global__ __launch_bounds__(256) void tapsum_dpass_c8(const __bf16* __restrict__ q, long long qbs,
+                                                       float* __restrict__ ws, int cout, int Di,
+                                                       int Hi, int Wi, int Do, float rd) {
+#pragma clang fp contract(off)
+  int r = blockIdx.y;  // ((b * cout + co) * Do + d) * 9 + khw
+  const int khw = r % 9;
+  r /= 9;
+  const int d = r % Do;
+  r /= Do;
+  const int co = r % cout;
+  const int b = r / cout;
+  const long long HWi = (long long)Hi * Wi;
+  const long long vol = HWi * Di;
+  const __bf16* qb = q + (long long)b * qbs;
+  float* yo = ws + (long long)blockIdx.y * HWi;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < HWi;
+       i += (long long)gridDim.x * blockDim.x) {
+    float acc = 0.f;
+#pragma unroll
+    for (int kd = 0; kd < 3; ++kd) {
+      const int pd = d + kd - 1;
+      if ((unsigned)pd >= (unsigned)Do) continue;
+      const Axis ad = axis_index(rd, pd, Di, Do, 1);
+      const int c = co * 27 + kd * 9 + khw;
+      const __bf16* qc = qb + (long long)(c / 8) * vol * 8 + (c % 8);
+      acc += ad.l0 * (float)qc[(ad.i0 * HWi + i) * 8] + ad.l1 * (float)qc[(ad.i1 * HWi + i) * 8];
+    }
+    yo[i] = acc;
+  }
+}
+
 // pass 2: one workgroup per output row (b, co, d, h); lanes along w
 __global__ __launch_bounds__(512) void tapsum_hwpass_f32(
     const float* __restrict__ ws, float* __restrict__ y, long long ybs, int cout, int Hi, int Wi,
@@ -124,6 +157,8 @@ extern "C" int lea_tapsum_upsample(const void* q, int64_t q_bstride, void* y, in
                                    int B, int cout, int Di, int Hi, int Wi, int Do, int Ho, int Wo,
                                    const float* scale, const float* shift, unsigned flags,
                                    void* workspace, int dtype, void* stream) {
+  // dtype LEA_BF16: q in the bf16 c8 layout (27*cout channels padded to a multiple
+  // of 8); y is f32 NCDHW either way (the disparity regression reads f32)
   using namespace lea;
   clear_error();
   LEA_CHECK_ARG(q && y && q != y && workspace, "lea_tapsum_upsample: null or aliased pointer");
@@ -133,13 +168,26 @@ extern "C" int lea_tapsum_upsample(const void* q, int64_t q_bstride, void* y, in
                 "lea_tapsum_upsample: bad shape");
   LEA_CHECK_ARG((long long)B * cout * Do * Ho < (1LL << 31) && (long long)B * cout * Do * 9 <= 65535,
                 "lea_tapsum_upsample: grid too large");
-  if (dtype != LEA_F32) {
+  if (dtype != LEA_F32 && dtype != LEA_BF16) {
     set_error("lea_tapsum_upsample: dtype %d unsupported", dtype);
     return LEA_E_UNSUPPORTED;
   }
   hipStream_t st = as_stream(stream);
   float* ws = (float*)workspace;
   const long long HWi = (long long)Hi * Wi;
+  if (dtype == LEA_BF16) {
+    dim3 g1((unsigned)((HWi + 255) / 256), (unsigned)(B * cout * Do * 9));
+    tapsum_dpass_c8<<<g1, 256, 0, st>>>((const __bf16*)q, q_bstride, ws, cout, Di, Hi, Wi, Do,
+                                        axis_ratio(Di, Do, 1));
+    const int rc = launch_status("lea_tapsum_upsample");
+    if (rc) return rc;
+    const int threads = Wo >= 512 ? 512 : ((Wo + 63) / 64) * 64;
+    dim3 g2((unsigned)((long long)B * cout * Do * Ho));
+    tapsum_hwpass_f32<<<g2, threads, 0, st>>>(ws, (float*)y, y_bstride, cout, Hi, Wi, Do, Ho, Wo,
+                                              axis_ratio(Hi, Ho, 1), axis_ratio(Wi, Wo, 1), scale,
+                                              shift, flags);
+    return launch_status("lea_tapsum_upsample");
+  }
   const bool vec = (HWi % 4) == 0 && ((uintptr_t)q % 16) == 0 && (q_bstride % 4) == 0 &&
                    ((long long)Di * HWi) % 4 == 0 && ((uintptr_t)ws % 16) == 0;
   const long long n = vec ? HWi / 4 : HWi;

@@ -369,3 +369,179 @@ def disparity_regression(cost: torch.Tensor, maxdisp: int) -> torch.Tensor:
                                                maxdisp, LEA_F32, _stream()),
           "lea_disparity_regression")
     return disp
+
+
+# ------------------------------------------------------------------ bf16 path (c8)
+# Activations: torch.bfloat16 [B, C/8, D, H, W, 8] ("c8": 8 channels per voxel word).
+
+def _require_c8(*ts):
+    for t in ts:
+        if t is not None and (not t.is_cuda or t.dtype != torch.bfloat16 or t.dim() != 6
+                              or t.shape[-1] != 8):
+            raise _lib.HipKernelError(
+                f"bf16 path needs [B, C/8, D, H, W, 8] bfloat16 ROCm tensors, got {t.dtype} "
+                f"{tuple(t.shape)} on {t.device}")
+
+
+def _check_c8_view(t: torch.Tensor, name: str):
+    b, cb, d, h, w, _ = t.shape
+    if t.stride()[1:] != (d * h * w * 8, h * w * 8, w * 8, 8, 1):
+        raise ValueError(f"{name}: c8 block slice with contiguous blocks required, strides {t.stride()}")
+    return t.stride(0)
+
+
+def c8_channels(t: torch.Tensor) -> int:
+    return t.shape[1] * 8
+
+
+def to_c8(x: torch.Tensor) -> torch.Tensor:
+    """f32 [B, C, D, H, W] (or [B, C, H, W] as D = 1) -> bf16 c8."""
+    _require_cuda(x)
+    x5 = x.unsqueeze(2) if x.dim() == 4 else x
+    b, c, d, h, w = x5.shape
+    xbs = _check_volume_view(x5, "x")
+    out = torch.empty((b, c // 8, d, h, w, 8), device=x.device, dtype=torch.bfloat16)
+    check(_lib.load().lea_to_c8_bf16(x5.data_ptr(), xbs, out.data_ptr(), out.stride(0), b, c,
+                                     d * h * w, _stream()), "lea_to_c8_bf16")
+    return out
+
+
+def from_c8(x: torch.Tensor) -> torch.Tensor:
+    """bf16 c8 -> f32 [B, C, D, H, W]."""
+    _require_c8(x)
+    b, cb, d, h, w, _ = x.shape
+    xbs = _check_c8_view(x, "x")
+    out = torch.empty((b, cb * 8, d, h, w), device=x.device, dtype=torch.float32)
+    check(_lib.load().lea_from_c8_bf16(x.data_ptr(), xbs, out.data_ptr(), out.stride(0), b, cb * 8,
+                                       d * h * w, _stream()), "lea_from_c8_bf16")
+    return out
+
+
+def pack_conv_weight_bf16(w: torch.Tensor) -> torch.Tensor:
+    """[cout, cin, k, k, k] f32 device weight -> packed bf16 fragments (bf16 engine)."""
+    _require_cuda(w)
+    w = w.detach().contiguous()
+    cout, cin, k = w.shape[0], w.shape[1], w.shape[-1]
+    lib = _lib.load()
+    n = lib.lea_conv3d_packed_elems_bf16(cout, cin, k)
+    if n == 0:
+        raise ValueError(f"unsupported bf16 conv shape cout={cout} cin={cin} k={k}")
+    packed = torch.empty(n, device=w.device, dtype=torch.bfloat16)
+    check(lib.lea_conv3d_pack_weights_bf16(w.data_ptr(), packed.data_ptr(), cout, cin, k, _stream()),
+          "lea_conv3d_pack_weights_bf16")
+    return packed
+
+
+def conv_kernel_name_bf16(b, cout, cin, d, h, w, k, costvolume=False):
+    name = _lib.load().lea_conv3d_kernel_name_bf16(b, cout, cin, d, h, w, k, 1 if costvolume else 0)
+    return name.decode() if name else None
+
+
+def conv3d_bnrelu_bf16(x: torch.Tensor, packed: torch.Tensor, cout: int, k: int,
+                       scale: torch.Tensor | None, shift: torch.Tensor | None, relu: bool = True,
+                       out: torch.Tensor | None = None, accumulate: bool = False,
+                       x2: torch.Tensor | None = None,
+                       residual: torch.Tensor | None = None) -> torch.Tensor:
+    """conv3d_bnrelu at dtype bf16 on c8 tensors (out may be a block slice)."""
+    _require_c8(x, x2, out, residual)
+    _require_cuda(scale, shift)
+    b, cb, d, h, w, _ = x.shape
+    xbs = _check_c8_view(x, "x")
+    cin2, x2bs = 0, 0
+    if x2 is not None:
+        if x2.shape[0] != b or tuple(x2.shape[2:5]) != (d, h, w):
+            raise ValueError("x2 must match x in batch and volume")
+        cin2 = x2.shape[1] * 8
+        x2bs = _check_c8_view(x2, "x2")
+    shape = (b, cout // 8, d, h, w, 8)
+    if out is None:
+        if accumulate:
+            raise ValueError("accumulate needs out")
+        out = torch.empty(shape, device=x.device, dtype=torch.bfloat16)
+    if tuple(out.shape) != shape:
+        raise ValueError(f"out shape {tuple(out.shape)} != {shape}")
+    ybs = _check_c8_view(out, "out")
+    if accumulate:
+        rptr, rbs = out.data_ptr(), ybs
+    elif residual is not None:
+        if tuple(residual.shape) != shape:
+            raise ValueError("residual shape mismatch")
+        rptr, rbs = residual.data_ptr(), _check_c8_view(residual, "residual")
+    else:
+        rptr, rbs = None, 0
+    flags = (LEA_RELU if relu else 0) | (LEA_RESIDUAL if rptr is not None else 0)
+    rec = _probe_begin(b, cb * 8 + cin2, cout, d, h, w, k, rptr is not None, b * d * h * w, False,
+                       name=conv_kernel_name_bf16(b, cout, cb * 8 + cin2, d, h, w, k))
+    check(_lib.load().lea_conv3d_bnrelu_bf16(
+        x.data_ptr(), xbs, x2.data_ptr() if x2 is not None else None, x2bs, cin2, packed.data_ptr(),
+        scale.data_ptr() if scale is not None else None,
+        shift.data_ptr() if shift is not None else None, rptr, rbs, out.data_ptr(), ybs, b,
+        cb * 8 + cin2, cout, d, h, w, k, flags, _stream()), "lea_conv3d_bnrelu_bf16")
+    _probe_end(rec)
+    return out
+
+
+def conv3d_bnrelu_costvolume_bf16(fl: torch.Tensor, fr: torch.Tensor, maxdisp: int,
+                                  packed: torch.Tensor, cout: int, scale, shift,
+                                  relu: bool = True) -> torch.Tensor:
+    """conv3d_bnrelu_costvolume at bf16: fl/fr c8 feature maps [B, C/8, 1, H, W, 8]."""
+    _require_c8(fl, fr)
+    if fl.shape != fr.shape or fl.shape[2] != 1:
+        raise ValueError("left/right c8 features must match and have D = 1")
+    fbs = _check_c8_view(fl, "left")
+    if _check_c8_view(fr, "right") != fbs:
+        raise ValueError("left/right batch strides differ")
+    b, cb, _, h, w, _ = fl.shape
+    d3 = int(maxdisp / 3)
+    out = torch.empty((b, cout // 8, d3, h, w, 8), device=fl.device, dtype=torch.bfloat16)
+    rec = _probe_begin(b, 2 * cb * 8, cout, d3, h, w, 3, False, 0, False,
+                       name=conv_kernel_name_bf16(b, cout, 2 * cb * 8, d3, h, w, 3, True))
+    check(_lib.load().lea_conv3d_bnrelu_costvolume_bf16(
+        fl.data_ptr(), fr.data_ptr(), fbs, packed.data_ptr(),
+        scale.data_ptr() if scale is not None else None,
+        shift.data_ptr() if shift is not None else None, out.data_ptr(), out.stride(0), b, cb * 8,
+        cout, d3, h, w, LEA_RELU if relu else 0, _stream()), "lea_conv3d_bnrelu_costvolume_bf16")
+    _probe_end(rec)
+    return out
+
+
+def resample_trilinear_bf16(x: torch.Tensor, size, align_corners: bool = True,
+                            out: torch.Tensor | None = None, scale=None, shift=None,
+                            relu: bool = False) -> torch.Tensor:
+    """resample_trilinear on c8 tensors."""
+    _require_c8(x, out)
+    b, cb, di, hi, wi, _ = x.shape
+    do, ho, wo = (int(s) for s in size)
+    xbs = _check_c8_view(x, "x")
+    if out is None:
+        out = torch.empty((b, cb, do, ho, wo, 8), device=x.device, dtype=torch.bfloat16)
+    if tuple(out.shape) != (b, cb, do, ho, wo, 8):
+        raise ValueError("out shape mismatch")
+    ybs = _check_c8_view(out, "out")
+    check(_lib.load().lea_resample3d_trilinear_bf16(
+        x.data_ptr(), xbs, out.data_ptr(), ybs, b, cb * 8, di, hi, wi, do, ho, wo,
+        1 if align_corners else 0, scale.data_ptr() if scale is not None else None,
+        shift.data_ptr() if shift is not None else None, LEA_RELU if relu else 0, _stream()),
+        "lea_resample3d_trilinear_bf16")
+    return out
+
+
+def tapsum_upsample_bf16(q: torch.Tensor, cout: int, size, scale=None, shift=None,
+                         relu: bool = False) -> torch.Tensor:
+    """tapsum_upsample with q in c8 (27*cout channels padded to a multiple of 8) -> f32."""
+    _require_c8(q)
+    b, cb, di, hi, wi, _ = q.shape
+    if cb * 8 < 27 * cout:
+        raise ValueError(f"q has {cb * 8} channels, need 27*{cout}")
+    qbs = _check_c8_view(q, "q")
+    do, ho, wo = (int(s) for s in size)
+    out = torch.empty((b, cout, do, ho, wo), device=q.device, dtype=torch.float32)
+    lib = _lib.load()
+    ws = torch.empty(lib.lea_tapsum_workspace_bytes(b, cout, hi, wi, do) // 4, device=q.device,
+                     dtype=torch.float32)
+    check(lib.lea_tapsum_upsample(
+        q.data_ptr(), qbs, out.data_ptr(), out.stride(0), b, cout, di, hi, wi, do, ho, wo,
+        scale.data_ptr() if scale is not None else None,
+        shift.data_ptr() if shift is not None else None, LEA_RELU if relu else 0, ws.data_ptr(),
+        _lib.LEA_BF16, _stream()), "lea_tapsum_upsample(bf16)")
+    return out

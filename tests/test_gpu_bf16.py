@@ -1,0 +1,111 @@
+"""GPU parity of the bf16 path (configs 3/4) against float64 torch on the same
+bf16-rounded inputs and weights.
+
+Tolerances: activations and weights are bf16 (8-bit mantissa), sums are f32 and
+outputs are rounded to bf16 again, so per op |d| <= 1e-2 * max|ref| (two bf16
+ulps at the output scale); layout converters and the cost-volume stem0 are exact.
+"""
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+from leastereo_amd import kernels
+from oracle import torch_ref as ref
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def _bf(t):
+    return t.to(torch.bfloat16).to(torch.float32)
+
+
+def _close(got, want, rel=1e-2):
+    got, want = got.double().cpu(), want.double().cpu()
+    scale = float(want.abs().max()) + 1e-6
+    err = float((got - want).abs().max())
+    assert err <= rel * scale, (err, scale)
+
+
+def test_c8_round_trip_is_exact_bf16_rounding():
+    x = torch.randn(2, 24, 3, 5, 7, device=DEV)
+    y = kernels.from_c8(kernels.to_c8(x))
+    assert torch.equal(y, _bf(x))
+
+
+@pytest.mark.parametrize("b,cin,cout,k,shape,mode", [
+    (1, 8, 8, 3, (5, 9, 40), None), (1, 16, 16, 3, (4, 12, 33), "acc"), (2, 32, 32, 3, (3, 8, 20), None),
+    (1, 64, 32, 3, (6, 20, 70), None), (1, 16, 48, 3, (4, 9, 40), None), (1, 32, 96, 3, (3, 6, 21), "res"),
+    (1, 8, 24, 3, (3, 10, 17), None), (2, 64, 8, 1, (3, 7, 11), None), (1, 32, 16, 1, (4, 6, 40), None),
+    (1, 128, 32, 1, (2, 5, 33), None), (1, 32, 32, 1, (3, 4, 50), None)])
+def test_conv_bf16_vs_torch(b, cin, cout, k, shape, mode):
+    g = torch.Generator().manual_seed(cin * 13 + cout + k)
+    x = _bf(torch.randn((b, cin) + shape, generator=g))
+    w = _bf(torch.randn(cout, cin, k, k, k, generator=g) / np.sqrt(cin * k ** 3))
+    scale = torch.rand(cout, generator=g) + 0.5
+    shift = torch.randn(cout, generator=g) * 0.1
+    r = _bf(torch.randn((b, cout) + shape, generator=g))
+    want = F.conv3d(x.double(), w.double(), None, 1, k // 2)
+    want = torch.relu(want * scale.double().view(1, -1, 1, 1, 1) + shift.double().view(1, -1, 1, 1, 1))
+    if mode:
+        want = want + r.double()
+    xc = kernels.to_c8(x.to(DEV))
+    rc = kernels.to_c8(r.to(DEV))
+    out = rc.clone() if mode == "acc" else None
+    y = kernels.conv3d_bnrelu_bf16(xc, kernels.pack_conv_weight_bf16(w.to(DEV)), cout, k,
+                                   scale.to(DEV), shift.to(DEV), relu=True, out=out,
+                                   accumulate=mode == "acc", residual=rc if mode == "res" else None)
+    _close(kernels.from_c8(y), want)
+
+
+def test_conv_bf16_two_sources_and_block_slices():
+    """cat(x, x2) read in place; output into a block slice of a bigger buffer."""
+    g = torch.Generator().manual_seed(5)
+    x = _bf(torch.randn(1, 64, 4, 9, 40, generator=g))
+    x2 = _bf(torch.randn(1, 64, 4, 9, 40, generator=g))
+    w = _bf(torch.randn(64, 128, 3, 3, 3, generator=g) / np.sqrt(128 * 27))
+    want = F.conv3d(torch.cat((x, x2), 1).double(), w.double(), None, 1, 1)
+    big = torch.zeros(1, 12, 4, 9, 40, 8, device=DEV, dtype=torch.bfloat16)
+    kernels.conv3d_bnrelu_bf16(kernels.to_c8(x.to(DEV)), kernels.pack_conv_weight_bf16(w.to(DEV)), 64,
+                               3, None, None, relu=False, out=big[:, 2:10], x2=kernels.to_c8(x2.to(DEV)))
+    _close(kernels.from_c8(big[:, 2:10].contiguous()), want)
+    assert float(big[:, :2].float().abs().sum()) == 0 and float(big[:, 10:].float().abs().sum()) == 0
+
+
+@pytest.mark.parametrize("c,cout,maxdisp,hw", [(32, 32, 48, (12, 40)), (16, 16, 27, (5, 19))])
+def test_costvolume_stem0_bf16_is_bit_identical(c, cout, maxdisp, hw):
+    g = torch.Generator().manual_seed(c + maxdisp)
+    fl = torch.randn((2, c) + hw, generator=g).to(DEV)
+    fr = torch.randn((2, c) + hw, generator=g).to(DEV)
+    w = (torch.randn(cout, 2 * c, 3, 3, 3, generator=g) / np.sqrt(2 * c * 27)).to(DEV)
+    packed = kernels.pack_conv_weight_bf16(w)
+    scale = torch.rand(cout, device=DEV) + 0.5
+    shift = torch.randn(cout, device=DEV) * 0.1
+    cost = kernels.to_c8(kernels.build_cost_volume(fl, fr, maxdisp))
+    want = kernels.conv3d_bnrelu_bf16(cost, packed, cout, 3, scale, shift)
+    got = kernels.conv3d_bnrelu_costvolume_bf16(kernels.to_c8(fl), kernels.to_c8(fr), maxdisp, packed,
+                                                cout, scale, shift)
+    assert torch.equal(got, want)
+
+
+@pytest.mark.parametrize("src,dst,ac", [((4, 6, 10), (8, 12, 20), True), ((9, 13, 17), (5, 7, 9), True),
+                                        ((4, 6, 10), (12, 18, 30), False)])
+def test_resample_bf16_vs_torch(src, dst, ac):
+    g = torch.Generator().manual_seed(3)
+    x = _bf(torch.randn((2, 16) + src, generator=g))
+    scale = torch.rand(16, generator=g) + 0.5
+    shift = torch.randn(16, generator=g) * 0.1
+    want = torch.relu(F.interpolate(x.double(), dst, mode="trilinear", align_corners=ac)
+                      * scale.double().view(1, -1, 1, 1, 1) + shift.double().view(1, -1, 1, 1, 1))
+    y = kernels.resample_trilinear_bf16(kernels.to_c8(x.to(DEV)), dst, ac, None, scale.to(DEV),
+                                        shift.to(DEV), relu=True)
+    _close(kernels.from_c8(y), want)
+
+
+def test_tapsum_bf16_matches_f32_on_same_values():
+    g = torch.Generator().manual_seed(9)
+    q = _bf(torch.randn(1, 32, 8, 12, 20, generator=g)).to(DEV)  # 27 taps + 5 pad channels
+    got = kernels.tapsum_upsample_bf16(kernels.to_c8(q), 1, (16, 24, 40))
+    want = kernels.tapsum_upsample(q[:, :27].contiguous(), 1, (16, 24, 40))
+    np.testing.assert_allclose(got.cpu().numpy(), want.cpu().numpy(), rtol=1e-6, atol=1e-6)
