@@ -44,6 +44,17 @@ FP32_MFMA_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md, fp32 (vector = MFMA) dens
 HBM_PEAK_GBS = 8000.0           # MI355X_MICROARCH.md, spec
 
 
+# BASELINE.json configs: c2 is the headline workload (defaults);
+# c3/c4 are the bf16 ones (c4 = 8 pairs per GPU of the 64-pair global batch)
+CONFIGS = {
+    "c2": dict(height=576, width=960, maxdisp=192, batch=1, precision="f32"),
+    "c3": dict(height=384, width=1248, maxdisp=192, batch=8, precision="bf16"),
+    "c4": dict(height=576, width=960, maxdisp=192, batch=8, precision="bf16"),
+    "c5": dict(height=1008, width=1512, maxdisp=264, batch=1, precision="f32"),
+}
+BF16_MFMA_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md, bf16 dense (no sparsity)
+
+
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
@@ -57,16 +68,24 @@ def parse():
     p.add_argument("--cpu-steps", type=int, default=2)
     p.add_argument("--epe", type=int, default=1, help="check EPE vs the reference golden disparity")
     p.add_argument("--breakdown", type=int, default=0, help="print per-kernel conv times to stderr")
-    return p.parse_args()
+    p.add_argument("--precision", choices=("f32", "bf16"), default="f32",
+                   help="matching-net arithmetic (bf16 = BASELINE configs 3/4)")
+    p.add_argument("--config", choices=sorted(CONFIGS), default=None,
+                   help="preset: c2 (default workload) / c3 / c4 (per GPU) / c5 of BASELINE.json")
+    a = p.parse_args()
+    if a.config:
+        for k, v in CONFIGS[a.config].items():
+            setattr(a, k, v)
+    return a
 
 
 def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def build_model(maxdisp, device):
+def build_model(maxdisp, device, precision="f32"):
     args = default_arch_args(LEAStereoArgs(maxdisp=maxdisp))
-    model = LEAStereo(args, device)
+    model = LEAStereo(args, device, precision=precision)
     shapes = {k: tuple(v.shape) for k, v in model.state_dict().items()}
     model.load_state_dict(synthetic_state_dict(shapes), strict=True)
     return model.to(device).eval()
@@ -115,7 +134,7 @@ def arch_arrays():
         ("net_arch_mat", "matching_network_path.npy"), ("cell_arch_mat", "matching_genotype.npy"))}
 
 
-def golden_epe(device):
+def golden_epe(device, precision="f32"):
     """HIP disparity vs the reference's own fp32 output (tests/golden/e2e.npz,
     produced by tools/gen_golden.py from /root/reference) on its seeded input."""
     import numpy as np
@@ -124,7 +143,7 @@ def golden_epe(device):
     with open(os.path.join(gold, "meta.json")) as f:
         case = json.load(f)["cases"]["e2e/b1_h96_w192_md48"]
     want = np.load(os.path.join(gold, "e2e.npz"))["b1_h96_w192_md48/disp32"]
-    m = build_model(case["maxdisp"], device)
+    m = build_model(case["maxdisp"], device, precision)
     shape = (1, 3, case["height"], case["width"])
     left = torch.from_numpy(seeded_normal(case["seeds"][0], shape)).to(device)
     right = torch.from_numpy(seeded_normal(case["seeds"][1], shape)).to(device)
@@ -144,7 +163,7 @@ def main():
     torch.backends.cudnn.allow_tf32 = False
     torch.backends.cuda.matmul.allow_tf32 = False
 
-    model = build_model(args.maxdisp, device)
+    model = build_model(args.maxdisp, device, args.precision)
     model.check_shape(args.height, args.width)
     # weak scaling: every rank owns args.batch pairs of the global batch (shard of
     # world*batch pairs), generated on its own device from a rank-seeded stream
@@ -182,7 +201,7 @@ def main():
 
     epe = None
     if args.epe:  # after the timed region: one all-gather of the per-rank parity check
-        e = torch.tensor([golden_epe(device)], device=device, dtype=torch.float32)
+        e = torch.tensor([golden_epe(device, args.precision)], device=device, dtype=torch.float32)
         epe = [float(v) for v in parallel.gather_per_pair(e).cpu()]
 
     flops_per_launch = dom["flops"] / dom["launches"]
@@ -194,6 +213,14 @@ def main():
         with open(tf_file) as f:
             traffic = json.load(f).get(dominant, {}).get("bytes_per_launch")
 
+    bf16 = args.precision == "bf16"
+    peak = BF16_MFMA_PEAK_TFLOPS if bf16 else FP32_MFMA_PEAK_TFLOPS
+    workload = {(576, 960, 192, 1, "f32"): "SceneFlow 576x960 D=192 fp32, batch 1 per GPU (BASELINE configs[1])",
+                (384, 1248, 192, 8, "bf16"): "KITTI2015 384x1248 D=192 bf16, batch 8 (BASELINE configs[2])",
+                (576, 960, 192, 8, "bf16"): "SceneFlow 576x960 D=192 bf16, 8 pairs per GPU (BASELINE configs[3])",
+                (1008, 1512, 264, 1, "f32"): "Middlebury 1008x1512 D=264 fp32, batch 1 (BASELINE configs[4], D256 is illegal)",
+                }.get((args.height, args.width, args.maxdisp, args.batch, args.precision),
+                      f"{args.height}x{args.width} D={args.maxdisp} {args.precision}, batch {args.batch} per GPU")
     result = {
         "metric": METRIC,
         "value": world * args.batch * args.steps / elapsed,
@@ -205,23 +232,24 @@ def main():
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": "f32",
+        "dtype": args.precision,
         "data": "synthetic N(0,1) stereo pairs generated on device; random-init weights of the "
                 "reference architecture (SceneFlow search result)",
-        "config": {"workload": f"SceneFlow {args.height}x{args.width} D={args.maxdisp} fp32, "
-                               f"batch {args.batch} per GPU (BASELINE configs[1])",
+        "config": {"workload": workload,
                    "height": args.height, "width": args.width, "maxdisp": args.maxdisp,
                    "global_batch": world * args.batch,
                    "parallelism": f"dp{world} (independent pairs per rank, no collective in the step)"},
         "roofline": {"bound": "mfma", "kernel": dominant, "achieved": achieved,
-                     "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
-                     "frac": achieved / FP32_MFMA_PEAK_TFLOPS, "traffic": traffic,
+                     "peak": peak, "unit": "TFLOP/s",
+                     "frac": achieved / peak, "traffic": traffic,
                      "launches_per_step": dom["launches"] / args.steps,
                      "flops_per_launch": flops_per_launch, "ms_per_launch": ms_per_launch},
         "epe_px": None if epe is None else {
             "vs": "reference LEAStereo fp32 disparity (tests/golden e2e b1_h96_w192_md48)",
             "max_over_ranks": max(epe), "per_rank": epe},
     }
+    if bf16 and result["epe_px"] is not None:
+        result["epe_px"]["vs"] += " (bf16 matching net: no upstream tolerance; see DESIGN.md)"
     if info.is_main and world == 1 and args.cpu_baseline:
         result["cpu_baseline"] = cpu_baseline(args, model, left[:1], right[:1], out[:1])
     if info.is_main:

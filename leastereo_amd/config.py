@@ -69,5 +69,7 @@ def obtain_predict_args(argv=None):
     for flag in ("sceneflow", "kitti2012", "kitti2015", "middlebury", "satellite", "mvs3d",
                  "new_tagil", "whu"):
         parser.add_argument("--" + flag, type=int, default=0)
+    parser.add_argument("--precision", choices=("f32", "bf16"), default="f32",
+                        help="matching-net arithmetic (bf16: configs 3/4; not in the reference)")
     add_leastereo_args(parser)
     return parser.parse_args(argv)

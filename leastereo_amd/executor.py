@@ -99,7 +99,7 @@ class CellGraphExecutor:
         cin = x.shape[1] + (x2.shape[1] if x2 is not None else 0)
         if cin != p.cin:
             raise ValueError(f"{name}: expected {p.cin} input channels, got {cin}")
-        resized = size is not None and tuple(size) != tuple(x.shape[2:])
+        resized = size is not None and tuple(size) != tuple(x.shape[2:5])
         if p.kind == "s3":
             return kernels.conv2d_s3_bnrelu(x, p.packed, p.scale, p.shift, p.relu)
         if p.kind == "2d":
@@ -121,6 +121,26 @@ class CellGraphExecutor:
         return kernels.conv3d_bnrelu(x, p.packed, p.cout, p.k, p.scale, p.shift, p.relu, out,
                                      accumulate, x2, residual)
 
+    # activation layout hooks (f32 NCDHW here; the bf16 executor overrides them)
+    def _empty(self, b, c, size, like):
+        return torch.empty((b, c) + tuple(size), device=like.device, dtype=like.dtype)
+
+    @staticmethod
+    def _channels(t, c0, c1):
+        return t[:, c0:c1]
+
+    @staticmethod
+    def _nchannels(t):
+        return t.shape[1]
+
+    @staticmethod
+    def _volume(t):
+        return tuple(t.shape[2:5])
+
+    @staticmethod
+    def _resample(x, size):
+        return kernels.resample_trilinear(x, size)
+
     def cell(self, i, s0, s1):
         """Cell.forward (skip_model_3d.py:41-75 / new_model_2d.py:41-75).  The level
         change of s1 (:44-48) and the size match of s0 (:49-51) are fused into the
@@ -128,23 +148,23 @@ class CellGraphExecutor:
         cell = self.m.cells[i]
         c = cell.c_out
         prev_input = s1
-        size = tuple(s1.shape[2:])
+        size = self._volume(s1)
         if cell.downup_sample != 0:
             sc = 0.5 if cell.downup_sample < 0 else 2
             # the D axis of a 2D map stays 1 (bilinear on H, W only)
             size = tuple(n if (cell.dims == 2 and ax == 0) else scale_dimension(n, sc)
                          for ax, n in enumerate(size))
         b = s1.shape[0]
-        d, h, w = size
         bm = cell.block_multiplier
         n_states = 2 + cell.steps
-        out = torch.empty((b, bm * c, d, h, w), device=s1.device, dtype=s1.dtype)
-        slot = {idx: out[:, k * c:(k + 1) * c] for k, idx in enumerate(range(n_states - bm, n_states))}
-        if s0.shape[1] != c:
+        out = self._empty(b, bm * c, size, s1)
+        slot = {idx: self._channels(out, k * c, (k + 1) * c)
+                for k, idx in enumerate(range(n_states - bm, n_states))}
+        if self._nchannels(s0) != c:
             s0 = self.conv(f"cells.{i}.pre_preprocess", s0, out=slot.get(0), size=size)
         else:
-            if tuple(s0.shape[2:]) != size:
-                s0 = kernels.resample_trilinear(s0, size)
+            if self._volume(s0) != size:
+                s0 = self._resample(s0, size)
             if 0 in slot:
                 slot[0].copy_(s0)
         s1 = self.conv(f"cells.{i}.preprocess", s1, out=slot.get(1), size=size)
@@ -153,13 +173,13 @@ class CellGraphExecutor:
         written = set()
         if group:  # ops on s1 of every step, one launch, straight into their slots
             k0 = 2 + group[0][0] - (n_states - bm)
-            self.conv(f"cells.{i}.s1_group", s1, out=out[:, k0 * c:(k0 + len(group)) * c])
+            self.conv(f"cells.{i}.s1_group", s1, out=self._channels(out, k0 * c, (k0 + len(group)) * c))
             written = {k for k, _ in group}
         done = set(group)
         for step, terms in enumerate(cell.plan):
             dst = slot.get(len(states))
             if dst is None:
-                dst = torch.empty((b, c, d, h, w), device=s1.device, dtype=s1.dtype)
+                dst = self._empty(b, c, size, s1)
             skips = [states[j] for k, j in terms if cell.op_kinds[k] != "conv"]
             for k, j in terms:
                 if (step, k) in done or cell.op_kinds[k] != "conv":
@@ -196,7 +216,7 @@ class MatchingExecutor(CellGraphExecutor):
         return self._from_stem0(stem0)
 
     def _from_stem0(self, stem0):
-        d, h, w = stem0.shape[2:]
+        d, h, w = self._volume(stem0)
         stem1 = self.conv("stem1", stem0)
         outs = []
         prev = (stem0, stem1)
@@ -212,13 +232,13 @@ class MatchingExecutor(CellGraphExecutor):
             outs.append(o)
             prev = o
         last = outs[-1][1]
-        lh = last.shape[3]
+        lh = self._volume(last)[1]
         full, half, quarter = (d, h, w), (d // 2, h // 2, w // 2), (d // 4, h // 4, w // 4)
         # head (:161-173): the 1x1 Upsample pairs run commuted (see conv()); the final
         # Upsample + last_3 run as per-tap partial sums at the low resolution, then one
         # 27-sample interpolating sum per output voxel (no full-resolution 32-ch tensor)
         if lh == h:
-            return self.conv("last_3", last)
+            return self._last3_same_size(last)
         if lh == h // 2:
             y = self.conv("last_6", last)
         elif lh == h // 4:
@@ -230,7 +250,14 @@ class MatchingExecutor(CellGraphExecutor):
             raise ValueError(f"matching-net output size {tuple(last.shape[2:])} has no head")
         p3 = self.p["last_3"]
         q = self.conv("last_3.taps", y)
+        return self._tapsum(q, p3, full)
+
+    @staticmethod
+    def _tapsum(q, p3, full):
         return kernels.tapsum_upsample(q, p3.cout, full, p3.scale, p3.shift, p3.relu)
+
+    def _last3_same_size(self, last):
+        return self.conv("last_3", last)
 
     def __init__(self, matching):
         super().__init__(matching)
@@ -273,3 +300,91 @@ class FeatureExecutor(CellGraphExecutor):
             # the reference raises UnboundLocalError here (new_model_2d.py:156-165)
             raise ValueError(f"feature size {tuple(x.shape[2:])} is not legal for the feature net")
         return self.conv("last_3", y).squeeze(2)
+
+
+class MatchingExecutorBF16(MatchingExecutor):
+    """newMatching.forward at bf16 (configs 3/4): activations in the c8 layout
+    ([B, C/8, D, H, W, 8] bfloat16), convs on the bf16 matrix cores with f32
+    accumulation and the f32 BN epilogue; the head's output (the matching cost)
+    is f32 for the disparity regression.  Same graph as MatchingExecutor."""
+
+    def __init__(self, matching):
+        from .model import ConvBR
+        super().__init__(matching)
+        with torch.no_grad():
+            # re-pack every f32 ConvParams into bf16 fragments (same scale/shift)
+            for name, p in list(self.p.items()):
+                if name == "last_3":
+                    continue  # runs through last_3.taps + tap-sum
+                if name == "last_3.taps":
+                    w = matching.last_3.conv.weight
+                    co, ci = w.shape[:2]
+                    taps = w.permute(0, 2, 3, 4, 1).reshape(co * 27, ci, 1, 1, 1)
+                    pad = (-taps.shape[0]) % 8  # c8: 27*cout channels padded to a block
+                    taps = torch.cat([taps, taps.new_zeros((pad,) + tuple(taps.shape[1:]))], 0)
+                    self.p[name] = ConvParams(kernels.pack_conv_weight_bf16(taps), None, None, ci,
+                                              taps.shape[0], 1, False, "bf16")
+                    continue
+                if name.endswith(".s1_group"):
+                    i = int(name.split(".")[1])
+                    mods = [matching.cells[i]._ops[op] for _, op in self.s1_group[i]]
+                    w = torch.cat([m.conv.weight for m in mods], 0)
+                else:
+                    mod = matching.get_submodule(name)
+                    assert isinstance(mod, ConvBR)
+                    w = mod.conv.weight
+                self.p[name] = ConvParams(kernels.pack_conv_weight_bf16(w), p.scale, p.shift, p.cin,
+                                          p.cout, p.k, p.relu, "bf16")
+
+    def _empty(self, b, c, size, like):
+        return torch.empty((b, c // 8) + tuple(size) + (8,), device=like.device, dtype=torch.bfloat16)
+
+    @staticmethod
+    def _channels(t, c0, c1):
+        return t[:, c0 // 8:c1 // 8]
+
+    @staticmethod
+    def _nchannels(t):
+        return t.shape[1] * 8
+
+    @staticmethod
+    def _resample(x, size):
+        return kernels.resample_trilinear_bf16(x, size)
+
+    @staticmethod
+    def _tapsum(q, p3, full):
+        return kernels.tapsum_upsample_bf16(q, p3.cout, full, p3.scale, p3.shift, p3.relu)
+
+    def _last3_same_size(self, last):
+        # per-tap partial sums + a tap-sum at the same size (identity interpolation)
+        return self._tapsum(self.conv("last_3.taps", last), self.p["last_3"], self._volume(last))
+
+    def conv(self, name, x, out=None, accumulate=False, x2=None, size=None, residual=None):
+        p = self.p[name]
+        cin = (x.shape[1] + (x2.shape[1] if x2 is not None else 0)) * 8
+        if cin != p.cin:
+            raise ValueError(f"{name}: expected {p.cin} input channels, got {cin}")
+        if size is not None and tuple(size) != tuple(x.shape[2:5]):
+            if x2 is not None or residual is not None or accumulate:
+                raise ValueError("resampled conv takes one input and no residual")
+            up = all(int(o) >= int(i) for o, i in zip(size, x.shape[2:5]))
+            if p.k == 1 and up:  # commuted: 1x1 at the low resolution, resample + BN/ReLU
+                z = kernels.conv3d_bnrelu_bf16(x, p.packed, p.cout, 1, None, None, relu=False)
+                return kernels.resample_trilinear_bf16(z, size, True, out, p.scale, p.shift, p.relu)
+            x = kernels.resample_trilinear_bf16(x, size)
+        return kernels.conv3d_bnrelu_bf16(x, p.packed, p.cout, p.k, p.scale, p.shift, p.relu, out,
+                                          accumulate, x2, residual)
+
+    def run(self, x):
+        """x: f32 cost volume [B, 64, D3, H3, W3] -> f32 matching cost [B, 1, D3, H3, W3]."""
+        return self._from_stem0(self.conv("stem0", kernels.to_c8(x)))
+
+    def run_features(self, fl, fr, maxdisp):
+        p = self.p["stem0"]
+        if fl.shape[1] * 2 != p.cin:
+            raise ValueError(f"stem0 expects {p.cin} cost-volume channels, got 2*{fl.shape[1]}")
+        f8 = kernels.to_c8(torch.cat((fl, fr), 0))  # [2B, C/8, 1, H, W, 8]
+        b = fl.shape[0]
+        stem0 = kernels.conv3d_bnrelu_costvolume_bf16(f8[:b], f8[b:], maxdisp, p.packed, p.cout,
+                                                      p.scale, p.shift, p.relu)
+        return self._from_stem0(stem0)

@@ -140,9 +140,19 @@ class NewFeature(_ExecutorCache, nn.Module):
 
 
 class NewMatching(_ExecutorCache, nn.Module):
-    """Matching net parameters (retrain/skip_model_3d.py:78-138); forward on HIP."""
+    """Matching net parameters (retrain/skip_model_3d.py:78-138); forward on HIP,
+    in f32 (MatchingExecutor) or, with precision "bf16", on the bf16 engine
+    (MatchingExecutorBF16, configs 3/4)."""
 
     _executor_cls = "MatchingExecutor"
+
+    def set_precision(self, precision: str):
+        if precision not in ("f32", "bf16"):
+            raise ValueError(f"precision must be 'f32' or 'bf16', got {precision!r}")
+        cls = "MatchingExecutorBF16" if precision == "bf16" else "MatchingExecutor"
+        if cls != self._executor_cls:
+            self._executor_cls = cls
+            self.invalidate()
 
     def __init__(self, network_arch, cell_arch, args):
         super().__init__()
@@ -177,7 +187,11 @@ class Disp(nn.Module):
 class LEAStereo(nn.Module):
     """retrain/LEAStereo.py:12-52 with the hot path on MI355X kernels."""
 
-    def __init__(self, args, device):
+    def __init__(self, args, device, precision=None):
+        """``precision``: "f32" (default; the reference's arithmetic) or "bf16"
+        (configs 3/4: matching net on bf16 activations with f32 accumulation; the
+        feature net and the disparity regression stay f32).  Also read from
+        ``args.precision`` when present."""
         super().__init__()
         network_path_fea = np.load(args.net_arch_fea)
         cell_arch_fea = np.load(args.cell_arch_fea)
@@ -189,6 +203,8 @@ class LEAStereo(nn.Module):
         self.disp = Disp(device, self.maxdisp)
         self.use_cuda = getattr(args, "cuda", True)
         self.device = device
+        self.precision = precision or getattr(args, "precision", None) or "f32"
+        self.matching.set_precision(self.precision)
 
     def check_shape(self, height: int, width: int):
         """Reject input sizes the reference cannot run."""

@@ -109,3 +109,40 @@ def test_tapsum_bf16_matches_f32_on_same_values():
     got = kernels.tapsum_upsample_bf16(kernels.to_c8(q), 1, (16, 24, 40))
     want = kernels.tapsum_upsample(q[:, :27].contiguous(), 1, (16, 24, 40))
     np.testing.assert_allclose(got.cpu().numpy(), want.cpu().numpy(), rtol=1e-6, atol=1e-6)
+
+
+# ----------------------------------------------------------------------- end to end
+def _model(maxdisp, precision):
+    from leastereo_amd.config import LEAStereoArgs, default_arch_args
+    from leastereo_amd.model import LEAStereo
+    from tests.golden_util import state_dict
+    m = LEAStereo(default_arch_args(LEAStereoArgs(maxdisp=maxdisp)), DEV, precision=precision)
+    m.load_state_dict(state_dict(), strict=True)
+    return m.to(DEV).eval()
+
+
+def test_bf16_e2e_vs_reference_fixture():
+    """bf16 matching net vs the reference's f32 disparity (e2e fixture).  No bf16
+    tolerance is stated upstream; measured r01: 0.06 px EPE (disparity std 3.6 px)."""
+    from tests.golden_util import golden, meta, normal
+    c = meta()["cases"]["e2e/b1_h96_w192_md48"]
+    left = normal(c["seeds"][0], (1, 3, 96, 192)).to(DEV)
+    right = normal(c["seeds"][1], (1, 3, 96, 192)).to(DEV)
+    with torch.no_grad():
+        d = _model(48, "bf16")(left, right).cpu()
+    assert torch.isfinite(d).all()
+    assert ref.epe(d, torch.from_numpy(golden("e2e")["b1_h96_w192_md48/disp32"])) < 0.25
+
+
+def test_bf16_full_size_vs_f32_and_batch_invariance():
+    """576x960 D192, batch 2: bf16 vs the f32 HIP path (measured r01: 0.48 px EPE),
+    and the batch of 2 equals two single runs bit for bit."""
+    from tests.golden_util import normal
+    mb, mf = _model(192, "bf16"), _model(192, "f32")
+    left = normal(21, (2, 3, 576, 960)).to(DEV)
+    right = normal(22, (2, 3, 576, 960)).to(DEV)
+    with torch.no_grad():
+        db, df = mb(left, right), mf(left, right)
+        one = torch.cat([mb(left[i:i + 1], right[i:i + 1]) for i in range(2)])
+    assert torch.equal(db, one)
+    assert ref.epe(db.cpu(), df.cpu()) < 1.0
