@@ -200,6 +200,11 @@ int lea_conv3d_bnrelu_costvolume_bf16(const void* left, const void* right, int64
                                       void* y, int64_t y_bstride, int B, int C, int cout, int D3,
                                       int H, int W, unsigned flags, void* stream);
 
+/* Tuning hook (tools/conv_sweep.py --bf16): force the bf16 conv tile -- th rows,
+ * td planes, mt 16-row tiles per wave -- on the calling thread; th <= 0 restores
+ * the planner. */
+int lea_conv3d_bf16_set_tile_override(int th, int td, int mt);
+
 /* Kernel instantiation the bf16 conv of this shape launches. */
 const char* lea_conv3d_kernel_name_bf16(int B, int cout, int cin, int D, int H, int W, int k,
                                         int costvolume);

@@ -346,18 +346,35 @@ struct Plan {
   int ks, mt, wc, th, td, nb;
 };
 
+thread_local int g_override[3] = {0, 0, 0};  // th, td, mt (lea_conv3d_bf16_set_tile_override)
+
 inline Plan plan(int B, int cout, int D, int H, int W, int ks, int cin) {
+  // r01 sweep (tools/conv_sweep.py --bf16, profiles/r01_conv_sweep_bf16.txt): one
+  // 16-row tile per wave with the waves splitting the couts beat 32-row tiles on
+  // every layer; 4-row tiles win on the small (L2) volumes; the 8-channel-input
+  // layers (one short K chunk) want deeper tiles to amortise staging.
   Plan p;
   p.ks = ks;
   const int cobv = cob_of(cout);
-  p.wc = cobv == 64 ? 2 : 1;
-  p.mt = cobv == 16 ? 1 : 2;
+  p.mt = 1;
+  p.wc = cobv / 16;
   p.nb = nb_of(cin, ks);
-  p.th = 8;
   p.td = (ks == 3) ? 2 : 1;
   const long long ncob = (cout + cobv - 1) / cobv;
-  const long long wgs = (long long)((W + 15) / 16) * ((H + p.th - 1) / p.th) * ((D + p.td - 1) / p.td) * B * ncob;
-  if (wgs < 512) p.th = 4;
+  auto wgs = [&](int th, int td) {
+    return (long long)((W + 15) / 16) * ((H + th - 1) / th) * ((D + td - 1) / td) * B * ncob;
+  };
+  p.th = wgs(8, p.td) < 8192 ? 4 : 8;
+  if (ks == 3 && p.nb == 1 && wgs(8, 4) >= 2048) {
+    p.th = 8;
+    p.td = 4;
+  }
+  if (g_override[0] > 0) {
+    p.th = g_override[0];
+    p.td = g_override[1];
+    p.mt = std::min(g_override[2], cobv / 16);
+    p.wc = cobv / 16 / p.mt;
+  }
   return p;
 }
 
@@ -373,16 +390,22 @@ inline Plan plan(int B, int cout, int D, int H, int W, int ks, int cin) {
     return launch_status("lea_conv3d(bf16)");                                         \
   }
 #define LEA_BF_TH(KS, MT, WC, TD, NB, CV) \
-  LEA_BF_CASE(KS, MT, WC, 8, TD, NB, CV) LEA_BF_CASE(KS, MT, WC, 4, TD, NB, CV)
-#define LEA_BF_MT(KS, TD, NB, CV) \
-  LEA_BF_TH(KS, 1, 1, TD, NB, CV) LEA_BF_TH(KS, 2, 1, TD, NB, CV) LEA_BF_TH(KS, 2, 2, TD, NB, CV)
+  LEA_BF_CASE(KS, MT, WC, 16, TD, NB, CV) LEA_BF_CASE(KS, MT, WC, 8, TD, NB, CV) LEA_BF_CASE(KS, MT, WC, 4, TD, NB, CV)
+#define LEA_BF_MT(KS, TD, NB, CV)                                                         \
+  LEA_BF_TH(KS, 1, 1, TD, NB, CV) LEA_BF_TH(KS, 2, 1, TD, NB, CV) LEA_BF_TH(KS, 1, 2, TD, NB, CV) \
+  LEA_BF_TH(KS, 2, 2, TD, NB, CV) LEA_BF_TH(KS, 1, 4, TD, NB, CV)
 
 int run(const Plan& p, Args a, int B, hipStream_t st, bool cv) {
   if (cv) {
     LEA_BF_MT(3, 2, 2, true)
+    LEA_BF_MT(3, 1, 2, true)
   } else {
     LEA_BF_MT(3, 2, 1, false)
     LEA_BF_MT(3, 2, 2, false)
+    LEA_BF_MT(3, 1, 1, false)
+    LEA_BF_MT(3, 1, 2, false)
+    LEA_BF_MT(3, 4, 1, false)
+    LEA_BF_MT(3, 4, 2, false)
     LEA_BF_MT(1, 1, 4, false)
   }
   set_error("lea_conv3d(bf16): no tile ks=%d mt=%d wc=%d th=%d td=%d nb=%d cv=%d", p.ks, p.mt, p.wc,
@@ -396,6 +419,20 @@ thread_local char g_bf_name[96];
 }  // namespace lea
 
 using namespace lea;
+
+extern "C" int lea_conv3d_bf16_set_tile_override(int th, int td, int mt) {
+  clear_error();
+  if (th <= 0) {
+    bf::g_override[0] = 0;
+    return 0;
+  }
+  LEA_CHECK_ARG((th == 4 || th == 8 || th == 16) && (td == 1 || td == 2 || td == 4) && (mt == 1 || mt == 2),
+                "lea_conv3d_bf16_set_tile_override: bad tile th=%d td=%d mt=%d", th, td, mt);
+  bf::g_override[0] = th;
+  bf::g_override[1] = td;
+  bf::g_override[2] = mt;
+  return 0;
+}
 
 extern "C" size_t lea_conv3d_packed_elems_bf16(int cout, int cin, int k) {
   if (cout <= 0 || cin <= 0 || cin % 8 != 0 || (k != 1 && k != 3)) return 0;
@@ -547,7 +584,10 @@ extern "C" int lea_resample3d_trilinear_bf16(const void* x, int64_t x_bstride, v
                 "lea_resample3d_trilinear_bf16: bad shape");
   const int ac = align_corners ? 1 : 0;
   const long long cells = (long long)Ho * Wo;
-  dim3 grid((unsigned)std::min<long long>((cells + 255) / 256, 64), B * (C / 8) * Do);
+  // one output word (8 channels) per thread: the 8 corner loads of many threads in
+  // flight hide the gather latency (r01: 64 workgroups per plane looping 4x ran at
+  // ~1.5 TB/s on the B=8 down-sampling)
+  dim3 grid((unsigned)((cells + 255) / 256), B * (C / 8) * Do);
   bf::resample_c8_kernel<<<grid, 256, 0, as_stream(stream)>>>(
       (const __bf16*)x, x_bstride, (__bf16*)y, y_bstride, C / 8, Di, Hi, Wi, Do, Ho, Wo,
       axis_ratio(Di, Do, ac), axis_ratio(Hi, Ho, ac), axis_ratio(Wi, Wo, ac), ac, scale, shift, flags);
