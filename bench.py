@@ -53,6 +53,9 @@ CONFIGS = {
     "c5": dict(height=1008, width=1512, maxdisp=264, batch=1, precision="f32"),
 }
 BF16_MFMA_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md, bf16 dense (no sparsity)
+# Whole-path roofline time per step, SURVEY.md §8d (sum over the matching net's
+# layers of max(FLOP/peak, bytes/8 TB/s), reference op accounting), per config
+T_ROOF_MS = {("c2", 1): 11.36, ("c3", 8): 10.91, ("c4", 8): 12.59, ("c5", 1): 43.1}
 
 
 def parse():
@@ -248,6 +251,12 @@ def main():
             "vs": "reference LEAStereo fp32 disparity (tests/golden e2e b1_h96_w192_md48)",
             "max_over_ranks": max(epe), "per_rank": epe},
     }
+    cfg = next((k for k, v in CONFIGS.items() if all(getattr(args, f) == x for f, x in v.items())), None)
+    t_roof = T_ROOF_MS.get((cfg, args.batch))
+    if t_roof is not None:
+        result["path_roofline"] = {"t_roof_ms": t_roof, "frac": t_roof / result["ms_per_step"],
+                                   "source": "SURVEY.md §8d: sum over matching-net layers of "
+                                             "max(FLOP / MFMA peak, bytes / 8 TB/s)"}
     if bf16 and result["epe_px"] is not None:
         result["epe_px"]["vs"] += " (bf16 matching net: no upstream tolerance; see DESIGN.md)"
     if info.is_main and world == 1 and args.cpu_baseline:
