@@ -453,9 +453,9 @@ inline Plan make_plan(int B, int cout, int D, int H, int W, int k, bool resample
   p.td = 1;
   if (resample) {
     // register-staged resampling engine; for k = 1 (the level-change preprocess,
-    // HBM-bound gathers) half-height tiles halve the LDS stage so 4 workgroups
-    // share a CU and keep more loads in flight
-    p.nt = (k == 1) ? (p.mt == 1 ? 4 : 2) : (p.mt == 1 ? 8 : 4);
+    // latency-bound gathers) quarter-height tiles shrink the LDS stage so 8
+    // workgroups share a CU and keep more loads in flight
+    p.nt = (k == 1) ? (p.mt == 1 ? 2 : 1) : (p.mt == 1 ? 8 : 4);
     return p;
   }
   const long long ncob = (cout + p.mt * 16 - 1) / (p.mt * 16);
@@ -538,10 +538,10 @@ int run_plan(const Plan& p, ConvArgs a, int B, int k, hipStream_t st) {
       if (p.mt == 3) return run_rs<3, 3, 4>(a, p.tw, B, st);
       return run_rs<3, 4, 4>(a, p.tw, B, st);
     }
-    if (p.mt == 1) return run_rs<1, 1, 4>(a, p.tw, B, st);
-    if (p.mt == 2) return run_rs<1, 2, 2>(a, p.tw, B, st);
-    if (p.mt == 3) return run_rs<1, 3, 2>(a, p.tw, B, st);
-    return run_rs<1, 4, 2>(a, p.tw, B, st);
+    if (p.mt == 1) return run_rs<1, 1, 2>(a, p.tw, B, st);
+    if (p.mt == 2) return run_rs<1, 2, 1>(a, p.tw, B, st);
+    if (p.mt == 3) return run_rs<1, 3, 1>(a, p.tw, B, st);
+    return run_rs<1, 4, 1>(a, p.tw, B, st);
   }
   // 1x1x1 without resample: streaming engine over the flat voxel run
   return run_1x1(p, a, B, st);
