@@ -74,7 +74,9 @@ struct Cfg {
 template <int KS, int MT, int WC, int TH, int TD, int NB, bool CV>
 __global__ __launch_bounds__(kThreads, 2) void conv_bf16_kernel(const Args a) {
   using C = Cfg<KS, MT, WC, TH, TD, NB, CV>;
-  __shared__ __attribute__((aligned(16))) bf16x8 smem[2 * C::STAGE];
+  // dynamic LDS: two stages, or one when the whole K is a single chunk (cin <= 16):
+  // half the footprint doubles the workgroups per CU for the small cell layers
+  extern __shared__ __attribute__((aligned(16))) bf16x8 smem[];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wc = wave % WC, wv = wave / WC;
@@ -386,7 +388,8 @@ inline Plan plan(int B, int cout, int D, int H, int W, int ks, int cin) {
     const long long nb_ = (long long)a.ntiles * a.ndz * B * a.ncob;                   \
     LEA_CHECK_ARG(nb_ < (1LL << 31), "lea_conv3d(bf16): grid too large");             \
     a.nblk = (int)nb_;                                                                \
-    conv_bf16_kernel<KS, MT, WC, TH, TD, NB, CV><<<dim3((unsigned)nb_), kThreads, 0, st>>>(a); \
+    const size_t lds_ = (size_t)(a.nchunks > 1 ? 2 : 1) * Cfg<KS, MT, WC, TH, TD, NB, CV>::STAGE * 16; \
+    conv_bf16_kernel<KS, MT, WC, TH, TD, NB, CV><<<dim3((unsigned)nb_), kThreads, lds_, st>>>(a); \
     return launch_status("lea_conv3d(bf16)");                                         \
   }
 #define LEA_BF_TH(KS, MT, WC, TD, NB, CV) \
