@@ -223,6 +223,15 @@ int lea_from_c8_bf16(const void* x, int64_t x_bstride, float* y, int64_t y_bstri
 
 /* lea_tapsum_upsample also takes dtype LEA_BF16: q in the c8 layout, output f32. */
 
+/* Feature-net ConvBR2d 3x3/s1/p1 (operations_2d.py:31-47) on c8 maps [B, C/8, 1, H, W, 8]
+ * (the bf16 counterpart of lea_conv2d_bnrelu); weights [cout, cin, 3, 3] f32. */
+size_t lea_conv2d_packed_elems_bf16(int cout, int cin);
+int lea_conv2d_pack_weights_bf16(const float* w, void* packed, int cout, int cin, void* stream);
+int lea_conv2d_bnrelu_bf16(const void* x, int64_t x_bstride, const void* w_packed,
+                           const float* scale, const float* shift, const void* residual,
+                           int64_t r_bstride, void* y, int64_t y_bstride, int B, int cin, int cout,
+                           int H, int W, unsigned flags, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

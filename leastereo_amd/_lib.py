@@ -63,6 +63,10 @@ SIGNATURES = {
     "lea_resample3d_trilinear_bf16": (_i, [_p, _i64, _p, _i64, _i, _i, _i, _i, _i, _i, _i, _i,
                                            _i, _p, _p, _u, _p]),
     "lea_to_c8_bf16": (_i, [_p, _i64, _p, _i64, _i, _i, _i64, _p]),
+    "lea_conv2d_packed_elems_bf16": (ctypes.c_size_t, [_i, _i]),
+    "lea_conv2d_pack_weights_bf16": (_i, [_p, _p, _i, _i, _p]),
+    "lea_conv2d_bnrelu_bf16": (_i, [_p, _i64, _p, _p, _p, _p, _i64, _p, _i64, _i, _i, _i, _i, _i,
+                                    _u, _p]),
     "lea_from_c8_bf16": (_i, [_p, _i64, _p, _i64, _i, _i, _i64, _p]),
 }
 

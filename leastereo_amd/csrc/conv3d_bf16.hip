@@ -53,16 +53,18 @@ __host__ __device__ constexpr int cob_of(int cout) { return cout <= 16 ? 16 : (c
 __host__ __device__ constexpr int nb_of(int cin, int ks) { return ks == 1 ? 4 : (cin <= 8 ? 1 : 2); }
 __host__ __device__ constexpr int ksteps(int ks, int nb) { return (ks * ks * ks * nb + 3) / 4; }
 
-template <int KS, int MT, int WC, int TH, int TD, int NB, bool CV>
+// KD = kernel depth: KS for the 3D convs, 1 for 2D 3x3 convs (feature net: the
+// D = 1 case of a (1, 3, 3) kernel)
+template <int KS, int MT, int WC, int TH, int TD, int NB, bool CV, int KD = KS>
 struct Cfg {
   static constexpr int WV = 4 / WC;
   static constexpr int VT = TH * TD;        // 16-voxel rows in the tile
   static constexpr int NV = VT / WV;        // per wave
   static_assert(VT % WV == 0, "rows per wave");
-  static constexpr int T = KS * KS * KS;
+  static constexpr int T = KD * KS * KS;
   static constexpr int S = (T * NB + 3) / 4;
   static constexpr int COB = WC * MT * 16;
-  static constexpr int PLANES = KS + TD - 1;
+  static constexpr int PLANES = KD + TD - 1;
   static constexpr int RH = TH + KS - 1, RW = 16 + KS - 1;
   static constexpr int PLANE = RH * RW;
   static constexpr int IMG = PLANES * PLANE;  // 16-B voxel-blocks per channel block
@@ -71,9 +73,9 @@ struct Cfg {
   static constexpr int PIECES_W = (PIECES + 3) / 4;
 };
 
-template <int KS, int MT, int WC, int TH, int TD, int NB, bool CV>
+template <int KS, int MT, int WC, int TH, int TD, int NB, bool CV, int KD = KS>
 __global__ __launch_bounds__(kThreads, 2) void conv_bf16_kernel(const Args a) {
-  using C = Cfg<KS, MT, WC, TH, TD, NB, CV>;
+  using C = Cfg<KS, MT, WC, TH, TD, NB, CV, KD>;
   // dynamic LDS: two stages, or one when the whole K is a single chunk (cin <= 16):
   // half the footprint doubles the workgroups per CU for the small cell layers
   extern __shared__ __attribute__((aligned(16))) bf16x8 smem[];
@@ -103,7 +105,7 @@ __global__ __launch_bounds__(kThreads, 2) void conv_bf16_kernel(const Args a) {
     if (e < C::IMG) {
       const int p = e / C::PLANE, r = e % C::PLANE;
       const int rr = r / C::RW, cc = r % C::RW;
-      const int d = d0 + p - KS / 2, h = h0 + rr - KS / 2, w = w0 + cc - KS / 2;
+      const int d = d0 + p - KD / 2, h = h0 + rr - KS / 2, w = w0 + cc - KS / 2;
       if ((unsigned)d < (unsigned)a.D && (unsigned)h < (unsigned)a.H && (unsigned)w < (unsigned)a.W) {
         if constexpr (CV) {
           if (w >= d) {
@@ -251,9 +253,8 @@ __global__ __launch_bounds__(kThreads, 2) void conv_bf16_kernel(const Args a) {
 
 // weights [cout][cin][k^3] f32 -> [cob][chunk][s][mtile][g][16][8] bf16
 __global__ void pack_bf16_kernel(const float* __restrict__ w, __bf16* __restrict__ packed, int cout,
-                                 int cin, int ks, int nb, int S, int mtiles, int nchunks,
+                                 int cin, int T, int nb, int S, int mtiles, int nchunks,
                                  long long total) {
-  const int T = ks * ks * ks;
   for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
        i += (long long)gridDim.x * blockDim.x) {
     long long r = i;
@@ -416,6 +417,27 @@ int run(const Plan& p, Args a, int B, hipStream_t st, bool cv) {
   return LEA_E_UNSUPPORTED;
 }
 
+#define LEA_BF2D_CASE(WC, TH, NB)                                                           \
+  if (p.wc == WC && p.th == TH && p.nb == NB) {                                             \
+    a.tiles_w = (a.W + 15) / 16;                                                            \
+    a.ntiles = a.tiles_w * ((a.H + TH - 1) / TH);                                           \
+    a.ndz = 1;                                                                              \
+    const long long nb_ = (long long)a.ntiles * B * a.ncob;                                 \
+    LEA_CHECK_ARG(nb_ < (1LL << 31), "lea_conv2d(bf16): grid too large");                   \
+    a.nblk = (int)nb_;                                                                      \
+    const size_t lds_ = (size_t)(a.nchunks > 1 ? 2 : 1) * Cfg<3, 1, WC, TH, 1, NB, false, 1>::STAGE * 16; \
+    conv_bf16_kernel<3, 1, WC, TH, 1, NB, false, 1><<<dim3((unsigned)nb_), kThreads, lds_, st>>>(a); \
+    return launch_status("lea_conv2d(bf16)");                                               \
+  }
+#define LEA_BF2D_NB(WC, NB) LEA_BF2D_CASE(WC, 8, NB) LEA_BF2D_CASE(WC, 4, NB)
+
+int run2d(const Plan& p, Args a, int B, hipStream_t st) {
+  LEA_BF2D_NB(1, 1) LEA_BF2D_NB(1, 2) LEA_BF2D_NB(2, 1) LEA_BF2D_NB(2, 2) LEA_BF2D_NB(4, 1)
+  LEA_BF2D_NB(4, 2)
+  set_error("lea_conv2d(bf16): no tile wc=%d th=%d nb=%d", p.wc, p.th, p.nb);
+  return LEA_E_UNSUPPORTED;
+}
+
 thread_local char g_bf_name[96];
 
 }  // namespace bf
@@ -454,8 +476,8 @@ extern "C" int lea_conv3d_pack_weights_bf16(const float* w, void* packed, int co
   const int nch = (cin / 8 + nb - 1) / nb;
   const long long total = (long long)lea_conv3d_packed_elems_bf16(cout, cin, k);
   const int grid = (int)std::min<long long>((total + 255) / 256, 4096);
-  bf::pack_bf16_kernel<<<grid, 256, 0, as_stream(stream)>>>(w, (__bf16*)packed, cout, cin, k, nb,
-                                                            bf::ksteps(k, nb), cobv / 16, nch, total);
+  bf::pack_bf16_kernel<<<grid, 256, 0, as_stream(stream)>>>(w, (__bf16*)packed, cout, cin, k * k * k,
+                                                            nb, bf::ksteps(k, nb), cobv / 16, nch, total);
   return launch_status("lea_conv3d_pack_weights_bf16");
 }
 
@@ -595,4 +617,70 @@ extern "C" int lea_resample3d_trilinear_bf16(const void* x, int64_t x_bstride, v
       (const __bf16*)x, x_bstride, (__bf16*)y, y_bstride, C / 8, Di, Hi, Wi, Do, Ho, Wo,
       axis_ratio(Di, Do, ac), axis_ratio(Hi, Ho, ac), axis_ratio(Wi, Wo, ac), ac, scale, shift, flags);
   return launch_status("lea_resample3d_trilinear_bf16");
+}
+
+// ---- 2D 3x3 (feature net) on the bf16 engine: the D = 1 case of a (1, 3, 3) kernel
+extern "C" size_t lea_conv2d_packed_elems_bf16(int cout, int cin) {
+  if (cout <= 0 || cin <= 0 || cin % 8 != 0) return 0;
+  const int cobv = bf::cob_of(cout), nb = bf::nb_of(cin, 3);
+  const int nch = (cin / 8 + nb - 1) / nb;
+  return (size_t)((cout + cobv - 1) / cobv) * nch * ((9 * nb + 3) / 4) * (cobv / 16) * 4 * 16 * 8;
+}
+
+extern "C" int lea_conv2d_pack_weights_bf16(const float* w, void* packed, int cout, int cin,
+                                            void* stream) {
+  clear_error();
+  LEA_CHECK_ARG(w && packed, "lea_conv2d_pack_weights_bf16: null pointer");
+  LEA_CHECK_ARG(cout > 0 && cin > 0 && cin % 8 == 0 && cout % 8 == 0,
+                "lea_conv2d_pack_weights_bf16: unsupported shape cout=%d cin=%d", cout, cin);
+  const int cobv = bf::cob_of(cout), nb = bf::nb_of(cin, 3);
+  const int nch = (cin / 8 + nb - 1) / nb;
+  const long long total = (long long)lea_conv2d_packed_elems_bf16(cout, cin);
+  const int grid = (int)std::min<long long>((total + 255) / 256, 4096);
+  bf::pack_bf16_kernel<<<grid, 256, 0, as_stream(stream)>>>(w, (__bf16*)packed, cout, cin, 9, nb,
+                                                            (9 * nb + 3) / 4, cobv / 16, nch, total);
+  return launch_status("lea_conv2d_pack_weights_bf16");
+}
+
+extern "C" int lea_conv2d_bnrelu_bf16(const void* x, int64_t x_bstride, const void* w_packed,
+                                      const float* scale, const float* shift, const void* residual,
+                                      int64_t r_bstride, void* y, int64_t y_bstride, int B, int cin,
+                                      int cout, int H, int W, unsigned flags, void* stream) {
+  clear_error();
+  bf::Args a{};
+  a.x = (const __bf16*)x;
+  a.xbs = x_bstride;
+  a.x2 = (const __bf16*)x;
+  a.cb1 = cin / 8;
+  a.wp = (const __bf16*)w_packed;
+  a.scale = scale;
+  a.shift = shift;
+  a.res = (const __bf16*)residual;
+  a.rbs = r_bstride;
+  a.y = (__bf16*)y;
+  a.ybs = y_bstride;
+  a.cin = cin;
+  a.cout = cout;
+  a.D = 1;
+  a.H = H;
+  a.W = W;
+  a.flags = flags;
+  LEA_CHECK_ARG(x && w_packed && y && x != y, "lea_conv2d_bnrelu_bf16: null or aliased pointer");
+  LEA_CHECK_ARG((scale == nullptr) == (shift == nullptr),
+                "lea_conv2d_bnrelu_bf16: scale/shift must both be set or both NULL");
+  LEA_CHECK_ARG(!(flags & LEA_RESIDUAL) || residual, "lea_conv2d_bnrelu_bf16: LEA_RESIDUAL without residual");
+  LEA_CHECK_ARG(B > 0 && cin > 0 && cout > 0 && H > 0 && W > 0 && cin % 8 == 0 && cout % 8 == 0,
+                "lea_conv2d_bnrelu_bf16: bad shape B=%d cin=%d cout=%d H=%d W=%d", B, cin, cout, H, W);
+  const int cobv = bf::cob_of(cout);
+  bf::Plan p;
+  p.ks = 3;
+  p.mt = 1;
+  p.wc = cobv / 16;
+  p.nb = bf::nb_of(cin, 3);
+  p.td = 1;
+  const long long wgs8 = (long long)((W + 15) / 16) * ((H + 7) / 8) * B * ((cout + cobv - 1) / cobv);
+  p.th = wgs8 >= 1024 ? 8 : 4;
+  a.ncob = (cout + cobv - 1) / cobv;
+  a.nchunks = (cin / 8 + p.nb - 1) / p.nb;
+  return bf::run2d(p, a, B, as_stream(stream));
 }

@@ -302,7 +302,48 @@ class FeatureExecutor(CellGraphExecutor):
         return self.conv("last_3", y).squeeze(2)
 
 
-class MatchingExecutorBF16(MatchingExecutor):
+class _C8Layout:
+    """Activation-layout hooks of the bf16 executors: c8 tensors
+    ([B, C/8, D, H, W, 8] bfloat16), channel slices on block boundaries."""
+
+    def _empty(self, b, c, size, like):
+        return torch.empty((b, c // 8) + tuple(size) + (8,), device=like.device, dtype=torch.bfloat16)
+
+    @staticmethod
+    def _channels(t, c0, c1):
+        return t[:, c0 // 8:c1 // 8]
+
+    @staticmethod
+    def _nchannels(t):
+        return t.shape[1] * 8
+
+    @staticmethod
+    def _resample(x, size):
+        return kernels.resample_trilinear_bf16(x, size)
+
+    def _conv_c8(self, name, x, out=None, accumulate=False, x2=None, size=None, residual=None):
+        p = self.p[name]
+        cin = (x.shape[1] + (x2.shape[1] if x2 is not None else 0)) * 8
+        if cin != p.cin:
+            raise ValueError(f"{name}: expected {p.cin} input channels, got {cin}")
+        if size is not None and tuple(size) != tuple(x.shape[2:5]):
+            if x2 is not None or residual is not None or accumulate:
+                raise ValueError("resampled conv takes one input and no residual")
+            up = all(int(o) >= int(i) for o, i in zip(size, x.shape[2:5]))
+            if p.k == 1 and up:  # commuted: 1x1 at the low resolution, resample + BN/ReLU
+                z = kernels.conv3d_bnrelu_bf16(x, p.packed, p.cout, 1, None, None, relu=False)
+                return kernels.resample_trilinear_bf16(z, size, True, out, p.scale, p.shift, p.relu)
+            x = kernels.resample_trilinear_bf16(x, size)
+        if p.kind == "bf16_2d":
+            if x2 is not None:
+                raise ValueError(f"{name}: 2D conv takes one input")
+            return kernels.conv2d_bnrelu_bf16(x, p.packed, p.cout, p.scale, p.shift, p.relu, out,
+                                              accumulate, residual)
+        return kernels.conv3d_bnrelu_bf16(x, p.packed, p.cout, p.k, p.scale, p.shift, p.relu, out,
+                                          accumulate, x2, residual)
+
+
+class MatchingExecutorBF16(_C8Layout, MatchingExecutor):
     """newMatching.forward at bf16 (configs 3/4): activations in the c8 layout
     ([B, C/8, D, H, W, 8] bfloat16), convs on the bf16 matrix cores with f32
     accumulation and the f32 BN epilogue; the head's output (the matching cost)
@@ -336,21 +377,6 @@ class MatchingExecutorBF16(MatchingExecutor):
                 self.p[name] = ConvParams(kernels.pack_conv_weight_bf16(w), p.scale, p.shift, p.cin,
                                           p.cout, p.k, p.relu, "bf16")
 
-    def _empty(self, b, c, size, like):
-        return torch.empty((b, c // 8) + tuple(size) + (8,), device=like.device, dtype=torch.bfloat16)
-
-    @staticmethod
-    def _channels(t, c0, c1):
-        return t[:, c0 // 8:c1 // 8]
-
-    @staticmethod
-    def _nchannels(t):
-        return t.shape[1] * 8
-
-    @staticmethod
-    def _resample(x, size):
-        return kernels.resample_trilinear_bf16(x, size)
-
     @staticmethod
     def _tapsum(q, p3, full):
         return kernels.tapsum_upsample_bf16(q, p3.cout, full, p3.scale, p3.shift, p3.relu)
@@ -359,21 +385,8 @@ class MatchingExecutorBF16(MatchingExecutor):
         # per-tap partial sums + a tap-sum at the same size (identity interpolation)
         return self._tapsum(self.conv("last_3.taps", last), self.p["last_3"], self._volume(last))
 
-    def conv(self, name, x, out=None, accumulate=False, x2=None, size=None, residual=None):
-        p = self.p[name]
-        cin = (x.shape[1] + (x2.shape[1] if x2 is not None else 0)) * 8
-        if cin != p.cin:
-            raise ValueError(f"{name}: expected {p.cin} input channels, got {cin}")
-        if size is not None and tuple(size) != tuple(x.shape[2:5]):
-            if x2 is not None or residual is not None or accumulate:
-                raise ValueError("resampled conv takes one input and no residual")
-            up = all(int(o) >= int(i) for o, i in zip(size, x.shape[2:5]))
-            if p.k == 1 and up:  # commuted: 1x1 at the low resolution, resample + BN/ReLU
-                z = kernels.conv3d_bnrelu_bf16(x, p.packed, p.cout, 1, None, None, relu=False)
-                return kernels.resample_trilinear_bf16(z, size, True, out, p.scale, p.shift, p.relu)
-            x = kernels.resample_trilinear_bf16(x, size)
-        return kernels.conv3d_bnrelu_bf16(x, p.packed, p.cout, p.k, p.scale, p.shift, p.relu, out,
-                                          accumulate, x2, residual)
+    def conv(self, *args, **kw):
+        return self._conv_c8(*args, **kw)
 
     def run(self, x):
         """x: f32 cost volume [B, 64, D3, H3, W3] -> f32 matching cost [B, 1, D3, H3, W3]."""
@@ -381,10 +394,69 @@ class MatchingExecutorBF16(MatchingExecutor):
 
     def run_features(self, fl, fr, maxdisp):
         p = self.p["stem0"]
-        if fl.shape[1] * 2 != p.cin:
-            raise ValueError(f"stem0 expects {p.cin} cost-volume channels, got 2*{fl.shape[1]}")
-        f8 = kernels.to_c8(torch.cat((fl, fr), 0))  # [2B, C/8, 1, H, W, 8]
-        b = fl.shape[0]
+        cf = fl.shape[1] * (8 if fl.dtype == torch.bfloat16 else 1)
+        if cf * 2 != p.cin:
+            raise ValueError(f"stem0 expects {p.cin} cost-volume channels, got 2*{cf}")
+        if fl.dtype == torch.bfloat16:  # the bf16 feature net already hands over c8 maps
+            f8, b = torch.cat((fl, fr), 0), fl.shape[0]
+        else:
+            f8 = kernels.to_c8(torch.cat((fl, fr), 0))  # [2B, C/8, 1, H, W, 8]
+            b = fl.shape[0]
         stem0 = kernels.conv3d_bnrelu_costvolume_bf16(f8[:b], f8[b:], maxdisp, p.packed, p.cout,
                                                       p.scale, p.shift, p.relu)
         return self._from_stem0(stem0)
+
+
+class FeatureExecutorBF16(_C8Layout, FeatureExecutor):
+    """newFeature.forward at bf16 (configs 3/4): stem0 (3 input channels) and the
+    stride-3 stem1 stay f32; from stem2 on the maps are c8 and the 3x3 convs run on
+    the bf16 engine's 2D tiles.  Returns c8 feature maps [N, 32/8, 1, H3, W3, 8],
+    which the bf16 matching net reads directly."""
+
+    def __init__(self, feature):
+        super().__init__(feature)
+        with torch.no_grad():
+            for name, p in list(self.p.items()):
+                if name in ("stem0", "stem1"):
+                    continue
+                if name.endswith(".s1_group"):
+                    i = int(name.split(".")[1])
+                    w = torch.cat([feature.cells[i]._ops[op].conv.weight for _, op in self.s1_group[i]], 0)
+                else:
+                    w = feature.get_submodule(name).conv.weight
+                if p.kind == "2d":
+                    self.p[name] = ConvParams(kernels.pack_conv2d_weight_bf16(w), p.scale, p.shift,
+                                              p.cin, p.cout, 3, p.relu, "bf16_2d")
+                else:  # 1x1
+                    self.p[name] = ConvParams(
+                        kernels.pack_conv_weight_bf16(w.reshape(p.cout, p.cin, 1, 1, 1)), p.scale,
+                        p.shift, p.cin, p.cout, 1, p.relu, "bf16")
+
+    def conv(self, name, x, *args, **kw):
+        if name in ("stem0", "stem1"):
+            return CellGraphExecutor.conv(self, name, x, *args, **kw)
+        return self._conv_c8(name, x, *args, **kw)
+
+    def run(self, x):
+        x5 = x.unsqueeze(2)
+        stem1 = kernels.to_c8(self.conv("stem1", self.conv("stem0", x5)))
+        stem2 = self.conv("stem2", stem1)
+        out = (stem1, stem2)
+        for i in range(len(self.m.cells)):
+            out = self.cell(i, out[0], out[1])
+        last = out[-1]
+        h, w = self._volume(stem2)[1:]
+        lh = self._volume(last)[1]
+        full, half, quarter = (1, h, w), (1, h // 2, w // 2), (1, h // 4, w // 4)
+        if lh == h:
+            y = last
+        elif lh == h // 2:
+            y = self._resample(self.conv("last_6", last), full)
+        elif lh == h // 4:
+            y = self._resample(self.conv("last_6", self.conv("last_12", last), size=half), full)
+        elif lh == h // 8:
+            y = self.conv("last_12", self.conv("last_24", last, size=quarter), size=half)
+            y = self._resample(self.conv("last_6", y, size=half), full)
+        else:
+            raise ValueError(f"feature size {tuple(x.shape[2:])} is not legal for the feature net")
+        return self.conv("last_3", y)

@@ -545,3 +545,54 @@ def tapsum_upsample_bf16(q: torch.Tensor, cout: int, size, scale=None, shift=Non
         shift.data_ptr() if shift is not None else None, LEA_RELU if relu else 0, ws.data_ptr(),
         _lib.LEA_BF16, _stream()), "lea_tapsum_upsample(bf16)")
     return out
+
+
+def pack_conv2d_weight_bf16(w: torch.Tensor) -> torch.Tensor:
+    """[cout, cin, 3, 3] f32 device weight -> packed bf16 fragments (2D engine)."""
+    _require_cuda(w)
+    w = w.detach().contiguous()
+    if w.dim() != 4 or tuple(w.shape[2:]) != (3, 3):
+        raise ValueError(f"expected a [cout, cin, 3, 3] weight, got {tuple(w.shape)}")
+    cout, cin = w.shape[:2]
+    lib = _lib.load()
+    n = lib.lea_conv2d_packed_elems_bf16(cout, cin)
+    if n == 0:
+        raise ValueError(f"unsupported bf16 conv2d shape cout={cout} cin={cin}")
+    packed = torch.empty(n, device=w.device, dtype=torch.bfloat16)
+    check(lib.lea_conv2d_pack_weights_bf16(w.data_ptr(), packed.data_ptr(), cout, cin, _stream()),
+          "lea_conv2d_pack_weights_bf16")
+    return packed
+
+
+def conv2d_bnrelu_bf16(x: torch.Tensor, packed: torch.Tensor, cout: int, scale, shift,
+                       relu: bool = True, out: torch.Tensor | None = None, accumulate: bool = False,
+                       residual: torch.Tensor | None = None) -> torch.Tensor:
+    """conv2d_bnrelu on c8 maps [B, C/8, 1, H, W, 8]."""
+    _require_c8(x, out, residual)
+    _require_cuda(scale, shift)
+    b, cb, d, h, w, _ = x.shape
+    if d != 1:
+        raise ValueError("conv2d_bnrelu_bf16 takes D = 1 maps")
+    xbs = _check_c8_view(x, "x")
+    shape = (b, cout // 8, 1, h, w, 8)
+    if out is None:
+        if accumulate:
+            raise ValueError("accumulate needs out")
+        out = torch.empty(shape, device=x.device, dtype=torch.bfloat16)
+    if tuple(out.shape) != shape:
+        raise ValueError(f"out shape {tuple(out.shape)} != {shape}")
+    ybs = _check_c8_view(out, "out")
+    if accumulate:
+        rptr, rbs = out.data_ptr(), ybs
+    elif residual is not None:
+        if tuple(residual.shape) != shape:
+            raise ValueError("residual shape mismatch")
+        rptr, rbs = residual.data_ptr(), _check_c8_view(residual, "residual")
+    else:
+        rptr, rbs = None, 0
+    flags = (LEA_RELU if relu else 0) | (LEA_RESIDUAL if rptr is not None else 0)
+    check(_lib.load().lea_conv2d_bnrelu_bf16(
+        x.data_ptr(), xbs, packed.data_ptr(), scale.data_ptr() if scale is not None else None,
+        shift.data_ptr() if shift is not None else None, rptr, rbs, out.data_ptr(), ybs, b, cb * 8,
+        cout, h, w, flags, _stream()), "lea_conv2d_bnrelu_bf16")
+    return out

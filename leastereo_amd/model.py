@@ -116,9 +116,15 @@ class _ExecutorCache:
 
 class NewFeature(_ExecutorCache, nn.Module):
     """2D feature net, retrain/new_model_2d.py:78-165, on the HIP kernels
-    (``executor.FeatureExecutor``)."""
+    (``executor.FeatureExecutor``; ``FeatureExecutorBF16`` at precision bf16)."""
 
     _executor_cls = "FeatureExecutor"
+
+    def set_precision(self, precision: str):
+        cls = "FeatureExecutorBF16" if precision == "bf16" else "FeatureExecutor"
+        if cls != self._executor_cls:
+            self._executor_cls = cls
+            self.invalidate()
 
     def __init__(self, network_arch, cell_arch, args):
         super().__init__()
@@ -205,6 +211,7 @@ class LEAStereo(nn.Module):
         self.device = device
         self.precision = precision or getattr(args, "precision", None) or "f32"
         self.matching.set_precision(self.precision)
+        self.feature.set_precision(self.precision)
 
     def check_shape(self, height: int, width: int):
         """Reject input sizes the reference cannot run."""

@@ -146,3 +146,35 @@ def test_bf16_full_size_vs_f32_and_batch_invariance():
         one = torch.cat([mb(left[i:i + 1], right[i:i + 1]) for i in range(2)])
     assert torch.equal(db, one)
     assert ref.epe(db.cpu(), df.cpu()) < 1.0
+
+
+def test_conv2d_bf16_vs_torch():
+    g = torch.Generator().manual_seed(17)
+    for b, cin, cout, hw, mode in [(2, 32, 32, (24, 40), None), (4, 8, 8, (19, 33), "res"),
+                                   (1, 16, 16, (9, 20), "acc")]:
+        x = _bf(torch.randn((b, cin) + hw, generator=g))
+        w = _bf(torch.randn(cout, cin, 3, 3, generator=g) / np.sqrt(cin * 9))
+        scale = torch.rand(cout, generator=g) + 0.5
+        shift = torch.randn(cout, generator=g) * 0.1
+        r = _bf(torch.randn((b, cout) + hw, generator=g))
+        want = F.conv2d(x.double(), w.double(), None, 1, 1)
+        want = torch.relu(want * scale.double().view(1, -1, 1, 1) + shift.double().view(1, -1, 1, 1))
+        if mode:
+            want = want + r.double()
+        rc = kernels.to_c8(r.to(DEV))
+        y = kernels.conv2d_bnrelu_bf16(kernels.to_c8(x.to(DEV)), kernels.pack_conv2d_weight_bf16(w.to(DEV)),
+                                       cout, scale.to(DEV), shift.to(DEV), relu=True,
+                                       out=rc.clone() if mode == "acc" else None,
+                                       accumulate=mode == "acc", residual=rc if mode == "res" else None)
+        _close(kernels.from_c8(y)[:, :, 0], want)
+
+
+def test_bf16_feature_net_vs_f32():
+    """bf16 feature maps (c8) vs the f32 feature net on the same images."""
+    from tests.golden_util import normal
+    mb, mf = _model(48, "bf16"), _model(48, "f32")
+    x = normal(31, (2, 3, 96, 192)).to(DEV)
+    with torch.no_grad():
+        fb = kernels.from_c8(mb.feature(x))[:, :, 0]
+        ff = mf.feature(x)
+    _close(fb, ff, rel=5e-2)
