@@ -169,7 +169,8 @@ int lea_tapsum_upsample(const void* q, int64_t q_bstride, void* y, int64_t y_bst
 /* Disparity regression.  Replaces models/build_model_2d.py:52-57 + :33-42:
  *   U = trilinear(cost, [maxdisp, 3*H3, 3*W3], align_corners=False)
  *   disp[b, h, w] = sum_d d * softmax(-U, dim=d)
- * fused, U never materialised.  cost: [B, 1, D3, H3, W3]; disp: [B, 3H3, 3W3] fp32. */
+ * fused, U never materialised.  cost: [B, 1, D3, H3, W3]; disp: [B, 3H3, 3W3] fp32.
+ * dtype LEA_BF16 (the bf16 path; cost still f32) uses the hardware exp. */
 int lea_disparity_regression(const void* cost, float* disp, int B, int D3, int H3, int W3,
                              int maxdisp, int dtype, void* stream);
 

@@ -48,6 +48,18 @@ constexpr int kDispChunk = 16;  // cost planes fetched per batch of loads
 
 // LDS: the depth axis table (identical for every pixel) and, per thread, one
 // batch of bilinearly interpolated cost planes (own column: conflict-free).
+// FAST: hardware exp (v_exp_f32 on x*log2e, ~1e-6 relative) for the bf16 path
+// (dtype LEA_BF16: its matching cost carries ~1e-2 relative error already); the
+// f32 path keeps the accurate expf.
+template <bool FAST>
+__device__ __forceinline__ float dexp(float x) {
+  if constexpr (FAST)
+    return __expf(x);
+  else
+    return expf(x);
+}
+
+template <bool FAST>
 __global__ __launch_bounds__(kDispThreads) void disparity_f32(const float* __restrict__ cost,
                                                               float* __restrict__ disp, int D3,
                                                               int H3, int W3, int maxdisp,
@@ -91,12 +103,12 @@ __global__ __launch_bounds__(kDispThreads) void disparity_f32(const float* __res
         s = 1.f;
         t = 0.f;
       } else if (u < m) {
-        const float f = expf(u - m);  // < 1: rescale what was summed against the old min
+        const float f = dexp<FAST>(u - m);  // < 1: rescale what was summed against the old min
         s = s * f + 1.f;
         t = t * f + (float)od;
         m = u;
       } else {
-        const float e = expf(m - u);
+        const float e = dexp<FAST>(m - u);
         s += e;
         t += (float)od * e;
       }
@@ -116,7 +128,7 @@ extern "C" int lea_disparity_regression(const void* cost, float* disp, int B, in
                 "lea_disparity_regression: bad shape B=%d D3=%d H3=%d W3=%d maxdisp=%d", B, D3, H3,
                 W3, maxdisp);
   LEA_CHECK_ARG(3 * H3 <= 65535 && B <= 65535, "lea_disparity_regression: grid too large");
-  if (dtype != LEA_F32) {
+  if (dtype != LEA_F32 && dtype != LEA_BF16) {
     set_error("lea_disparity_regression: dtype %d unsupported", dtype);
     return LEA_E_UNSUPPORTED;
   }
@@ -125,7 +137,8 @@ extern "C" int lea_disparity_regression(const void* cost, float* disp, int B, in
   LEA_CHECK_ARG(lds <= 65536, "lea_disparity_regression: maxdisp %d too large", maxdisp);
   dim3 block(kDispThreads);
   dim3 grid((Wo + kDispThreads - 1) / kDispThreads, 3 * H3, B);
-  disparity_f32<<<grid, block, lds, as_stream(stream)>>>(
+  auto kern = dtype == LEA_BF16 ? disparity_f32<true> : disparity_f32<false>;
+  kern<<<grid, block, lds, as_stream(stream)>>>(
       (const float*)cost, disp, D3, H3, W3, maxdisp, (float)D3 / (float)maxdisp,
       (float)H3 / (float)(3 * H3), (float)W3 / (float)(3 * W3));
   return launch_status("lea_disparity_regression");

@@ -357,8 +357,9 @@ def tapsum_upsample(q: torch.Tensor, cout: int, size, scale: torch.Tensor | None
     return out
 
 
-def disparity_regression(cost: torch.Tensor, maxdisp: int) -> torch.Tensor:
-    """Disp + DisparityRegression (build_model_2d.py:52-57, 33-42): [B,1,D3,H3,W3] -> [B,3H3,3W3]."""
+def disparity_regression(cost: torch.Tensor, maxdisp: int, fast_exp: bool = False) -> torch.Tensor:
+    """Disp + DisparityRegression (build_model_2d.py:52-57, 33-42): [B,1,D3,H3,W3] -> [B,3H3,3W3].
+    ``fast_exp``: hardware exp (the bf16 path)."""
     _require_cuda(cost)
     if cost.dim() != 5 or cost.shape[1] != 1:
         raise ValueError("cost must be [B, 1, D3, H3, W3]")
@@ -366,7 +367,8 @@ def disparity_regression(cost: torch.Tensor, maxdisp: int) -> torch.Tensor:
     b, _, d3, h3, w3 = cost.shape
     disp = torch.empty((b, 3 * h3, 3 * w3), device=cost.device, dtype=torch.float32)
     check(_lib.load().lea_disparity_regression(cost.data_ptr(), disp.data_ptr(), b, d3, h3, w3,
-                                               maxdisp, LEA_F32, _stream()),
+                                               maxdisp, _lib.LEA_BF16 if fast_exp else LEA_F32,
+                                               _stream()),
           "lea_disparity_regression")
     return disp
 

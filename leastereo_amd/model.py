@@ -186,8 +186,8 @@ class Disp(nn.Module):
         self.maxdisp = maxdisp
         self.device = device
 
-    def forward(self, x):
-        return kernels.disparity_regression(x, self.maxdisp)
+    def forward(self, x, fast_exp=False):
+        return kernels.disparity_regression(x, self.maxdisp, fast_exp)
 
 
 class LEAStereo(nn.Module):
@@ -229,4 +229,4 @@ class LEAStereo(nn.Module):
         fx, fy = f[: x.shape[0]], f[x.shape[0]:]
         # cost volume (:34-48) + matching (:50): stem0 reads the volume in place
         cost = self.matching.executor().run_features(fx, fy, self.maxdisp)
-        return self.disp(cost)
+        return self.disp(cost, fast_exp=self.precision == "bf16")

@@ -63,7 +63,7 @@ def test_invalid_arguments_are_rejected_before_launch():
     assert lib.lea_conv3d_kernel_name(1, 8, 64, 192, 320, 1, 1).startswith(b"conv3d_reg_kernel<1, 1")
     assert lib.lea_conv3d_kernel_name(1, 8, 32, 96, 160, 1, 0) == b"conv1x1_kernel<1, 4>"
     # unsupported dtype is reported as such
-    assert lib.lea_disparity_regression(x, x, 1, 1, 1, 1, 1, 1, None) == 1002
+    assert lib.lea_disparity_regression(x, x, 1, 1, 1, 1, 1, 7, None) == 1002
     assert lib.lea_resample3d_trilinear(x, 0, x, 0, 1, 1, 1, 1, 1, 1, 1, 1, 1, None, None, 0, 0,
                                         None) == 1001
     assert lib.lea_resample3d_trilinear(x, 0, y, 0, 1, 1, 1, 1, 1, 1, 1, 1, 1, x, None, 0, 0,
