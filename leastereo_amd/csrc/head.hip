@@ -21,6 +21,8 @@
 // (lea_tapsum_workspace_bytes).  Same sums in a different association order.
 #include "common.h"
 
+using bf16x8_t = __attribute__((ext_vector_type(8))) __bf16;
+
 namespace lea {
 
 // pass 1: grid (quads of one low-res plane, (b, co, d, kh*3+kw)); float4 when Wi % 4 == 0
@@ -68,37 +70,61 @@ __global__ __launch_bounds__(256) void tapsum_dpass_f32(const float* __restrict_
   }
 }
 
-// pass 1 with q in the bf16 c8 layout (dtype LEA_BF16): channel co*27 + tap at
-// block (co*27 + tap) / 8, lane (co*27 + tap) % 8
+// pass 1 with q in the bf16 c8 layout (dtype LEA_BF16): one thread per low-res
+// voxel and output plane d computes all 9 (kh, kw) partial sums; the 9 channels
+// co*27 + kd*9 + (0..8) of one kd span exactly two 16-byte channel words, so each
+// (kd, source plane) costs two vector loads.  OFF = (co*27 + kd*9) % 8 is uniform
+// per workgroup and selects a specialised unpacking.
+template <int OFF>
+__device__ __forceinline__ void tapsum_acc9(float (&acc)[9], const bf16x8_t& a0, const bf16x8_t& a1,
+                                            const bf16x8_t& b0, const bf16x8_t& b1, float l0, float l1) {
+#pragma clang fp contract(off)
+#pragma unroll
+  for (int k = 0; k < 9; ++k) {
+    const int c = OFF + k;
+    const float v0 = c < 8 ? (float)a0[c] : (float)a1[c - 8];
+    const float v1 = c < 8 ? (float)b0[c] : (float)b1[c - 8];
+    acc[k] += l0 * v0 + l1 * v1;
+  }
+}
+
 __global__ __launch_bounds__(256) void tapsum_dpass_c8(const __bf16* __restrict__ q, long long qbs,
                                                        float* __restrict__ ws, int cout, int Di,
                                                        int Hi, int Wi, int Do, float rd) {
-#pragma clang fp contract(off)
-  int r = blockIdx.y;  // ((b * cout + co) * Do + d) * 9 + khw
-  const int khw = r % 9;
-  r /= 9;
+  const int r = blockIdx.y;  // (b * cout + co) * Do + d
   const int d = r % Do;
-  r /= Do;
-  const int co = r % cout;
-  const int b = r / cout;
+  const int bc = r / Do;
+  const int co = bc % cout, b = bc / cout;
   const long long HWi = (long long)Hi * Wi;
   const long long vol = HWi * Di;
-  const __bf16* qb = q + (long long)b * qbs;
-  float* yo = ws + (long long)blockIdx.y * HWi;
-  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < HWi;
-       i += (long long)gridDim.x * blockDim.x) {
-    float acc = 0.f;
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= HWi) return;
+  const bf16x8_t* qw = reinterpret_cast<const bf16x8_t*>(q + (long long)b * qbs);
+  float acc[9] = {};
 #pragma unroll
-    for (int kd = 0; kd < 3; ++kd) {
-      const int pd = d + kd - 1;
-      if ((unsigned)pd >= (unsigned)Do) continue;
-      const Axis ad = axis_index(rd, pd, Di, Do, 1);
-      const int c = co * 27 + kd * 9 + khw;
-      const __bf16* qc = qb + (long long)(c / 8) * vol * 8 + (c % 8);
-      acc += ad.l0 * (float)qc[(ad.i0 * HWi + i) * 8] + ad.l1 * (float)qc[(ad.i1 * HWi + i) * 8];
+  for (int kd = 0; kd < 3; ++kd) {
+    const int pd = d + kd - 1;
+    if ((unsigned)pd >= (unsigned)Do) continue;
+    const Axis ad = axis_index(rd, pd, Di, Do, 1);
+    const int cb = co * 27 + kd * 9;
+    const bf16x8_t* blk0 = qw + (long long)(cb / 8) * vol;
+    const bf16x8_t* blk1 = blk0 + vol;  // next channel word (always exists: 27*cout padded to 8)
+    const bf16x8_t a0 = blk0[ad.i0 * HWi + i], a1 = blk1[ad.i0 * HWi + i];
+    const bf16x8_t b0 = blk0[ad.i1 * HWi + i], b1 = blk1[ad.i1 * HWi + i];
+    switch (cb % 8) {
+      case 0: tapsum_acc9<0>(acc, a0, a1, b0, b1, ad.l0, ad.l1); break;
+      case 1: tapsum_acc9<1>(acc, a0, a1, b0, b1, ad.l0, ad.l1); break;
+      case 2: tapsum_acc9<2>(acc, a0, a1, b0, b1, ad.l0, ad.l1); break;
+      case 3: tapsum_acc9<3>(acc, a0, a1, b0, b1, ad.l0, ad.l1); break;
+      case 4: tapsum_acc9<4>(acc, a0, a1, b0, b1, ad.l0, ad.l1); break;
+      case 5: tapsum_acc9<5>(acc, a0, a1, b0, b1, ad.l0, ad.l1); break;
+      case 6: tapsum_acc9<6>(acc, a0, a1, b0, b1, ad.l0, ad.l1); break;
+      default: tapsum_acc9<7>(acc, a0, a1, b0, b1, ad.l0, ad.l1);
     }
-    yo[i] = acc;
   }
+  float* yo = ws + (long long)r * 9 * HWi + i;
+#pragma unroll
+  for (int k = 0; k < 9; ++k) yo[k * HWi] = acc[k];
 }
 
 // pass 2: one workgroup per output row (b, co, d, h); lanes along w
@@ -176,7 +202,7 @@ extern "C" int lea_tapsum_upsample(const void* q, int64_t q_bstride, void* y, in
   float* ws = (float*)workspace;
   const long long HWi = (long long)Hi * Wi;
   if (dtype == LEA_BF16) {
-    dim3 g1((unsigned)((HWi + 255) / 256), (unsigned)(B * cout * Do * 9));
+    dim3 g1((unsigned)((HWi + 255) / 256), (unsigned)(B * cout * Do));
     tapsum_dpass_c8<<<g1, 256, 0, st>>>((const __bf16*)q, q_bstride, ws, cout, Di, Hi, Wi, Do,
                                         axis_ratio(Di, Do, 1));
     const int rc = launch_status("lea_tapsum_upsample");
