@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define LEA_ABI_VERSION 3
+#define LEA_ABI_VERSION 4
 
 #define LEA_F32 0
 #define LEA_BF16 1
@@ -232,6 +232,42 @@ int lea_conv2d_bnrelu_bf16(const void* x, int64_t x_bstride, const void* w_packe
                            const float* scale, const float* shift, const void* residual,
                            int64_t r_bstride, void* y, int64_t y_bstride, int B, int cin, int cout,
                            int H, int W, unsigned flags, void* stream);
+
+/* ---- host steps either side of forward ---- */
+
+/* load_data + test_transform of predict.py, fused: replaces predict.py:162-184
+ * (per image channel (x - mean) / std over the WHOLE image, np.mean / np.std in
+ * float64, population std, stored float32) and predict.py:144-159 (zero-pad
+ * top-left when H <= crop_h and W <= crop_w, else centre-crop at
+ * start = int((H - crop) / 2); an image that neither fits nor covers the crop is
+ * rejected, as the reference's copy into the crop fails).
+ *   left/right: B uint8 HWC images [B, H, W, pix_stride] (RGB = 3, RGBA = 4; the
+ *               first 3 channels are used, predict.py:170-182)
+ *   out_left/out_right: [B, 3, crop_h, crop_w] float32
+ *   workspace: lea_standardize_workspace_bytes(B) bytes of device memory (cleared
+ *              by the call; holds the exact integer sums).                       */
+size_t lea_standardize_workspace_bytes(int B);
+int lea_standardize_crop_u8(const void* left, const void* right, int B, int H, int W,
+                            int pix_stride, float* out_left, float* out_right, int crop_h,
+                            int crop_w, void* workspace, void* stream);
+
+/* Disparity metrics of one batch, per pair b (device out[b][8], float64):
+ *   [0] n    of evaluation.py:287 mask (gt >= 0.001 & gt <= maxdisp)
+ *   [1] sum |pred - gt| over that mask          (EPE = [1] / [0], evaluation.py:288)
+ *   [2] n    of utils/metrics.py:6-8 validity (gt > 0.001 & gt < maxdisp)
+ *   [3] n correct, utils/metrics.py:16-19        (3-px error = 1 - [3] / [2])
+ *   [4..6] n with abs_diff <= thr1..thr3, :41-43 (bad-thr = 1 - [4+i] / [2])
+ * abs_diff follows the reference's int64 array: |gt - pred| truncated toward zero
+ * on valid pixels, 10000 elsewhere.  round_pred applies evaluation.py:169
+ * (pred.round() + z_shift, half-to-even) first.  correct (optional, [B, H*W]
+ * uint8) receives the 3-px correct mask of calculate_3px_error_and_correct_mask.
+ * pred/gt: [B, H, W] float32 with batch strides in elements.
+ * workspace: lea_disparity_metrics_workspace_bytes(B, H, W) bytes.               */
+size_t lea_disparity_metrics_workspace_bytes(int B, int H, int W);
+int lea_disparity_metrics(const float* pred, int64_t pred_bstride, const float* gt,
+                          int64_t gt_bstride, int B, int H, int W, float maxdisp, int round_pred,
+                          int z_shift, int thr1, int thr2, int thr3, unsigned char* correct,
+                          double* out, void* workspace, void* stream);
 
 #ifdef __cplusplus
 }

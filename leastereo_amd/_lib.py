@@ -12,11 +12,12 @@ LIB_PATH = os.environ.get(
     "LEASTEREO_HIP_LIB",
     os.path.join(os.path.dirname(os.path.abspath(__file__)), "libleastereo_hip.so"))
 
-ABI_VERSION = 3
+ABI_VERSION = 4
 LEA_F32 = 0
 LEA_BF16 = 1
 LEA_RELU = 1
 LEA_RESIDUAL = 2
+LEA_E_INVALID = 1001
 
 _p = ctypes.c_void_p
 _i = ctypes.c_int
@@ -68,6 +69,12 @@ SIGNATURES = {
     "lea_conv2d_bnrelu_bf16": (_i, [_p, _i64, _p, _p, _p, _p, _i64, _p, _i64, _i, _i, _i, _i, _i,
                                     _u, _p]),
     "lea_from_c8_bf16": (_i, [_p, _i64, _p, _i64, _i, _i, _i64, _p]),
+    # host steps either side of forward: predict.py load_data/test_transform, metrics
+    "lea_standardize_workspace_bytes": (ctypes.c_size_t, [_i]),
+    "lea_standardize_crop_u8": (_i, [_p, _p, _i, _i, _i, _i, _p, _p, _i, _i, _p, _p]),
+    "lea_disparity_metrics_workspace_bytes": (ctypes.c_size_t, [_i, _i, _i]),
+    "lea_disparity_metrics": (_i, [_p, _i64, _p, _i64, _i, _i, _i, ctypes.c_float, _i, _i,
+                                   _i, _i, _i, _p, _p, _p, _p]),
 }
 
 _lib = None

