@@ -19,6 +19,7 @@ and the 3x3 convs run on the 2D entry of the same MFMA engine.
 """
 from __future__ import annotations
 
+import os
 from dataclasses import dataclass
 
 import torch
@@ -37,6 +38,12 @@ class ConvParams:
     k: int
     relu: bool
     kind: str = "3d"          # "3d" (k 1/3), "2d" (3x3 s1), "s3" (3x3 stride 3)
+    wino: torch.Tensor | None = None  # Winograd-packed weight (f32 3D k=3 layers)
+
+
+# f32 3x3x3 layers run on the Winograd F(2,3)-along-W engine (2/3 of the direct
+# engine's MFMA work); LEASTEREO_WINOGRAD=0 keeps them on the direct engine.
+WINOGRAD = os.environ.get("LEASTEREO_WINOGRAD", "1") != "0"
 
 
 def _conv_params(mod, w=None, folded=None):
@@ -118,8 +125,27 @@ class CellGraphExecutor:
                 return kernels.resample_trilinear(z, size, True, out, p.scale, p.shift, p.relu)
             return kernels.conv3d_bnrelu_resampled(x, size, p.packed, p.cout, p.k, p.scale,
                                                    p.shift, p.relu, out, accumulate)
+        if p.wino is not None:
+            return kernels.conv3d_bnrelu_wino(x, p.wino, p.cout, p.scale, p.shift, p.relu, out,
+                                              accumulate, x2, residual)
         return kernels.conv3d_bnrelu(x, p.packed, p.cout, p.k, p.scale, p.shift, p.relu, out,
                                      accumulate, x2, residual)
+
+    def _use_winograd(self):
+        """Pack the eligible 3x3x3 layers for the Winograd engine (f32 executors)."""
+        if not WINOGRAD:
+            return
+        with torch.no_grad():
+            for name, p in self.p.items():
+                if p.kind != "3d" or not kernels.wino_eligible(p.cout, p.cin, p.k):
+                    continue
+                if name.endswith("s1_group"):
+                    i = int(name.split(".")[1])
+                    mods = [self.m.cells[i]._ops[op] for _, op in self.s1_group[i]]
+                    w = torch.cat([m.conv.weight for m in mods], 0)
+                else:
+                    w = self.m.get_submodule(name).conv.weight
+                p.wino = kernels.pack_conv_weight_wino(w)
 
     # activation layout hooks (f32 NCDHW here; the bf16 executor overrides them)
     def _empty(self, b, c, size, like):
@@ -211,8 +237,12 @@ class MatchingExecutor(CellGraphExecutor):
         p = self.p["stem0"]
         if fl.shape[1] * 2 != p.cin:
             raise ValueError(f"stem0 expects {p.cin} cost-volume channels, got 2*{fl.shape[1]}")
-        stem0 = kernels.conv3d_bnrelu_costvolume(fl, fr, maxdisp, p.packed, p.cout, p.scale,
-                                                 p.shift, p.relu)
+        if p.wino is not None:
+            stem0 = kernels.conv3d_bnrelu_costvolume_wino(fl, fr, maxdisp, p.wino, p.cout, p.scale,
+                                                          p.shift, p.relu)
+        else:
+            stem0 = kernels.conv3d_bnrelu_costvolume(fl, fr, maxdisp, p.packed, p.cout, p.scale,
+                                                     p.shift, p.relu)
         return self._from_stem0(stem0)
 
     def _from_stem0(self, stem0):
@@ -269,6 +299,7 @@ class MatchingExecutor(CellGraphExecutor):
             taps = last3.permute(0, 2, 3, 4, 1).reshape(co * 27, ci, 1, 1, 1)
             self.p["last_3.taps"] = ConvParams(kernels.pack_conv_weight(taps), None, None,
                                                ci, co * 27, 1, False)
+        self._use_winograd()
 
 
 class FeatureExecutor(CellGraphExecutor):
@@ -376,6 +407,9 @@ class MatchingExecutorBF16(_C8Layout, MatchingExecutor):
                     w = mod.conv.weight
                 self.p[name] = ConvParams(kernels.pack_conv_weight_bf16(w), p.scale, p.shift, p.cin,
                                           p.cout, p.k, p.relu, "bf16")
+
+    def _use_winograd(self):
+        """bf16 layers stay on the bf16 engine."""
 
     @staticmethod
     def _tapsum(q, p3, full):

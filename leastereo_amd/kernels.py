@@ -661,3 +661,89 @@ def disparity_metrics(pred: torch.Tensor, gt: torch.Tensor, maxdisp: float, roun
                                     mask.data_ptr() if mask is not None else None, out.data_ptr(),
                                     ws.data_ptr(), _stream()), "lea_disparity_metrics")
     return out, mask
+
+
+# ---- Winograd F(2,3)-along-W 3x3x3 convs (csrc/conv3d_wino.hip), fp32 ----
+
+def wino_eligible(cout: int, cin: int, k: int) -> bool:
+    """Layers the Winograd engine takes: k = 3, channels in chunks of 4, and more
+    than 8 output channels (couts <= 8 keep the direct engine's depth pairing)."""
+    return k == 3 and cin % 4 == 0 and cout > 8
+
+
+def wino_kernel_name(b, cout, d, h, w, costvolume=False):
+    name = _lib.load().lea_conv3d_wino_kernel_name(b, cout, d, h, w, 1 if costvolume else 0)
+    return name.decode() if name else None
+
+
+def pack_conv_weight_wino(w: torch.Tensor) -> torch.Tensor:
+    """[cout, cin, 3, 3, 3] fp32 device weight -> U = G g per kw row, the layout of
+    lea_conv3d_bnrelu_wino."""
+    _require_cuda(w)
+    w = w.detach().contiguous()
+    if w.dim() != 5 or tuple(w.shape[2:]) != (3, 3, 3):
+        raise ValueError(f"expected a [cout, cin, 3, 3, 3] weight, got {tuple(w.shape)}")
+    cout, cin = w.shape[0], w.shape[1]
+    n = _lib.load().lea_conv3d_wino_packed_floats(cout, cin)
+    if n == 0:
+        raise ValueError(f"unsupported Winograd conv shape cout={cout} cin={cin}")
+    packed = torch.empty(n, device=w.device, dtype=torch.float32)
+    check(_lib.load().lea_conv3d_wino_pack_weights(w.data_ptr(), packed.data_ptr(), cout, cin,
+                                                   _stream()), "lea_conv3d_wino_pack_weights")
+    return packed
+
+
+def conv3d_bnrelu_wino(x: torch.Tensor, packed: torch.Tensor, cout: int,
+                       scale: torch.Tensor | None, shift: torch.Tensor | None, relu: bool = True,
+                       out: torch.Tensor | None = None, accumulate: bool = False,
+                       x2: torch.Tensor | None = None,
+                       residual: torch.Tensor | None = None) -> torch.Tensor:
+    """``conv3d_bnrelu`` (k = 3) on the Winograd engine: same semantics, weights
+    packed by ``pack_conv_weight_wino``."""
+    _require_cuda(x, x2, packed, scale, shift, out)
+    b, cin, d, h, w = x.shape
+    xbs = _check_volume_view(x, "x")
+    cin2, x2bs = 0, 0
+    if x2 is not None:
+        if x2.shape[0] != b or tuple(x2.shape[2:]) != (d, h, w):
+            raise ValueError("x2 must match x in batch and volume")
+        cin2 = x2.shape[1]
+        x2bs = _check_volume_view(x2, "x2")
+    out, ybs = _conv_out(x.shape, cout, (d, h, w), out, accumulate, x.device, x.dtype)
+    rptr, rbs = _residual(out, accumulate, residual, ybs)
+    flags = (LEA_RELU if relu else 0) | (LEA_RESIDUAL if rptr is not None else 0)
+    rec = _probe_begin(b, cin + cin2, cout, d, h, w, 3, rptr is not None, b * d * h * w, False,
+                       name=wino_kernel_name(b, cout, d, h, w))
+    check(_lib.load().lea_conv3d_bnrelu_wino(
+        x.data_ptr(), xbs, x2.data_ptr() if x2 is not None else None, x2bs, cin2,
+        packed.data_ptr(),
+        scale.data_ptr() if scale is not None else None,
+        shift.data_ptr() if shift is not None else None,
+        rptr, rbs, out.data_ptr(), ybs, b, cin + cin2, cout, d, h, w, flags, LEA_F32, _stream()),
+        "lea_conv3d_bnrelu_wino")
+    _probe_end(rec)
+    return out
+
+
+def conv3d_bnrelu_costvolume_wino(fl: torch.Tensor, fr: torch.Tensor, maxdisp: int,
+                                  packed: torch.Tensor, cout: int, scale: torch.Tensor | None,
+                                  shift: torch.Tensor | None, relu: bool = True) -> torch.Tensor:
+    """``conv3d_bnrelu_costvolume`` on the Winograd engine (the cost volume of
+    LEAStereo.py:34-48 read in place, never materialised)."""
+    _require_cuda(fl, fr, packed, scale, shift)
+    if fl.shape != fr.shape or fl.dim() != 4:
+        raise ValueError("left/right features must both be [B, C, H, W]")
+    if fl.stride() != fr.stride() or fl.stride()[1:] != (fl.shape[2] * fl.shape[3], fl.shape[3], 1):
+        raise ValueError("left/right features need contiguous C,H,W and equal strides")
+    b, c, h, w = fl.shape
+    d3 = int(maxdisp / 3)
+    out = torch.empty((b, cout, d3, h, w), device=fl.device, dtype=fl.dtype)
+    rec = _probe_begin(b, 2 * c, cout, d3, h, w, 3, False, 0, False,
+                       name=wino_kernel_name(b, cout, d3, h, w, True))
+    check(_lib.load().lea_conv3d_bnrelu_costvolume_wino(
+        fl.data_ptr(), fr.data_ptr(), fl.stride(0), packed.data_ptr(),
+        scale.data_ptr() if scale is not None else None,
+        shift.data_ptr() if shift is not None else None, out.data_ptr(), out.stride(0), b, c, cout,
+        d3, h, w, LEA_RELU if relu else 0, LEA_F32, _stream()), "lea_conv3d_bnrelu_costvolume_wino")
+    _probe_end(rec)
+    return out

@@ -1,0 +1,122 @@
+"""GPU parity of the Winograd F(2,3)-along-W conv engine (csrc/conv3d_wino.hip)
+against float64 torch, with the tolerance of the direct fp32 engine
+(|d| <= 1e-4 + 1e-4 |ref|, test_gpu_parity.py) -- the transforms add a few fp32
+roundings per product, far inside it -- and against the direct engine itself.
+End to end the model runs on this engine by default, so test_gpu_parity.py's
+e2e / config-1 / full-size cases cover it at EPE <= 1e-3 px."""
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+from leastereo_amd import _lib, kernels
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def _ref(x, w, scale, shift, relu, res=None):
+    y = F.conv3d(x.double(), w.double(), None, 1, 1)
+    if scale is not None:
+        y = y * scale.double().view(1, -1, 1, 1, 1) + shift.double().view(1, -1, 1, 1, 1)
+    if relu:
+        y = torch.relu(y)
+    if res is not None:
+        y = y + res.double()
+    return y
+
+
+@pytest.mark.parametrize("b,cin,cout,shape,mode", [
+    (1, 64, 32, (6, 20, 70), None), (2, 128, 64, (5, 9, 40), "acc"), (1, 16, 16, (7, 33, 17), "acc"),
+    (1, 16, 48, (4, 9, 40), None), (1, 32, 96, (3, 6, 21), "res"), (1, 8, 24, (3, 10, 17), None),
+    (1, 12, 20, (3, 4, 5), "acc"), (2, 32, 32, (9, 13, 31), "res"), (1, 4, 12, (1, 1, 1), None),
+    (1, 32, 32, (2, 3, 2), "acc")])
+def test_wino_vs_torch(b, cin, cout, shape, mode):
+    """Odd and even W (the last pair half-masked), ragged H/D tiles, every epilogue."""
+    g = torch.Generator().manual_seed(cin * 7 + cout)
+    x = torch.randn((b, cin) + shape, generator=g)
+    w = torch.randn(cout, cin, 3, 3, 3, generator=g) / np.sqrt(cin * 27)
+    scale = torch.rand(cout, generator=g) + 0.5
+    shift = torch.randn(cout, generator=g) * 0.1
+    r = torch.randn((b, cout) + shape, generator=g)
+    want = _ref(x, w, scale, shift, True, r if mode else None)
+    out = r.to(DEV).clone() if mode == "acc" else None
+    y = kernels.conv3d_bnrelu_wino(x.to(DEV), kernels.pack_conv_weight_wino(w.to(DEV)), cout,
+                                   scale.to(DEV), shift.to(DEV), relu=True, out=out,
+                                   accumulate=mode == "acc",
+                                   residual=r.to(DEV) if mode == "res" else None)
+    np.testing.assert_allclose(y.cpu().double().numpy(), want.numpy(), rtol=1e-4, atol=1e-4)
+
+
+@pytest.mark.parametrize("np_,td", [(1, 1), (1, 2), (2, 1), (2, 2)])
+@pytest.mark.parametrize("cout", [16, 64])
+def test_wino_every_tile(np_, td, cout):
+    lib = _lib.load()
+    g = torch.Generator().manual_seed(np_ * 10 + td + cout)
+    x = torch.randn((2, 32, 5, 11, 45), generator=g)
+    w = torch.randn(cout, 32, 3, 3, 3, generator=g) / np.sqrt(32 * 27)
+    r = torch.randn((2, cout, 5, 11, 45), generator=g)
+    want = _ref(x, w, None, None, False, r)
+    assert lib.lea_conv3d_wino_set_tile_override(np_, td) == 0
+    try:
+        name = kernels.wino_kernel_name(2, cout, 5, 11, 45)
+        assert name == f"conv3d_wino_kernel<{1 if cout <= 16 else 2}, {np_}, {td}, false>", name
+        out = r.to(DEV).clone()
+        kernels.conv3d_bnrelu_wino(x.to(DEV), kernels.pack_conv_weight_wino(w.to(DEV)), cout, None,
+                                   None, relu=False, out=out, accumulate=True)
+    finally:
+        lib.lea_conv3d_wino_set_tile_override(0, 0)
+    np.testing.assert_allclose(out.cpu().double().numpy(), want.numpy(), rtol=1e-4, atol=1e-4)
+
+
+def test_wino_two_sources_into_a_channel_slice():
+    """conv1/conv2 shape: cat(x, x2) read in place, output into a slice of a cat buffer."""
+    g = torch.Generator().manual_seed(11)
+    x = torch.randn((1, 64, 4, 10, 40), generator=g)
+    x2 = torch.randn((1, 64, 4, 10, 40), generator=g)
+    w = torch.randn(64, 128, 3, 3, 3, generator=g) / np.sqrt(128 * 27)
+    want = _ref(torch.cat((x, x2), 1), w, None, None, False)
+    big = torch.zeros((1, 96, 4, 10, 40), device=DEV)
+    kernels.conv3d_bnrelu_wino(x.to(DEV), kernels.pack_conv_weight_wino(w.to(DEV)), 64, None, None,
+                               relu=False, out=big[:, 16:80], x2=x2.to(DEV))
+    np.testing.assert_allclose(big[:, 16:80].cpu().double().numpy(), want.numpy(), rtol=1e-4, atol=1e-4)
+    assert float(big[:, :16].abs().sum()) == 0 and float(big[:, 80:].abs().sum()) == 0
+
+
+@pytest.mark.parametrize("b,c,cout,maxdisp,hw", [(1, 32, 32, 48, (12, 40)), (2, 16, 16, 27, (5, 19))])
+def test_wino_costvolume_is_bit_identical_to_the_materialised_volume(b, c, cout, maxdisp, hw):
+    """stem0 reading the cost volume in place == the same engine on the built volume."""
+    g = torch.Generator().manual_seed(c + maxdisp)
+    fl = torch.randn((b, c) + hw, generator=g).to(DEV)
+    fr = torch.randn((b, c) + hw, generator=g).to(DEV)
+    w = (torch.randn(cout, 2 * c, 3, 3, 3, generator=g) / np.sqrt(2 * c * 27)).to(DEV)
+    packed = kernels.pack_conv_weight_wino(w)
+    scale = torch.rand(cout, device=DEV) + 0.5
+    shift = torch.randn(cout, device=DEV) * 0.1
+    cost = kernels.build_cost_volume(fl, fr, maxdisp)
+    want = kernels.conv3d_bnrelu_wino(cost, packed, cout, scale, shift)
+    got = kernels.conv3d_bnrelu_costvolume_wino(fl, fr, maxdisp, packed, cout, scale, shift)
+    assert torch.equal(got, want)
+    ref = _ref(cost.cpu(), w.cpu(), scale.cpu(), shift.cpu(), True)
+    np.testing.assert_allclose(got.cpu().double().numpy(), ref.numpy(), rtol=1e-4, atol=1e-4)
+
+
+def test_wino_matches_the_direct_engine_at_full_size():
+    """conv1/conv2 at config 2 (128 -> 64 at 32x96x160): Winograd vs direct engine."""
+    g = torch.Generator(device=DEV).manual_seed(3)
+    x = torch.randn((1, 128, 32, 96, 160), device=DEV, generator=g)
+    w = torch.randn(64, 128, 3, 3, 3, device=DEV, generator=g) / np.sqrt(128 * 27)
+    a = kernels.conv3d_bnrelu(x, kernels.pack_conv_weight(w), 64, 3, None, None, relu=False)
+    b = kernels.conv3d_bnrelu_wino(x, kernels.pack_conv_weight_wino(w), 64, None, None, relu=False)
+    err = float((a - b).abs().max())
+    assert err <= 1e-4 * float(a.abs().max()), err
+
+
+def test_model_uses_the_winograd_engine():
+    from leastereo_amd import executor
+    from leastereo_amd.config import LEAStereoArgs, default_arch_args
+    from leastereo_amd.model import LEAStereo
+    m = LEAStereo(default_arch_args(LEAStereoArgs(maxdisp=48)), DEV).to(DEV).eval()
+    ex = m.matching.executor()
+    wino = {n for n, p in ex.p.items() if p.wino is not None}
+    assert executor.WINOGRAD and {"stem0", "stem1", "conv1", "conv2"} <= wino
