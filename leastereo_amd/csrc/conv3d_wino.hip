@@ -311,14 +311,18 @@ struct Plan {
 thread_local int g_override[2] = {0, 0};  // np, td (lea_conv3d_wino_set_tile_override)
 
 inline Plan make_plan(int B, int cout, int D, int H, int W) {
+  // r01 sweep (tools/wino_sweep.py, profiles/r01_wino_sweep.txt): 8-row x 2-plane
+  // tiles for the 32-channel blocks (stem0/stem1/conv1/conv2: 0.72-0.81x the
+  // direct engine's time), 4 x 2 for the 16-channel cells; single planes only when
+  // the volume is too shallow to fill the chip.
   Plan p;
   p.mt = mt_of(cout);
   const long long ncob = (cout + 16 * p.mt - 1) / (16 * p.mt);
   auto wgs = [&](int np, int td) {
     return (long long)((W + 31) / 32) * ((H + 4 * np - 1) / (4 * np)) * ((D + td - 1) / td) * B * ncob;
   };
-  p.np = 1;
-  p.td = wgs(1, 2) >= 768 ? 2 : 1;
+  p.np = (p.mt == 2 && wgs(2, 2) >= 512) ? 2 : 1;
+  p.td = wgs(p.np, 2) >= 384 ? 2 : 1;
   if (g_override[0] > 0) {
     p.np = g_override[0];
     p.td = g_override[1];

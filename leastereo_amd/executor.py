@@ -125,7 +125,7 @@ class CellGraphExecutor:
                 return kernels.resample_trilinear(z, size, True, out, p.scale, p.shift, p.relu)
             return kernels.conv3d_bnrelu_resampled(x, size, p.packed, p.cout, p.k, p.scale,
                                                    p.shift, p.relu, out, accumulate)
-        if p.wino is not None:
+        if p.wino is not None and kernels.wino_preferred(x.shape[0], p.cout, p.cin, *x.shape[2:5]):
             return kernels.conv3d_bnrelu_wino(x, p.wino, p.cout, p.scale, p.shift, p.relu, out,
                                               accumulate, x2, residual)
         return kernels.conv3d_bnrelu(x, p.packed, p.cout, p.k, p.scale, p.shift, p.relu, out,
@@ -237,7 +237,8 @@ class MatchingExecutor(CellGraphExecutor):
         p = self.p["stem0"]
         if fl.shape[1] * 2 != p.cin:
             raise ValueError(f"stem0 expects {p.cin} cost-volume channels, got 2*{fl.shape[1]}")
-        if p.wino is not None:
+        if p.wino is not None and kernels.wino_preferred(fl.shape[0], p.cout, p.cin, int(maxdisp / 3),
+                                                         *fl.shape[2:4]):
             stem0 = kernels.conv3d_bnrelu_costvolume_wino(fl, fr, maxdisp, p.wino, p.cout, p.scale,
                                                           p.shift, p.relu)
         else:

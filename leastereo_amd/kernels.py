@@ -671,6 +671,20 @@ def wino_eligible(cout: int, cin: int, k: int) -> bool:
     return k == 3 and cin % 4 == 0 and cout > 8
 
 
+WINO_MIN_VOXELS = 200_000  # below this the direct engine's smaller tiles fill the chip better
+
+
+def wino_preferred(b, cout, cin, d, h, w) -> bool:
+    """Per-call engine choice for an eligible layer (tools/wino_sweep.py at config 2):
+    Winograd wins on the large volumes when the output channels fill its 16/32-row
+    blocks (stem0, stem1, conv1/2, the 16-channel L1 cells, the 8->24 L0 group);
+    the direct engine keeps the small L2 volumes and the 48-channel groups (a
+    third of a 32-row block would be padding)."""
+    if b * d * h * w < WINO_MIN_VOXELS:
+        return False
+    return cout == 16 or cout == 24 or cout % 32 == 0
+
+
 def wino_kernel_name(b, cout, d, h, w, costvolume=False):
     name = _lib.load().lea_conv3d_wino_kernel_name(b, cout, d, h, w, 1 if costvolume else 0)
     return name.decode() if name else None

@@ -120,3 +120,27 @@ def test_model_uses_the_winograd_engine():
     ex = m.matching.executor()
     wino = {n for n, p in ex.p.items() if p.wino is not None}
     assert executor.WINOGRAD and {"stem0", "stem1", "conv1", "conv2"} <= wino
+
+
+def test_e2e_golden_with_every_eligible_layer_on_winograd(monkeypatch):
+    """The reference's end-to-end golden case (96x192 D48) with the Winograd engine
+    forced onto every eligible layer (the size threshold would keep this small
+    case on the direct engine): EPE vs the reference fp32 / fp64 disparity."""
+    from leastereo_amd.config import LEAStereoArgs, default_arch_args
+    from leastereo_amd.model import LEAStereo
+    from oracle import torch_ref as ref
+    from tests.golden_util import golden, meta, normal, state_dict
+    monkeypatch.setattr(kernels, "WINO_MIN_VOXELS", 0)
+    for name, c in meta()["cases"].items():
+        if not name.startswith("e2e/"):
+            continue
+        key = name.split("/", 1)[1]
+        m = LEAStereo(default_arch_args(LEAStereoArgs(maxdisp=c["maxdisp"])), DEV)
+        m.load_state_dict(state_dict(), strict=True)
+        m = m.to(DEV).eval()
+        shape = (c.get("batch", 1), 3, c["height"], c["width"])
+        with torch.no_grad():
+            d = m(normal(c["seeds"][0], shape).to(DEV), normal(c["seeds"][1], shape).to(DEV)).cpu()
+        g = golden("e2e")
+        assert ref.epe(d, torch.from_numpy(g[key + "/disp32"])) < 1e-3
+        assert ref.epe(d, torch.from_numpy(g[key + "/disp64"])) < 1e-3
