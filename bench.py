@@ -210,6 +210,7 @@ def main():
     flops_per_launch = dom["flops"] / dom["launches"]
     ms_per_launch = dom["ms"] / dom["launches"]
     achieved = flops_per_launch / (ms_per_launch * 1e-3) / 1e12
+    mfma_tflops = dom["mfma_flops"] / dom["launches"] / (ms_per_launch * 1e-3) / 1e12
     traffic = None
     tf_file = os.path.join(REPO, "profiles", "hbm_traffic.json")
     if os.path.exists(tf_file):
@@ -246,7 +247,11 @@ def main():
                      "peak": peak, "unit": "TFLOP/s",
                      "frac": achieved / peak, "traffic": traffic,
                      "launches_per_step": dom["launches"] / args.steps,
-                     "flops_per_launch": flops_per_launch, "ms_per_launch": ms_per_launch},
+                     "flops_per_launch": flops_per_launch, "ms_per_launch": ms_per_launch,
+                     # products the kernel actually issues: Winograd F(2,3) does 4 per 6 of
+                     # the direct convolution whose FLOPs define `achieved`
+                     "algorithm": "winograd F(2,3) along W" if "wino" in dominant else "direct",
+                     "mfma_executed": mfma_tflops, "mfma_executed_frac": mfma_tflops / peak},
         "epe_px": None if epe is None else {
             "vs": "reference LEAStereo fp32 disparity (tests/golden e2e b1_h96_w192_md48)",
             "max_over_ranks": max(epe), "per_rank": epe},

@@ -27,7 +27,7 @@ class KernelProbe:
 
     def __init__(self, names=None):
         self.names = None if names is None else set(names)
-        self.records = []  # (name, flops, bytes, start_event, end_event)
+        self.records = []  # (name, flops, bytes, start_event, end_event, mfma_flops)
 
     def __enter__(self):
         global _probe
@@ -41,12 +41,14 @@ class KernelProbe:
     def summary(self):
         torch.cuda.synchronize()
         out = {}
-        for name, flops, nbytes, e0, e1 in self.records:
-            d = out.setdefault(name, {"launches": 0, "flops": 0.0, "bytes": 0.0, "ms": 0.0})
+        for name, flops, nbytes, e0, e1, mfma in self.records:
+            d = out.setdefault(name, {"launches": 0, "flops": 0.0, "bytes": 0.0, "ms": 0.0,
+                                      "mfma_flops": 0.0})
             d["launches"] += 1
             d["flops"] += flops
             d["bytes"] += nbytes
             d["ms"] += e0.elapsed_time(e1)
+            d["mfma_flops"] += mfma
         return out
 
 
@@ -106,8 +108,12 @@ def pack_conv_weight(w: torch.Tensor) -> torch.Tensor:
     return packed
 
 
-def _probe_begin(b, cin, cout, d, h, w, k, accumulate, in_vox, resampled, name=None):
-    """Start HIP-event timing of this launch if the active probe wants its kernel."""
+def _probe_begin(b, cin, cout, d, h, w, k, accumulate, in_vox, resampled, name=None, mfma_scale=1.0,
+                 esz=4):
+    """Start HIP-event timing of this launch if the active probe wants its kernel.
+    ``flops`` is the direct convolution's (the reference algorithm's) count;
+    ``mfma_scale`` converts it to the products the kernel actually issues (2/3 for
+    Winograd F(2,3), times its cout padding); ``esz`` is the activation element size."""
     probe = _probe
     if probe is None:
         return None
@@ -117,18 +123,18 @@ def _probe_begin(b, cin, cout, d, h, w, k, accumulate, in_vox, resampled, name=N
         return None
     vox = b * d * h * w
     flops = 2.0 * vox * cout * cin * k ** 3
-    nbytes = 4.0 * (in_vox * cin + vox * cout * (2 if accumulate else 1) + cout * cin * k ** 3)
+    nbytes = esz * (in_vox * cin + vox * cout * (2 if accumulate else 1)) + 4.0 * cout * cin * k ** 3
     e0 = torch.cuda.Event(enable_timing=True)
     e0.record()
-    return probe, name, flops, nbytes, e0
+    return probe, name, flops, nbytes, e0, flops * mfma_scale
 
 
 def _probe_end(rec):
     if rec is not None:
-        probe, name, flops, nbytes, e0 = rec
+        probe, name, flops, nbytes, e0, mfma = rec
         e1 = torch.cuda.Event(enable_timing=True)
         e1.record()
-        probe.records.append((name, flops, nbytes, e0, e1))
+        probe.records.append((name, flops, nbytes, e0, e1, mfma))
 
 
 def _conv_out(x_shape5, cout, spatial, out, accumulate, device, dtype):
@@ -473,7 +479,7 @@ def conv3d_bnrelu_bf16(x: torch.Tensor, packed: torch.Tensor, cout: int, k: int,
         rptr, rbs = None, 0
     flags = (LEA_RELU if relu else 0) | (LEA_RESIDUAL if rptr is not None else 0)
     rec = _probe_begin(b, cb * 8 + cin2, cout, d, h, w, k, rptr is not None, b * d * h * w, False,
-                       name=conv_kernel_name_bf16(b, cout, cb * 8 + cin2, d, h, w, k))
+                       name=conv_kernel_name_bf16(b, cout, cb * 8 + cin2, d, h, w, k), esz=2)
     check(_lib.load().lea_conv3d_bnrelu_bf16(
         x.data_ptr(), xbs, x2.data_ptr() if x2 is not None else None, x2bs, cin2, packed.data_ptr(),
         scale.data_ptr() if scale is not None else None,
@@ -497,7 +503,7 @@ def conv3d_bnrelu_costvolume_bf16(fl: torch.Tensor, fr: torch.Tensor, maxdisp: i
     d3 = int(maxdisp / 3)
     out = torch.empty((b, cout // 8, d3, h, w, 8), device=fl.device, dtype=torch.bfloat16)
     rec = _probe_begin(b, 2 * cb * 8, cout, d3, h, w, 3, False, 0, False,
-                       name=conv_kernel_name_bf16(b, cout, 2 * cb * 8, d3, h, w, 3, True))
+                       name=conv_kernel_name_bf16(b, cout, 2 * cb * 8, d3, h, w, 3, True), esz=2)
     check(_lib.load().lea_conv3d_bnrelu_costvolume_bf16(
         fl.data_ptr(), fr.data_ptr(), fbs, packed.data_ptr(),
         scale.data_ptr() if scale is not None else None,
@@ -685,6 +691,13 @@ def wino_preferred(b, cout, cin, d, h, w) -> bool:
     return cout == 16 or cout == 24 or cout % 32 == 0
 
 
+def wino_mfma_scale(cout: int) -> float:
+    """MFMA products issued per direct-convolution product: 4 per 6 (F(2,3)), times
+    the padding of cout to the engine's 16/32-row block."""
+    cop = 16 if cout <= 16 else 32
+    return (2.0 / 3.0) * (-(-cout // cop) * cop) / cout
+
+
 def wino_kernel_name(b, cout, d, h, w, costvolume=False):
     name = _lib.load().lea_conv3d_wino_kernel_name(b, cout, d, h, w, 1 if costvolume else 0)
     return name.decode() if name else None
@@ -727,7 +740,7 @@ def conv3d_bnrelu_wino(x: torch.Tensor, packed: torch.Tensor, cout: int,
     rptr, rbs = _residual(out, accumulate, residual, ybs)
     flags = (LEA_RELU if relu else 0) | (LEA_RESIDUAL if rptr is not None else 0)
     rec = _probe_begin(b, cin + cin2, cout, d, h, w, 3, rptr is not None, b * d * h * w, False,
-                       name=wino_kernel_name(b, cout, d, h, w))
+                       name=wino_kernel_name(b, cout, d, h, w), mfma_scale=wino_mfma_scale(cout))
     check(_lib.load().lea_conv3d_bnrelu_wino(
         x.data_ptr(), xbs, x2.data_ptr() if x2 is not None else None, x2bs, cin2,
         packed.data_ptr(),
@@ -753,7 +766,7 @@ def conv3d_bnrelu_costvolume_wino(fl: torch.Tensor, fr: torch.Tensor, maxdisp: i
     d3 = int(maxdisp / 3)
     out = torch.empty((b, cout, d3, h, w), device=fl.device, dtype=fl.dtype)
     rec = _probe_begin(b, 2 * c, cout, d3, h, w, 3, False, 0, False,
-                       name=wino_kernel_name(b, cout, d3, h, w, True))
+                       name=wino_kernel_name(b, cout, d3, h, w, True), mfma_scale=wino_mfma_scale(cout))
     check(_lib.load().lea_conv3d_bnrelu_costvolume_wino(
         fl.data_ptr(), fr.data_ptr(), fl.stride(0), packed.data_ptr(),
         scale.data_ptr() if scale is not None else None,

@@ -29,7 +29,7 @@ def load(d, counter):
 
 
 def short(n):
-    m = re.search(r"lea::(\w+)<([^>]*)>", n)
+    m = re.search(r"lea::(?:\w+::)*(\w+)<([^>]*)>", n)
     return f"{m.group(1)}<{m.group(2)}>" if m else None
 
 
