@@ -230,3 +230,40 @@ class LEAStereo(nn.Module):
         # cost volume (:34-48) + matching (:50): stem0 reads the volume in place
         cost = self.matching.executor().run_features(fx, fy, self.maxdisp)
         return self.disp(cost, fast_exp=self.precision == "bf16")
+
+    def graphed(self, batch: int, height: int, width: int):
+        """``forward`` for one input shape captured into a HIP graph (SURVEY.md §7:
+        one host call per batch instead of ~140 launches, for serving and for ranks
+        that share a node's host CPUs).  The forward issues only library kernels on
+        the current stream and never synchronises, so it captures as is."""
+        return GraphedForward(self, batch, height, width)
+
+
+class GraphedForward:
+    """``forward`` captured once into a torch.cuda.CUDAGraph (a hipGraph on ROCm)
+    with static input/output buffers; ``__call__(x, y)`` copies the inputs in,
+    replays, and returns the static output (overwritten by the next call)."""
+
+    def __init__(self, model: LEAStereo, batch: int, height: int, width: int):
+        if not torch.cuda.is_available():
+            raise RuntimeError("HIP graphs need a ROCm device")
+        model.check_shape(height, width)
+        dev = next(model.parameters()).device
+        self.model = model
+        self.x = torch.zeros(batch, 3, height, width, device=dev)
+        self.y = torch.zeros_like(self.x)
+        side = torch.cuda.Stream(device=dev)
+        side.wait_stream(torch.cuda.current_stream(dev))
+        with torch.no_grad(), torch.cuda.stream(side):
+            for _ in range(2):  # packs the weights and warms the allocator outside the capture
+                model(self.x, self.y)
+        torch.cuda.current_stream(dev).wait_stream(side)
+        self.graph = torch.cuda.CUDAGraph()
+        with torch.no_grad(), torch.cuda.graph(self.graph):
+            self.out = model(self.x, self.y)
+
+    def __call__(self, x, y):
+        self.x.copy_(x, non_blocking=True)
+        self.y.copy_(y, non_blocking=True)
+        self.graph.replay()
+        return self.out

@@ -144,3 +144,23 @@ def test_e2e_golden_with_every_eligible_layer_on_winograd(monkeypatch):
         g = golden("e2e")
         assert ref.epe(d, torch.from_numpy(g[key + "/disp32"])) < 1e-3
         assert ref.epe(d, torch.from_numpy(g[key + "/disp64"])) < 1e-3
+
+
+def test_graphed_forward_replays_the_eager_result():
+    """LEAStereo.graphed: the forward captured into a HIP graph replays to the eager
+    output bit for bit, for new inputs copied into its static buffers."""
+    from leastereo_amd.config import LEAStereoArgs, default_arch_args
+    from leastereo_amd.model import LEAStereo
+    from tests.golden_util import normal, state_dict
+    m = LEAStereo(default_arch_args(LEAStereoArgs(maxdisp=48)), DEV)
+    m.load_state_dict(state_dict(), strict=True)
+    m = m.to(DEV).eval()
+    g = m.graphed(2, 96, 192)
+    for seed in (5, 6):
+        x = normal(seed, (2, 3, 96, 192)).to(DEV)
+        y = normal(seed + 10, (2, 3, 96, 192)).to(DEV)
+        with torch.no_grad():
+            want = m(x, y)
+        got = g(x, y)
+        torch.cuda.synchronize()
+        assert torch.equal(got, want)
