@@ -5,12 +5,14 @@
 // For a pair of outputs y[w], y[w+1] along W and a fixed (kd, kh):
 //     y[w + j] = sum_kw g[kw] x[w - 1 + j + kw]
 //   = A^T [ (G g) . (B^T x) ],  x = x[w-1 .. w+2],
-//     G g  = (g0, (g0+g1+g2)/2, (g0-g1+g2)/2, g2)          (packed once per weight load)
+//     G g  = (g0, (g0+g1+g2)/2, (g0-g1+g2)/2, g2)          (packed, or formed in-kernel)
 //     B^T x = (x0 - x2, x1 + x2, x2 - x1, x1 - x3)          (4 VALU adds per lane)
 //     A^T m = (m0 + m1 + m2, m1 - m2 - m3)
 // so per 2 outputs and (kd, kh) the GEMM does 4 products instead of 6.  All of it
 // is fp32: the transforms are exact up to one rounding per add (G's halves are
-// exact), the products and sums are the MFMA's fp32.
+// exact), the products and sums are the MFMA's fp32.  48-cout blocks form U = G g
+// in the kernel from staged g rows (a quarter less LDS for the weight stage, which
+// keeps two workgroups per CU); 16/32-cout blocks stage the packed U.
 //
 // GEMM view per transform point xi in 0..3 and (kd, kh):
 //     M_xi[co][pair] += sum_ci U_xi[kd][kh][co][ci] * V_xi[ci][pair]
@@ -23,7 +25,7 @@
 // row) and COP = 16 MT output channels.  K is streamed in chunks of 4 input channels
 // (one MFMA K step): the input halo by LDS-DMA (buffer_load_dword ... lds, one
 // buffer resource per channel, out-of-range offsets return the zero padding), the
-// chunk's transformed weights (9 x 4 x 4 x COP floats) by global_load_lds_dwordx4;
+// chunk's weights (9 x 4 (or 3) x 4 x COP floats) by global_load_lds_dwordx4;
 // two stages, one vmcnt(0) + barrier per chunk (the direct engine's pipeline).
 #include "conv3d_impl.h"
 
@@ -32,7 +34,11 @@ namespace wino {
 
 constexpr int CIN_B = 4;
 
-__host__ __device__ constexpr int mt_of(int cout) { return cout <= 16 ? 1 : 2; }
+// 16-row MFMA tiles per cout block: 16, 32 or 48 couts (48 for 48k couts that are not
+// multiples of 32: the L1 16->48 sibling groups would pad a 64-row block by a third)
+__host__ __device__ constexpr int mt_of(int cout) {
+  return cout <= 16 ? 1 : (cout % 32 != 0 && cout % 48 == 0) ? 3 : 2;
+}
 __host__ __device__ constexpr int round_32mod64(int n) { return n % 64 <= 32 ? n + (32 - n % 64) : n + (96 - n % 64); }
 
 template <int MT, int NP, int TD>
@@ -48,9 +54,14 @@ struct Cfg {
   // group read disjoint halves of the 64 banks
   static constexpr int CIS = round_32mod64(IMG);
   static constexpr int XS = CIN_B * CIS;
-  static constexpr int WS = 9 * 4 * CIN_B * COP;  // transformed weights of one chunk
+  // 48-row blocks stage the plain weights g (3 rows per (kd,kh)) and form U = G g in
+  // the kernel, so two stages of two workgroups fit the LDS; 16/32-row blocks stage
+  // U (4 rows), which saves the per-step VALU (measured 1-2.5 % faster)
+  static constexpr bool GW = MT == 3;
+  static constexpr int KW_ROWS = GW ? 3 : 4;
+  static constexpr int WS = 9 * KW_ROWS * CIN_B * COP;
   static constexpr int STAGE = XS + WS;
-  static_assert(XS % 16 == 0 && WS % 256 == 0, "16-byte aligned LDS regions, whole 1-KB pieces");
+  static_assert(XS % 16 == 0 && WS % 16 == 0, "16-byte aligned LDS regions");
 };
 
 __device__ __forceinline__ int a_col(int m, int ci, int n, bool swz) { return ((swz ? (m ^ (ci & 1)) : m) * 16) + n; }
@@ -60,7 +71,7 @@ __global__ __launch_bounds__(kConvThreads, 2) void conv3d_wino_kernel(const Conv
   using C = Cfg<MT, NP, TD>;
   constexpr int XSLOTS = (C::IMG + 63) / 64;
   constexpr int XSLOTS_W = (XSLOTS + kConvWaves - 1) / kConvWaves;
-  constexpr int WSLOTS = C::WS / 256;
+  constexpr int WSLOTS = (C::WS + 255) / 256;
   constexpr int WSLOTS_W = (WSLOTS + kConvWaves - 1) / kConvWaves;
   __shared__ __attribute__((aligned(16))) float smem[2 * C::STAGE];
 
@@ -120,7 +131,7 @@ __global__ __launch_bounds__(kConvThreads, 2) void conv3d_wino_kernel(const Conv
 #pragma unroll
     for (int t = 0; t < WSLOTS_W; ++t) {
       const int j = wave + kConvWaves * t;
-      if (j < WSLOTS)
+      if (j < WSLOTS && j * 256 + lane * 4 < C::WS)
         __builtin_amdgcn_global_load_lds(wsrc + j * 256 + lane * 4, (lds_void*)(wdst + j * 256), 16, 0, 0);
     }
     const long long cvol = CV ? (long long)HW : (long long)HW * a.D;  // channel stride
@@ -204,12 +215,26 @@ __global__ __launch_bounds__(kConvThreads, 2) void conv3d_wino_kernel(const Conv
             vb[t][j][2] = hi.x - lo.y;
             vb[t][j][3] = lo.y - hi.y;
           }
-        const float* wk = ws + (kd * 3 + kh) * 4 * CIN_B * C::COP;
+        const float* wk = ws + (kd * 3 + kh) * C::KW_ROWS * CIN_B * C::COP;
+        float u[4][MT];
+#pragma unroll
+        for (int m = 0; m < MT; ++m) {
+          if constexpr (C::GW) {  // U = G g of this lane's kw row (exact halves)
+            const float g0 = wk[woff[m]], g1 = wk[CIN_B * C::COP + woff[m]];
+            const float g2 = wk[2 * CIN_B * C::COP + woff[m]];
+            const float t = g0 + g2;
+            u[0][m] = g0;
+            u[1][m] = (t + g1) * 0.5f;
+            u[2][m] = (t - g1) * 0.5f;
+            u[3][m] = g2;
+          } else {
+#pragma unroll
+            for (int x = 0; x < 4; ++x) u[x][m] = wk[x * CIN_B * C::COP + woff[m]];
+          }
+        }
 #pragma unroll
         for (int x = 0; x < 4; ++x) {
-          float av[MT];
-#pragma unroll
-          for (int m = 0; m < MT; ++m) av[m] = wk[x * CIN_B * C::COP + woff[m]];
+          const float (&av)[MT] = u[x];
 #pragma unroll
           for (int t = 0; t < TD; ++t)
 #pragma unroll
@@ -274,19 +299,22 @@ __global__ __launch_bounds__(kConvThreads, 2) void conv3d_wino_kernel(const Conv
   }
 }
 
-// weights [cout][cin][3][3][3] -> per (cout block, chunk): [kd*3+kh][xi][ci][COP col]
-// holding U_xi = (G g)_xi of the kw row g, computed in double and rounded once
+// weights [cout][cin][3][3][3] -> per (cout block, chunk): [kd*3+kh][row][ci][COP col],
+// rows = U_xi = (G g)_xi (computed in double, rounded once) for 16/32-row blocks,
+// rows = g[kw] for 48-row blocks (the kernel forms U)
 template <int MT>
 __global__ void pack_wino_kernel(const float* __restrict__ w, float* __restrict__ packed, int cout,
                                  int cin, int nchunks, long long total) {
   constexpr int COP = 16 * MT;
   constexpr bool SWZ = (COP % 32) == 0;
+  constexpr bool GW = MT == 3;
+  constexpr int ROWS = GW ? 3 : 4;
   for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
        i += (long long)gridDim.x * blockDim.x) {
     long long q = i;
     const int col = (int)(q % COP); q /= COP;
     const int ci = (int)(q % CIN_B); q /= CIN_B;
-    const int x = (int)(q % 4); q /= 4;
+    const int row = (int)(q % ROWS); q /= ROWS;
     const int kdkh = (int)(q % 9); q /= 9;
     const int ch = (int)(q % nchunks);
     const int cb = (int)(q / nchunks);
@@ -297,8 +325,13 @@ __global__ void pack_wino_kernel(const float* __restrict__ w, float* __restrict_
     float v = 0.f;
     if (co < cout && c < cin) {
       const float* g = w + (((long long)co * cin + c) * 9 + kdkh) * 3;  // [kd][kh][kw]
-      const double g0 = g[0], g1 = g[1], g2 = g[2];
-      v = x == 0 ? (float)g0 : x == 3 ? (float)g2 : x == 1 ? (float)((g0 + g1 + g2) * 0.5) : (float)((g0 - g1 + g2) * 0.5);
+      if (GW) {
+        v = g[row];
+      } else {
+        const double g0 = g[0], g1 = g[1], g2 = g[2];
+        v = row == 0 ? (float)g0 : row == 3 ? (float)g2 : row == 1 ? (float)((g0 + g1 + g2) * 0.5)
+                                                                   : (float)((g0 - g1 + g2) * 0.5);
+      }
     }
     packed[i] = v;
   }
@@ -321,7 +354,7 @@ inline Plan make_plan(int B, int cout, int D, int H, int W) {
   auto wgs = [&](int np, int td) {
     return (long long)((W + 31) / 32) * ((H + 4 * np - 1) / (4 * np)) * ((D + td - 1) / td) * B * ncob;
   };
-  p.np = (p.mt == 2 && wgs(2, 2) >= 512) ? 2 : 1;
+  p.np = (p.mt == 2 && wgs(2, 2) >= 512) ? 2 : 1;  // MT=3: two stages of 8 rows exceed the LDS
   p.td = wgs(p.np, 2) >= 384 ? 2 : 1;
   if (g_override[0] > 0) {
     p.np = g_override[0];
@@ -344,7 +377,8 @@ inline Plan make_plan(int B, int cout, int D, int H, int W) {
 #define LEA_WINO_TILES(CV)                                                                      \
   LEA_WINO_CASE(1, 1, 1, CV) LEA_WINO_CASE(1, 1, 2, CV) LEA_WINO_CASE(1, 2, 1, CV)              \
   LEA_WINO_CASE(1, 2, 2, CV) LEA_WINO_CASE(2, 1, 1, CV) LEA_WINO_CASE(2, 1, 2, CV)              \
-  LEA_WINO_CASE(2, 2, 1, CV) LEA_WINO_CASE(2, 2, 2, CV)
+  LEA_WINO_CASE(2, 2, 1, CV) LEA_WINO_CASE(2, 2, 2, CV) LEA_WINO_CASE(3, 1, 1, CV)              \
+  LEA_WINO_CASE(3, 1, 2, CV)
 
 int run(const Plan& p, ConvArgs a, int B, hipStream_t st, bool cv) {
   a.ncob = (a.cout + 16 * p.mt - 1) / (16 * p.mt);
@@ -396,7 +430,8 @@ using namespace lea;
 extern "C" size_t lea_conv3d_wino_packed_floats(int cout, int cin) {
   if (cout <= 0 || cin <= 0 || cin % wino::CIN_B != 0) return 0;
   const int cop = 16 * wino::mt_of(cout);
-  return (size_t)((cout + cop - 1) / cop) * (cin / wino::CIN_B) * 9 * 4 * wino::CIN_B * cop;
+  const int rows = wino::mt_of(cout) == 3 ? 3 : 4;
+  return (size_t)((cout + cop - 1) / cop) * (cin / wino::CIN_B) * 9 * rows * wino::CIN_B * cop;
 }
 
 extern "C" int lea_conv3d_wino_pack_weights(const float* w, float* packed, int cout, int cin,
@@ -408,10 +443,11 @@ extern "C" int lea_conv3d_wino_pack_weights(const float* w, float* packed, int c
   const long long total = (long long)lea_conv3d_wino_packed_floats(cout, cin);
   const int grid = (int)std::min<long long>((total + 255) / 256, 4096);
   hipStream_t st = as_stream(stream);
-  if (wino::mt_of(cout) == 1)
-    wino::pack_wino_kernel<1><<<grid, 256, 0, st>>>(w, packed, cout, cin, cin / wino::CIN_B, total);
-  else
-    wino::pack_wino_kernel<2><<<grid, 256, 0, st>>>(w, packed, cout, cin, cin / wino::CIN_B, total);
+  switch (wino::mt_of(cout)) {
+    case 1: wino::pack_wino_kernel<1><<<grid, 256, 0, st>>>(w, packed, cout, cin, cin / wino::CIN_B, total); break;
+    case 3: wino::pack_wino_kernel<3><<<grid, 256, 0, st>>>(w, packed, cout, cin, cin / wino::CIN_B, total); break;
+    default: wino::pack_wino_kernel<2><<<grid, 256, 0, st>>>(w, packed, cout, cin, cin / wino::CIN_B, total);
+  }
   return launch_status("lea_conv3d_wino_pack_weights");
 }
 

@@ -685,16 +685,16 @@ def wino_preferred(b, cout, cin, d, h, w) -> bool:
     Winograd wins on the large volumes when the output channels fill its 16/32-row
     blocks (stem0, stem1, conv1/2, the 16-channel L1 cells, the 8->24 L0 group);
     the direct engine keeps the small L2 volumes and the 48-channel groups (a
-    third of a 32-row block would be padding)."""
+    third of a 32-row block would be padding; they get a 48-row block)."""
     if b * d * h * w < WINO_MIN_VOXELS:
         return False
-    return cout == 16 or cout == 24 or cout % 32 == 0
+    return cout == 16 or cout == 24 or cout % 32 == 0 or cout % 48 == 0
 
 
 def wino_mfma_scale(cout: int) -> float:
     """MFMA products issued per direct-convolution product: 4 per 6 (F(2,3)), times
     the padding of cout to the engine's 16/32-row block."""
-    cop = 16 if cout <= 16 else 32
+    cop = 16 if cout <= 16 else (48 if cout % 32 != 0 and cout % 48 == 0 else 32)
     return (2.0 / 3.0) * (-(-cout // cop) * cop) / cout
 
 

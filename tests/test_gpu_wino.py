@@ -49,8 +49,10 @@ def test_wino_vs_torch(b, cin, cout, shape, mode):
 
 
 @pytest.mark.parametrize("np_,td", [(1, 1), (1, 2), (2, 1), (2, 2)])
-@pytest.mark.parametrize("cout", [16, 64])
+@pytest.mark.parametrize("cout", [16, 48, 64])
 def test_wino_every_tile(np_, td, cout):
+    if cout == 48 and np_ == 2:
+        pytest.skip("48-row blocks are instantiated with one row per wave (LDS budget)")
     lib = _lib.load()
     g = torch.Generator().manual_seed(np_ * 10 + td + cout)
     x = torch.randn((2, 32, 5, 11, 45), generator=g)
@@ -60,7 +62,8 @@ def test_wino_every_tile(np_, td, cout):
     assert lib.lea_conv3d_wino_set_tile_override(np_, td) == 0
     try:
         name = kernels.wino_kernel_name(2, cout, 5, 11, 45)
-        assert name == f"conv3d_wino_kernel<{1 if cout <= 16 else 2}, {np_}, {td}, false>", name
+        mt = {16: 1, 48: 3, 64: 2}[cout]
+        assert name == f"conv3d_wino_kernel<{mt}, {np_}, {td}, false>", name
         out = r.to(DEV).clone()
         kernels.conv3d_bnrelu_wino(x.to(DEV), kernels.pack_conv_weight_wino(w.to(DEV)), cout, None,
                                    None, relu=False, out=out, accumulate=True)
