@@ -233,13 +233,14 @@ int lea_conv2d_bnrelu_bf16(const void* x, int64_t x_bstride, const void* w_packe
                            int64_t r_bstride, void* y, int64_t y_bstride, int B, int cin, int cout,
                            int H, int W, unsigned flags, void* stream);
 
-/* ---- Winograd F(2,3)-along-W ConvBR3d, k = 3, fp32 (csrc/conv3d_wino.hip) ----
+/* ---- Winograd F(2,3) / F(4,3)-along-W ConvBR3d, k = 3, fp32 (csrc/conv3d_wino.hip) ----
  * Same operation and arguments as lea_conv3d_bnrelu / lea_conv3d_bnrelu_costvolume
  * (models/operations_3d.py:31-47, retrain/LEAStereo.py:34-48), computed as
- * y[w..w+1] = A^T[(G g) . (B^T x)] per (kd, kh): 2/3 of the direct form's MFMA
- * products, all in fp32.  Weights are packed by lea_conv3d_wino_pack_weights
- * (a layout of their own: U = G g per kw row); cin (and the first source's
- * channels, and C for the cost volume) must be multiples of 4.                 */
+ * y[w..w+F-1] = A^T[(G g) . (B^T x)] per (kd, kh): 2/3 (F = 2) or 1/2 (F = 4, on
+ * widths that fill 64-wide tile rows) of the direct form's MFMA products, all in
+ * fp32.  Weights are packed by lea_conv3d_wino_pack_weights (a layout of their own);
+ * cin (and the first source's channels, and C for the cost volume) must be
+ * multiples of 4.                                                              */
 size_t lea_conv3d_wino_packed_floats(int cout, int cin);
 int lea_conv3d_wino_pack_weights(const float* w, float* packed, int cout, int cin, void* stream);
 int lea_conv3d_bnrelu_wino(const void* x, int64_t x_bstride, const void* x2, int64_t x2_bstride,
@@ -252,11 +253,12 @@ int lea_conv3d_bnrelu_costvolume_wino(const void* left, const void* right, int64
                                       const float* shift, void* y, int64_t y_bstride, int B, int C,
                                       int cout, int D3, int H, int W, unsigned flags, int dtype,
                                       void* stream);
-/* Kernel instantiation the Winograd entries launch for this shape; tile override
- * (np in {1, 2} 32-wide rows per wave, td in {1, 2} planes; np = 0 resets) for
- * the tuning tools. */
+/* Kernel instantiation the Winograd entries launch for this shape
+ * ("conv3d_wino_kernel<F, MT, NP, TD, CV>"); tile override for the tuning tools
+ * (np in {1, 2} tile rows per wave, td in {1, 2} planes, f in {0 = planner, 2, 4};
+ * np = 0 resets). */
 const char* lea_conv3d_wino_kernel_name(int B, int cout, int D, int H, int W, int costvolume);
-int lea_conv3d_wino_set_tile_override(int np, int td);
+int lea_conv3d_wino_set_tile_override(int np, int td, int f);
 
 /* ---- host steps either side of forward ---- */
 

@@ -77,7 +77,7 @@ SIGNATURES = {
     "lea_conv3d_bnrelu_costvolume_wino": (_i, [_p, _p, _i64, _p, _p, _p, _p, _i64, _i, _i, _i,
                                                _i, _i, _i, _u, _i, _p]),
     "lea_conv3d_wino_kernel_name": (ctypes.c_char_p, [_i, _i, _i, _i, _i, _i]),
-    "lea_conv3d_wino_set_tile_override": (_i, [_i, _i]),
+    "lea_conv3d_wino_set_tile_override": (_i, [_i, _i, _i]),
     # host steps either side of forward: predict.py load_data/test_transform, metrics
     "lea_standardize_workspace_bytes": (ctypes.c_size_t, [_i]),
     "lea_standardize_crop_u8": (_i, [_p, _p, _i, _i, _i, _i, _p, _p, _i, _i, _p, _p]),

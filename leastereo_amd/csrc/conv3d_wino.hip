@@ -1,32 +1,42 @@
-// ConvBR3d k=3 (fp32) with Winograd F(2,3) along W on the fp32 matrix cores.
-// Replaces models/operations_3d.py:31-47 for the matching net's 3x3x3 layers, as
-// the direct engine (conv3d_impl.h) does, with 2/3 of its MFMA work.
+// ConvBR3d k=3 (fp32) with Winograd F(2,3) / F(4,3) along W on the fp32 matrix
+// cores.  Replaces models/operations_3d.py:31-47 for the matching net's 3x3x3
+// layers, as the direct engine (conv3d_impl.h) does, with 2/3 (F(2,3)) or 1/2
+// (F(4,3)) of its MFMA work.
 //
-// For a pair of outputs y[w], y[w+1] along W and a fixed (kd, kh):
-//     y[w + j] = sum_kw g[kw] x[w - 1 + j + kw]
-//   = A^T [ (G g) . (B^T x) ],  x = x[w-1 .. w+2],
-//     G g  = (g0, (g0+g1+g2)/2, (g0-g1+g2)/2, g2)          (packed, or formed in-kernel)
-//     B^T x = (x0 - x2, x1 + x2, x2 - x1, x1 - x3)          (4 VALU adds per lane)
-//     A^T m = (m0 + m1 + m2, m1 - m2 - m3)
-// so per 2 outputs and (kd, kh) the GEMM does 4 products instead of 6.  All of it
-// is fp32: the transforms are exact up to one rounding per add (G's halves are
-// exact), the products and sums are the MFMA's fp32.  48-cout blocks form U = G g
-// in the kernel from staged g rows (a quarter less LDS for the weight stage, which
-// keeps two workgroups per CU); 16/32-cout blocks stage the packed U.
+// For F consecutive outputs y[w .. w+F-1] along W and a fixed (kd, kh):
+//     y[w + j] = sum_kw g[kw] x[w - 1 + j + kw]  =  A^T [ (G g) . (B^T x) ],
+// x = x[w-1 .. w+F], F + 2 transform points xi.
+//   F(2,3): G g  = (g0, (g0+g1+g2)/2, (g0-g1+g2)/2, g2)
+//           B^T x = (x0 - x2, x1 + x2, x2 - x1, x1 - x3)
+//           A^T m = (m0 + m1 + m2, m1 - m2 - m3)
+//   F(4,3) (points 0, +-1, +-2, inf):
+//           G g  = (g0/4, -(g0+g1+g2)/6, -(g0-g1+g2)/6, (g0+2g1+4g2)/24, (g0-2g1+4g2)/24, g2)
+//           B^T x = (4x0-5x2+x4, -4x1-4x2+x3+x4, 4x1-4x2-x3+x4, -2x1-x2+2x3+x4,
+//                    2x1-x2-2x3+x4, 4x1-5x3+x5)
+//           A^T m = (m0+m1+m2+m3+m4, m1-m2+2(m3-m4), m1+m2+4(m3+m4), m1-m2+8(m3-m4)+m5)
+// so per F outputs and (kd, kh) the GEMM does F+2 products instead of 3F.  All of it
+// is fp32: the products and sums are the MFMA's fp32; the transforms add a few
+// roundings per value (F(4,3)'s coefficients are larger, its error a few times
+// F(2,3)'s -- both far inside the conv tolerance, tests/test_gpu_wino.py).
+// U = G g is formed in the kernel from the staged weights g (3 LDS reads and a few
+// VALU per row and step): the weight stage is 3 rows per (kd, kh) whatever F, which
+// is what keeps two workgroups per CU with F(4,3)'s wider halo.
 //
-// GEMM view per transform point xi in 0..3 and (kd, kh):
-//     M_xi[co][pair] += sum_ci U_xi[kd][kh][co][ci] * V_xi[ci][pair]
+// GEMM view per transform point xi and (kd, kh):
+//     M_xi[co][group] += sum_ci U_xi[kd][kh][co][ci] * V_xi[ci][group]
 // on v_mfma_f32_16x16x4_f32: A (lane l) = U_xi[co = 16 m + (l & 15)][ci = l >> 4],
-// B (lane l) = V_xi[ci = l >> 4][pair = l & 15] (computed by the lane from 4 staged
-// inputs, two ds_read_b64), D (lane, reg r) = M_xi[co = 16 m + 4 (l >> 4) + r][pair].
-// The epilogue applies A^T and stores the two outputs of its pair as one float2.
+// B (lane l) = V_xi[ci = l >> 4][group = l & 15] (computed by the lane from F + 2
+// staged inputs, F/2 + 1 ds_read_b64), D (lane, reg r) = M_xi[co = 16 m + 4 (l >> 4)
+// + r][group].  The epilogue applies A^T and stores the F outputs of its group as
+// one float2 / float4.
 //
-// Workgroup = 4 waves over a TH x 32 x TD output tile (TH = 4 NP rows, 16 pairs per
-// row) and COP = 16 MT output channels.  K is streamed in chunks of 4 input channels
-// (one MFMA K step): the input halo by LDS-DMA (buffer_load_dword ... lds, one
-// buffer resource per channel, out-of-range offsets return the zero padding), the
-// chunk's weights (9 x 4 (or 3) x 4 x COP floats) by global_load_lds_dwordx4;
-// two stages, one vmcnt(0) + barrier per chunk (the direct engine's pipeline).
+// Workgroup = 4 waves over a TH x 16F x TD output tile (TH = 4 NP rows, 16 groups of
+// F outputs per row) and COP = 16 MT output channels.  K is streamed in chunks of 4
+// input channels (one MFMA K step): the input halo by LDS-DMA (buffer_load_dword ...
+// lds, one buffer resource per channel, out-of-range offsets return the zero
+// padding), the chunk's weights (9 x 3 x 4 x COP floats) by global_load_lds_dwordx4;
+// two stages, one vmcnt(0) + barrier per chunk (the direct engine's pipeline); a
+// step's LDS reads are issued before the previous step's MFMAs.
 #include "conv3d_impl.h"
 
 namespace lea {
@@ -41,12 +51,14 @@ __host__ __device__ constexpr int mt_of(int cout) {
 }
 __host__ __device__ constexpr int round_32mod64(int n) { return n % 64 <= 32 ? n + (32 - n % 64) : n + (96 - n % 64); }
 
-template <int MT, int NP, int TD>
+template <int F, int MT, int NP, int TD>
 struct Cfg {
+  static constexpr int NX = F + 2;              // transform points
   static constexpr int COP = 16 * MT;
   static constexpr bool SWZ = (COP % 32) == 0;  // odd-ci rows: 16-column halves swapped
+  static constexpr int TW = 16 * F;             // outputs per tile row
   static constexpr int TH = 4 * NP;
-  static constexpr int RH = TH + 2, RW = 34;
+  static constexpr int RH = TH + 2, RW = TW + 2;
   static constexpr int PLANE = RH * RW;
   static constexpr int PLANES = TD + 2;
   static constexpr int IMG = PLANES * PLANE;
@@ -54,21 +66,18 @@ struct Cfg {
   // group read disjoint halves of the 64 banks
   static constexpr int CIS = round_32mod64(IMG);
   static constexpr int XS = CIN_B * CIS;
-  // 48-row blocks stage the plain weights g (3 rows per (kd,kh)) and form U = G g in
-  // the kernel, so two stages of two workgroups fit the LDS; 16/32-row blocks stage
-  // U (4 rows), which saves the per-step VALU (measured 1-2.5 % faster)
-  static constexpr bool GW = MT == 3;
-  static constexpr int KW_ROWS = GW ? 3 : 4;
-  static constexpr int WS = 9 * KW_ROWS * CIN_B * COP;
+  static constexpr int WS = 9 * 3 * CIN_B * COP;  // the chunk's weights g[kd,kh][kw][ci][co]
   static constexpr int STAGE = XS + WS;
   static_assert(XS % 16 == 0 && WS % 16 == 0, "16-byte aligned LDS regions");
+  static_assert(2 * STAGE * 4 * 2 <= 160 * 1024, "two double-buffered workgroups per CU");
 };
 
 __device__ __forceinline__ int a_col(int m, int ci, int n, bool swz) { return ((swz ? (m ^ (ci & 1)) : m) * 16) + n; }
 
-template <int MT, int NP, int TD, bool CV>
+template <int F, int MT, int NP, int TD, bool CV>
 __global__ __launch_bounds__(kConvThreads, 2) void conv3d_wino_kernel(const ConvArgs a) {
-  using C = Cfg<MT, NP, TD>;
+  using C = Cfg<F, MT, NP, TD>;
+  constexpr int NX = C::NX;
   constexpr int XSLOTS = (C::IMG + 63) / 64;
   constexpr int XSLOTS_W = (XSLOTS + kConvWaves - 1) / kConvWaves;
   constexpr int WSLOTS = (C::WS + 255) / 256;
@@ -88,7 +97,7 @@ __global__ __launch_bounds__(kConvThreads, 2) void conv3d_wino_kernel(const Conv
   const int tile = (lin / a.ndz) % a.ntiles;
   const int bc = lin / (a.ndz * a.ntiles);
   const int h0 = (tile / a.tiles_w) * C::TH;
-  const int w0 = (tile % a.tiles_w) * 32;
+  const int w0 = (tile % a.tiles_w) * C::TW;
   const int d0 = dz * TD;
   const int b = bc / a.ncob;
   const int cob = bc - b * a.ncob;
@@ -162,9 +171,9 @@ __global__ __launch_bounds__(kConvThreads, 2) void conv3d_wino_kernel(const Conv
   };
 
   const int ci = lane >> 4, p = lane & 15;
-  int xoff[NP];  // staged input column 2p (w0 + 2p - 1) of row (wave NP + j), channel ci
+  int xoff[NP];  // staged input column F*p (w0 + F p - 1) of row (wave NP + j), channel ci
 #pragma unroll
-  for (int j = 0; j < NP; ++j) xoff[j] = ci * C::CIS + (wave * NP + j) * C::RW + 2 * p;
+  for (int j = 0; j < NP; ++j) xoff[j] = ci * C::CIS + (wave * NP + j) * C::RW + F * p;
   int woff[MT];
 #pragma unroll
   for (int m = 0; m < MT; ++m) woff[m] = ci * C::COP + a_col(m, ci, p, C::SWZ);
@@ -181,9 +190,9 @@ __global__ __launch_bounds__(kConvThreads, 2) void conv3d_wino_kernel(const Conv
       sh[m][r] = (cv && a.shift) ? a.shift[co] : 0.f;
     }
 
-  f32x4 acc[4][TD][MT][NP];
+  f32x4 acc[NX][TD][MT][NP];
 #pragma unroll
-  for (int x = 0; x < 4; ++x)
+  for (int x = 0; x < NX; ++x)
 #pragma unroll
     for (int t = 0; t < TD; ++t)
 #pragma unroll
@@ -198,59 +207,92 @@ __global__ __launch_bounds__(kConvThreads, 2) void conv3d_wino_kernel(const Conv
     if (ch + 1 < nchunks) issue(ch + 1, smem + ((ch + 1) & 1) * C::STAGE);
     const float* xs = smem + (ch & 1) * C::STAGE;
     const float* ws = xs + C::XS;
+    // one (kd, kh) step: raw inputs (F + 2 per lane as float2s) and weight rows g
+    struct StepOps {
+      float2 x2[TD][NP][F / 2 + 1];
+      float g[3][MT];
+    };
+    auto load_step = [&](int step, StepOps& o) {
+      const int kd = step / 3, kh = step % 3;
 #pragma unroll
-    for (int kd = 0; kd < 3; ++kd) {
+      for (int t = 0; t < TD; ++t)
 #pragma unroll
-      for (int kh = 0; kh < 3; ++kh) {
-        float vb[TD][NP][4];
+        for (int j = 0; j < NP; ++j) {
+          const float* sp = xs + xoff[j] + (t + kd) * C::PLANE + kh * C::RW;
+#pragma unroll
+          for (int q = 0; q <= F / 2; ++q) o.x2[t][j][q] = *reinterpret_cast<const float2*>(sp + 2 * q);
+        }
+      const float* wk = ws + step * 3 * CIN_B * C::COP;
+#pragma unroll
+      for (int m = 0; m < MT; ++m)
+#pragma unroll
+        for (int r = 0; r < 3; ++r) o.g[r][m] = wk[r * CIN_B * C::COP + woff[m]];
+    };
+    StepOps ops[2];
+    load_step(0, ops[0]);
+#pragma unroll
+    for (int step = 0; step < 9; ++step) {
+      if (step + 1 < 9) load_step(step + 1, ops[(step + 1) & 1]);
+      const StepOps& o = ops[step & 1];
+      float vb[TD][NP][NX];
+#pragma unroll
+      for (int t = 0; t < TD; ++t)
+#pragma unroll
+        for (int j = 0; j < NP; ++j) {
+          const float x0 = o.x2[t][j][0].x, x1 = o.x2[t][j][0].y, x2 = o.x2[t][j][1].x, x3 = o.x2[t][j][1].y;
+          if constexpr (F == 2) {
+            vb[t][j][0] = x0 - x2;
+            vb[t][j][1] = x1 + x2;
+            vb[t][j][2] = x2 - x1;
+            vb[t][j][3] = x1 - x3;
+          } else {
+            const float x4 = o.x2[t][j][F / 2].x, x5 = o.x2[t][j][F / 2].y;
+            const float pa = fmaf(-4.f, x2, x4), pb = fmaf(-4.f, x1, x3);
+            const float pc = x4 - x2, pd = 2.f * (x3 - x1);
+            vb[t][j][0] = fmaf(4.f, x0, fmaf(-5.f, x2, x4));
+            vb[t][j][1] = pa + pb;
+            vb[t][j][2] = pa - pb;
+            vb[t][j][3] = pc + pd;
+            vb[t][j][4] = pc - pd;
+            vb[t][j][NX - 1] = fmaf(4.f, x1, fmaf(-5.f, x3, x5));
+          }
+        }
+      float u[NX][MT];
+#pragma unroll
+      for (int m = 0; m < MT; ++m) {
+        const float g0 = o.g[0][m], g1 = o.g[1][m], g2 = o.g[2][m];
+        if constexpr (F == 2) {
+          const float s = g0 + g2;
+          u[0][m] = g0;
+          u[1][m] = (s + g1) * 0.5f;
+          u[2][m] = (s - g1) * 0.5f;
+          u[3][m] = g2;
+        } else {
+          const float s = g0 + g2, s4 = fmaf(4.f, g2, g0), t2 = 2.f * g1;
+          u[0][m] = 0.25f * g0;
+          u[1][m] = (s + g1) * (-1.f / 6.f);
+          u[2][m] = (s - g1) * (-1.f / 6.f);
+          u[3][m] = (s4 + t2) * (1.f / 24.f);
+          u[4][m] = (s4 - t2) * (1.f / 24.f);
+          u[NX - 1][m] = g2;
+        }
+      }
+#pragma unroll
+      for (int x = 0; x < NX; ++x)
 #pragma unroll
         for (int t = 0; t < TD; ++t)
 #pragma unroll
-          for (int j = 0; j < NP; ++j) {
-            const float* s = xs + xoff[j] + (t + kd) * C::PLANE + kh * C::RW;
-            const float2 lo = *reinterpret_cast<const float2*>(s);
-            const float2 hi = *reinterpret_cast<const float2*>(s + 2);
-            vb[t][j][0] = lo.x - hi.x;
-            vb[t][j][1] = lo.y + hi.x;
-            vb[t][j][2] = hi.x - lo.y;
-            vb[t][j][3] = lo.y - hi.y;
-          }
-        const float* wk = ws + (kd * 3 + kh) * C::KW_ROWS * CIN_B * C::COP;
-        float u[4][MT];
+          for (int m = 0; m < MT; ++m)
 #pragma unroll
-        for (int m = 0; m < MT; ++m) {
-          if constexpr (C::GW) {  // U = G g of this lane's kw row (exact halves)
-            const float g0 = wk[woff[m]], g1 = wk[CIN_B * C::COP + woff[m]];
-            const float g2 = wk[2 * CIN_B * C::COP + woff[m]];
-            const float t = g0 + g2;
-            u[0][m] = g0;
-            u[1][m] = (t + g1) * 0.5f;
-            u[2][m] = (t - g1) * 0.5f;
-            u[3][m] = g2;
-          } else {
-#pragma unroll
-            for (int x = 0; x < 4; ++x) u[x][m] = wk[x * CIN_B * C::COP + woff[m]];
-          }
-        }
-#pragma unroll
-        for (int x = 0; x < 4; ++x) {
-          const float (&av)[MT] = u[x];
-#pragma unroll
-          for (int t = 0; t < TD; ++t)
-#pragma unroll
-            for (int m = 0; m < MT; ++m)
-#pragma unroll
-              for (int j = 0; j < NP; ++j)
-                acc[x][t][m][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[m], vb[t][j][x], acc[x][t][m][j], 0, 0, 0);
-        }
-      }
+            for (int j = 0; j < NP; ++j)
+              acc[x][t][m][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(u[x][m], vb[t][j][x], acc[x][t][m][j], 0, 0, 0);
     }
   }
 
-  // epilogue: A^T, folded BN, ReLU, residual; lane stores outputs (w0+2p, w0+2p+1)
+  // epilogue: A^T, folded BN, ReLU, residual; lane stores outputs w0 + F p .. + F - 1
   const bool relu = a.flags & LEA_RELU, resid = a.flags & LEA_RESIDUAL;
   const long long DHW = (long long)HW * a.D;
-  const int w = w0 + 2 * p;
+  const int w = w0 + F * p;
 #pragma unroll
   for (int t = 0; t < TD; ++t) {
     const int d = d0 + t;
@@ -258,63 +300,82 @@ __global__ __launch_bounds__(kConvThreads, 2) void conv3d_wino_kernel(const Conv
     for (int j = 0; j < NP; ++j) {
       const int h = h0 + wave * NP + j;
       if (d >= a.D || h >= a.H || w >= a.W) continue;
-      const bool two = w + 1 < a.W;
+      const int nv = min(F, a.W - w);  // valid outputs of this group
 #pragma unroll
       for (int m = 0; m < MT; ++m)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int co = co0 + 16 * m + 4 * ci + r;
           if (co >= a.cout) continue;
-          const float m0 = acc[0][t][m][j][r], m1 = acc[1][t][m][j][r];
-          const float m2 = acc[2][t][m][j][r], m3 = acc[3][t][m][j][r];
-          float y0 = (m0 + m1) + m2;
-          float y1 = (m1 - m2) - m3;
-          y0 = y0 * sc[m][r] + sh[m][r];
-          y1 = y1 * sc[m][r] + sh[m][r];
-          if (relu) {
-            y0 = fmaxf(y0, 0.f);
-            y1 = fmaxf(y1, 0.f);
+          float y[F];
+          if constexpr (F == 2) {
+            const float m0 = acc[0][t][m][j][r], m1 = acc[1][t][m][j][r];
+            const float m2 = acc[2][t][m][j][r], m3 = acc[3][t][m][j][r];
+            y[0] = (m0 + m1) + m2;
+            y[1] = (m1 - m2) - m3;
+          } else {
+            const float m0 = acc[0][t][m][j][r], m1 = acc[1][t][m][j][r], m2 = acc[2][t][m][j][r];
+            const float m3 = acc[3][t][m][j][r], m4 = acc[4][t][m][j][r], m5 = acc[NX - 1][t][m][j][r];
+            const float sp = m1 + m2, sm = m1 - m2, tp = m3 + m4, tm = m3 - m4;
+            y[0] = (m0 + sp) + tp;
+            y[1] = fmaf(2.f, tm, sm);
+            y[F / 2] = fmaf(4.f, tp, sp);
+            y[F - 1] = fmaf(8.f, tm, sm) + m5;
+          }
+#pragma unroll
+          for (int e = 0; e < F; ++e) {
+            y[e] = y[e] * sc[m][r] + sh[m][r];
+            if (relu) y[e] = fmaxf(y[e], 0.f);
           }
           const long long o = (long long)co * DHW + (long long)d * HW + (long long)h * a.W + w;
           float* yp = a.y + (long long)b * a.ybs + o;
           const float* rp = a.res + (long long)b * a.rbs + o;
-          const bool vec = two && ((reinterpret_cast<uintptr_t>(yp) | (resid ? reinterpret_cast<uintptr_t>(rp) : 0)) & 7) == 0;
+          const bool vec = nv == F &&
+              ((reinterpret_cast<uintptr_t>(yp) | (resid ? reinterpret_cast<uintptr_t>(rp) : 0)) & (4 * F - 1)) == 0;
           if (vec) {
-            if (resid) {
-              const float2 rv = *reinterpret_cast<const float2*>(rp);
-              y0 += rv.x;
-              y1 += rv.y;
+            if constexpr (F == 2) {
+              if (resid) {
+                const float2 rv = *reinterpret_cast<const float2*>(rp);
+                y[0] += rv.x;
+                y[1] += rv.y;
+              }
+              *reinterpret_cast<float2*>(yp) = make_float2(y[0], y[1]);
+            } else {
+              if (resid) {
+                const float4 rv = *reinterpret_cast<const float4*>(rp);
+                y[0] += rv.x;
+                y[1] += rv.y;
+                y[F / 2] += rv.z;
+                y[F - 1] += rv.w;
+              }
+              *reinterpret_cast<float4*>(yp) = make_float4(y[0], y[1], y[F / 2], y[F - 1]);
             }
-            *reinterpret_cast<float2*>(yp) = make_float2(y0, y1);
           } else {
-            if (resid) y0 += rp[0];
-            yp[0] = y0;
-            if (two) {
-              if (resid) y1 += rp[1];
-              yp[1] = y1;
-            }
+#pragma unroll
+            for (int e = 0; e < F; ++e)
+              if (e < nv) {
+                if (resid) y[e] += rp[e];
+                yp[e] = y[e];
+              }
           }
         }
     }
   }
 }
 
-// weights [cout][cin][3][3][3] -> per (cout block, chunk): [kd*3+kh][row][ci][COP col],
-// rows = U_xi = (G g)_xi (computed in double, rounded once) for 16/32-row blocks,
-// rows = g[kw] for 48-row blocks (the kernel forms U)
+// weights [cout][cin][3][3][3] -> per (cout block, chunk): [kd*3+kh][kw][ci][COP col]
+// (the kernel forms U = G g from each staged kw row)
 template <int MT>
 __global__ void pack_wino_kernel(const float* __restrict__ w, float* __restrict__ packed, int cout,
                                  int cin, int nchunks, long long total) {
   constexpr int COP = 16 * MT;
   constexpr bool SWZ = (COP % 32) == 0;
-  constexpr bool GW = MT == 3;
-  constexpr int ROWS = GW ? 3 : 4;
   for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
        i += (long long)gridDim.x * blockDim.x) {
     long long q = i;
     const int col = (int)(q % COP); q /= COP;
     const int ci = (int)(q % CIN_B); q /= CIN_B;
-    const int row = (int)(q % ROWS); q /= ROWS;
+    const int kw = (int)(q % 3); q /= 3;
     const int kdkh = (int)(q % 9); q /= 9;
     const int ch = (int)(q % nchunks);
     const int cb = (int)(q / nchunks);
@@ -322,63 +383,56 @@ __global__ void pack_wino_kernel(const float* __restrict__ w, float* __restrict_
     const int m = SWZ ? (mm ^ (ci & 1)) : mm;
     const int co = cb * COP + 16 * m + n;
     const int c = ch * CIN_B + ci;
-    float v = 0.f;
-    if (co < cout && c < cin) {
-      const float* g = w + (((long long)co * cin + c) * 9 + kdkh) * 3;  // [kd][kh][kw]
-      if (GW) {
-        v = g[row];
-      } else {
-        const double g0 = g[0], g1 = g[1], g2 = g[2];
-        v = row == 0 ? (float)g0 : row == 3 ? (float)g2 : row == 1 ? (float)((g0 + g1 + g2) * 0.5)
-                                                                   : (float)((g0 - g1 + g2) * 0.5);
-      }
-    }
-    packed[i] = v;
+    packed[i] = (co < cout && c < cin) ? w[(((long long)co * cin + c) * 9 + kdkh) * 3 + kw] : 0.f;
   }
 }
 
 struct Plan {
-  int mt, np, td;
+  int f, mt, np, td;
 };
 
-thread_local int g_override[2] = {0, 0};  // np, td (lea_conv3d_wino_set_tile_override)
+thread_local int g_override[3] = {0, 0, 0};  // np, td, f (lea_conv3d_wino_set_tile_override)
 
 inline Plan make_plan(int B, int cout, int D, int H, int W) {
-  // r01 sweep (tools/wino_sweep.py, profiles/r01_wino_sweep.txt): 8-row x 2-plane
-  // tiles for the 32-channel blocks (stem0/stem1/conv1/conv2: 0.72-0.81x the
-  // direct engine's time), 4 x 2 for the 16-channel cells; single planes only when
-  // the volume is too shallow to fill the chip.
+  // r01 sweeps (tools/wino_sweep.py, profiles/r01_wino_sweep*.txt): F(4,3) where
+  // 64-wide tile rows waste little of W (the L0 volumes), else F(2,3); 8-row x
+  // 2-plane F(2,3) tiles for the 32-channel blocks, 4 x 2 for the 16/48-channel
+  // ones; single planes only when the volume is too shallow to fill the chip.
   Plan p;
   p.mt = mt_of(cout);
   const long long ncob = (cout + 16 * p.mt - 1) / (16 * p.mt);
+  p.f = (p.mt != 3 && (W + 63) / 64 * 64 * 10 <= W * 11) ? 4 : 2;
   auto wgs = [&](int np, int td) {
-    return (long long)((W + 31) / 32) * ((H + 4 * np - 1) / (4 * np)) * ((D + td - 1) / td) * B * ncob;
+    const int tw = 16 * p.f;
+    return (long long)((W + tw - 1) / tw) * ((H + 4 * np - 1) / (4 * np)) * ((D + td - 1) / td) * B * ncob;
   };
-  p.np = (p.mt == 2 && wgs(2, 2) >= 512) ? 2 : 1;  // MT=3: two stages of 8 rows exceed the LDS
+  p.np = (p.f == 2 && p.mt == 2 && wgs(2, 2) >= 512) ? 2 : 1;
   p.td = wgs(p.np, 2) >= 384 ? 2 : 1;
   if (g_override[0] > 0) {
     p.np = g_override[0];
     p.td = g_override[1];
+    if (g_override[2] > 0) p.f = g_override[2];
   }
   return p;
 }
 
-#define LEA_WINO_CASE(MT, NP, TD, CV)                                                   \
-  if (p.mt == MT && p.np == NP && p.td == TD) {                                         \
-    a.tiles_w = (a.W + 31) / 32;                                                        \
-    a.ntiles = a.tiles_w * ((a.H + 4 * NP - 1) / (4 * NP));                             \
-    a.ndz = (a.D + TD - 1) / TD;                                                        \
-    const long long n_ = (long long)a.ntiles * a.ndz * B * a.ncob;                      \
-    LEA_CHECK_ARG(n_ < (1LL << 31), "lea_conv3d(wino): grid too large");                \
-    a.nblk = (int)n_;                                                                   \
-    conv3d_wino_kernel<MT, NP, TD, CV><<<dim3((unsigned)n_), kConvThreads, 0, st>>>(a); \
-    return launch_status("lea_conv3d(wino)");                                          \
+#define LEA_WINO_CASE(F, MT, NP, TD, CV)                                                   \
+  if (p.f == F && p.mt == MT && p.np == NP && p.td == TD) {                                \
+    a.tiles_w = (a.W + 16 * F - 1) / (16 * F);                                             \
+    a.ntiles = a.tiles_w * ((a.H + 4 * NP - 1) / (4 * NP));                                \
+    a.ndz = (a.D + TD - 1) / TD;                                                           \
+    const long long n_ = (long long)a.ntiles * a.ndz * B * a.ncob;                         \
+    LEA_CHECK_ARG(n_ < (1LL << 31), "lea_conv3d(wino): grid too large");                   \
+    a.nblk = (int)n_;                                                                      \
+    conv3d_wino_kernel<F, MT, NP, TD, CV><<<dim3((unsigned)n_), kConvThreads, 0, st>>>(a); \
+    return launch_status("lea_conv3d(wino)");                                             \
   }
-#define LEA_WINO_TILES(CV)                                                                      \
-  LEA_WINO_CASE(1, 1, 1, CV) LEA_WINO_CASE(1, 1, 2, CV) LEA_WINO_CASE(1, 2, 1, CV)              \
-  LEA_WINO_CASE(1, 2, 2, CV) LEA_WINO_CASE(2, 1, 1, CV) LEA_WINO_CASE(2, 1, 2, CV)              \
-  LEA_WINO_CASE(2, 2, 1, CV) LEA_WINO_CASE(2, 2, 2, CV) LEA_WINO_CASE(3, 1, 1, CV)              \
-  LEA_WINO_CASE(3, 1, 2, CV)
+#define LEA_WINO_TILES(CV)                                                                            \
+  LEA_WINO_CASE(2, 1, 1, 1, CV) LEA_WINO_CASE(2, 1, 1, 2, CV) LEA_WINO_CASE(2, 1, 2, 1, CV)           \
+  LEA_WINO_CASE(2, 1, 2, 2, CV) LEA_WINO_CASE(2, 2, 1, 1, CV) LEA_WINO_CASE(2, 2, 1, 2, CV)           \
+  LEA_WINO_CASE(2, 2, 2, 1, CV) LEA_WINO_CASE(2, 2, 2, 2, CV) LEA_WINO_CASE(2, 3, 1, 1, CV)           \
+  LEA_WINO_CASE(2, 3, 1, 2, CV) LEA_WINO_CASE(4, 1, 1, 1, CV) LEA_WINO_CASE(4, 1, 1, 2, CV)           \
+  LEA_WINO_CASE(4, 2, 1, 1, CV) LEA_WINO_CASE(4, 2, 1, 2, CV)
 
 int run(const Plan& p, ConvArgs a, int B, hipStream_t st, bool cv) {
   a.ncob = (a.cout + 16 * p.mt - 1) / (16 * p.mt);
@@ -387,14 +441,14 @@ int run(const Plan& p, ConvArgs a, int B, hipStream_t st, bool cv) {
   } else {
     LEA_WINO_TILES(false)
   }
-  set_error("lea_conv3d(wino): no tile mt=%d np=%d td=%d", p.mt, p.np, p.td);
+  set_error("lea_conv3d(wino): no tile f=%d mt=%d np=%d td=%d", p.f, p.mt, p.np, p.td);
   return LEA_E_UNSUPPORTED;
 }
 
 thread_local char g_name[96];
 
 const char* name(const Plan& p, bool cv) {
-  snprintf(g_name, sizeof(g_name), "conv3d_wino_kernel<%d, %d, %d, %s>", p.mt, p.np, p.td,
+  snprintf(g_name, sizeof(g_name), "conv3d_wino_kernel<%d, %d, %d, %d, %s>", p.f, p.mt, p.np, p.td,
            cv ? "true" : "false");
   return g_name;
 }
@@ -411,7 +465,7 @@ int common(ConvArgs& a, int B, bool cv, int dtype, void* stream) {
                 "lea_conv3d(wino): input channels (%d, first source %d) must be multiples of %d",
                 a.cin, a.cin1, CIN_B);
   LEA_CHECK_ARG((long long)a.D * a.H * a.W * 4 < (1LL << 32) &&
-                    (long long)(a.cout + 31) * a.D * a.H * a.W < (1LL << 31),
+                    (long long)(a.cout + 47) * a.D * a.H * a.W < (1LL << 31),
                 "lea_conv3d(wino): volume too large");
   LEA_CHECK_ARG(a.x != a.y && a.x2 != a.y, "lea_conv3d(wino): input aliases output");
   if (dtype != LEA_F32) {
@@ -430,8 +484,7 @@ using namespace lea;
 extern "C" size_t lea_conv3d_wino_packed_floats(int cout, int cin) {
   if (cout <= 0 || cin <= 0 || cin % wino::CIN_B != 0) return 0;
   const int cop = 16 * wino::mt_of(cout);
-  const int rows = wino::mt_of(cout) == 3 ? 3 : 4;
-  return (size_t)((cout + cop - 1) / cop) * (cin / wino::CIN_B) * 9 * rows * wino::CIN_B * cop;
+  return (size_t)((cout + cop - 1) / cop) * (cin / wino::CIN_B) * 9 * 3 * wino::CIN_B * cop;
 }
 
 extern "C" int lea_conv3d_wino_pack_weights(const float* w, float* packed, int cout, int cin,
@@ -456,16 +509,17 @@ extern "C" const char* lea_conv3d_wino_kernel_name(int B, int cout, int D, int H
   return wino::name(wino::make_plan(B, cout, D, H, W), costvolume != 0);
 }
 
-extern "C" int lea_conv3d_wino_set_tile_override(int np, int td) {
+extern "C" int lea_conv3d_wino_set_tile_override(int np, int td, int f) {
   clear_error();
   if (np <= 0) {
     wino::g_override[0] = 0;
     return 0;
   }
-  LEA_CHECK_ARG((np == 1 || np == 2) && (td == 1 || td == 2),
-                "lea_conv3d_wino_set_tile_override: bad tile np=%d td=%d", np, td);
+  LEA_CHECK_ARG((np == 1 || np == 2) && (td == 1 || td == 2) && (f == 0 || f == 2 || f == 4),
+                "lea_conv3d_wino_set_tile_override: bad tile np=%d td=%d f=%d", np, td, f);
   wino::g_override[0] = np;
   wino::g_override[1] = td;
+  wino::g_override[2] = f;
   return 0;
 }
 

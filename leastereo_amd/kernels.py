@@ -691,11 +691,13 @@ def wino_preferred(b, cout, cin, d, h, w) -> bool:
     return cout == 16 or cout == 24 or cout % 32 == 0 or cout % 48 == 0
 
 
-def wino_mfma_scale(cout: int) -> float:
-    """MFMA products issued per direct-convolution product: 4 per 6 (F(2,3)), times
-    the padding of cout to the engine's 16/32-row block."""
+def wino_mfma_scale(cout: int, name: str) -> float:
+    """MFMA products issued per direct-convolution product: (F + 2) per 3F for the
+    kernel's F (first template argument of ``name``), times the padding of cout to
+    the engine's 16/32/48-row block."""
+    f = int(name.split("<", 1)[1].split(",", 1)[0])
     cop = 16 if cout <= 16 else (48 if cout % 32 != 0 and cout % 48 == 0 else 32)
-    return (2.0 / 3.0) * (-(-cout // cop) * cop) / cout
+    return (f + 2) / (3.0 * f) * (-(-cout // cop) * cop) / cout
 
 
 def wino_kernel_name(b, cout, d, h, w, costvolume=False):
@@ -739,8 +741,9 @@ def conv3d_bnrelu_wino(x: torch.Tensor, packed: torch.Tensor, cout: int,
     out, ybs = _conv_out(x.shape, cout, (d, h, w), out, accumulate, x.device, x.dtype)
     rptr, rbs = _residual(out, accumulate, residual, ybs)
     flags = (LEA_RELU if relu else 0) | (LEA_RESIDUAL if rptr is not None else 0)
+    name = wino_kernel_name(b, cout, d, h, w)
     rec = _probe_begin(b, cin + cin2, cout, d, h, w, 3, rptr is not None, b * d * h * w, False,
-                       name=wino_kernel_name(b, cout, d, h, w), mfma_scale=wino_mfma_scale(cout))
+                       name=name, mfma_scale=wino_mfma_scale(cout, name))
     check(_lib.load().lea_conv3d_bnrelu_wino(
         x.data_ptr(), xbs, x2.data_ptr() if x2 is not None else None, x2bs, cin2,
         packed.data_ptr(),
@@ -765,8 +768,9 @@ def conv3d_bnrelu_costvolume_wino(fl: torch.Tensor, fr: torch.Tensor, maxdisp: i
     b, c, h, w = fl.shape
     d3 = int(maxdisp / 3)
     out = torch.empty((b, cout, d3, h, w), device=fl.device, dtype=fl.dtype)
+    name = wino_kernel_name(b, cout, d3, h, w, True)
     rec = _probe_begin(b, 2 * c, cout, d3, h, w, 3, False, 0, False,
-                       name=wino_kernel_name(b, cout, d3, h, w, True), mfma_scale=wino_mfma_scale(cout))
+                       name=name, mfma_scale=wino_mfma_scale(cout, name))
     check(_lib.load().lea_conv3d_bnrelu_costvolume_wino(
         fl.data_ptr(), fr.data_ptr(), fl.stride(0), packed.data_ptr(),
         scale.data_ptr() if scale is not None else None,

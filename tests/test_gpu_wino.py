@@ -27,7 +27,8 @@ def _ref(x, w, scale, shift, relu, res=None):
 
 
 @pytest.mark.parametrize("b,cin,cout,shape,mode", [
-    (1, 64, 32, (6, 20, 70), None), (2, 128, 64, (5, 9, 40), "acc"), (1, 16, 16, (7, 33, 17), "acc"),
+    (1, 64, 32, (6, 20, 70), None), (1, 32, 32, (5, 9, 320), "acc"), (2, 8, 24, (3, 7, 130), "res"),
+    (1, 16, 16, (4, 5, 127), "acc"), (2, 128, 64, (5, 9, 40), "acc"), (1, 16, 16, (7, 33, 17), "acc"),
     (1, 16, 48, (4, 9, 40), None), (1, 32, 96, (3, 6, 21), "res"), (1, 8, 24, (3, 10, 17), None),
     (1, 12, 20, (3, 4, 5), "acc"), (2, 32, 32, (9, 13, 31), "res"), (1, 4, 12, (1, 1, 1), None),
     (1, 32, 32, (2, 3, 2), "acc")])
@@ -48,27 +49,32 @@ def test_wino_vs_torch(b, cin, cout, shape, mode):
     np.testing.assert_allclose(y.cpu().double().numpy(), want.numpy(), rtol=1e-4, atol=1e-4)
 
 
+@pytest.mark.parametrize("f", [2, 4])
 @pytest.mark.parametrize("np_,td", [(1, 1), (1, 2), (2, 1), (2, 2)])
 @pytest.mark.parametrize("cout", [16, 48, 64])
-def test_wino_every_tile(np_, td, cout):
-    if cout == 48 and np_ == 2:
-        pytest.skip("48-row blocks are instantiated with one row per wave (LDS budget)")
+def test_wino_every_tile(np_, td, cout, f):
+    """Every instantiated (F, rows, planes) tile on a ragged volume (W = 45: a partial
+    last group of outputs for both F) with the accumulate epilogue."""
+    if np_ == 2 and (cout == 48 or f == 4):
+        pytest.skip("48-row blocks and F(4,3) tiles are instantiated with one row per wave (LDS budget)")
+    if cout == 48 and f == 4:
+        pytest.skip("48-row blocks run F(2,3) only")
     lib = _lib.load()
     g = torch.Generator().manual_seed(np_ * 10 + td + cout)
     x = torch.randn((2, 32, 5, 11, 45), generator=g)
     w = torch.randn(cout, 32, 3, 3, 3, generator=g) / np.sqrt(32 * 27)
     r = torch.randn((2, cout, 5, 11, 45), generator=g)
     want = _ref(x, w, None, None, False, r)
-    assert lib.lea_conv3d_wino_set_tile_override(np_, td) == 0
+    assert lib.lea_conv3d_wino_set_tile_override(np_, td, f) == 0
     try:
         name = kernels.wino_kernel_name(2, cout, 5, 11, 45)
         mt = {16: 1, 48: 3, 64: 2}[cout]
-        assert name == f"conv3d_wino_kernel<{mt}, {np_}, {td}, false>", name
+        assert name == f"conv3d_wino_kernel<{f}, {mt}, {np_}, {td}, false>", name
         out = r.to(DEV).clone()
         kernels.conv3d_bnrelu_wino(x.to(DEV), kernels.pack_conv_weight_wino(w.to(DEV)), cout, None,
                                    None, relu=False, out=out, accumulate=True)
     finally:
-        lib.lea_conv3d_wino_set_tile_override(0, 0)
+        lib.lea_conv3d_wino_set_tile_override(0, 0, 0)
     np.testing.assert_allclose(out.cpu().double().numpy(), want.numpy(), rtol=1e-4, atol=1e-4)
 
 

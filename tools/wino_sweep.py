@@ -33,12 +33,13 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--batch", type=int, default=1)
+    ap.add_argument("--only", default="")
     a = ap.parse_args()
     lib = _lib.load()
     dev = "cuda"
     out = {}
     for name, (cin, cout, k, (d, h, w), count, *acc) in LAYERS.items():
-        if k != 3 or not kernels.wino_eligible(cout, cin, k):
+        if k != 3 or not kernels.wino_eligible(cout, cin, k) or (a.only and name not in a.only.split(",")):
             continue
         acc = bool(acc and acc[0])
         x = torch.randn(a.batch, cin, d, h, w, device=dev)
@@ -50,15 +51,15 @@ def main():
         pd, pw = kernels.pack_conv_weight(wt), kernels.pack_conv_weight_wino(wt)
         res = {"direct": timed(lambda: kernels.conv3d_bnrelu(x, pd, cout, 3, scale, shift, True, y, acc),
                                a.iters)}
-        for np_ in (1, 2):
-            for td in (1, 2):
-                lib.lea_conv3d_wino_set_tile_override(np_, td)
+        for f, np_, td in [(f, n, t) for f in (2, 4) for n in (1, 2) for t in (1, 2)]:
+            if True:
+                lib.lea_conv3d_wino_set_tile_override(np_, td, f)
                 try:
-                    res[f"wino np={np_} td={td}"] = timed(
+                    res[f"wino f={f} np={np_} td={td}"] = timed(
                         lambda: kernels.conv3d_bnrelu_wino(x, pw, cout, scale, shift, True, y, acc), a.iters)
                 except _lib.HipKernelError:
                     pass  # tile not instantiated for this block size
-        lib.lea_conv3d_wino_set_tile_override(0, 0)
+        lib.lea_conv3d_wino_set_tile_override(0, 0, 0)
         res["wino default"] = timed(lambda: kernels.conv3d_bnrelu_wino(x, pw, cout, scale, shift, True, y, acc),
                                     a.iters)
         default = kernels.wino_kernel_name(a.batch, cout, d, h, w)
