@@ -254,9 +254,9 @@ int lea_conv3d_bnrelu_costvolume_wino(const void* left, const void* right, int64
                                       int cout, int D3, int H, int W, unsigned flags, int dtype,
                                       void* stream);
 /* Kernel instantiation the Winograd entries launch for this shape
- * ("conv3d_wino_kernel<F, MT, NP, TD, CV>"); tile override for the tuning tools
- * (np in {1, 2} tile rows per wave, td in {1, 2} planes, f in {0 = planner, 2, 4};
- * np = 0 resets). */
+ * ("conv3d_wino_kernel<F, Q, MT, NP, TD, CV>"); tile override for the tuning tools
+ * (np in {1, 2} tile rows per wave, td in {1, 2} planes, f in {0 = planner, 2, 4,
+ * 8 = F(4,3) on 32-wide row pairs}; np = 0 resets). */
 const char* lea_conv3d_wino_kernel_name(int B, int cout, int D, int H, int W, int costvolume);
 int lea_conv3d_wino_set_tile_override(int np, int td, int f);
 

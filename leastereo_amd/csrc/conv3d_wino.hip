@@ -30,8 +30,9 @@
 // + r][group].  The epilogue applies A^T and stores the F outputs of its group as
 // one float2 / float4.
 //
-// Workgroup = 4 waves over a TH x 16F x TD output tile (TH = 4 NP rows, 16 groups of
-// F outputs per row) and COP = 16 MT output channels.  K is streamed in chunks of 4
+// Workgroup = 4 waves over a TH x F Q x TD output tile (a lane group of 16 covers
+// 16/Q rows of Q groups of F outputs; TH = 4 NP 16/Q rows) and COP = 16 MT output
+// channels.  K is streamed in chunks of 4
 // input channels (one MFMA K step): the input halo by LDS-DMA (buffer_load_dword ...
 // lds, one buffer resource per channel, out-of-range offsets return the zero
 // padding), the chunk's weights (9 x 3 x 4 x COP floats) by global_load_lds_dwordx4;
@@ -49,34 +50,56 @@ constexpr int CIN_B = 4;
 __host__ __device__ constexpr int mt_of(int cout) {
   return cout <= 16 ? 1 : (cout % 32 != 0 && cout % 48 == 0) ? 3 : 2;
 }
-__host__ __device__ constexpr int round_32mod64(int n) { return n % 64 <= 32 ? n + (32 - n % 64) : n + (96 - n % 64); }
 
-template <int F, int MT, int NP, int TD>
+// Lane group (16 lanes of one input channel) -> output groups: Q groups of F outputs
+// per tile row and 16/Q rows (Q = 8 lets F(4,3) tile a 32-wide row pair).
+template <int F, int Q>
+__host__ __device__ constexpr int lane_dword(int lane, int cis, int rw) {
+  return (lane >> 4) * cis + ((lane & 15) / Q) * rw + F * ((lane & 15) % Q);
+}
+// The two channels of a 32-lane ds_read_b64 group must hit disjoint banks: pick the
+// smallest even channel stride >= img for which the first read's 64 dwords of lanes
+// 0..31 fall on 64 distinct banks.
+template <int F, int Q>
+__host__ __device__ constexpr int conflict_free_cis(int img, int rw) {
+  for (int cis = img + (img & 1);; cis += 2) {
+    bool used[64] = {};
+    bool ok = true;
+    for (int l = 0; l < 32 && ok; ++l)
+      for (int k = 0; k < 2 && ok; ++k) {
+        const int bank = (lane_dword<F, Q>(l, cis, rw) + k) % 64;
+        ok = !used[bank];
+        used[bank] = true;
+      }
+    if (ok) return cis;
+  }
+}
+
+template <int F, int Q, int MT, int NP, int TD>
 struct Cfg {
   static constexpr int NX = F + 2;              // transform points
   static constexpr int COP = 16 * MT;
   static constexpr bool SWZ = (COP % 32) == 0;  // odd-ci rows: 16-column halves swapped
-  static constexpr int TW = 16 * F;             // outputs per tile row
-  static constexpr int TH = 4 * NP;
+  static constexpr int RPG = 16 / Q;            // tile rows per lane group
+  static constexpr int TW = F * Q;              // outputs per tile row
+  static constexpr int TH = 4 * NP * RPG;
   static constexpr int RH = TH + 2, RW = TW + 2;
   static constexpr int PLANE = RH * RW;
   static constexpr int PLANES = TD + 2;
   static constexpr int IMG = PLANES * PLANE;
-  // channel stride = 32 mod 64 floats: the two channels of a 32-lane ds_read_b64
-  // group read disjoint halves of the 64 banks
-  static constexpr int CIS = round_32mod64(IMG);
+  static constexpr int CIS = conflict_free_cis<F, Q>(IMG, RW);
   static constexpr int XS = CIN_B * CIS;
   static constexpr int WS = 9 * 3 * CIN_B * COP;  // the chunk's weights g[kd,kh][kw][ci][co]
   static constexpr int STAGE = XS + WS;
-  static_assert(XS % 16 == 0 && WS % 16 == 0, "16-byte aligned LDS regions");
+  static_assert(XS % 4 == 0 && WS % 4 == 0 && RW % 2 == 0 && PLANE % 2 == 0, "aligned LDS regions and b64 reads");
   static_assert(2 * STAGE * 4 * 2 <= 160 * 1024, "two double-buffered workgroups per CU");
 };
 
 __device__ __forceinline__ int a_col(int m, int ci, int n, bool swz) { return ((swz ? (m ^ (ci & 1)) : m) * 16) + n; }
 
-template <int F, int MT, int NP, int TD, bool CV>
+template <int F, int Q, int MT, int NP, int TD, bool CV>
 __global__ __launch_bounds__(kConvThreads, 2) void conv3d_wino_kernel(const ConvArgs a) {
-  using C = Cfg<F, MT, NP, TD>;
+  using C = Cfg<F, Q, MT, NP, TD>;
   constexpr int NX = C::NX;
   constexpr int XSLOTS = (C::IMG + 63) / 64;
   constexpr int XSLOTS_W = (XSLOTS + kConvWaves - 1) / kConvWaves;
@@ -171,9 +194,10 @@ __global__ __launch_bounds__(kConvThreads, 2) void conv3d_wino_kernel(const Conv
   };
 
   const int ci = lane >> 4, p = lane & 15;
-  int xoff[NP];  // staged input column F*p (w0 + F p - 1) of row (wave NP + j), channel ci
+  const int pq = p % Q, pr = p / Q;  // output group within the row, row within the lane group
+  int xoff[NP];  // staged input column F pq (w0 + F pq - 1) of tile row (wave NP + j) RPG + pr
 #pragma unroll
-  for (int j = 0; j < NP; ++j) xoff[j] = ci * C::CIS + (wave * NP + j) * C::RW + F * p;
+  for (int j = 0; j < NP; ++j) xoff[j] = ci * C::CIS + ((wave * NP + j) * C::RPG + pr) * C::RW + F * pq;
   int woff[MT];
 #pragma unroll
   for (int m = 0; m < MT; ++m) woff[m] = ci * C::COP + a_col(m, ci, p, C::SWZ);
@@ -292,13 +316,13 @@ __global__ __launch_bounds__(kConvThreads, 2) void conv3d_wino_kernel(const Conv
   // epilogue: A^T, folded BN, ReLU, residual; lane stores outputs w0 + F p .. + F - 1
   const bool relu = a.flags & LEA_RELU, resid = a.flags & LEA_RESIDUAL;
   const long long DHW = (long long)HW * a.D;
-  const int w = w0 + F * p;
+  const int w = w0 + F * pq;
 #pragma unroll
   for (int t = 0; t < TD; ++t) {
     const int d = d0 + t;
 #pragma unroll
     for (int j = 0; j < NP; ++j) {
-      const int h = h0 + wave * NP + j;
+      const int h = h0 + (wave * NP + j) * C::RPG + pr;
       if (d >= a.D || h >= a.H || w >= a.W) continue;
       const int nv = min(F, a.W - w);  // valid outputs of this group
 #pragma unroll
@@ -388,51 +412,62 @@ __global__ void pack_wino_kernel(const float* __restrict__ w, float* __restrict_
 }
 
 struct Plan {
-  int f, mt, np, td;
+  int f, q, mt, np, td;
 };
 
 thread_local int g_override[3] = {0, 0, 0};  // np, td, f (lea_conv3d_wino_set_tile_override)
 
 inline Plan make_plan(int B, int cout, int D, int H, int W) {
-  // r01 sweeps (tools/wino_sweep.py, profiles/r01_wino_sweep*.txt): F(4,3) where
-  // 64-wide tile rows waste little of W (the L0 volumes), else F(2,3); 8-row x
-  // 2-plane F(2,3) tiles for the 32-channel blocks, 4 x 2 for the 16/48-channel
-  // ones; single planes only when the volume is too shallow to fill the chip.
+  // r01 sweeps (tools/wino_sweep.py, profiles/r01_wino_sweep*.txt): F(4,3) on
+  // 64-wide tile rows where they waste little of W (the L0 volumes), else on
+  // 32-wide row pairs (L1, L2), F(2,3) for the 48-row blocks (their LDS budget);
+  // two output planes per workgroup unless the volume is too shallow to fill the chip.
   Plan p;
   p.mt = mt_of(cout);
   const long long ncob = (cout + 16 * p.mt - 1) / (16 * p.mt);
-  p.f = (p.mt != 3 && (W + 63) / 64 * 64 * 10 <= W * 11) ? 4 : 2;
+  auto fits = [&](int tw) { return (W + tw - 1) / tw * tw * 10 <= W * 11; };  // <= 10 % padding
+  p.f = 2;
+  p.q = 16;
+  if (p.mt != 3) {
+    p.f = 4;
+    if (!fits(64)) p.q = 8;  // F(4,3) over 32-wide row pairs: F(2,3)'s tile width, 3/4 its MFMAs
+  }
   auto wgs = [&](int np, int td) {
-    const int tw = 16 * p.f;
-    return (long long)((W + tw - 1) / tw) * ((H + 4 * np - 1) / (4 * np)) * ((D + td - 1) / td) * B * ncob;
+    const int tw = p.f * p.q, th = 4 * np * (16 / p.q);
+    return (long long)((W + tw - 1) / tw) * ((H + th - 1) / th) * ((D + td - 1) / td) * B * ncob;
   };
   p.np = (p.f == 2 && p.mt == 2 && wgs(2, 2) >= 512) ? 2 : 1;
   p.td = wgs(p.np, 2) >= 384 ? 2 : 1;
   if (g_override[0] > 0) {
     p.np = g_override[0];
     p.td = g_override[1];
-    if (g_override[2] > 0) p.f = g_override[2];
+    if (g_override[2] > 0) {
+      p.f = g_override[2] == 8 ? 4 : g_override[2];
+      p.q = g_override[2] == 8 ? 8 : 16;
+    }
   }
   return p;
 }
 
-#define LEA_WINO_CASE(F, MT, NP, TD, CV)                                                   \
-  if (p.f == F && p.mt == MT && p.np == NP && p.td == TD) {                                \
-    a.tiles_w = (a.W + 16 * F - 1) / (16 * F);                                             \
-    a.ntiles = a.tiles_w * ((a.H + 4 * NP - 1) / (4 * NP));                                \
-    a.ndz = (a.D + TD - 1) / TD;                                                           \
-    const long long n_ = (long long)a.ntiles * a.ndz * B * a.ncob;                         \
-    LEA_CHECK_ARG(n_ < (1LL << 31), "lea_conv3d(wino): grid too large");                   \
-    a.nblk = (int)n_;                                                                      \
-    conv3d_wino_kernel<F, MT, NP, TD, CV><<<dim3((unsigned)n_), kConvThreads, 0, st>>>(a); \
-    return launch_status("lea_conv3d(wino)");                                             \
+#define LEA_WINO_CASE(F, Q, MT, NP, TD, CV)                                                   \
+  if (p.f == F && p.q == Q && p.mt == MT && p.np == NP && p.td == TD) {                       \
+    using C_ = Cfg<F, Q, MT, NP, TD>;                                                         \
+    a.tiles_w = (a.W + C_::TW - 1) / C_::TW;                                                  \
+    a.ntiles = a.tiles_w * ((a.H + C_::TH - 1) / C_::TH);                                     \
+    a.ndz = (a.D + TD - 1) / TD;                                                              \
+    const long long n_ = (long long)a.ntiles * a.ndz * B * a.ncob;                            \
+    LEA_CHECK_ARG(n_ < (1LL << 31), "lea_conv3d(wino): grid too large");                      \
+    a.nblk = (int)n_;                                                                         \
+    conv3d_wino_kernel<F, Q, MT, NP, TD, CV><<<dim3((unsigned)n_), kConvThreads, 0, st>>>(a); \
+    return launch_status("lea_conv3d(wino)");                                                \
   }
-#define LEA_WINO_TILES(CV)                                                                            \
-  LEA_WINO_CASE(2, 1, 1, 1, CV) LEA_WINO_CASE(2, 1, 1, 2, CV) LEA_WINO_CASE(2, 1, 2, 1, CV)           \
-  LEA_WINO_CASE(2, 1, 2, 2, CV) LEA_WINO_CASE(2, 2, 1, 1, CV) LEA_WINO_CASE(2, 2, 1, 2, CV)           \
-  LEA_WINO_CASE(2, 2, 2, 1, CV) LEA_WINO_CASE(2, 2, 2, 2, CV) LEA_WINO_CASE(2, 3, 1, 1, CV)           \
-  LEA_WINO_CASE(2, 3, 1, 2, CV) LEA_WINO_CASE(4, 1, 1, 1, CV) LEA_WINO_CASE(4, 1, 1, 2, CV)           \
-  LEA_WINO_CASE(4, 2, 1, 1, CV) LEA_WINO_CASE(4, 2, 1, 2, CV)
+#define LEA_WINO_TILES(CV)                                                                                  \
+  LEA_WINO_CASE(2, 16, 1, 1, 1, CV) LEA_WINO_CASE(2, 16, 1, 1, 2, CV) LEA_WINO_CASE(2, 16, 1, 2, 1, CV)     \
+  LEA_WINO_CASE(2, 16, 1, 2, 2, CV) LEA_WINO_CASE(2, 16, 2, 1, 1, CV) LEA_WINO_CASE(2, 16, 2, 1, 2, CV)     \
+  LEA_WINO_CASE(2, 16, 2, 2, 1, CV) LEA_WINO_CASE(2, 16, 2, 2, 2, CV) LEA_WINO_CASE(2, 16, 3, 1, 1, CV)     \
+  LEA_WINO_CASE(2, 16, 3, 1, 2, CV) LEA_WINO_CASE(4, 16, 1, 1, 1, CV) LEA_WINO_CASE(4, 16, 1, 1, 2, CV)     \
+  LEA_WINO_CASE(4, 16, 2, 1, 1, CV) LEA_WINO_CASE(4, 16, 2, 1, 2, CV) LEA_WINO_CASE(4, 8, 1, 1, 1, CV)      \
+  LEA_WINO_CASE(4, 8, 1, 1, 2, CV) LEA_WINO_CASE(4, 8, 2, 1, 1, CV) LEA_WINO_CASE(4, 8, 2, 1, 2, CV)
 
 int run(const Plan& p, ConvArgs a, int B, hipStream_t st, bool cv) {
   a.ncob = (a.cout + 16 * p.mt - 1) / (16 * p.mt);
@@ -441,15 +476,15 @@ int run(const Plan& p, ConvArgs a, int B, hipStream_t st, bool cv) {
   } else {
     LEA_WINO_TILES(false)
   }
-  set_error("lea_conv3d(wino): no tile f=%d mt=%d np=%d td=%d", p.f, p.mt, p.np, p.td);
+  set_error("lea_conv3d(wino): no tile f=%d q=%d mt=%d np=%d td=%d", p.f, p.q, p.mt, p.np, p.td);
   return LEA_E_UNSUPPORTED;
 }
 
 thread_local char g_name[96];
 
 const char* name(const Plan& p, bool cv) {
-  snprintf(g_name, sizeof(g_name), "conv3d_wino_kernel<%d, %d, %d, %d, %s>", p.f, p.mt, p.np, p.td,
-           cv ? "true" : "false");
+  snprintf(g_name, sizeof(g_name), "conv3d_wino_kernel<%d, %d, %d, %d, %d, %s>", p.f, p.q, p.mt, p.np,
+           p.td, cv ? "true" : "false");
   return g_name;
 }
 
@@ -515,7 +550,7 @@ extern "C" int lea_conv3d_wino_set_tile_override(int np, int td, int f) {
     wino::g_override[0] = 0;
     return 0;
   }
-  LEA_CHECK_ARG((np == 1 || np == 2) && (td == 1 || td == 2) && (f == 0 || f == 2 || f == 4),
+  LEA_CHECK_ARG((np == 1 || np == 2) && (td == 1 || td == 2) && (f == 0 || f == 2 || f == 4 || f == 8),
                 "lea_conv3d_wino_set_tile_override: bad tile np=%d td=%d f=%d", np, td, f);
   wino::g_override[0] = np;
   wino::g_override[1] = td;

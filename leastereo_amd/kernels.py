@@ -682,12 +682,12 @@ WINO_MIN_VOXELS = 200_000  # below this the direct engine's smaller tiles fill t
 
 def wino_preferred(b, cout, cin, d, h, w) -> bool:
     """Per-call engine choice for an eligible layer (tools/wino_sweep.py at config 2):
-    Winograd wins on the large volumes when the output channels fill its 16/32-row
-    blocks (stem0, stem1, conv1/2, the 16-channel L1 cells, the 8->24 L0 group);
-    the direct engine keeps the small L2 volumes and the 48-channel groups (a
-    third of a 32-row block would be padding; they get a 48-row block)."""
+    Winograd wins on the large volumes when the output channels fill its 16/32/48-row
+    blocks (stem0, stem1, conv1/2, the L1 cells and sibling groups, the 8->24 L0
+    group); on the small L2 volumes only the 96-channel sibling groups gain, the
+    32-channel cells stay on the direct engine."""
     if b * d * h * w < WINO_MIN_VOXELS:
-        return False
+        return cout >= 64 and cout % 32 == 0  # small volumes: only wide blocks amortise the tile
     return cout == 16 or cout == 24 or cout % 32 == 0 or cout % 48 == 0
 
 
@@ -695,7 +695,7 @@ def wino_mfma_scale(cout: int, name: str) -> float:
     """MFMA products issued per direct-convolution product: (F + 2) per 3F for the
     kernel's F (first template argument of ``name``), times the padding of cout to
     the engine's 16/32/48-row block."""
-    f = int(name.split("<", 1)[1].split(",", 1)[0])
+    f = int(name.split("<", 1)[1].split(",", 1)[0])  # conv3d_wino_kernel<F, Q, MT, ...>
     cop = 16 if cout <= 16 else (48 if cout % 32 != 0 and cout % 48 == 0 else 32)
     return (f + 2) / (3.0 * f) * (-(-cout // cop) * cop) / cout
 

@@ -49,15 +49,15 @@ def test_wino_vs_torch(b, cin, cout, shape, mode):
     np.testing.assert_allclose(y.cpu().double().numpy(), want.numpy(), rtol=1e-4, atol=1e-4)
 
 
-@pytest.mark.parametrize("f", [2, 4])
+@pytest.mark.parametrize("f", [2, 4, 8])
 @pytest.mark.parametrize("np_,td", [(1, 1), (1, 2), (2, 1), (2, 2)])
 @pytest.mark.parametrize("cout", [16, 48, 64])
 def test_wino_every_tile(np_, td, cout, f):
     """Every instantiated (F, rows, planes) tile on a ragged volume (W = 45: a partial
     last group of outputs for both F) with the accumulate epilogue."""
-    if np_ == 2 and (cout == 48 or f == 4):
+    if np_ == 2 and (cout == 48 or f != 2):
         pytest.skip("48-row blocks and F(4,3) tiles are instantiated with one row per wave (LDS budget)")
-    if cout == 48 and f == 4:
+    if cout == 48 and f != 2:
         pytest.skip("48-row blocks run F(2,3) only")
     lib = _lib.load()
     g = torch.Generator().manual_seed(np_ * 10 + td + cout)
@@ -69,7 +69,8 @@ def test_wino_every_tile(np_, td, cout, f):
     try:
         name = kernels.wino_kernel_name(2, cout, 5, 11, 45)
         mt = {16: 1, 48: 3, 64: 2}[cout]
-        assert name == f"conv3d_wino_kernel<{f}, {mt}, {np_}, {td}, false>", name
+        ff, q = (4, 8) if f == 8 else (f, 16)
+        assert name == f"conv3d_wino_kernel<{ff}, {q}, {mt}, {np_}, {td}, false>", name
         out = r.to(DEV).clone()
         kernels.conv3d_bnrelu_wino(x.to(DEV), kernels.pack_conv_weight_wino(w.to(DEV)), cout, None,
                                    None, relu=False, out=out, accumulate=True)

@@ -51,7 +51,7 @@ def main():
         pd, pw = kernels.pack_conv_weight(wt), kernels.pack_conv_weight_wino(wt)
         res = {"direct": timed(lambda: kernels.conv3d_bnrelu(x, pd, cout, 3, scale, shift, True, y, acc),
                                a.iters)}
-        for f, np_, td in [(f, n, t) for f in (2, 4) for n in (1, 2) for t in (1, 2)]:
+        for f, np_, td in [(f, n, t) for f in (2, 4, 8) for n in (1, 2) for t in (1, 2)]:
             if True:
                 lib.lea_conv3d_wino_set_tile_override(np_, td, f)
                 try:
