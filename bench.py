@@ -265,7 +265,8 @@ def main():
                      "flops_per_launch": flops_per_launch, "ms_per_launch": ms_per_launch,
                      # products the kernel actually issues: Winograd F(2,3) does 4 per 6 of
                      # the direct convolution whose FLOPs define `achieved`
-                     "algorithm": "winograd F(2,3) along W" if "wino" in dominant else "direct",
+                     "algorithm": (f"winograd F({dominant.split('<')[1].split(',')[0]},3) along W"
+                                   if "wino" in dominant else "direct convolution"),
                      "mfma_executed": mfma_tflops, "mfma_executed_frac": mfma_tflops / peak},
         "epe_px": None if epe is None else {
             "vs": "reference LEAStereo fp32 disparity (tests/golden e2e b1_h96_w192_md48)",

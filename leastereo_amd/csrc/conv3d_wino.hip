@@ -431,13 +431,16 @@ inline Plan make_plan(int B, int cout, int D, int H, int W) {
   if (p.mt != 3) {
     p.f = 4;
     if (!fits(64)) p.q = 8;  // F(4,3) over 32-wide row pairs: F(2,3)'s tile width, 3/4 its MFMAs
+  } else if (fits(32)) {
+    p.f = 4;  // 48-row blocks: row pairs one plane deep fit the LDS (F(2,3) otherwise)
+    p.q = 8;
   }
   auto wgs = [&](int np, int td) {
     const int tw = p.f * p.q, th = 4 * np * (16 / p.q);
     return (long long)((W + tw - 1) / tw) * ((H + th - 1) / th) * ((D + td - 1) / td) * B * ncob;
   };
   p.np = (p.f == 2 && p.mt == 2 && wgs(2, 2) >= 512) ? 2 : 1;
-  p.td = wgs(p.np, 2) >= 384 ? 2 : 1;
+  p.td = (wgs(p.np, 2) >= 384 && !(p.mt == 3 && p.f == 4)) ? 2 : 1;
   if (g_override[0] > 0) {
     p.np = g_override[0];
     p.td = g_override[1];
@@ -467,7 +470,8 @@ inline Plan make_plan(int B, int cout, int D, int H, int W) {
   LEA_WINO_CASE(2, 16, 2, 2, 1, CV) LEA_WINO_CASE(2, 16, 2, 2, 2, CV) LEA_WINO_CASE(2, 16, 3, 1, 1, CV)     \
   LEA_WINO_CASE(2, 16, 3, 1, 2, CV) LEA_WINO_CASE(4, 16, 1, 1, 1, CV) LEA_WINO_CASE(4, 16, 1, 1, 2, CV)     \
   LEA_WINO_CASE(4, 16, 2, 1, 1, CV) LEA_WINO_CASE(4, 16, 2, 1, 2, CV) LEA_WINO_CASE(4, 8, 1, 1, 1, CV)      \
-  LEA_WINO_CASE(4, 8, 1, 1, 2, CV) LEA_WINO_CASE(4, 8, 2, 1, 1, CV) LEA_WINO_CASE(4, 8, 2, 1, 2, CV)
+  LEA_WINO_CASE(4, 8, 1, 1, 2, CV) LEA_WINO_CASE(4, 8, 2, 1, 1, CV) LEA_WINO_CASE(4, 8, 2, 1, 2, CV)      \
+  LEA_WINO_CASE(4, 8, 3, 1, 1, CV)
 
 int run(const Plan& p, ConvArgs a, int B, hipStream_t st, bool cv) {
   a.ncob = (a.cout + 16 * p.mt - 1) / (16 * p.mt);
