@@ -5,7 +5,7 @@ set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 mkdir -p gpurun_out/traffic
-TAG=${TAG:-v17}
+TAG=${TAG:-v18}
 B="python3 bench.py --steps 3 --warmup 1 --cpu-baseline 0 --epe 0"
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d gpurun_out/traffic/fetch -o run -- $B > gpurun_out/traffic/fetch.log 2>&1
 rc=$?; echo "fetch rc=$rc"; [ $rc -eq 0 ] || exit $rc
