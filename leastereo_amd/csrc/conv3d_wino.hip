@@ -87,13 +87,37 @@ struct Cfg {
   static constexpr int PLANE = RH * RW;
   static constexpr int PLANES = TD + 2;
   static constexpr int IMG = PLANES * PLANE;
-  static constexpr int CIS = conflict_free_cis<F, Q>(IMG, RW);
+  static constexpr int XSLOTS = (IMG + 63) / 64;  // 64-lane DMA pieces per channel
+  // channel stride >= whole pieces: the last piece's surplus lanes land in padding,
+  // so no piece needs a per-lane exec mask
+  static constexpr int CIS = conflict_free_cis<F, Q>(64 * XSLOTS, RW);
   static constexpr int XS = CIN_B * CIS;
   static constexpr int WS = 9 * 3 * CIN_B * COP;  // the chunk's weights g[kd,kh][kw][ci][co]
-  static constexpr int STAGE = XS + WS;
+  static constexpr int WSLOTS = (WS + 255) / 256;  // 256-float pieces (padded the same way)
+  static constexpr int STAGE = XS + 256 * WSLOTS;
   static_assert(XS % 4 == 0 && WS % 4 == 0 && RW % 2 == 0 && PLANE % 2 == 0, "aligned LDS regions and b64 reads");
   static_assert(2 * STAGE * 4 * 2 <= 160 * 1024, "two double-buffered workgroups per CU");
 };
+
+// LDS-DMA pieces as inline asm: with the builtins hipcc treats every in-flight
+// DMA as a possible write to any LDS word and waits vmcnt(0) before the first
+// ds_read of each chunk -- i.e. for the NEXT chunk's halo, which de-pipelines the
+// double buffer (r01 PMC: 17 % of wave cycles parked).  As asm they are invisible
+// to its wait bookkeeping; the kernel's own vmcnt(0) + barrier at the chunk head is
+// the one wait they need.  M0 (the LDS destination base) is saved and restored.
+__device__ __forceinline__ unsigned lds_addr(const float* p) {
+  return __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)(lds_void*)p);
+}
+__device__ __forceinline__ void dma_dword(__amdgpu_buffer_rsrc_t rs, unsigned voff, unsigned lds) {
+  unsigned keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dword %1, %2, 0 offen lds\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep) : "v"(voff), "s"(rs), "s"(lds) : "memory");
+}
+__device__ __forceinline__ void dma_dwordx4(const float* src, unsigned lds) {
+  unsigned keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep) : "v"(src), "s"(lds) : "memory");
+}
 
 __device__ __forceinline__ int a_col(int m, int ci, int n, bool swz) { return ((swz ? (m ^ (ci & 1)) : m) * 16) + n; }
 
@@ -101,11 +125,12 @@ template <int F, int Q, int MT, int NP, int TD, bool CV>
 __global__ __launch_bounds__(kConvThreads, 2) void conv3d_wino_kernel(const ConvArgs a) {
   using C = Cfg<F, Q, MT, NP, TD>;
   constexpr int NX = C::NX;
-  constexpr int XSLOTS = (C::IMG + 63) / 64;
+  constexpr int XSLOTS = C::XSLOTS;
   constexpr int XSLOTS_W = (XSLOTS + kConvWaves - 1) / kConvWaves;
-  constexpr int WSLOTS = (C::WS + 255) / 256;
+  constexpr int WSLOTS = C::WSLOTS;
   constexpr int WSLOTS_W = (WSLOTS + kConvWaves - 1) / kConvWaves;
   __shared__ __attribute__((aligned(16))) float smem[2 * C::STAGE];
+  const unsigned lds0 = lds_addr(smem);
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -163,8 +188,8 @@ __global__ __launch_bounds__(kConvThreads, 2) void conv3d_wino_kernel(const Conv
 #pragma unroll
     for (int t = 0; t < WSLOTS_W; ++t) {
       const int j = wave + kConvWaves * t;
-      if (j < WSLOTS && j * 256 + lane * 4 < C::WS)
-        __builtin_amdgcn_global_load_lds(wsrc + j * 256 + lane * 4, (lds_void*)(wdst + j * 256), 16, 0, 0);
+      if (j < WSLOTS)  // the last piece reads into the next chunk / the buffer's tail pad
+        dma_dwordx4(wsrc + j * 256 + lane * 4, lds0 + 4 * (unsigned)(wdst - smem + j * 256));
     }
     const long long cvol = CV ? (long long)HW : (long long)HW * a.D;  // channel stride
     const unsigned crec = CV ? (unsigned)HW * 4u : nrec;
@@ -187,8 +212,7 @@ __global__ __launch_bounds__(kConvThreads, 2) void conv3d_wino_kernel(const Conv
         const int j = wave + kConvWaves * t;
         unsigned vo = voff[t];
         if constexpr (CV) vo = voff[t] ^ ((voff[t] ^ voffr[t]) & rmask);
-        if (j < XSLOTS && j * 64 + lane < C::IMG)
-          __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void*)(st + ci * C::CIS + j * 64), 4, vo, 0, 0, 0);
+        if (j < XSLOTS) dma_dword(rs, vo, lds0 + 4 * (unsigned)(st - smem + ci * C::CIS + j * 64));
       }
     }
   };
@@ -252,55 +276,51 @@ __global__ __launch_bounds__(kConvThreads, 2) void conv3d_wino_kernel(const Conv
 #pragma unroll
         for (int r = 0; r < 3; ++r) o.g[r][m] = wk[r * CIN_B * C::COP + woff[m]];
     };
-    StepOps ops[2];
-    load_step(0, ops[0]);
-#pragma unroll
-    for (int step = 0; step < 9; ++step) {
-      if (step + 1 < 9) load_step(step + 1, ops[(step + 1) & 1]);
-      const StepOps& o = ops[step & 1];
+    // transforms of one step: V = B^T x per (plane, row) and U = G' g per cout tile,
+    // G' = G with its rows' constant factors moved into the epilogue (kScale)
+    struct Xf {
       float vb[TD][NP][NX];
+      float u[NX][MT];
+    };
+    auto xform = [&](const StepOps& o, Xf& T) {
 #pragma unroll
       for (int t = 0; t < TD; ++t)
 #pragma unroll
         for (int j = 0; j < NP; ++j) {
           const float x0 = o.x2[t][j][0].x, x1 = o.x2[t][j][0].y, x2 = o.x2[t][j][1].x, x3 = o.x2[t][j][1].y;
           if constexpr (F == 2) {
-            vb[t][j][0] = x0 - x2;
-            vb[t][j][1] = x1 + x2;
-            vb[t][j][2] = x2 - x1;
-            vb[t][j][3] = x1 - x3;
+            T.vb[t][j][0] = x0 - x2;
+            T.vb[t][j][1] = x1 + x2;
+            T.vb[t][j][2] = x2 - x1;
+            T.vb[t][j][3] = x1 - x3;
           } else {
             const float x4 = o.x2[t][j][F / 2].x, x5 = o.x2[t][j][F / 2].y;
             const float pa = fmaf(-4.f, x2, x4), pb = fmaf(-4.f, x1, x3);
             const float pc = x4 - x2, pd = 2.f * (x3 - x1);
-            vb[t][j][0] = fmaf(4.f, x0, fmaf(-5.f, x2, x4));
-            vb[t][j][1] = pa + pb;
-            vb[t][j][2] = pa - pb;
-            vb[t][j][3] = pc + pd;
-            vb[t][j][4] = pc - pd;
-            vb[t][j][NX - 1] = fmaf(4.f, x1, fmaf(-5.f, x3, x5));
+            T.vb[t][j][0] = fmaf(4.f, x0, fmaf(-5.f, x2, x4));
+            T.vb[t][j][1] = pa + pb;
+            T.vb[t][j][2] = pa - pb;
+            T.vb[t][j][3] = pc + pd;
+            T.vb[t][j][4] = pc - pd;
+            T.vb[t][j][NX - 1] = fmaf(4.f, x1, fmaf(-5.f, x3, x5));
           }
         }
-      float u[NX][MT];
 #pragma unroll
       for (int m = 0; m < MT; ++m) {
         const float g0 = o.g[0][m], g1 = o.g[1][m], g2 = o.g[2][m];
-        if constexpr (F == 2) {
-          const float s = g0 + g2;
-          u[0][m] = g0;
-          u[1][m] = (s + g1) * 0.5f;
-          u[2][m] = (s - g1) * 0.5f;
-          u[3][m] = g2;
-        } else {
-          const float s = g0 + g2, s4 = fmaf(4.f, g2, g0), t2 = 2.f * g1;
-          u[0][m] = 0.25f * g0;
-          u[1][m] = (s + g1) * (-1.f / 6.f);
-          u[2][m] = (s - g1) * (-1.f / 6.f);
-          u[3][m] = (s4 + t2) * (1.f / 24.f);
-          u[4][m] = (s4 - t2) * (1.f / 24.f);
-          u[NX - 1][m] = g2;
+        const float s = g0 + g2;
+        T.u[0][m] = g0;
+        T.u[1][m] = s + g1;
+        T.u[2][m] = s - g1;
+        if constexpr (F == 4) {
+          const float s4 = fmaf(4.f, g2, g0);
+          T.u[3][m] = fmaf(2.f, g1, s4);
+          T.u[4][m] = fmaf(-2.f, g1, s4);
         }
+        T.u[NX - 1][m] = g2;
       }
+    };
+    auto mfmas = [&](const Xf& T) {
 #pragma unroll
       for (int x = 0; x < NX; ++x)
 #pragma unroll
@@ -309,7 +329,20 @@ __global__ __launch_bounds__(kConvThreads, 2) void conv3d_wino_kernel(const Conv
           for (int m = 0; m < MT; ++m)
 #pragma unroll
             for (int j = 0; j < NP; ++j)
-              acc[x][t][m][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(u[x][m], vb[t][j][x], acc[x][t][m][j], 0, 0, 0);
+              acc[x][t][m][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(T.u[x][m], T.vb[t][j][x], acc[x][t][m][j], 0, 0, 0);
+    };
+    // software pipeline over the 9 steps: LDS reads two steps ahead, transforms one
+    // step ahead, so a step's VALU runs under the previous step's MFMAs
+    StepOps ops[2];
+    Xf xf[2];
+    load_step(0, ops[0]);
+    load_step(1, ops[1]);
+    xform(ops[0], xf[0]);
+#pragma unroll
+    for (int step = 0; step < 9; ++step) {
+      if (step + 1 < 9) xform(ops[(step + 1) & 1], xf[(step + 1) & 1]);
+      if (step + 2 < 9) load_step(step + 2, ops[step & 1]);
+      mfmas(xf[step & 1]);
     }
   }
 
@@ -333,13 +366,15 @@ __global__ __launch_bounds__(kConvThreads, 2) void conv3d_wino_kernel(const Conv
           if (co >= a.cout) continue;
           float y[F];
           if constexpr (F == 2) {
-            const float m0 = acc[0][t][m][j][r], m1 = acc[1][t][m][j][r];
-            const float m2 = acc[2][t][m][j][r], m3 = acc[3][t][m][j][r];
+            const float m0 = acc[0][t][m][j][r], m1 = 0.5f * acc[1][t][m][j][r];
+            const float m2 = 0.5f * acc[2][t][m][j][r], m3 = acc[3][t][m][j][r];
             y[0] = (m0 + m1) + m2;
             y[1] = (m1 - m2) - m3;
           } else {
-            const float m0 = acc[0][t][m][j][r], m1 = acc[1][t][m][j][r], m2 = acc[2][t][m][j][r];
-            const float m3 = acc[3][t][m][j][r], m4 = acc[4][t][m][j][r], m5 = acc[NX - 1][t][m][j][r];
+            const float m0 = 0.25f * acc[0][t][m][j][r];
+            const float m1 = (-1.f / 6.f) * acc[1][t][m][j][r], m2 = (-1.f / 6.f) * acc[2][t][m][j][r];
+            const float m3 = (1.f / 24.f) * acc[3][t][m][j][r], m4 = (1.f / 24.f) * acc[4][t][m][j][r];
+            const float m5 = acc[NX - 1][t][m][j][r];
             const float sp = m1 + m2, sm = m1 - m2, tp = m3 + m4, tm = m3 - m4;
             y[0] = (m0 + sp) + tp;
             y[1] = fmaf(2.f, tm, sm);
@@ -523,7 +558,8 @@ using namespace lea;
 extern "C" size_t lea_conv3d_wino_packed_floats(int cout, int cin) {
   if (cout <= 0 || cin <= 0 || cin % wino::CIN_B != 0) return 0;
   const int cop = 16 * wino::mt_of(cout);
-  return (size_t)((cout + cop - 1) / cop) * (cin / wino::CIN_B) * 9 * 3 * wino::CIN_B * cop;
+  // + one 256-float tail: the kernel stages whole 256-float pieces per chunk
+  return (size_t)((cout + cop - 1) / cop) * (cin / wino::CIN_B) * 9 * 3 * wino::CIN_B * cop + 256;
 }
 
 extern "C" int lea_conv3d_wino_pack_weights(const float* w, float* packed, int cout, int cin,
