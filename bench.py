@@ -157,6 +157,14 @@ def golden_epe(device, precision="f32"):
     return float(np.abs(got - want).mean())
 
 
+def _quantile(xs, q):
+    """Linear-interpolated quantile of a sorted list."""
+    pos = q * (len(xs) - 1)
+    i = int(pos)
+    j = min(i + 1, len(xs) - 1)
+    return xs[i] + (xs[j] - xs[i]) * (pos - i)
+
+
 def main():
     args = parse()
     info = parallel.rank_info()
@@ -204,9 +212,14 @@ def main():
         parallel.barrier()
         torch.cuda.synchronize()
         with kernels.KernelProbe([dominant]) as probe:
+            # per-step latency: HIP events between consecutive steps (SURVEY §8d's
+            # median and p10/p90), on the stream the forward is launched on
+            ev = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps + 1)]
             t0 = time.perf_counter()
-            for _ in range(args.steps):
+            ev[0].record()
+            for i in range(args.steps):
                 out = step()
+                ev[i + 1].record()
             torch.cuda.synchronize()
             parallel.barrier()
             elapsed = time.perf_counter() - t0
@@ -214,6 +227,7 @@ def main():
             with kernels.KernelProbe([dominant]) as probe:
                 model(left, right)
         dom = probe.summary()[dominant]
+        step_ms = sorted(ev[i].elapsed_time(ev[i + 1]) for i in range(args.steps))
     elapsed = parallel.max_over_ranks(elapsed, device)
 
     epe = None
@@ -247,6 +261,8 @@ def main():
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": elapsed / args.steps * 1e3,
+        "step_ms": {"median": _quantile(step_ms, 0.5), "p10": _quantile(step_ms, 0.1),
+                    "p90": _quantile(step_ms, 0.9), "source": "HIP events between steps, this rank"},
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,

@@ -18,9 +18,11 @@
 // is fp32: the products and sums are the MFMA's fp32; the transforms add a few
 // roundings per value (F(4,3)'s coefficients are larger, its error a few times
 // F(2,3)'s -- both far inside the conv tolerance, tests/test_gpu_wino.py).
-// U = G g is formed in the kernel from the staged weights g (3 LDS reads and a few
-// VALU per row and step): the weight stage is 3 rows per (kd, kh) whatever F, which
-// is what keeps two workgroups per CU with F(4,3)'s wider halo.
+// U = G' g is formed in the kernel from the staged weights g (3 LDS reads and 4-6
+// VALU per row and step; G' = G with each row's constant factor -- 1/4, -1/6, 1/24,
+// 1/2 -- moved onto the accumulator M_xi in the epilogue): the weight stage is 3
+// rows per (kd, kh) whatever F, which is what keeps two workgroups per CU with
+// F(4,3)'s wider halo.
 //
 // GEMM view per transform point xi and (kd, kh):
 //     M_xi[co][group] += sum_ci U_xi[kd][kh][co][ci] * V_xi[ci][group]
@@ -36,8 +38,10 @@
 // input channels (one MFMA K step): the input halo by LDS-DMA (buffer_load_dword ...
 // lds, one buffer resource per channel, out-of-range offsets return the zero
 // padding), the chunk's weights (9 x 3 x 4 x COP floats) by global_load_lds_dwordx4;
-// two stages, one vmcnt(0) + barrier per chunk (the direct engine's pipeline); a
-// step's LDS reads are issued before the previous step's MFMAs.
+// two stages, one vmcnt(0) + barrier per chunk (the direct engine's pipeline).
+// Within a chunk the 9 (kd, kh) steps are software-pipelined: LDS reads two steps
+// ahead, the V / U transforms one step ahead, so a step's VALU issues under the
+// previous step's MFMAs.
 #include "conv3d_impl.h"
 
 namespace lea {
@@ -47,9 +51,12 @@ constexpr int CIN_B = 4;
 
 // 16-row MFMA tiles per cout block: 16, 32 or 48 couts (48 for 48k couts that are not
 // multiples of 32: the L1 16->48 sibling groups would pad a 64-row block by a third)
+// MT = 0: the depth-paired block for couts <= 8 -- one 16-row tile holding the couts
+// of TWO output planes (as the direct engine's KD = 4 tile, conv3d_impl.h)
 __host__ __device__ constexpr int mt_of(int cout) {
-  return cout <= 16 ? 1 : (cout % 32 != 0 && cout % 48 == 0) ? 3 : 2;
+  return cout <= 8 ? 0 : cout <= 16 ? 1 : (cout % 32 != 0 && cout % 48 == 0) ? 3 : 2;
 }
+__host__ __device__ constexpr int cop_of(int mt) { return 16 * (mt > 0 ? mt : 1); }
 
 // Lane group (16 lanes of one input channel) -> output groups: Q groups of F outputs
 // per tile row and 16/Q rows (Q = 8 lets F(4,3) tile a 32-wide row pair).
@@ -77,8 +84,13 @@ __host__ __device__ constexpr int conflict_free_cis(int img, int rw) {
 
 template <int F, int Q, int MT, int NP, int TD>
 struct Cfg {
+  static constexpr bool DP = MT == 0;           // depth-paired (couts <= 8)
+  static constexpr int MTE = DP ? 1 : MT;       // 16-row tiles per wave
+  static constexpr int TDA = DP ? 1 : TD;       // accumulator sets along D
+  static constexpr int NSTEP = DP ? 12 : 9;     // (kd, kh) steps; depth-paired: (staged plane, kh)
+  static_assert(!DP || TD == 2, "a depth-paired tile covers two output planes");
   static constexpr int NX = F + 2;              // transform points
-  static constexpr int COP = 16 * MT;
+  static constexpr int COP = 16 * MTE;
   static constexpr bool SWZ = (COP % 32) == 0;  // odd-ci rows: 16-column halves swapped
   static constexpr int RPG = 16 / Q;            // tile rows per lane group
   static constexpr int TW = F * Q;              // outputs per tile row
@@ -92,7 +104,7 @@ struct Cfg {
   // so no piece needs a per-lane exec mask
   static constexpr int CIS = conflict_free_cis<F, Q>(64 * XSLOTS, RW);
   static constexpr int XS = CIN_B * CIS;
-  static constexpr int WS = 9 * 3 * CIN_B * COP;  // the chunk's weights g[kd,kh][kw][ci][co]
+  static constexpr int WS = NSTEP * 3 * CIN_B * COP;  // the chunk's weights g[step][kw][ci][co]
   static constexpr int WSLOTS = (WS + 255) / 256;  // 256-float pieces (padded the same way)
   static constexpr int STAGE = XS + 256 * WSLOTS;
   static_assert(XS % 4 == 0 && WS % 4 == 0 && RW % 2 == 0 && PLANE % 2 == 0, "aligned LDS regions and b64 reads");
@@ -222,29 +234,30 @@ __global__ __launch_bounds__(kConvThreads, 2) void conv3d_wino_kernel(const Conv
   int xoff[NP];  // staged input column F pq (w0 + F pq - 1) of tile row (wave NP + j) RPG + pr
 #pragma unroll
   for (int j = 0; j < NP; ++j) xoff[j] = ci * C::CIS + ((wave * NP + j) * C::RPG + pr) * C::RW + F * pq;
-  int woff[MT];
+  int woff[C::MTE];
 #pragma unroll
-  for (int m = 0; m < MT; ++m) woff[m] = ci * C::COP + a_col(m, ci, p, C::SWZ);
+  for (int m = 0; m < C::MTE; ++m) woff[m] = ci * C::COP + a_col(m, ci, p, C::SWZ);
 
   // folded BN of this lane's couts, fetched now so the epilogue does not wait
-  float sc[MT][4], sh[MT][4];
+  // (depth-paired: accumulator row 4 ci + r = cout (row & 7) of plane d0 + (row >> 3))
+  float sc[C::MTE][4], sh[C::MTE][4];
 #pragma unroll
-  for (int m = 0; m < MT; ++m)
+  for (int m = 0; m < C::MTE; ++m)
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      const int co = co0 + 16 * m + 4 * ci + r;
+      const int co = C::DP ? 4 * (ci & 1) + r : co0 + 16 * m + 4 * ci + r;
       const bool cv = co < a.cout;
       sc[m][r] = (cv && a.scale) ? a.scale[co] : 1.f;
       sh[m][r] = (cv && a.shift) ? a.shift[co] : 0.f;
     }
 
-  f32x4 acc[NX][TD][MT][NP];
+  f32x4 acc[NX][C::TDA][C::MTE][NP];
 #pragma unroll
   for (int x = 0; x < NX; ++x)
 #pragma unroll
-    for (int t = 0; t < TD; ++t)
+    for (int t = 0; t < C::TDA; ++t)
 #pragma unroll
-      for (int m = 0; m < MT; ++m)
+      for (int m = 0; m < C::MTE; ++m)
 #pragma unroll
         for (int j = 0; j < NP; ++j) acc[x][t][m][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
@@ -255,15 +268,16 @@ __global__ __launch_bounds__(kConvThreads, 2) void conv3d_wino_kernel(const Conv
     if (ch + 1 < nchunks) issue(ch + 1, smem + ((ch + 1) & 1) * C::STAGE);
     const float* xs = smem + (ch & 1) * C::STAGE;
     const float* ws = xs + C::XS;
-    // one (kd, kh) step: raw inputs (F + 2 per lane as float2s) and weight rows g
+    // one (kd, kh) step: raw inputs (F + 2 per lane as float2s) and weight rows g.
+    // Depth-paired, step (p, kh) reads staged plane p once for both output planes.
     struct StepOps {
-      float2 x2[TD][NP][F / 2 + 1];
-      float g[3][MT];
+      float2 x2[C::TDA][NP][F / 2 + 1];
+      float g[3][C::MTE];
     };
     auto load_step = [&](int step, StepOps& o) {
       const int kd = step / 3, kh = step % 3;
 #pragma unroll
-      for (int t = 0; t < TD; ++t)
+      for (int t = 0; t < C::TDA; ++t)
 #pragma unroll
         for (int j = 0; j < NP; ++j) {
           const float* sp = xs + xoff[j] + (t + kd) * C::PLANE + kh * C::RW;
@@ -272,19 +286,19 @@ __global__ __launch_bounds__(kConvThreads, 2) void conv3d_wino_kernel(const Conv
         }
       const float* wk = ws + step * 3 * CIN_B * C::COP;
 #pragma unroll
-      for (int m = 0; m < MT; ++m)
+      for (int m = 0; m < C::MTE; ++m)
 #pragma unroll
         for (int r = 0; r < 3; ++r) o.g[r][m] = wk[r * CIN_B * C::COP + woff[m]];
     };
     // transforms of one step: V = B^T x per (plane, row) and U = G' g per cout tile,
     // G' = G with its rows' constant factors moved into the epilogue (kScale)
     struct Xf {
-      float vb[TD][NP][NX];
-      float u[NX][MT];
+      float vb[C::TDA][NP][NX];
+      float u[NX][C::MTE];
     };
     auto xform = [&](const StepOps& o, Xf& T) {
 #pragma unroll
-      for (int t = 0; t < TD; ++t)
+      for (int t = 0; t < C::TDA; ++t)
 #pragma unroll
         for (int j = 0; j < NP; ++j) {
           const float x0 = o.x2[t][j][0].x, x1 = o.x2[t][j][0].y, x2 = o.x2[t][j][1].x, x3 = o.x2[t][j][1].y;
@@ -306,7 +320,7 @@ __global__ __launch_bounds__(kConvThreads, 2) void conv3d_wino_kernel(const Conv
           }
         }
 #pragma unroll
-      for (int m = 0; m < MT; ++m) {
+      for (int m = 0; m < C::MTE; ++m) {
         const float g0 = o.g[0][m], g1 = o.g[1][m], g2 = o.g[2][m];
         const float s = g0 + g2;
         T.u[0][m] = g0;
@@ -324,14 +338,14 @@ __global__ __launch_bounds__(kConvThreads, 2) void conv3d_wino_kernel(const Conv
 #pragma unroll
       for (int x = 0; x < NX; ++x)
 #pragma unroll
-        for (int t = 0; t < TD; ++t)
+        for (int t = 0; t < C::TDA; ++t)
 #pragma unroll
-          for (int m = 0; m < MT; ++m)
+          for (int m = 0; m < C::MTE; ++m)
 #pragma unroll
             for (int j = 0; j < NP; ++j)
               acc[x][t][m][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(T.u[x][m], T.vb[t][j][x], acc[x][t][m][j], 0, 0, 0);
     };
-    // software pipeline over the 9 steps: LDS reads two steps ahead, transforms one
+    // software pipeline over the NSTEP steps: LDS reads two steps ahead, transforms one
     // step ahead, so a step's VALU runs under the previous step's MFMAs
     StepOps ops[2];
     Xf xf[2];
@@ -339,9 +353,9 @@ __global__ __launch_bounds__(kConvThreads, 2) void conv3d_wino_kernel(const Conv
     load_step(1, ops[1]);
     xform(ops[0], xf[0]);
 #pragma unroll
-    for (int step = 0; step < 9; ++step) {
-      if (step + 1 < 9) xform(ops[(step + 1) & 1], xf[(step + 1) & 1]);
-      if (step + 2 < 9) load_step(step + 2, ops[step & 1]);
+    for (int step = 0; step < C::NSTEP; ++step) {
+      if (step + 1 < C::NSTEP) xform(ops[(step + 1) & 1], xf[(step + 1) & 1]);
+      if (step + 2 < C::NSTEP) load_step(step + 2, ops[step & 1]);
       mfmas(xf[step & 1]);
     }
   }
@@ -351,18 +365,18 @@ __global__ __launch_bounds__(kConvThreads, 2) void conv3d_wino_kernel(const Conv
   const long long DHW = (long long)HW * a.D;
   const int w = w0 + F * pq;
 #pragma unroll
-  for (int t = 0; t < TD; ++t) {
-    const int d = d0 + t;
+  for (int t = 0; t < C::TDA; ++t) {
+    const int d = C::DP ? d0 + (ci >> 1) : d0 + t;
 #pragma unroll
     for (int j = 0; j < NP; ++j) {
       const int h = h0 + (wave * NP + j) * C::RPG + pr;
       if (d >= a.D || h >= a.H || w >= a.W) continue;
       const int nv = min(F, a.W - w);  // valid outputs of this group
 #pragma unroll
-      for (int m = 0; m < MT; ++m)
+      for (int m = 0; m < C::MTE; ++m)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const int co = co0 + 16 * m + 4 * ci + r;
+          const int co = C::DP ? 4 * (ci & 1) + r : co0 + 16 * m + 4 * ci + r;
           if (co >= a.cout) continue;
           float y[F];
           if constexpr (F == 2) {
@@ -446,6 +460,27 @@ __global__ void pack_wino_kernel(const float* __restrict__ w, float* __restrict_
   }
 }
 
+// depth-paired weights (couts <= 8) -> per chunk: [p * 3 + kh][kw][ci][8 t + c] =
+// W[c][ci][kd = p - t][kh][kw] (zero outside kd in 0..2): staged plane p feeds
+// output plane d0 + t through tap kd = p - t
+__global__ void pack_wino_dp_kernel(const float* __restrict__ w, float* __restrict__ packed, int cout,
+                                    int cin, int nchunks, long long total) {
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
+       i += (long long)gridDim.x * blockDim.x) {
+    long long q = i;
+    const int col = (int)(q % 16); q /= 16;
+    const int ci = (int)(q % CIN_B); q /= CIN_B;
+    const int kw = (int)(q % 3); q /= 3;
+    const int step = (int)(q % 12); q /= 12;
+    const int ch = (int)q;  // >= nchunks in the tail pad
+    const int co = col & 7, kd = step / 3 - (col >> 3), kh = step % 3;
+    const int c = ch * CIN_B + ci;
+    packed[i] = (ch < nchunks && co < cout && c < cin && kd >= 0 && kd <= 2)
+                    ? w[(((long long)co * cin + c) * 9 + kd * 3 + kh) * 3 + kw]
+                    : 0.f;
+  }
+}
+
 struct Plan {
   int f, q, mt, np, td;
 };
@@ -459,7 +494,7 @@ inline Plan make_plan(int B, int cout, int D, int H, int W) {
   // two output planes per workgroup unless the volume is too shallow to fill the chip.
   Plan p;
   p.mt = mt_of(cout);
-  const long long ncob = (cout + 16 * p.mt - 1) / (16 * p.mt);
+  const long long ncob = (cout + cop_of(p.mt) - 1) / cop_of(p.mt);
   auto fits = [&](int tw) { return (W + tw - 1) / tw * tw * 10 <= W * 11; };  // <= 10 % padding
   p.f = 2;
   p.q = 16;
@@ -484,6 +519,11 @@ inline Plan make_plan(int B, int cout, int D, int H, int W) {
       p.q = g_override[2] == 8 ? 8 : 16;
     }
   }
+  if (p.mt == 0) {  // depth-paired: F(4,3), one row set, two planes (the instantiated tiles)
+    p.f = 4;
+    p.np = 1;
+    p.td = 2;
+  }
   return p;
 }
 
@@ -506,10 +546,10 @@ inline Plan make_plan(int B, int cout, int D, int H, int W) {
   LEA_WINO_CASE(2, 16, 3, 1, 2, CV) LEA_WINO_CASE(4, 16, 1, 1, 1, CV) LEA_WINO_CASE(4, 16, 1, 1, 2, CV)     \
   LEA_WINO_CASE(4, 16, 2, 1, 1, CV) LEA_WINO_CASE(4, 16, 2, 1, 2, CV) LEA_WINO_CASE(4, 8, 1, 1, 1, CV)      \
   LEA_WINO_CASE(4, 8, 1, 1, 2, CV) LEA_WINO_CASE(4, 8, 2, 1, 1, CV) LEA_WINO_CASE(4, 8, 2, 1, 2, CV)      \
-  LEA_WINO_CASE(4, 8, 3, 1, 1, CV)
+  LEA_WINO_CASE(4, 8, 3, 1, 1, CV) LEA_WINO_CASE(4, 16, 0, 1, 2, CV) LEA_WINO_CASE(4, 8, 0, 1, 2, CV)
 
 int run(const Plan& p, ConvArgs a, int B, hipStream_t st, bool cv) {
-  a.ncob = (a.cout + 16 * p.mt - 1) / (16 * p.mt);
+  a.ncob = (a.cout + cop_of(p.mt) - 1) / cop_of(p.mt);
   if (cv) {
     LEA_WINO_TILES(true)
   } else {
@@ -557,9 +597,9 @@ using namespace lea;
 
 extern "C" size_t lea_conv3d_wino_packed_floats(int cout, int cin) {
   if (cout <= 0 || cin <= 0 || cin % wino::CIN_B != 0) return 0;
-  const int cop = 16 * wino::mt_of(cout);
+  const int mt = wino::mt_of(cout), cop = wino::cop_of(mt), nstep = mt == 0 ? 12 : 9;
   // + one 256-float tail: the kernel stages whole 256-float pieces per chunk
-  return (size_t)((cout + cop - 1) / cop) * (cin / wino::CIN_B) * 9 * 3 * wino::CIN_B * cop + 256;
+  return (size_t)((cout + cop - 1) / cop) * (cin / wino::CIN_B) * nstep * 3 * wino::CIN_B * cop + 256;
 }
 
 extern "C" int lea_conv3d_wino_pack_weights(const float* w, float* packed, int cout, int cin,
@@ -572,6 +612,7 @@ extern "C" int lea_conv3d_wino_pack_weights(const float* w, float* packed, int c
   const int grid = (int)std::min<long long>((total + 255) / 256, 4096);
   hipStream_t st = as_stream(stream);
   switch (wino::mt_of(cout)) {
+    case 0: wino::pack_wino_dp_kernel<<<grid, 256, 0, st>>>(w, packed, cout, cin, cin / wino::CIN_B, total); break;
     case 1: wino::pack_wino_kernel<1><<<grid, 256, 0, st>>>(w, packed, cout, cin, cin / wino::CIN_B, total); break;
     case 3: wino::pack_wino_kernel<3><<<grid, 256, 0, st>>>(w, packed, cout, cin, cin / wino::CIN_B, total); break;
     default: wino::pack_wino_kernel<2><<<grid, 256, 0, st>>>(w, packed, cout, cin, cin / wino::CIN_B, total);

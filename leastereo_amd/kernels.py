@@ -672,9 +672,9 @@ def disparity_metrics(pred: torch.Tensor, gt: torch.Tensor, maxdisp: float, roun
 # ---- Winograd F(2,3)-along-W 3x3x3 convs (csrc/conv3d_wino.hip), fp32 ----
 
 def wino_eligible(cout: int, cin: int, k: int) -> bool:
-    """Layers the Winograd engine takes: k = 3, channels in chunks of 4, and more
-    than 8 output channels (couts <= 8 keep the direct engine's depth pairing)."""
-    return k == 3 and cin % 4 == 0 and cout > 8
+    """Layers the Winograd engine takes: k = 3 and input channels in chunks of 4
+    (couts <= 8 run depth-paired: the couts of two output planes in one 16-row tile)."""
+    return k == 3 and cin % 4 == 0
 
 
 WINO_MIN_VOXELS = 200_000  # below this the direct engine's smaller tiles fill the chip better
@@ -688,7 +688,7 @@ def wino_preferred(b, cout, cin, d, h, w) -> bool:
     32-channel cells stay on the direct engine."""
     if b * d * h * w < WINO_MIN_VOXELS:
         return cout >= 64 and cout % 32 == 0  # small volumes: only wide blocks amortise the tile
-    return cout == 16 or cout == 24 or cout % 32 == 0 or cout % 48 == 0
+    return cout <= 8 or cout == 16 or cout == 24 or cout % 32 == 0 or cout % 48 == 0
 
 
 def wino_mfma_scale(cout: int, name: str) -> float:
@@ -696,6 +696,8 @@ def wino_mfma_scale(cout: int, name: str) -> float:
     kernel's F (first template argument of ``name``), times the padding of cout to
     the engine's 16/32/48-row block."""
     f = int(name.split("<", 1)[1].split(",", 1)[0])  # conv3d_wino_kernel<F, Q, MT, ...>
+    if cout <= 8:  # depth-paired: 12 (plane, kh) steps per 9 taps, 16 rows = 8 couts x 2 planes
+        return (f + 2) / (3.0 * f) * 12 / 9 * 8 / cout
     cop = 16 if cout <= 16 else (48 if cout % 32 != 0 and cout % 48 == 0 else 32)
     return (f + 2) / (3.0 * f) * (-(-cout // cop) * cop) / cout
 

@@ -31,7 +31,10 @@ def _ref(x, w, scale, shift, relu, res=None):
     (1, 16, 16, (4, 5, 127), "acc"), (2, 128, 64, (5, 9, 40), "acc"), (1, 16, 16, (7, 33, 17), "acc"),
     (1, 16, 48, (4, 9, 40), None), (1, 32, 96, (3, 6, 21), "res"), (1, 8, 24, (3, 10, 17), None),
     (1, 12, 20, (3, 4, 5), "acc"), (2, 32, 32, (9, 13, 31), "res"), (1, 4, 12, (1, 1, 1), None),
-    (1, 32, 32, (2, 3, 2), "acc")])
+    (1, 32, 32, (2, 3, 2), "acc"),
+    # depth-paired (couts <= 8): odd D (the last pair's second plane masked), D = 1
+    (1, 8, 8, (5, 9, 70), "res"), (2, 16, 8, (4, 7, 33), "acc"), (1, 8, 4, (1, 3, 64), None),
+    (1, 32, 8, (6, 20, 130), None), (1, 8, 8, (3, 12, 320), "acc"), (1, 4, 6, (2, 5, 9), "res")])
 def test_wino_vs_torch(b, cin, cout, shape, mode):
     """Odd and even W (the last pair half-masked), ragged H/D tiles, every epilogue."""
     g = torch.Generator().manual_seed(cin * 7 + cout)
@@ -118,6 +121,19 @@ def test_wino_matches_the_direct_engine_at_full_size():
     w = torch.randn(64, 128, 3, 3, 3, device=DEV, generator=g) / np.sqrt(128 * 27)
     a = kernels.conv3d_bnrelu(x, kernels.pack_conv_weight(w), 64, 3, None, None, relu=False)
     b = kernels.conv3d_bnrelu_wino(x, kernels.pack_conv_weight_wino(w), 64, None, None, relu=False)
+    err = float((a - b).abs().max())
+    assert err <= 1e-4 * float(a.abs().max()), err
+
+
+def test_depth_paired_tile_matches_the_direct_engine_at_full_size():
+    """The L0 8->8 cell op at config 2 (8 channels, 64x192x320): the depth-paired
+    Winograd tile (couts of two planes per 16-row MFMA tile) vs the direct engine."""
+    assert kernels.wino_kernel_name(1, 8, 64, 192, 320) == "conv3d_wino_kernel<4, 16, 0, 1, 2, false>"
+    g = torch.Generator(device=DEV).manual_seed(4)
+    x = torch.randn((1, 8, 64, 192, 320), device=DEV, generator=g)
+    w = torch.randn(8, 8, 3, 3, 3, device=DEV, generator=g) / np.sqrt(8 * 27)
+    a = kernels.conv3d_bnrelu(x, kernels.pack_conv_weight(w), 8, 3, None, None, relu=False)
+    b = kernels.conv3d_bnrelu_wino(x, kernels.pack_conv_weight_wino(w), 8, None, None, relu=False)
     err = float((a - b).abs().max())
     assert err <= 1e-4 * float(a.abs().max()), err
 
