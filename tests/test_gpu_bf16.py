@@ -103,6 +103,22 @@ def test_resample_bf16_vs_torch(src, dst, ac):
     _close(kernels.from_c8(y), want)
 
 
+@pytest.mark.parametrize("src,dst,ac", [((16, 24, 40), (32, 48, 80), True), ((5, 7, 9), (9, 13, 17), True),
+                                        ((8, 12, 20), (16, 24, 40), False), ((9, 13, 17), (5, 7, 9), True),
+                                        ((16, 48, 80), (32, 96, 160), True)])
+def test_resample_bf16_is_the_f32_kernel_rounded(src, dst, ac):
+    """The c8 resample (up and down) evaluates the f32 engine's trilinear expression
+    in the same order: bit-identical after rounding to bf16."""
+    g = torch.Generator().manual_seed(5)
+    x = _bf(torch.randn((1, 16) + src, generator=g)).to(DEV)
+    scale = (torch.rand(16, generator=g) + 0.5).to(DEV)
+    shift = (torch.randn(16, generator=g) * 0.1).to(DEV)
+    got = kernels.from_c8(kernels.resample_trilinear_bf16(kernels.to_c8(x), dst, ac, None, scale, shift,
+                                                          relu=True))
+    want = kernels.resample_trilinear(x, dst, ac, None, scale, shift, relu=True)
+    assert torch.equal(got, want.to(torch.bfloat16).float())
+
+
 def test_tapsum_bf16_matches_f32_on_same_values():
     g = torch.Generator().manual_seed(9)
     q = _bf(torch.randn(1, 32, 8, 12, 20, generator=g)).to(DEV)  # 27 taps + 5 pad channels
