@@ -238,9 +238,11 @@ int lea_conv2d_bnrelu_bf16(const void* x, int64_t x_bstride, const void* w_packe
  * (models/operations_3d.py:31-47, retrain/LEAStereo.py:34-48), computed as
  * y[w..w+F-1] = A^T[(G g) . (B^T x)] per (kd, kh): 2/3 (F = 2) or 1/2 (F = 4, on
  * widths that fill 64-wide tile rows) of the direct form's MFMA products, all in
- * fp32.  Weights are packed by lea_conv3d_wino_pack_weights (a layout of their own);
- * cin (and the first source's channels, and C for the cost volume) must be
- * multiples of 4.                                                              */
+ * fp32.  couts <= 8 run depth-paired (the couts of two output planes share one
+ * 16-row MFMA tile, MT = 0 in the kernel name).  Weights are packed by
+ * lea_conv3d_wino_pack_weights (a layout of their own, ending in a 256-float zero
+ * tail: size the buffer with lea_conv3d_wino_packed_floats); cin (and the first
+ * source's channels, and C for the cost volume) must be multiples of 4.        */
 size_t lea_conv3d_wino_packed_floats(int cout, int cin);
 int lea_conv3d_wino_pack_weights(const float* w, float* packed, int cout, int cin, void* stream);
 int lea_conv3d_bnrelu_wino(const void* x, int64_t x_bstride, const void* x2, int64_t x2_bstride,
@@ -256,7 +258,8 @@ int lea_conv3d_bnrelu_costvolume_wino(const void* left, const void* right, int64
 /* Kernel instantiation the Winograd entries launch for this shape
  * ("conv3d_wino_kernel<F, Q, MT, NP, TD, CV>"); tile override for the tuning tools
  * (np in {1, 2} tile rows per wave, td in {1, 2} planes, f in {0 = planner, 2, 4,
- * 8 = F(4,3) on 32-wide row pairs}; np = 0 resets). */
+ * 8 = F(4,3) on 32-wide row pairs}; np = 0 resets; depth-paired shapes keep np = 1,
+ * td = 2 and F(4,3)). */
 const char* lea_conv3d_wino_kernel_name(int B, int cout, int D, int H, int W, int costvolume);
 int lea_conv3d_wino_set_tile_override(int np, int td, int f);
 
