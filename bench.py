@@ -243,7 +243,10 @@ def main():
     tf_file = os.path.join(REPO, "profiles", "hbm_traffic.json")
     if os.path.exists(tf_file):
         with open(tf_file) as f:
-            traffic = json.load(f).get(dominant, {}).get("bytes_per_launch")
+            tf = json.load(f)
+        # per-config entries (tools/traffic_merge.py) first: bytes per launch depend on shapes
+        cfg_name = next((k for k, v in CONFIGS.items() if all(getattr(args, f) == x for f, x in v.items())), None)
+        traffic = (tf.get(f"{dominant}@{cfg_name}") or tf.get(dominant, {})).get("bytes_per_launch")
 
     bf16 = args.precision == "bf16"
     peak = BF16_MFMA_PEAK_TFLOPS if bf16 else FP32_MFMA_PEAK_TFLOPS
