@@ -146,6 +146,8 @@ def test_model_uses_the_winograd_engine():
     ex = m.matching.executor()
     wino = {n for n, p in ex.p.items() if p.wino is not None}
     assert executor.WINOGRAD and {"stem0", "stem1", "conv1", "conv2"} <= wino
+    # the L0 8-channel cell ops run depth-paired on the same engine
+    assert any(ex.p[n].cout <= 8 and ex.p[n].k == 3 for n in wino)
 
 
 def test_e2e_golden_with_every_eligible_layer_on_winograd(monkeypatch):
