@@ -9,7 +9,7 @@ import sys
 
 f = glob.glob(f"{sys.argv[1]}/**/*kernel_trace.csv", recursive=True)[0]
 rows = sorted(csv.DictReader(open(f)), key=lambda r: int(r["Start_Timestamp"]))
-disp = [i for i, r in enumerate(rows) if "disparity_f32" in r["Kernel_Name"]]
+disp = [i for i, r in enumerate(rows) if "disparity" in r["Kernel_Name"] and "_f32" in r["Kernel_Name"]]
 seg = rows[disp[-2] + 1: disp[-1] + 1]
 t0, t1 = int(rows[disp[-2]]["End_Timestamp"]), int(rows[disp[-1]]["End_Timestamp"])
 busy = sum(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in seg)
