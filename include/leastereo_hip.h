@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define LEA_ABI_VERSION 5
+#define LEA_ABI_VERSION 6
 
 #define LEA_F32 0
 #define LEA_BF16 1
@@ -262,6 +262,13 @@ int lea_conv3d_bnrelu_costvolume_wino(const void* left, const void* right, int64
  * td = 2 and F(4,3)). */
 const char* lea_conv3d_wino_kernel_name(int B, int cout, int D, int H, int W, int costvolume);
 int lea_conv3d_wino_set_tile_override(int np, int td, int f);
+/* Engine variant for the Winograd entries (same packed weights): 0 = the planner's
+ * choice, 1 = F(4,3) along W only, 2..4 = F(4,3) along W x F(2,3) along D
+ * (csrc/conv3d_wino2.hip: "conv3d_wino2_kernel<Q, WC, MTE, NW, OCC, CV>") where the
+ * cout block allows it (16 or 32 couts per block): 2 = four waves of one 16-row
+ * cout tile, 3 = eight waves, 4 = two cout tiles per wave at one wave per SIMD.
+ * Per calling thread, like the tile override. */
+int lea_conv3d_wino_set_variant(int variant);
 
 /* ---- host steps either side of forward ---- */
 

@@ -12,7 +12,7 @@ LIB_PATH = os.environ.get(
     "LEASTEREO_HIP_LIB",
     os.path.join(os.path.dirname(os.path.abspath(__file__)), "libleastereo_hip.so"))
 
-ABI_VERSION = 5
+ABI_VERSION = 6
 LEA_F32 = 0
 LEA_BF16 = 1
 LEA_RELU = 1
@@ -78,6 +78,7 @@ SIGNATURES = {
                                                _i, _i, _i, _u, _i, _p]),
     "lea_conv3d_wino_kernel_name": (ctypes.c_char_p, [_i, _i, _i, _i, _i, _i]),
     "lea_conv3d_wino_set_tile_override": (_i, [_i, _i, _i]),
+    "lea_conv3d_wino_set_variant": (_i, [_i]),
     # host steps either side of forward: predict.py load_data/test_transform, metrics
     "lea_standardize_workspace_bytes": (ctypes.c_size_t, [_i]),
     "lea_standardize_crop_u8": (_i, [_p, _p, _i, _i, _i, _i, _p, _p, _i, _i, _p, _p]),

@@ -42,45 +42,10 @@
 // Within a chunk the 9 (kd, kh) steps are software-pipelined: LDS reads two steps
 // ahead, the V / U transforms one step ahead, so a step's VALU issues under the
 // previous step's MFMAs.
-#include "conv3d_impl.h"
+#include "wino_common.h"
 
 namespace lea {
 namespace wino {
-
-constexpr int CIN_B = 4;
-
-// 16-row MFMA tiles per cout block: 16, 32 or 48 couts (48 for 48k couts that are not
-// multiples of 32: the L1 16->48 sibling groups would pad a 64-row block by a third)
-// MT = 0: the depth-paired block for couts <= 8 -- one 16-row tile holding the couts
-// of TWO output planes (as the direct engine's KD = 4 tile, conv3d_impl.h)
-__host__ __device__ constexpr int mt_of(int cout) {
-  return cout <= 8 ? 0 : cout <= 16 ? 1 : (cout % 32 != 0 && cout % 48 == 0) ? 3 : 2;
-}
-__host__ __device__ constexpr int cop_of(int mt) { return 16 * (mt > 0 ? mt : 1); }
-
-// Lane group (16 lanes of one input channel) -> output groups: Q groups of F outputs
-// per tile row and 16/Q rows (Q = 8 lets F(4,3) tile a 32-wide row pair).
-template <int F, int Q>
-__host__ __device__ constexpr int lane_dword(int lane, int cis, int rw) {
-  return (lane >> 4) * cis + ((lane & 15) / Q) * rw + F * ((lane & 15) % Q);
-}
-// The two channels of a 32-lane ds_read_b64 group must hit disjoint banks: pick the
-// smallest even channel stride >= img for which the first read's 64 dwords of lanes
-// 0..31 fall on 64 distinct banks.
-template <int F, int Q>
-__host__ __device__ constexpr int conflict_free_cis(int img, int rw) {
-  for (int cis = img + (img & 1);; cis += 2) {
-    bool used[64] = {};
-    bool ok = true;
-    for (int l = 0; l < 32 && ok; ++l)
-      for (int k = 0; k < 2 && ok; ++k) {
-        const int bank = (lane_dword<F, Q>(l, cis, rw) + k) % 64;
-        ok = !used[bank];
-        used[bank] = true;
-      }
-    if (ok) return cis;
-  }
-}
 
 template <int F, int Q, int MT, int NP, int TD>
 struct Cfg {
@@ -110,28 +75,6 @@ struct Cfg {
   static_assert(XS % 4 == 0 && WS % 4 == 0 && RW % 2 == 0 && PLANE % 2 == 0, "aligned LDS regions and b64 reads");
   static_assert(2 * STAGE * 4 * 2 <= 160 * 1024, "two double-buffered workgroups per CU");
 };
-
-// LDS-DMA pieces as inline asm: with the builtins hipcc treats every in-flight
-// DMA as a possible write to any LDS word and waits vmcnt(0) before the first
-// ds_read of each chunk -- i.e. for the NEXT chunk's halo, which de-pipelines the
-// double buffer (r01 PMC: 17 % of wave cycles parked).  As asm they are invisible
-// to its wait bookkeeping; the kernel's own vmcnt(0) + barrier at the chunk head is
-// the one wait they need.  M0 (the LDS destination base) is saved and restored.
-__device__ __forceinline__ unsigned lds_addr(const float* p) {
-  return __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)(lds_void*)p);
-}
-__device__ __forceinline__ void dma_dword(__amdgpu_buffer_rsrc_t rs, unsigned voff, unsigned lds) {
-  unsigned keep;
-  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dword %1, %2, 0 offen lds\n\ts_mov_b32 m0, %0"
-               : "=&s"(keep) : "v"(voff), "s"(rs), "s"(lds) : "memory");
-}
-__device__ __forceinline__ void dma_dwordx4(const float* src, unsigned lds) {
-  unsigned keep;
-  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
-               : "=&s"(keep) : "v"(src), "s"(lds) : "memory");
-}
-
-__device__ __forceinline__ int a_col(int m, int ci, int n, bool swz) { return ((swz ? (m ^ (ci & 1)) : m) * 16) + n; }
 
 template <int F, int Q, int MT, int NP, int TD, bool CV>
 __global__ __launch_bounds__(kConvThreads, 2) void conv3d_wino_kernel(const ConvArgs a) {
@@ -483,9 +426,42 @@ __global__ void pack_wino_dp_kernel(const float* __restrict__ w, float* __restri
 
 struct Plan {
   int f, q, mt, np, td;
+  bool d2;   // two-dimensional engine (conv3d_wino2.hip) with tile p2
+  Plan2 p2;
 };
 
 thread_local int g_override[3] = {0, 0, 0};  // np, td, f (lea_conv3d_wino_set_tile_override)
+// lea_conv3d_wino_set_variant: 0 = the planner's choice (5), 1 = F(4,3)-along-W engine only,
+// 2..4 = the W x D engine's tiles where it applies (2: four waves, one cout tile each;
+// 3: eight waves; 4: two cout tiles per wave at one wave per SIMD), 5..7 = the same
+// with the inputs transformed once per chunk into LDS (32-cout blocks; 16-cout blocks
+// keep 2)
+thread_local int g_variant = 0;
+
+// W x D engine tile for variant v (2..4), or nullptr-equivalent (q = 0) when the
+// layer's cout block has no such tile (couts <= 8 and the 48-row blocks stay 1-D)
+inline Plan2 plan2(int v, int mt, int q) {
+  Plan2 t{0, 0, 0, 0, 0, false};
+  if (mt != 1 && mt != 2) return t;
+  if (v >= 5) {
+    t.pv = mt == 2;
+    v -= 3;
+  }
+  t.q = q;
+  t.mte = 1;
+  t.wc = mt;
+  t.nw = 4;
+  t.occ = 2;
+  if (v == 3 && mt == 2) t.nw = 8;
+  if (v == 4 && mt == 2) {
+    t.wc = 1;
+    t.mte = 2;
+    t.occ = 1;
+  }
+  if (t.q == 16 && t.wc == 2 && t.nw == 4) t.q = 8;  // 64-wide rows would leave a 2-row tile
+  if (t.pv) t.q = 8;  // the transformed 64-wide halo does not fit beside the stages
+  return t;
+}
 
 inline Plan make_plan(int B, int cout, int D, int H, int W) {
   // r01 sweeps (tools/wino_sweep.py, profiles/r01_wino_sweep*.txt): F(4,3) on
@@ -524,6 +500,16 @@ inline Plan make_plan(int B, int cout, int D, int H, int W) {
     p.np = 1;
     p.td = 2;
   }
+  p.d2 = false;
+  // r02 sweep (tools/wino2_sweep.py, profiles/r02_wino2_sweep.txt): the W x D engine
+  // with the per-chunk transform pass wins on every 32-cout block (stem0 -14 %,
+  // conv1/2 -14 %), the per-lane form on the 16-cout L1 cells (-11 %)
+  // (a 1-D tile override from the tuning tools keeps the planner on the 1-D engine)
+  const int v = g_variant == 0 ? (g_override[0] > 0 ? 1 : 5) : g_variant;
+  if (v >= 2) {
+    p.p2 = plan2(v, p.mt, fits(64) ? 16 : 8);
+    p.d2 = p.p2.q > 0;
+  }
   return p;
 }
 
@@ -549,6 +535,7 @@ inline Plan make_plan(int B, int cout, int D, int H, int W) {
   LEA_WINO_CASE(4, 8, 3, 1, 1, CV) LEA_WINO_CASE(4, 16, 0, 1, 2, CV) LEA_WINO_CASE(4, 8, 0, 1, 2, CV)
 
 int run(const Plan& p, ConvArgs a, int B, hipStream_t st, bool cv) {
+  if (p.d2) return run2(p.p2, a, B, st, cv);
   a.ncob = (a.cout + cop_of(p.mt) - 1) / cop_of(p.mt);
   if (cv) {
     LEA_WINO_TILES(true)
@@ -562,6 +549,7 @@ int run(const Plan& p, ConvArgs a, int B, hipStream_t st, bool cv) {
 thread_local char g_name[96];
 
 const char* name(const Plan& p, bool cv) {
+  if (p.d2) return name2(p.p2, cv);
   snprintf(g_name, sizeof(g_name), "conv3d_wino_kernel<%d, %d, %d, %d, %d, %s>", p.f, p.q, p.mt, p.np,
            p.td, cv ? "true" : "false");
   return g_name;
@@ -636,6 +624,13 @@ extern "C" int lea_conv3d_wino_set_tile_override(int np, int td, int f) {
   wino::g_override[0] = np;
   wino::g_override[1] = td;
   wino::g_override[2] = f;
+  return 0;
+}
+
+extern "C" int lea_conv3d_wino_set_variant(int variant) {
+  clear_error();
+  LEA_CHECK_ARG(variant >= 0 && variant <= 7, "lea_conv3d_wino_set_variant: bad variant %d", variant);
+  wino::g_variant = variant;
   return 0;
 }
 

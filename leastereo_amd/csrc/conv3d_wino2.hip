@@ -1,0 +1,464 @@
+// ConvBR3d k=3 (fp32) with two-dimensional Winograd: F(4,3) along W x F(2,3) along D
+// on the fp32 matrix cores.  Replaces models/operations_3d.py:31-47 for the matching
+// net's 3x3x3 layers, as conv3d_wino.hip (F(4,3) along W only) does, with 2/3 of its
+// MFMA work: per output group of 4 (W) x 2 (D) voxels and kernel row kh,
+//     y[d0 + t][w + j] = sum_{kd, kw} g[kd][kh][kw] x[d0 - 1 + t + kd][w - 1 + j + kw]
+//                      = A_D^T [ A_W^T ( (G_W g G_D^T) . (B_W^T x B_D) ) ]
+// takes 6 x 4 = 24 products per input channel, against 2 planes x 3 kd x 6 = 36 for
+// F(4,3) along W alone and 8 x 9 = 72 for the direct convolution.
+//   W: points 0, +-1, +-2, inf (conv3d_wino.hip's transforms, G's row factors 1/4,
+//      -1/6, -1/6, 1/24, 1/24, 1 applied to the accumulators in the epilogue)
+//   D: F(2,3): B^T x = (x0 - x2, x1 + x2, x2 - x1, x1 - x3),
+//      G g = (g0, (g0+g1+g2)/2, (g0-g1+g2)/2, g2), A^T m = (m0+m1+m2, m1-m2-m3)
+// The two output planes of a group are exactly the TD = 2 planes the 1-D engine
+// stages (4 input planes), so the halo, its LDS-DMA and the weight stage (the raw g
+// rows of a 4-channel chunk) are the 1-D engine's; what changes is the step loop
+// (3 kh steps of 24 points instead of 9 (kd, kh) steps of 6 points x 2 planes) and
+// the accumulators (24 per 16 x 16 tile: 3 per output instead of 1.5).
+//
+// GEMM per point (xi, eta) and kh:
+//     M[xi][eta][co][group] += sum_ci U[xi][eta][kh][co][ci] * V[xi][eta][kh][ci][group]
+// on v_mfma_f32_16x16x4_f32 with the 1-D engine's lane map: A (lane l) = U[co = 16 m +
+// (l & 15)][ci = l >> 4], B (lane l) = V[ci = l >> 4][group = l & 15].  Each lane forms
+// its V from 4 planes x 6 staged inputs (12 ds_read_b64) and U from its cout's 9 g
+// values of the step (B_W per plane row then B_D per point; G_W per kd row then G_D).
+//
+// Workgroup = NW waves = WR row sets x WC cout tiles; a wave owns MTE 16-row cout
+// tiles (MTE = 2 only at one wave per SIMD: 192 accumulator registers).
+#include "wino_common.h"
+
+namespace lea {
+namespace wino {
+
+template <int Q, int WC, int MTE, int NW, int OCC, bool PV>
+struct Cfg2 {
+  static constexpr int F = 4, NX = 6, NE = 4, TD = 2;
+  static constexpr int WR = NW / WC;             // row sets (waves along H)
+  static_assert(WR * WC == NW, "waves = row sets x cout tiles");
+  static constexpr int COP = 16 * WC * MTE;      // couts per workgroup (packed block)
+  static constexpr bool SWZ = (COP % 32) == 0;   // the packer's odd-ci half swap
+  static constexpr int RPG = 16 / Q;             // tile rows per lane group
+  static constexpr int TW = F * Q;               // outputs per tile row
+  static constexpr int TH = WR * RPG;
+  static constexpr int RH = TH + 2, RW = TW + 2;
+  static constexpr int PLANE = RH * RW;
+  static constexpr int PLANES = TD + 2;
+  static constexpr int IMG = PLANES * PLANE;
+  static constexpr int XSLOTS = (IMG + 63) / 64;
+  // channel stride: for the per-lane V path, the 1-D engine's (the two channels of a
+  // 32-lane ds_read_b64 group on disjoint banks); for PV, = 32 mod 64 dwords, which
+  // with RW = 34 puts the transform pass's 32-lane reads (8 groups x 2 rows x 2
+  // channels, see below) on 64 distinct banks
+  static constexpr int CIS = PV ? (64 * XSLOTS + 32) : conflict_free_cis<F, Q>(64 * XSLOTS, RW);
+  static constexpr int XS = CIN_B * CIS;
+  static constexpr int WS = 27 * CIN_B * COP;    // g[kd*3+kh][kw][ci][co] of one chunk
+  static constexpr int WSLOTS = (WS + 255) / 256;
+  static constexpr int STAGE = XS + 256 * WSLOTS;
+  // PV: the chunk's V = B_W^T x B_D for every (channel, halo row, group), formed once
+  // per chunk by the whole workgroup into T[ci][row][group][eta][xi] (24 floats per
+  // group: six ds_read_b128 per lane and step) instead of per lane and step
+  // ds_read_b128 of 16 lanes (4 groups x 2 rows x 2 channels per LDS cycle): groups
+  // 24 floats apart take 8 of the 16 16-B slots of a bank row, a row stride of 4
+  // mod 8 floats the other 8, a channel stride of 0 mod 64 keeps the channel pairs
+  // apart -- conflict-free
+  static constexpr int TRS = Q * 24 + 4;         // floats per halo row
+  static constexpr int TCS = (RH * TRS + 63) / 64 * 64;  // floats per channel
+  static constexpr int TS = PV ? CIN_B * TCS : 0;
+  static constexpr int NUNIT = CIN_B * RH * Q;   // (channel, row, group) transforms per chunk
+  static constexpr int WG_PER_CU = 4 * OCC / NW;
+  static_assert(WG_PER_CU >= 1, "occupancy");
+  static_assert(XS % 4 == 0 && WS % 4 == 0 && RW % 2 == 0 && PLANE % 2 == 0, "aligned LDS regions");
+  static_assert((2 * STAGE + TS) * 4 * WG_PER_CU <= 160 * 1024, "double-buffered stages fit the LDS");
+};
+
+// F(4,3) along W: B^T x of 6 staged inputs, G' g of one kernel row (G without its
+// row factors), A^T (with the factors) of 6 accumulators -> 4 outputs.
+__device__ __forceinline__ void bw4(const float x0, const float x1, const float x2, const float x3,
+                                    const float x4, const float x5, float* v) {
+  const float pa = fmaf(-4.f, x2, x4), pb = fmaf(-4.f, x1, x3);
+  const float pc = x4 - x2, pd = 2.f * (x3 - x1);
+  v[0] = fmaf(4.f, x0, fmaf(-5.f, x2, x4));
+  v[1] = pa + pb;
+  v[2] = pa - pb;
+  v[3] = pc + pd;
+  v[4] = pc - pd;
+  v[5] = fmaf(4.f, x1, fmaf(-5.f, x3, x5));
+}
+__device__ __forceinline__ void gw4(const float g0, const float g1, const float g2, float* u) {
+  const float s = g0 + g2, s4 = fmaf(4.f, g2, g0);
+  u[0] = g0;
+  u[1] = s + g1;
+  u[2] = s - g1;
+  u[3] = fmaf(2.f, g1, s4);
+  u[4] = fmaf(-2.f, g1, s4);
+  u[5] = g2;
+}
+__device__ __forceinline__ void aw4(const float a0, const float a1, const float a2, const float a3,
+                                    const float a4, const float a5, float* y) {
+  const float m0 = 0.25f * a0;
+  const float m1 = (-1.f / 6.f) * a1, m2 = (-1.f / 6.f) * a2;
+  const float m3 = (1.f / 24.f) * a3, m4 = (1.f / 24.f) * a4;
+  const float sp = m1 + m2, sm = m1 - m2, tp = m3 + m4, tm = m3 - m4;
+  y[0] = (m0 + sp) + tp;
+  y[1] = fmaf(2.f, tm, sm);
+  y[2] = fmaf(4.f, tp, sp);
+  y[3] = fmaf(8.f, tm, sm) + a5;
+}
+
+template <int Q, int WC, int MTE, int NW, int OCC, bool PV, bool CV>
+__global__ __launch_bounds__(NW * 64, OCC) void conv3d_wino2_kernel(const ConvArgs a) {
+  using C = Cfg2<Q, WC, MTE, NW, OCC, PV>;
+  constexpr int F = C::F, NX = C::NX, NE = C::NE;
+  constexpr int XSLOTS = C::XSLOTS;
+  constexpr int XSLOTS_W = (XSLOTS + NW - 1) / NW;
+  constexpr int WSLOTS = C::WSLOTS;
+  constexpr int WSLOTS_W = (WSLOTS + NW - 1) / NW;
+  __shared__ __attribute__((aligned(16))) float smem[2 * C::STAGE + C::TS];
+  float* const tv = smem + 2 * C::STAGE;  // PV: the chunk's transformed inputs
+  const unsigned lds0 = lds_addr(smem);
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wc = wave % WC, wr = wave / WC;
+  // XCD-aware 1-D order (as the 1-D engine): each XCD walks a contiguous range of
+  // (batch/cout-block, tile, depth pair), depth pair fastest
+  const int nblk = a.nblk;
+  const int xcd = blockIdx.x % 8, idx = blockIdx.x / 8;
+  const int q8 = nblk / 8, r8 = nblk % 8;
+  const int lin = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + idx;
+  const int dz = lin % a.ndz;
+  const int tile = (lin / a.ndz) % a.ntiles;
+  const int bc = lin / (a.ndz * a.ntiles);
+  const int h0 = (tile / a.tiles_w) * C::TH;
+  const int w0 = (tile % a.tiles_w) * C::TW;
+  const int d0 = dz * C::TD;
+  const int b = bc / a.ncob;
+  const int cob = bc - b * a.ncob;
+  const int co0 = cob * C::COP;
+  const int nchunks = a.cin / CIN_B;
+  const float* wp = a.wp + (long long)cob * nchunks * C::WS;
+  const int HW = a.H * a.W;  // host checks D*H*W*4 < 2^32
+  const unsigned nrec = (unsigned)(HW * a.D) * 4u;
+
+  // per-lane byte offsets of this wave's DMA pieces inside one channel volume
+  unsigned voff[XSLOTS_W], voffr[CV ? XSLOTS_W : 1];
+#pragma unroll
+  for (int t = 0; t < XSLOTS_W; ++t) {
+    const int e = (wave + NW * t) * 64 + lane;
+    unsigned v = 0xFFFFFFF0u, vr = 0xFFFFFFF0u;
+    if (e < C::IMG) {
+      const int p = e / C::PLANE;
+      const int r = e - p * C::PLANE;
+      const int rr = r / C::RW;
+      const int cc = r - rr * C::RW;
+      const int d = d0 + p - 1, h = h0 + rr - 1, w = w0 + cc - 1;
+      if ((unsigned)d < (unsigned)a.D && (unsigned)h < (unsigned)a.H && (unsigned)w < (unsigned)a.W) {
+        if constexpr (CV) {
+          if (w >= d) {
+            v = (unsigned)(h * a.W + w) * 4u;
+            vr = (unsigned)(h * a.W + w - d) * 4u;
+          }
+        } else {
+          v = (unsigned)(d * HW + h * a.W + w) * 4u;
+        }
+      }
+    }
+    voff[t] = v;
+    if constexpr (CV) voffr[t] = vr;
+  }
+
+  auto issue = [&](int ch, float* st) {
+    const float* wsrc = wp + (long long)ch * C::WS;
+    float* wdst = st + C::XS;
+#pragma unroll
+    for (int t = 0; t < WSLOTS_W; ++t) {
+      const int j = wave + NW * t;
+      if (j < WSLOTS)  // the last piece reads into the next chunk / the buffer's tail pad
+        dma_dwordx4(wsrc + j * 256 + lane * 4, lds0 + 4 * (unsigned)(wdst - smem + j * 256));
+    }
+    const long long cvol = CV ? (long long)HW : (long long)HW * a.D;  // channel stride
+    const unsigned crec = CV ? (unsigned)HW * 4u : nrec;
+#pragma unroll
+    for (int ci = 0; ci < CIN_B; ++ci) {
+      const int c = ch * CIN_B + ci;
+      const float* base = a.x;
+      unsigned n = 0;
+      if (c < a.cin1) {
+        base = a.x + (long long)b * a.xbs + (long long)c * cvol;
+        n = crec;
+      } else if (c < a.cin) {
+        base = a.x2 + (long long)b * a.x2bs + (long long)(c - a.cin1) * cvol;
+        n = crec;
+      }
+      const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)base, 0, n, 0x00020000);
+      const unsigned rmask = (CV && c >= a.cin1) ? 0xFFFFFFFFu : 0u;  // chunks never straddle cin1
+#pragma unroll
+      for (int t = 0; t < XSLOTS_W; ++t) {
+        const int j = wave + NW * t;
+        unsigned vo = voff[t];
+        if constexpr (CV) vo = voff[t] ^ ((voff[t] ^ voffr[t]) & rmask);
+        if (j < XSLOTS) dma_dword(rs, vo, lds0 + 4 * (unsigned)(st - smem + ci * C::CIS + j * 64));
+      }
+    }
+  };
+
+  const int ci = lane >> 4, p = lane & 15;
+  const int pq = p % Q, pr = p / Q;  // output group within the row, row within the lane group
+  const int xoff = ci * C::CIS + (wr * C::RPG + pr) * C::RW + F * pq;
+  const int toff = ci * C::TCS + (wr * C::RPG + pr) * C::TRS + 24 * pq;
+  int woff[MTE];
+#pragma unroll
+  for (int m = 0; m < MTE; ++m) woff[m] = ci * C::COP + a_col(wc * MTE + m, ci, p, C::SWZ);
+
+  // folded BN of this lane's couts, fetched now so the epilogue does not wait
+  float sc[MTE][4], sh[MTE][4];
+#pragma unroll
+  for (int m = 0; m < MTE; ++m)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int co = co0 + 16 * (wc * MTE + m) + 4 * ci + r;
+      const bool cv = co < a.cout;
+      sc[m][r] = (cv && a.scale) ? a.scale[co] : 1.f;
+      sh[m][r] = (cv && a.shift) ? a.shift[co] : 0.f;
+    }
+
+  f32x4 acc[NX][NE][MTE];
+#pragma unroll
+  for (int x = 0; x < NX; ++x)
+#pragma unroll
+    for (int e = 0; e < NE; ++e)
+#pragma unroll
+      for (int m = 0; m < MTE; ++m) acc[x][e][m] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  issue(0, smem);
+  for (int ch = 0; ch < nchunks; ++ch) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's pieces of chunk ch landed
+    __syncthreads();  // ... and everyone's; chunk ch-1's stage is free
+    if (ch + 1 < nchunks) issue(ch + 1, smem + ((ch + 1) & 1) * C::STAGE);
+    const float* xs = smem + (ch & 1) * C::STAGE;
+    const float* ws = xs + C::XS;
+    if constexpr (PV) {
+      // the workgroup transforms the chunk's halo once: unit (ci, row, group) reads
+      // 4 planes x 6 inputs and writes its 24 V values
+      static_assert(!PV || (C::RW % 64 == 34 && C::CIS % 64 == 32 && C::RH % 2 == 0 && Q == 8),
+                    "transform pass bank map");
+      for (int u = tid; u < C::NUNIT; u += NW * 64) {
+        // 32 consecutive units = 8 groups x 2 rows x 2 channels: the b64 reads' dword
+        // offsets 4 g + {0, RW, CIS, RW + CIS} cover the 64 banks once
+        const int g = u % Q, t = u / Q;
+        const int rl = t & 1, cl = (t >> 1) & 1, t2 = t >> 2;
+        const int r = 2 * (t2 % (C::RH / 2)) + rl, c = 2 * (t2 / (C::RH / 2)) + cl;
+        float bw[C::PLANES][NX];
+#pragma unroll
+        for (int pl = 0; pl < C::PLANES; ++pl) {
+          const float* sp = xs + c * C::CIS + pl * C::PLANE + r * C::RW + F * g;
+          const float2 a0 = *reinterpret_cast<const float2*>(sp);
+          const float2 a1 = *reinterpret_cast<const float2*>(sp + 2);
+          const float2 a2 = *reinterpret_cast<const float2*>(sp + 4);
+          bw4(a0.x, a0.y, a1.x, a1.y, a2.x, a2.y, bw[pl]);
+        }
+        float v[NE][NX];
+#pragma unroll
+        for (int x = 0; x < NX; ++x) {
+          v[0][x] = bw[0][x] - bw[2][x];
+          v[1][x] = bw[1][x] + bw[2][x];
+          v[2][x] = bw[2][x] - bw[1][x];
+          v[3][x] = bw[1][x] - bw[3][x];
+        }
+        float4* tp = reinterpret_cast<float4*>(tv + c * C::TCS + r * C::TRS + 24 * g);
+        const float* vf = &v[0][0];
+#pragma unroll
+        for (int k = 0; k < 6; ++k) tp[k] = make_float4(vf[4 * k], vf[4 * k + 1], vf[4 * k + 2], vf[4 * k + 3]);
+      }
+      __syncthreads();
+    }
+    // one kh step: the inputs (4 planes x 6 staged values as float2s, or the 24
+    // pre-transformed V as float4s) and the 9 g values (kd, kw) per cout tile
+    struct Raw {
+      float2 x2[PV ? 1 : C::PLANES][3];
+      float4 v4[PV ? 6 : 1];
+      float g[9][MTE];
+    };
+    auto load_step = [&](int kh, Raw& o) {
+      if constexpr (PV) {
+        const float4* tp = reinterpret_cast<const float4*>(tv + toff + kh * C::TRS);
+#pragma unroll
+        for (int k = 0; k < 6; ++k) o.v4[k] = tp[k];
+      } else {
+#pragma unroll
+        for (int pl = 0; pl < C::PLANES; ++pl) {
+          const float* sp = xs + xoff + pl * C::PLANE + kh * C::RW;
+#pragma unroll
+          for (int q = 0; q < 3; ++q) o.x2[pl][q] = *reinterpret_cast<const float2*>(sp + 2 * q);
+        }
+      }
+#pragma unroll
+      for (int kd = 0; kd < 3; ++kd)
+#pragma unroll
+        for (int kw = 0; kw < 3; ++kw)
+#pragma unroll
+          for (int m = 0; m < MTE; ++m)
+            o.g[kd * 3 + kw][m] = ws[((kd * 3 + kh) * 3 + kw) * CIN_B * C::COP + woff[m]];
+    };
+    struct Xf {
+      float v[NX][NE];
+      float u[NX][NE][MTE];
+    };
+    auto xform = [&](const Raw& o, Xf& T) {
+      if constexpr (PV) {
+#pragma unroll
+        for (int k = 0; k < 6; ++k) {
+          const float e4[4] = {o.v4[k].x, o.v4[k].y, o.v4[k].z, o.v4[k].w};
+#pragma unroll
+          for (int i = 0; i < 4; ++i) T.v[(4 * k + i) % NX][(4 * k + i) / NX] = e4[i];
+        }
+      } else {
+        float bw[C::PLANES][NX];
+#pragma unroll
+        for (int pl = 0; pl < C::PLANES; ++pl)
+          bw4(o.x2[pl][0].x, o.x2[pl][0].y, o.x2[pl][1].x, o.x2[pl][1].y, o.x2[pl][2].x, o.x2[pl][2].y, bw[pl]);
+#pragma unroll
+        for (int x = 0; x < NX; ++x) {
+          T.v[x][0] = bw[0][x] - bw[2][x];
+          T.v[x][1] = bw[1][x] + bw[2][x];
+          T.v[x][2] = bw[2][x] - bw[1][x];
+          T.v[x][3] = bw[1][x] - bw[3][x];
+        }
+      }
+#pragma unroll
+      for (int m = 0; m < MTE; ++m) {
+        float uw[3][NX];
+#pragma unroll
+        for (int kd = 0; kd < 3; ++kd) gw4(o.g[kd * 3][m], o.g[kd * 3 + 1][m], o.g[kd * 3 + 2][m], uw[kd]);
+#pragma unroll
+        for (int x = 0; x < NX; ++x) {
+          const float s = uw[0][x] + uw[2][x];
+          T.u[x][0][m] = uw[0][x];
+          T.u[x][1][m] = s + uw[1][x];
+          T.u[x][2][m] = s - uw[1][x];
+          T.u[x][3][m] = uw[2][x];
+        }
+      }
+    };
+    auto mfmas = [&](const Xf& T) {
+#pragma unroll
+      for (int x = 0; x < NX; ++x)
+#pragma unroll
+        for (int e = 0; e < NE; ++e)
+#pragma unroll
+          for (int m = 0; m < MTE; ++m)
+            acc[x][e][m] = __builtin_amdgcn_mfma_f32_16x16x4f32(T.u[x][e][m], T.v[x][e], acc[x][e][m], 0, 0, 0);
+    };
+    // 3 kh steps: LDS reads two steps ahead, transforms one step ahead
+    Raw raw[2];
+    Xf xf[2];
+    load_step(0, raw[0]);
+    load_step(1, raw[1]);
+    xform(raw[0], xf[0]);
+    load_step(2, raw[0]);
+    xform(raw[1], xf[1]);
+    mfmas(xf[0]);
+    xform(raw[0], xf[0]);
+    mfmas(xf[1]);
+    mfmas(xf[0]);
+  }
+
+  // epilogue: A_W^T per D point, A_D^T (with G_D's 1/2 factors), folded BN, ReLU,
+  // residual; the lane stores 4 outputs along W for each of the two planes
+  const bool relu = a.flags & LEA_RELU, resid = a.flags & LEA_RESIDUAL;
+  const long long DHW = (long long)HW * a.D;
+  const int w = w0 + F * pq;
+  const int h = h0 + wr * C::RPG + pr;
+  if (h >= a.H || w >= a.W) return;
+  const int nv = min(F, a.W - w);  // valid outputs of this group
+#pragma unroll
+  for (int m = 0; m < MTE; ++m)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int co = co0 + 16 * (wc * MTE + m) + 4 * ci + r;
+      if (co >= a.cout) continue;
+      float n[NE][F];
+#pragma unroll
+      for (int e = 0; e < NE; ++e)
+        aw4(acc[0][e][m][r], acc[1][e][m][r], acc[2][e][m][r], acc[3][e][m][r], acc[4][e][m][r],
+            acc[5][e][m][r], n[e]);
+#pragma unroll
+      for (int t = 0; t < C::TD; ++t) {
+        const int d = d0 + t;
+        if (d >= a.D) break;
+        float y[F];
+#pragma unroll
+        for (int j = 0; j < F; ++j) {
+          const float s = t == 0 ? 0.5f * (n[1][j] + n[2][j]) : 0.5f * (n[1][j] - n[2][j]);
+          y[j] = t == 0 ? n[0][j] + s : s - n[3][j];
+          y[j] = y[j] * sc[m][r] + sh[m][r];
+          if (relu) y[j] = fmaxf(y[j], 0.f);
+        }
+        const long long o = (long long)co * DHW + (long long)d * HW + (long long)h * a.W + w;
+        float* yp = a.y + (long long)b * a.ybs + o;
+        const float* rp = a.res + (long long)b * a.rbs + o;
+        const bool vec = nv == F &&
+            ((reinterpret_cast<uintptr_t>(yp) | (resid ? reinterpret_cast<uintptr_t>(rp) : 0)) & 15) == 0;
+        if (vec) {
+          if (resid) {
+            const float4 rv = *reinterpret_cast<const float4*>(rp);
+            y[0] += rv.x;
+            y[1] += rv.y;
+            y[2] += rv.z;
+            y[3] += rv.w;
+          }
+          *reinterpret_cast<float4*>(yp) = make_float4(y[0], y[1], y[2], y[3]);
+        } else {
+#pragma unroll
+          for (int j = 0; j < F; ++j)
+            if (j < nv) {
+              if (resid) y[j] += rp[j];
+              yp[j] = y[j];
+            }
+        }
+      }
+    }
+}
+
+thread_local char g_name2[96];
+
+#define LEA_WINO2_CASE(Q, WC, MTE, NW, OCC, PV, CV)                                                \
+  if (p.q == Q && p.wc == WC && p.mte == MTE && p.nw == NW && p.occ == OCC && p.pv == PV) {        \
+    using C_ = Cfg2<Q, WC, MTE, NW, OCC, PV>;                                                      \
+    a.ncob = (a.cout + C_::COP - 1) / C_::COP;                                                     \
+    a.tiles_w = (a.W + C_::TW - 1) / C_::TW;                                                       \
+    a.ntiles = a.tiles_w * ((a.H + C_::TH - 1) / C_::TH);                                          \
+    a.ndz = (a.D + C_::TD - 1) / C_::TD;                                                           \
+    const long long n_ = (long long)a.ntiles * a.ndz * B * a.ncob;                                 \
+    LEA_CHECK_ARG(n_ < (1LL << 31), "lea_conv3d(wino2): grid too large");                          \
+    a.nblk = (int)n_;                                                                              \
+    conv3d_wino2_kernel<Q, WC, MTE, NW, OCC, PV, CV><<<dim3((unsigned)n_), NW * 64, 0, st>>>(a);   \
+    return launch_status("lea_conv3d(wino2)");                                                    \
+  }
+#define LEA_WINO2_TILES(CV)                                                                        \
+  LEA_WINO2_CASE(8, 1, 1, 4, 2, false, CV) LEA_WINO2_CASE(8, 2, 1, 4, 2, false, CV)                \
+  LEA_WINO2_CASE(8, 2, 1, 8, 2, false, CV) LEA_WINO2_CASE(8, 1, 2, 4, 1, false, CV)                \
+  LEA_WINO2_CASE(16, 1, 1, 4, 2, false, CV) LEA_WINO2_CASE(16, 2, 1, 8, 2, false, CV)              \
+  LEA_WINO2_CASE(16, 1, 2, 4, 1, false, CV) LEA_WINO2_CASE(8, 2, 1, 4, 2, true, CV)                \
+  LEA_WINO2_CASE(8, 2, 1, 8, 2, true, CV) LEA_WINO2_CASE(8, 1, 2, 4, 1, true, CV)
+
+int run2(const Plan2& p, ConvArgs a, int B, hipStream_t st, bool cv) {
+  if (cv) {
+    LEA_WINO2_TILES(true)
+  } else {
+    LEA_WINO2_TILES(false)
+  }
+  set_error("lea_conv3d(wino2): no tile q=%d wc=%d mte=%d nw=%d occ=%d pv=%d", p.q, p.wc, p.mte, p.nw,
+            p.occ, (int)p.pv);
+  return LEA_E_UNSUPPORTED;
+}
+
+const char* name2(const Plan2& p, bool cv) {
+  snprintf(g_name2, sizeof(g_name2), "conv3d_wino2_kernel<%d, %d, %d, %d, %d, %s, %s>", p.q, p.wc, p.mte,
+           p.nw, p.occ, p.pv ? "true" : "false", cv ? "true" : "false");
+  return g_name2;
+}
+
+}  // namespace wino
+}  // namespace lea

@@ -1,0 +1,80 @@
+// Shared pieces of the Winograd conv engines (conv3d_wino.hip: F(2,3) / F(4,3)
+// along W; conv3d_wino2.hip: F(4,3) along W x F(2,3) along D): the lane -> output
+// group map, the bank-conflict-free channel stride of the staged halo, and the
+// LDS-DMA issue as inline asm.
+#pragma once
+#include "conv3d_impl.h"
+
+namespace lea {
+namespace wino {
+
+constexpr int CIN_B = 4;
+
+// 16-row MFMA tiles per cout block: 16, 32 or 48 couts (48 for 48k couts that are not
+// multiples of 32: the L1 16->48 sibling groups would pad a 64-row block by a third)
+// MT = 0: the depth-paired block for couts <= 8 -- one 16-row tile holding the couts
+// of TWO output planes (as the direct engine's KD = 4 tile, conv3d_impl.h)
+__host__ __device__ constexpr int mt_of(int cout) {
+  return cout <= 8 ? 0 : cout <= 16 ? 1 : (cout % 32 != 0 && cout % 48 == 0) ? 3 : 2;
+}
+__host__ __device__ constexpr int cop_of(int mt) { return 16 * (mt > 0 ? mt : 1); }
+
+// Lane group (16 lanes of one input channel) -> output groups: Q groups of F outputs
+// per tile row and 16/Q rows (Q = 8 lets F(4,3) tile a 32-wide row pair).
+template <int F, int Q>
+__host__ __device__ constexpr int lane_dword(int lane, int cis, int rw) {
+  return (lane >> 4) * cis + ((lane & 15) / Q) * rw + F * ((lane & 15) % Q);
+}
+// The two channels of a 32-lane ds_read_b64 group must hit disjoint banks: pick the
+// smallest even channel stride >= img for which the first read's 64 dwords of lanes
+// 0..31 fall on 64 distinct banks.
+template <int F, int Q>
+__host__ __device__ constexpr int conflict_free_cis(int img, int rw) {
+  for (int cis = img + (img & 1);; cis += 2) {
+    bool used[64] = {};
+    bool ok = true;
+    for (int l = 0; l < 32 && ok; ++l)
+      for (int k = 0; k < 2 && ok; ++k) {
+        const int bank = (lane_dword<F, Q>(l, cis, rw) + k) % 64;
+        ok = !used[bank];
+        used[bank] = true;
+      }
+    if (ok) return cis;
+  }
+}
+
+// LDS-DMA pieces as inline asm: with the builtins hipcc treats every in-flight
+// DMA as a possible write to any LDS word and waits vmcnt(0) before the first
+// ds_read of each chunk -- i.e. for the NEXT chunk's halo, which de-pipelines the
+// double buffer (r01 PMC: 17 % of wave cycles parked).  As asm they are invisible
+// to its wait bookkeeping; the kernel's own vmcnt(0) + barrier at the chunk head is
+// the one wait they need.  M0 (the LDS destination base) is saved and restored.
+__device__ __forceinline__ unsigned lds_addr(const float* p) {
+  return __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)(lds_void*)p);
+}
+__device__ __forceinline__ void dma_dword(__amdgpu_buffer_rsrc_t rs, unsigned voff, unsigned lds) {
+  unsigned keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dword %1, %2, 0 offen lds\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep) : "v"(voff), "s"(rs), "s"(lds) : "memory");
+}
+__device__ __forceinline__ void dma_dwordx4(const float* src, unsigned lds) {
+  unsigned keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep) : "v"(src), "s"(lds) : "memory");
+}
+
+__device__ __forceinline__ int a_col(int m, int ci, int n, bool swz) { return ((swz ? (m ^ (ci & 1)) : m) * 16) + n; }
+
+// Two-dimensional engine (conv3d_wino2.hip): Q output groups of 4 per tile row,
+// WC cout tiles x (NW / WC) row sets of waves, MTE 16-row cout tiles per wave, OCC
+// waves per SIMD (launch bound), PV = inputs transformed once per chunk into LDS; the packed weights are the 1-D engine's for the
+// block of 16 WC MTE couts.
+struct Plan2 {
+  int q, wc, mte, nw, occ;
+  bool pv;  // V transformed once per chunk into LDS by the workgroup
+};
+int run2(const Plan2& p, ConvArgs a, int B, hipStream_t st, bool cv);
+const char* name2(const Plan2& p, bool cv);
+
+}  // namespace wino
+}  // namespace lea

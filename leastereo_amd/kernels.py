@@ -694,7 +694,12 @@ def wino_preferred(b, cout, cin, d, h, w) -> bool:
 def wino_mfma_scale(cout: int, name: str) -> float:
     """MFMA products issued per direct-convolution product: (F + 2) per 3F for the
     kernel's F (first template argument of ``name``), times the padding of cout to
-    the engine's 16/32/48-row block."""
+    the engine's 16/32/48-row block.  The W x D engine (conv3d_wino2_kernel<Q, WC, MTE,
+    ...>) issues 24 products per 72: 1/3, with couts padded to 16 WC MTE."""
+    if name.startswith("conv3d_wino2_kernel<"):
+        _, wc, mte = (int(t) for t in name.split("<", 1)[1].split(",")[:3])
+        cop = 16 * wc * mte
+        return (-(-cout // cop) * cop) / cout / 3.0
     f = int(name.split("<", 1)[1].split(",", 1)[0])  # conv3d_wino_kernel<F, Q, MT, ...>
     if cout <= 8:  # depth-paired: 12 (plane, kh) steps per 9 taps, 16 rows = 8 couts x 2 planes
         return (f + 2) / (3.0 * f) * 12 / 9 * 8 / cout

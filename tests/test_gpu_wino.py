@@ -150,15 +150,25 @@ def test_model_uses_the_winograd_engine():
     assert any(ex.p[n].cout <= 8 and ex.p[n].k == 3 for n in wino)
 
 
-def test_e2e_golden_with_every_eligible_layer_on_winograd(monkeypatch):
+@pytest.mark.parametrize("variant", [0, 1])
+def test_e2e_golden_with_every_eligible_layer_on_winograd(monkeypatch, variant):
     """The reference's end-to-end golden case (96x192 D48) with the Winograd engine
     forced onto every eligible layer (the size threshold would keep this small
-    case on the direct engine): EPE vs the reference fp32 / fp64 disparity."""
+    case on the direct engine): EPE vs the reference fp32 / fp64 disparity, with the
+    planner's engines (variant 0: W x D where it applies) and F(4,3) along W only."""
+    monkeypatch.setattr(kernels, "WINO_MIN_VOXELS", 0)
+    assert _lib.load().lea_conv3d_wino_set_variant(variant) == 0
+    try:
+        _e2e_golden_cases()
+    finally:
+        _lib.load().lea_conv3d_wino_set_variant(0)
+
+
+def _e2e_golden_cases():
     from leastereo_amd.config import LEAStereoArgs, default_arch_args
     from leastereo_amd.model import LEAStereo
     from oracle import torch_ref as ref
     from tests.golden_util import golden, meta, normal, state_dict
-    monkeypatch.setattr(kernels, "WINO_MIN_VOXELS", 0)
     for name, c in meta()["cases"].items():
         if not name.startswith("e2e/"):
             continue
@@ -192,3 +202,93 @@ def test_graphed_forward_replays_the_eager_result():
         got = g(x, y)
         torch.cuda.synchronize()
         assert torch.equal(got, want)
+
+
+# ---- F(4,3) along W x F(2,3) along D (csrc/conv3d_wino2.hip) ----
+
+@pytest.fixture
+def wino_variant():
+    lib = _lib.load()
+
+    def use(v):
+        assert lib.lea_conv3d_wino_set_variant(v) == 0
+    yield use
+    lib.lea_conv3d_wino_set_variant(0)
+
+
+@pytest.mark.parametrize("variant", [2, 3, 4, 5, 6, 7])
+@pytest.mark.parametrize("b,cin,cout,shape,mode", [
+    (1, 64, 32, (6, 20, 70), None), (1, 32, 32, (5, 9, 320), "acc"), (2, 8, 24, (3, 7, 130), "res"),
+    (1, 16, 16, (4, 5, 127), "acc"), (2, 128, 64, (5, 9, 40), "acc"), (1, 16, 16, (7, 33, 17), "acc"),
+    (1, 12, 20, (3, 4, 5), "acc"), (2, 32, 32, (9, 13, 31), "res"), (1, 4, 12, (1, 1, 1), None),
+    (1, 32, 32, (2, 3, 2), "acc"), (1, 32, 96, (3, 6, 21), "res"), (1, 16, 16, (1, 6, 64), None)])
+def test_wino2_vs_torch(wino_variant, variant, b, cin, cout, shape, mode):
+    """The W x D engine's tiles: odd D (the last pair's second plane masked), D = 1,
+    W not a multiple of 4, ragged H tiles, every epilogue, couts padding a block."""
+    wino_variant(variant)
+    name = kernels.wino_kernel_name(b, cout, *shape)
+    assert name.startswith("conv3d_wino2_kernel<"), name
+    g = torch.Generator().manual_seed(cin * 7 + cout + variant)
+    x = torch.randn((b, cin) + shape, generator=g)
+    w = torch.randn(cout, cin, 3, 3, 3, generator=g) / np.sqrt(cin * 27)
+    scale = torch.rand(cout, generator=g) + 0.5
+    shift = torch.randn(cout, generator=g) * 0.1
+    r = torch.randn((b, cout) + shape, generator=g)
+    want = _ref(x, w, scale, shift, True, r if mode else None)
+    out = r.to(DEV).clone() if mode == "acc" else None
+    y = kernels.conv3d_bnrelu_wino(x.to(DEV), kernels.pack_conv_weight_wino(w.to(DEV)), cout,
+                                   scale.to(DEV), shift.to(DEV), relu=True, out=out,
+                                   accumulate=mode == "acc",
+                                   residual=r.to(DEV) if mode == "res" else None)
+    np.testing.assert_allclose(y.cpu().double().numpy(), want.numpy(), rtol=1e-4, atol=1e-4)
+
+
+@pytest.mark.parametrize("variant", [2, 3, 4, 5, 6, 7])
+def test_wino2_keeps_the_1d_engine_where_it_has_no_tile(wino_variant, variant):
+    """couts <= 8 (depth-paired) and 48-row blocks stay on F(4,3) along W."""
+    wino_variant(variant)
+    assert kernels.wino_kernel_name(1, 8, 64, 192, 320).startswith("conv3d_wino_kernel<")
+    assert kernels.wino_kernel_name(1, 48, 32, 96, 160).startswith("conv3d_wino_kernel<")
+
+
+@pytest.mark.parametrize("variant", [2, 3, 4, 5, 6, 7])
+def test_wino2_costvolume_and_two_sources(wino_variant, variant):
+    """stem0 on the in-place cost volume == the same tile on the built volume (bit for
+    bit); conv1/conv2's two-source read into a channel slice."""
+    wino_variant(variant)
+    g = torch.Generator().manual_seed(5 + variant)
+    fl = torch.randn((2, 32, 12, 40), generator=g).to(DEV)
+    fr = torch.randn((2, 32, 12, 40), generator=g).to(DEV)
+    w = (torch.randn(32, 64, 3, 3, 3, generator=g) / np.sqrt(64 * 27)).to(DEV)
+    packed = kernels.pack_conv_weight_wino(w)
+    scale = torch.rand(32, device=DEV) + 0.5
+    shift = torch.randn(32, device=DEV) * 0.1
+    cost = kernels.build_cost_volume(fl, fr, 45)
+    want = kernels.conv3d_bnrelu_wino(cost, packed, 32, scale, shift)
+    got = kernels.conv3d_bnrelu_costvolume_wino(fl, fr, 45, packed, 32, scale, shift)
+    assert torch.equal(got, want)
+    ref = _ref(cost.cpu(), w.cpu(), scale.cpu(), shift.cpu(), True)
+    np.testing.assert_allclose(got.cpu().double().numpy(), ref.numpy(), rtol=1e-4, atol=1e-4)
+    x = torch.randn((1, 64, 4, 10, 40), generator=g)
+    x2 = torch.randn((1, 64, 4, 10, 40), generator=g)
+    w2 = torch.randn(64, 128, 3, 3, 3, generator=g) / np.sqrt(128 * 27)
+    want = _ref(torch.cat((x, x2), 1), w2, None, None, False)
+    big = torch.zeros((1, 96, 4, 10, 40), device=DEV)
+    kernels.conv3d_bnrelu_wino(x.to(DEV), kernels.pack_conv_weight_wino(w2.to(DEV)), 64, None, None,
+                               relu=False, out=big[:, 16:80], x2=x2.to(DEV))
+    np.testing.assert_allclose(big[:, 16:80].cpu().double().numpy(), want.numpy(), rtol=1e-4, atol=1e-4)
+    assert float(big[:, :16].abs().sum()) == 0 and float(big[:, 80:].abs().sum()) == 0
+
+
+@pytest.mark.parametrize("variant", [2, 3, 4, 5, 6, 7])
+def test_wino2_matches_the_direct_engine_at_full_size(wino_variant, variant):
+    """conv1/conv2 and stem0 at config 2 on the W x D engine vs the direct engine."""
+    wino_variant(variant)
+    g = torch.Generator(device=DEV).manual_seed(3)
+    for cin, cout, shape in ((128, 64, (32, 96, 160)), (64, 32, (64, 192, 320))):
+        x = torch.randn((1, cin) + shape, device=DEV, generator=g)
+        w = torch.randn(cout, cin, 3, 3, 3, device=DEV, generator=g) / np.sqrt(cin * 27)
+        a = kernels.conv3d_bnrelu(x, kernels.pack_conv_weight(w), cout, 3, None, None, relu=False)
+        b = kernels.conv3d_bnrelu_wino(x, kernels.pack_conv_weight_wino(w), cout, None, None, relu=False)
+        err = float((a - b).abs().max())
+        assert err <= 1e-4 * float(a.abs().max()), (cin, cout, err)

@@ -1,10 +1,10 @@
 #!/bin/bash
+# W x D Winograd engine: its parity tests (wino2 cases only), then the variant sweep
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
-timeout -k 10 300 python -u -m pytest tests/test_gpu_wino.py -x -q -m gpu --timeout 120 --timeout-method thread > gpurun_out/pytest_wino.log 2>&1
-rc=$?; tail -3 gpurun_out/pytest_wino.log; [ $rc -eq 0 ] || exit $rc
-timeout -k 10 400 python3 tools/wino_sweep.py --iters 10 > gpurun_out/wino_sweep.txt 2>&1
-rc=$?; grep -v "^{" gpurun_out/wino_sweep.txt | grep -v amdgpu.ids; [ $rc -eq 0 ] || exit $rc
-timeout -k 10 300 python bench.py --steps 20 --warmup 5 --breakdown 1 --cpu-baseline 0 > gpurun_out/bench_c2.json 2> gpurun_out/bench_c2.err
-rc=$?; python3 -c "import json; d=json.load(open('gpurun_out/bench_c2.json')); print(round(d['value'],2), round(d['ms_per_step'],3), d['roofline']['kernel'], d['roofline']['frac'], d['roofline']['mfma_executed_frac'], d['epe_px']['max_over_ranks'])"; grep -v amdgpu.ids gpurun_out/bench_c2.err | head -12; exit $rc
+timeout -k 10 300 python -u -m pytest tests/test_gpu_wino.py -x -q -m gpu -k wino2 --timeout 120 --timeout-method thread \
+  > gpurun_out/pytest_wino2.log 2>&1
+rc=$?; tail -15 gpurun_out/pytest_wino2.log; [ $rc -eq 0 ] || exit $rc
+timeout -k 10 300 python -u tools/wino2_sweep.py --iters 10 ${SWEEP_ARGS:-} > gpurun_out/wino2_sweep.txt 2> gpurun_out/wino2_sweep.err
+rc=$?; grep -v '^{' gpurun_out/wino2_sweep.txt; tail -3 gpurun_out/wino2_sweep.err; exit $rc
