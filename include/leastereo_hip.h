@@ -205,6 +205,10 @@ int lea_conv3d_bnrelu_costvolume_bf16(const void* left, const void* right, int64
  * td planes, mt 16-row tiles per wave -- on the calling thread; th <= 0 restores
  * the planner. */
 int lea_conv3d_bf16_set_tile_override(int th, int td, int mt);
+/* bf16 engine variant: 0 = the planner's choice (single-chunk 3x3x3 layers, cin <= 16,
+ * stream along D: "conv_bf16_stream_kernel<MT, WC, TH, NB>"), 1 = the tile kernel for
+ * every layer.  Per calling thread. */
+int lea_conv3d_bf16_set_variant(int variant);
 
 /* Kernel instantiation the bf16 conv of this shape launches. */
 const char* lea_conv3d_kernel_name_bf16(int B, int cout, int cin, int D, int H, int W, int k,

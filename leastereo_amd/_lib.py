@@ -61,6 +61,7 @@ SIGNATURES = {
                                                _i, _i, _u, _p]),
     "lea_conv3d_kernel_name_bf16": (ctypes.c_char_p, [_i, _i, _i, _i, _i, _i, _i, _i]),
     "lea_conv3d_bf16_set_tile_override": (_i, [_i, _i, _i]),
+    "lea_conv3d_bf16_set_variant": (_i, [_i]),
     "lea_resample3d_trilinear_bf16": (_i, [_p, _i64, _p, _i64, _i, _i, _i, _i, _i, _i, _i, _i,
                                            _i, _p, _p, _u, _p]),
     "lea_to_c8_bf16": (_i, [_p, _i64, _p, _i64, _i, _i, _i64, _p]),

@@ -345,11 +345,240 @@ __global__ __launch_bounds__(256) void resample_c8_kernel(
   }
 }
 
+// ---- D-streaming form for the single-chunk 3x3x3 layers (cin <= 16: the whole K is
+// one chunk).  The tile kernel above stages a (TH+2) x 18 x (TD+2) halo per TH x 16 x TD
+// tile and waits for it: r01 counters put these layers' waves 60-78 % parked on that
+// DMA, with 2.1-2.8x halo re-reads.  Here a workgroup owns one (16 W x TH H) column
+// and walks D two output planes per step through an LDS ring of 8 input planes:
+// step s uses planes 2s-1 .. 2s+2 and issues planes 2s+5, 2s+6 (two steps ahead) as
+// inline-asm LDS-DMA (invisible to the compiler's vmcnt bookkeeping; the kernel
+// waits with counted vmcnt), so each input plane is fetched once per column (halo
+// re-reads (TH+2)/TH along H only) and the fetch of step s+2 overlaps steps s, s+1.
+// The weights (one chunk) sit in registers for the whole walk; the residual /
+// accumulate operand of each step is LDS-DMA'd by the wave that consumes it (no
+// barrier), and BN scale/shift are read once, so no compiler-visible load inside the
+// walk drains the prefetch.
+template <int MT, int WC, int TH, int NB>
+struct SCfg {
+  static constexpr int TD = 2, WV = 4 / WC, VT = TH * TD, NV = VT / WV;
+  static_assert(VT % WV == 0, "rows per wave");
+  static constexpr int T = 27, S = (T * NB + 3) / 4;
+  static constexpr int COB = WC * MT * 16;
+  static constexpr int RH = TH + 2, RW = 18, PLANE = RH * RW;   // 16-B words per plane and block
+  static constexpr int PIECES = (PLANE + 63) / 64;              // 64-word DMA pieces per plane and block
+  static constexpr int PLANEP = 64 * PIECES;
+  static constexpr int SLOTW = NB * PLANEP;                      // words per ring slot
+  static constexpr int PPW = (NB * PIECES + 3) / 4;              // pieces per wave and plane (padded)
+  static constexpr int RING = 8;
+  static constexpr int RESW = MT * 2 * NV * 16;                  // residual words per wave and step
+  static constexpr int RPW = RESW / 64;                          // residual pieces per wave
+  static constexpr int RINGW = RING * SLOTW + 64 * (4 * PPW - NB * PIECES);  // + padding pieces
+  static constexpr int LDSW = RINGW + 4 * 3 * RESW;  // with the residual slots (dynamic LDS)
+  static_assert(RESW % 64 == 0, "whole residual pieces");
+  static_assert(LDSW * 16 <= 160 * 1024, "ring + residual");
+};
+
+__device__ __forceinline__ void dma_x4(__amdgpu_buffer_rsrc_t rs, unsigned voff, unsigned lds) {
+  unsigned keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, 0 offen lds\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep) : "v"(voff), "s"(rs), "s"(lds) : "memory");
+}
+template <int N>
+__device__ __forceinline__ void wait_vm() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+template <int MT, int WC, int TH, int NB>
+__global__ __launch_bounds__(kThreads, 2) void conv_bf16_stream_kernel(const Args a, int nsplit) {
+  using C = SCfg<MT, WC, TH, NB>;
+  extern __shared__ __attribute__((aligned(16))) bf16x8 smem[];  // RINGW (+ residual slots)
+  const unsigned lds0 = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)(lds_void*)smem);
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wc = wave % WC, wv = wave / WC;
+  const int g = lane >> 4, n = lane & 15;
+
+  const int xcd = blockIdx.x % 8, idx = blockIdx.x / 8;
+  const int q8 = a.nblk / 8, r8 = a.nblk % 8;
+  const int lin = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + idx;
+  const int sp = lin % nsplit;
+  const int tile = (lin / nsplit) % a.ntiles;
+  const int bc = lin / (nsplit * a.ntiles);
+  const int b = bc / a.ncob, cob = bc - b * a.ncob;
+  const int h0 = (tile / a.tiles_w) * TH, w0 = (tile % a.tiles_w) * 16;
+  const int HW = a.H * a.W;
+  const int DHW = HW * a.D;
+  const int nst = (a.D + 1) / 2;
+  const int s0 = sp * nst / nsplit, s1 = (sp + 1) * nst / nsplit;
+
+  // DMA pieces of one plane: piece q = wave + 4t -> (block q / PIECES, words 64 (q % PIECES)
+  // + lane); one buffer resource over the batch element's blocks (host: < 4 GiB)
+  unsigned hwo[C::PPW];
+  unsigned ldo[C::PPW];
+#pragma unroll
+  for (int t = 0; t < C::PPW; ++t) {
+    const int q = wave + 4 * t;
+    const int blk = q / C::PIECES, e = (q % C::PIECES) * 64 + lane;
+    unsigned v = 0xFFFFFFF0u;
+    if (q < NB * C::PIECES && e < C::PLANE) {
+      const int rr = e / C::RW, cc = e % C::RW;
+      const int h = h0 + rr - 1, w = w0 + cc - 1;
+      if ((unsigned)h < (unsigned)a.H && (unsigned)w < (unsigned)a.W)
+        v = (unsigned)blk * (unsigned)DHW * 16u + (unsigned)(h * a.W + w) * 16u;
+    }
+    hwo[t] = v;
+    // padding pieces (q >= NB * PIECES) land past the ring
+    ldo[t] = q < NB * C::PIECES ? (unsigned)(blk * C::PLANEP + (q % C::PIECES) * 64)
+                                : (unsigned)(C::RING * C::SLOTW + (q - NB * C::PIECES) * 64);
+  }
+  const __amdgpu_buffer_rsrc_t xrs = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(a.x + (long long)b * a.xbs), 0, (unsigned)(a.cin / 8) * (unsigned)DHW * 16u, 0x00020000);
+  auto load_plane = [&](int d) {  // plane d (zeros outside 0..D-1) -> ring slot d & 7
+    const bool dv = (unsigned)d < (unsigned)a.D;
+    const unsigned slot = (unsigned)(d & 7) * C::SLOTW;
+#pragma unroll
+    for (int t = 0; t < C::PPW; ++t) {
+      const unsigned vo = (dv && hwo[t] != 0xFFFFFFF0u) ? hwo[t] + (unsigned)d * (unsigned)HW * 16u : 0xFFFFFFF0u;
+      const unsigned dst = ldo[t] < (unsigned)(C::RING * C::SLOTW) ? slot + ldo[t] : ldo[t];
+      dma_x4(xrs, vo, lds0 + 16u * dst);
+    }
+  };
+
+  // this wave's residual words per step: (m-tile, block of its 2, row i, column) -> its own
+  // slot; one resource over the batch element's output blocks
+  const bool resid = a.flags & LEA_RESIDUAL;
+  const unsigned resbase = (unsigned)(C::RING * C::SLOTW + 64 * (4 * C::PPW - NB * C::PIECES) + wave * 3 * C::RESW);
+  const __amdgpu_buffer_rsrc_t rrs = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(a.res + (long long)b * a.rbs), 0, (unsigned)((a.cout + 7) / 8) * (unsigned)DHW * 16u, 0x00020000);
+  auto load_res = [&](int s) {  // step s's operand -> this wave's residual slot s % 3
+    const unsigned rslot = resbase + (unsigned)(s % 3) * C::RESW;
+#pragma unroll
+    for (int t = 0; t < C::RPW; ++t) {
+      const int e = t * 64 + lane;  // word: ((m * 2 + blk2) * NV + i) * 16 + col
+      const int col = e % 16, i = (e / 16) % C::NV, mb = e / (16 * C::NV);
+      const int m = mb / 2, blk2 = mb % 2;
+      const int qrow = wv * C::NV + i;
+      const int d = 2 * s + qrow / TH, h = h0 + qrow % TH, w = w0 + col;
+      const int cblk = (cob * C::COB + (wc * MT + m) * 16) / 8 + blk2;
+      unsigned vo = 0xFFFFFFF0u;
+      if (d < a.D && h < a.H && w < a.W && cblk * 8 < a.cout)
+        vo = (unsigned)cblk * (unsigned)DHW * 16u + (unsigned)(d * HW + h * a.W + w) * 16u;
+      dma_x4(rrs, vo, lds0 + 16u * (rslot + (unsigned)t * 64u));
+    }
+  };
+
+  // per-lane K slot geometry: k-step ks, lane group g -> tap (kd, kh, kw), block
+  int kdv[C::S], koff[C::S];
+#pragma unroll
+  for (int ks = 0; ks < C::S; ++ks) {
+    const int slot = 4 * ks + g;
+    const int tap = min(slot / NB, C::T - 1);  // slots past the last tap carry zero weights
+    const int blk = slot % NB;
+    kdv[ks] = tap / 9;
+    koff[ks] = blk * C::PLANEP + ((tap / 3) % 3) * C::RW + tap % 3;
+  }
+  // A fragments of the (single) chunk, resident for the whole walk
+  const int mtile0 = wc * MT;
+  const bf16x8* wpv = reinterpret_cast<const bf16x8*>(a.wp);
+  bf16x8 av[C::S][MT];
+#pragma unroll
+  for (int ks = 0; ks < C::S; ++ks)
+#pragma unroll
+    for (int m = 0; m < MT; ++m)
+      av[ks][m] = wpv[(((long long)cob * C::S + ks) * (WC * MT) + mtile0 + m) * 64 + g * 16 + n];
+  float sc[MT][4], sh[MT][4];
+#pragma unroll
+  for (int m = 0; m < MT; ++m)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int co = cob * C::COB + (mtile0 + m) * 16 + 4 * g + r;
+      sc[m][r] = (a.scale && co < a.cout) ? a.scale[co] : 1.f;
+      sh[m][r] = (a.shift && co < a.cout) ? a.shift[co] : 0.f;
+    }
+  const bool relu = a.flags & LEA_RELU;
+
+  // Pipeline (issue order = completion order for vmcnt): the end of step s issues step
+  // s+2's residual, then planes 2s+5, 2s+6 (into the slots of planes 2s-3, 2s-2, which
+  // only step s-1 read); the top of step s+1 waits for all but those -- i.e. for step
+  // s+1's planes and residual (issued at the end of step s-1) and step s's stores.
+  if (resid) load_res(s0);
+  for (int j = -1; j <= 2; ++j) load_plane(2 * s0 + j);
+  if (resid) load_res(s0 + 1);  // (past s1: a fetch of zeros, keeping the count uniform)
+  load_plane(2 * s0 + 3);
+  load_plane(2 * s0 + 4);
+  for (int s = s0; s < s1; ++s) {
+    if (resid)
+      wait_vm<2 * C::PPW + C::RPW>();
+    else
+      wait_vm<2 * C::PPW>();
+    __syncthreads();  // everyone's planes landed; everyone done with step s-1
+    f32x4 acc[MT][C::NV];
+#pragma unroll
+    for (int m = 0; m < MT; ++m)
+#pragma unroll
+      for (int i = 0; i < C::NV; ++i) acc[m][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+    const int base = 2 * s - 1;
+#pragma unroll
+    for (int ks = 0; ks < C::S; ++ks)
+#pragma unroll
+      for (int i = 0; i < C::NV; ++i) {
+        const int qrow = wv * C::NV + i;
+        const int t = qrow / TH, r = qrow % TH;
+        const int word = ((base + t + kdv[ks]) & 7) * C::SLOTW + koff[ks] + r * C::RW + n;
+        const bf16x8 bv = smem[word];
+#pragma unroll
+        for (int m = 0; m < MT; ++m)
+          acc[m][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[ks][m], bv, acc[m][i], 0, 0, 0);
+      }
+    const unsigned rslot = resbase + (unsigned)(s % 3) * C::RESW;
+#pragma unroll
+    for (int m = 0; m < MT; ++m) {
+      const int co = cob * C::COB + (mtile0 + m) * 16 + 4 * g;
+      if (co >= a.cout) continue;
+      const long long cofs = (long long)(co / 8) * DHW * 8 + (co % 8);
+#pragma unroll
+      for (int i = 0; i < C::NV; ++i) {
+        const int qrow = wv * C::NV + i;
+        const int d = 2 * s + qrow / TH, h = h0 + qrow % TH, w = w0 + n;
+        if (d >= a.D || h >= a.H || w >= a.W) continue;
+        float v[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          v[r] = acc[m][i][r] * sc[m][r] + sh[m][r];
+          if (relu) v[r] = fmaxf(v[r], 0.f);
+        }
+        if (resid) {
+          // word ((m * 2 + 4g / 8) * NV + i) * 16 + n of this wave's slot, bf16 (4g) % 8 on
+          const bf16x4 rv = *reinterpret_cast<const bf16x4*>(
+              reinterpret_cast<const __bf16*>(smem + rslot + ((m * 2 + (4 * g) / 8) * C::NV + i) * 16 + n) + (4 * g) % 8);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) v[r] += (float)rv[r];
+        }
+        bf16x4 out;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) out[r] = (__bf16)v[r];
+        *reinterpret_cast<bf16x4*>(a.y + (long long)b * a.ybs + cofs + ((long long)d * HW + h * a.W + w) * 8) = out;
+      }
+    }
+    if (resid && s + 2 < s1) load_res(s + 2);
+    else if (resid) {  // keep the per-step count uniform: a dummy residual fetch into slot (s+2) % 3
+      const unsigned rslot2 = resbase + (unsigned)((s + 2) % 3) * C::RESW;
+#pragma unroll
+      for (int t = 0; t < C::RPW; ++t) dma_x4(rrs, 0xFFFFFFF0u, lds0 + 16u * (rslot2 + (unsigned)t * 64u));
+    }
+    load_plane(2 * s + 5);
+    load_plane(2 * s + 6);
+  }
+  wait_vm<0>();  // no LDS-DMA may outlive the workgroup
+}
+
 struct Plan {
   int ks, mt, wc, th, td, nb;
+  int nsplit;  // > 0: the D-streaming kernel with nsplit column segments along D
 };
 
 thread_local int g_override[3] = {0, 0, 0};  // th, td, mt (lea_conv3d_bf16_set_tile_override)
+thread_local int g_variant = 0;              // lea_conv3d_bf16_set_variant: 0 planner, 1 tile kernel only
 
 inline Plan plan(int B, int cout, int D, int H, int W, int ks, int cin) {
   // r01 sweep (tools/conv_sweep.py --bf16, profiles/r01_conv_sweep_bf16.txt): one
@@ -378,6 +607,20 @@ inline Plan plan(int B, int cout, int D, int H, int W, int ks, int cin) {
     p.mt = std::min(g_override[2], cobv / 16);
     p.wc = cobv / 16 / p.mt;
   }
+  p.nsplit = 0;
+  if (ks == 3 && cin <= 8 * p.nb && g_variant == 0 && g_override[0] == 0 && D >= 4) {
+    // single-chunk layer: stream along D; column segments so the grid holds >= 6
+    // workgroups per CU, each walking >= 4 steps
+    p.mt = 1;
+    p.wc = cobv / 16;
+    p.th = p.nb == 1 ? 8 : 4;
+    p.td = 2;
+    const long long cols = (long long)((W + 15) / 16) * ((H + p.th - 1) / p.th) * B * ncob;
+    const int nst = (D + 1) / 2;
+    long long ns = (1536 + cols - 1) / cols;
+    ns = std::min<long long>(ns, std::max(1, nst / 4));
+    p.nsplit = (int)std::max<long long>(ns, 1);
+  }
   return p;
 }
 
@@ -399,7 +642,26 @@ inline Plan plan(int B, int cout, int D, int H, int W, int ks, int cin) {
   LEA_BF_TH(KS, 1, 1, TD, NB, CV) LEA_BF_TH(KS, 2, 1, TD, NB, CV) LEA_BF_TH(KS, 1, 2, TD, NB, CV) \
   LEA_BF_TH(KS, 2, 2, TD, NB, CV) LEA_BF_TH(KS, 1, 4, TD, NB, CV)
 
+#define LEA_BFS_CASE(WC, TH, NB)                                                              \
+  if (p.wc == WC && p.th == TH && p.nb == NB) {                                               \
+    a.tiles_w = (a.W + 15) / 16;                                                              \
+    a.ntiles = a.tiles_w * ((a.H + TH - 1) / TH);                                             \
+    const long long nb_ = (long long)a.ntiles * p.nsplit * B * a.ncob;                        \
+    LEA_CHECK_ARG(nb_ < (1LL << 31), "lea_conv3d(bf16 stream): grid too large");              \
+    a.nblk = (int)nb_;                                                                        \
+    using S_ = SCfg<1, WC, TH, NB>;                                                           \
+    const size_t lds_ = (size_t)((a.flags & LEA_RESIDUAL) ? S_::LDSW : S_::RINGW) * 16;       \
+    conv_bf16_stream_kernel<1, WC, TH, NB><<<dim3((unsigned)nb_), kThreads, lds_, st>>>(a, p.nsplit); \
+    return launch_status("lea_conv3d(bf16 stream)");                                         \
+  }
+
 int run(const Plan& p, Args a, int B, hipStream_t st, bool cv) {
+  if (p.nsplit > 0 && !cv && a.cb1 * 8 == a.cin) {  // (one source: the ring walks one tensor)
+    LEA_CHECK_ARG((long long)std::max(a.cin, a.cout + 7) / 8 * a.D * a.H * a.W * 16 < 0xFFFFFFF0LL,
+                  "lea_conv3d(bf16 stream): volume too large");
+    LEA_BFS_CASE(1, 8, 1) LEA_BFS_CASE(2, 8, 1) LEA_BFS_CASE(4, 8, 1)
+    LEA_BFS_CASE(1, 4, 2) LEA_BFS_CASE(2, 4, 2) LEA_BFS_CASE(4, 4, 2)
+  }
   if (cv) {
     LEA_BF_MT(3, 2, 2, true)
     LEA_BF_MT(3, 1, 2, true)
@@ -459,6 +721,13 @@ extern "C" int lea_conv3d_bf16_set_tile_override(int th, int td, int mt) {
   return 0;
 }
 
+extern "C" int lea_conv3d_bf16_set_variant(int variant) {
+  clear_error();
+  LEA_CHECK_ARG(variant == 0 || variant == 1, "lea_conv3d_bf16_set_variant: bad variant %d", variant);
+  bf::g_variant = variant;
+  return 0;
+}
+
 extern "C" size_t lea_conv3d_packed_elems_bf16(int cout, int cin, int k) {
   if (cout <= 0 || cin <= 0 || cin % 8 != 0 || (k != 1 && k != 3)) return 0;
   const int cobv = bf::cob_of(cout), nb = bf::nb_of(cin, k);
@@ -485,8 +754,11 @@ extern "C" const char* lea_conv3d_kernel_name_bf16(int B, int cout, int cin, int
                                                    int k, int costvolume) {
   if (B <= 0 || cout <= 0 || cin <= 0 || (k != 1 && k != 3) || D <= 0 || H <= 0 || W <= 0) return nullptr;
   const bf::Plan p = bf::plan(B, cout, D, H, W, k, cin);
-  snprintf(bf::g_bf_name, sizeof(bf::g_bf_name), "conv_bf16_kernel<%d, %d, %d, %d, %d, %d, %s>",
-           p.ks, p.mt, p.wc, p.th, p.td, p.nb, costvolume ? "true" : "false");
+  if (p.nsplit > 0 && !costvolume)
+    snprintf(bf::g_bf_name, sizeof(bf::g_bf_name), "conv_bf16_stream_kernel<1, %d, %d, %d>", p.wc, p.th, p.nb);
+  else
+    snprintf(bf::g_bf_name, sizeof(bf::g_bf_name), "conv_bf16_kernel<%d, %d, %d, %d, %d, %d, %s>",
+             p.ks, p.mt, p.wc, p.th, p.td, p.nb, costvolume ? "true" : "false");
   return bf::g_bf_name;
 }
 

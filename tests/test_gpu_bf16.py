@@ -194,3 +194,50 @@ def test_bf16_feature_net_vs_f32():
         fb = kernels.from_c8(mb.feature(x))[:, :, 0]
         ff = mf.feature(x)
     _close(fb, ff, rel=5e-2)
+
+
+# ---- D-streaming kernel for the single-chunk 3x3x3 layers (cin <= 16) ----
+
+@pytest.mark.parametrize("b,cin,cout,shape,mode", [
+    (1, 8, 8, (64, 24, 40), "acc"), (2, 8, 8, (9, 13, 37), "res"), (1, 16, 16, (32, 12, 33), "acc"),
+    (2, 16, 16, (7, 9, 20), None), (1, 8, 24, (16, 17, 50), None), (1, 16, 48, (12, 9, 40), None),
+    (1, 8, 8, (4, 3, 5), "acc"), (1, 16, 16, (5, 8, 16), "res"), (3, 8, 16, (6, 10, 31), "acc")])
+def test_stream_kernel_is_the_tile_kernel(b, cin, cout, shape, mode):
+    """The streaming kernel (ring of planes along D, weights in registers, residual by
+    LDS-DMA) computes the tile kernel's sums in the same order: bit-identical outputs,
+    on odd D (a half last step), ragged H/W, column segments along D, every epilogue,
+    an output block slice, and vs float64 torch within the bf16 tolerance."""
+    from leastereo_amd import _lib
+    lib = _lib.load()
+    d, h, w = shape
+    g = torch.Generator().manual_seed(cin + cout + d)
+    x = _bf(torch.randn((b, cin) + shape, generator=g))
+    wt = _bf(torch.randn(cout, cin, 3, 3, 3, generator=g) / np.sqrt(cin * 27))
+    scale = torch.rand(cout, generator=g) + 0.5
+    shift = torch.randn(cout, generator=g) * 0.1
+    r = _bf(torch.randn((b, cout) + shape, generator=g))
+    xc, rc = kernels.to_c8(x.to(DEV)), kernels.to_c8(r.to(DEV))
+    packed = kernels.pack_conv_weight_bf16(wt.to(DEV))
+    outs = []
+    for variant in (0, 1):
+        assert lib.lea_conv3d_bf16_set_variant(variant) == 0
+        try:
+            name = kernels.conv_kernel_name_bf16(b, cout, cin, d, h, w, 3)
+            assert name.startswith("conv_bf16_stream_kernel<" if variant == 0 else "conv_bf16_kernel<"), name
+            big = torch.zeros((b, cout // 8 + 2, d, h, w, 8), device=DEV, dtype=torch.bfloat16)
+            big[:, 1:1 + cout // 8] = rc
+            out = big[:, 1:1 + cout // 8]
+            kernels.conv3d_bnrelu_bf16(xc, packed, cout, 3, scale.to(DEV), shift.to(DEV), relu=True,
+                                       out=out if mode == "acc" else (out if mode is None else out),
+                                       accumulate=mode == "acc", residual=rc if mode == "res" else None)
+            torch.cuda.synchronize()
+            assert float(big[:, 0].float().abs().sum()) == 0 and float(big[:, -1].float().abs().sum()) == 0
+            outs.append(out.clone())
+        finally:
+            lib.lea_conv3d_bf16_set_variant(0)
+    assert torch.equal(outs[0], outs[1])
+    want = F.conv3d(x.double(), wt.double(), None, 1, 1)
+    want = torch.relu(want * scale.double().view(1, -1, 1, 1, 1) + shift.double().view(1, -1, 1, 1, 1))
+    if mode:
+        want = want + r.double()
+    _close(kernels.from_c8(outs[0]), want)
