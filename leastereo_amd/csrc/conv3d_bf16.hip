@@ -358,24 +358,25 @@ __global__ __launch_bounds__(256) void resample_c8_kernel(
 // accumulate operand of each step is LDS-DMA'd by the wave that consumes it (no
 // barrier), and BN scale/shift are read once, so no compiler-visible load inside the
 // walk drains the prefetch.
-template <int MT, int WC, int TH, int NB>
+template <int MT, int WC, int TH, int NB, int NCH>
 struct SCfg {
   static constexpr int TD = 2, WV = 4 / WC, VT = TH * TD, NV = VT / WV;
   static_assert(VT % WV == 0, "rows per wave");
-  static constexpr int T = 27, S = (T * NB + 3) / 4;
+  static constexpr int T = 27, S = (T * NB + 3) / 4;             // k-steps per chunk
+  static constexpr int NBK = NB * NCH;                           // channel blocks in the ring
   static constexpr int COB = WC * MT * 16;
   static constexpr int RH = TH + 2, RW = 18, PLANE = RH * RW;   // 16-B words per plane and block
   static constexpr int PIECES = (PLANE + 63) / 64;              // 64-word DMA pieces per plane and block
   static constexpr int PLANEP = 64 * PIECES;
-  static constexpr int SLOTW = NB * PLANEP;                      // words per ring slot
-  static constexpr int PPW = (NB * PIECES + 3) / 4;              // pieces per wave and plane (padded)
+  static constexpr int SLOTW = NBK * PLANEP;                     // words per ring slot
+  static constexpr int PPW = (NBK * PIECES + 3) / 4;             // pieces per wave and plane (padded)
   static constexpr int RING = 8;
   static constexpr int RESW = MT * 2 * NV * 16;                  // residual words per wave and step
   static constexpr int RPW = RESW / 64;                          // residual pieces per wave
-  static constexpr int RINGW = RING * SLOTW + 64 * (4 * PPW - NB * PIECES);  // + padding pieces
-  static constexpr int LDSW = RINGW + 4 * 3 * RESW;  // with the residual slots (dynamic LDS)
+  static constexpr int RINGW = RING * SLOTW + 64 * (4 * PPW - NBK * PIECES);  // + padding pieces
+  static constexpr int LDSW = RINGW + 4 * 2 * RESW;  // with two residual slots per wave (dynamic LDS)
   static_assert(RESW % 64 == 0, "whole residual pieces");
-  static_assert(LDSW * 16 <= 160 * 1024, "ring + residual");
+  static_assert(LDSW * 16 <= 96 * 1024, "ring + residual");
 };
 
 __device__ __forceinline__ void dma_x4(__amdgpu_buffer_rsrc_t rs, unsigned voff, unsigned lds) {
@@ -388,9 +389,9 @@ __device__ __forceinline__ void wait_vm() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
-template <int MT, int WC, int TH, int NB>
+template <int MT, int WC, int TH, int NB, int NCH>
 __global__ __launch_bounds__(kThreads, 2) void conv_bf16_stream_kernel(const Args a, int nsplit) {
-  using C = SCfg<MT, WC, TH, NB>;
+  using C = SCfg<MT, WC, TH, NB, NCH>;
   extern __shared__ __attribute__((aligned(16))) bf16x8 smem[];  // RINGW (+ residual slots)
   const unsigned lds0 = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)(lds_void*)smem);
   const int tid = threadIdx.x, lane = tid & 63;
@@ -420,16 +421,16 @@ __global__ __launch_bounds__(kThreads, 2) void conv_bf16_stream_kernel(const Arg
     const int q = wave + 4 * t;
     const int blk = q / C::PIECES, e = (q % C::PIECES) * 64 + lane;
     unsigned v = 0xFFFFFFF0u;
-    if (q < NB * C::PIECES && e < C::PLANE) {
+    if (q < C::NBK * C::PIECES && e < C::PLANE && blk * 8 < a.cin) {
       const int rr = e / C::RW, cc = e % C::RW;
       const int h = h0 + rr - 1, w = w0 + cc - 1;
       if ((unsigned)h < (unsigned)a.H && (unsigned)w < (unsigned)a.W)
         v = (unsigned)blk * (unsigned)DHW * 16u + (unsigned)(h * a.W + w) * 16u;
     }
     hwo[t] = v;
-    // padding pieces (q >= NB * PIECES) land past the ring
-    ldo[t] = q < NB * C::PIECES ? (unsigned)(blk * C::PLANEP + (q % C::PIECES) * 64)
-                                : (unsigned)(C::RING * C::SLOTW + (q - NB * C::PIECES) * 64);
+    // padding pieces (q >= NBK * PIECES) land past the ring
+    ldo[t] = q < C::NBK * C::PIECES ? (unsigned)(blk * C::PLANEP + (q % C::PIECES) * 64)
+                                    : (unsigned)(C::RING * C::SLOTW + (q - C::NBK * C::PIECES) * 64);
   }
   const __amdgpu_buffer_rsrc_t xrs = __builtin_amdgcn_make_buffer_rsrc(
       (void*)(a.x + (long long)b * a.xbs), 0, (unsigned)(a.cin / 8) * (unsigned)DHW * 16u, 0x00020000);
@@ -445,13 +446,13 @@ __global__ __launch_bounds__(kThreads, 2) void conv_bf16_stream_kernel(const Arg
   };
 
   // this wave's residual words per step: (m-tile, block of its 2, row i, column) -> its own
-  // slot; one resource over the batch element's output blocks
+  // slot s & 1; one resource over the batch element's output blocks
   const bool resid = a.flags & LEA_RESIDUAL;
-  const unsigned resbase = (unsigned)(C::RING * C::SLOTW + 64 * (4 * C::PPW - NB * C::PIECES) + wave * 3 * C::RESW);
+  const unsigned resbase = (unsigned)(C::RINGW + wave * 2 * C::RESW);
   const __amdgpu_buffer_rsrc_t rrs = __builtin_amdgcn_make_buffer_rsrc(
       (void*)(a.res + (long long)b * a.rbs), 0, (unsigned)((a.cout + 7) / 8) * (unsigned)DHW * 16u, 0x00020000);
-  auto load_res = [&](int s) {  // step s's operand -> this wave's residual slot s % 3
-    const unsigned rslot = resbase + (unsigned)(s % 3) * C::RESW;
+  auto load_res = [&](int s) {
+    const unsigned rslot = resbase + (unsigned)(s & 1) * C::RESW;
 #pragma unroll
     for (int t = 0; t < C::RPW; ++t) {
       const int e = t * 64 + lane;  // word: ((m * 2 + blk2) * NV + i) * 16 + col
@@ -467,7 +468,7 @@ __global__ __launch_bounds__(kThreads, 2) void conv_bf16_stream_kernel(const Arg
     }
   };
 
-  // per-lane K slot geometry: k-step ks, lane group g -> tap (kd, kh, kw), block
+  // per-lane K slot geometry: k-step ks of a chunk, lane group g -> tap (kd, kh, kw), block
   int kdv[C::S], koff[C::S];
 #pragma unroll
   for (int ks = 0; ks < C::S; ++ks) {
@@ -477,15 +478,17 @@ __global__ __launch_bounds__(kThreads, 2) void conv_bf16_stream_kernel(const Arg
     kdv[ks] = tap / 9;
     koff[ks] = blk * C::PLANEP + ((tap / 3) % 3) * C::RW + tap % 3;
   }
-  // A fragments of the (single) chunk, resident for the whole walk
+  // A fragments of every chunk, resident for the whole walk
   const int mtile0 = wc * MT;
   const bf16x8* wpv = reinterpret_cast<const bf16x8*>(a.wp);
-  bf16x8 av[C::S][MT];
+  bf16x8 av[NCH][C::S][MT];
 #pragma unroll
-  for (int ks = 0; ks < C::S; ++ks)
+  for (int c = 0; c < NCH; ++c)
 #pragma unroll
-    for (int m = 0; m < MT; ++m)
-      av[ks][m] = wpv[(((long long)cob * C::S + ks) * (WC * MT) + mtile0 + m) * 64 + g * 16 + n];
+    for (int ks = 0; ks < C::S; ++ks)
+#pragma unroll
+      for (int m = 0; m < MT; ++m)
+        av[c][ks][m] = wpv[((((long long)cob * NCH + c) * C::S + ks) * (WC * MT) + mtile0 + m) * 64 + g * 16 + n];
   float sc[MT][4], sh[MT][4];
 #pragma unroll
   for (int m = 0; m < MT; ++m)
@@ -497,21 +500,17 @@ __global__ __launch_bounds__(kThreads, 2) void conv_bf16_stream_kernel(const Arg
     }
   const bool relu = a.flags & LEA_RELU;
 
-  // Pipeline (issue order = completion order for vmcnt): the end of step s issues step
-  // s+2's residual, then planes 2s+5, 2s+6 (into the slots of planes 2s-3, 2s-2, which
-  // only step s-1 read); the top of step s+1 waits for all but those -- i.e. for step
-  // s+1's planes and residual (issued at the end of step s-1) and step s's stores.
+  // Pipeline (issue order = completion order for vmcnt): after step s's barrier the wave
+  // issues step s+1's residual into its slot (s+1) & 1; the end of step s issues planes
+  // 2s+5, 2s+6 (into the slots of planes 2s-3, 2s-2, which only step s-1 read); the top
+  // of step s+1 waits for all but those two planes -- i.e. for step s+1's planes (issued
+  // at the end of step s-1), its residual and step s's stores.
   if (resid) load_res(s0);
-  for (int j = -1; j <= 2; ++j) load_plane(2 * s0 + j);
-  if (resid) load_res(s0 + 1);  // (past s1: a fetch of zeros, keeping the count uniform)
-  load_plane(2 * s0 + 3);
-  load_plane(2 * s0 + 4);
+  for (int j = -1; j <= 4; ++j) load_plane(2 * s0 + j);
   for (int s = s0; s < s1; ++s) {
-    if (resid)
-      wait_vm<2 * C::PPW + C::RPW>();
-    else
-      wait_vm<2 * C::PPW>();
+    wait_vm<2 * C::PPW>();
     __syncthreads();  // everyone's planes landed; everyone done with step s-1
+    if (resid && s + 1 < s1) load_res(s + 1);
     f32x4 acc[MT][C::NV];
 #pragma unroll
     for (int m = 0; m < MT; ++m)
@@ -519,18 +518,20 @@ __global__ __launch_bounds__(kThreads, 2) void conv_bf16_stream_kernel(const Arg
       for (int i = 0; i < C::NV; ++i) acc[m][i] = f32x4{0.f, 0.f, 0.f, 0.f};
     const int base = 2 * s - 1;
 #pragma unroll
-    for (int ks = 0; ks < C::S; ++ks)
+    for (int c = 0; c < NCH; ++c)
 #pragma unroll
-      for (int i = 0; i < C::NV; ++i) {
-        const int qrow = wv * C::NV + i;
-        const int t = qrow / TH, r = qrow % TH;
-        const int word = ((base + t + kdv[ks]) & 7) * C::SLOTW + koff[ks] + r * C::RW + n;
-        const bf16x8 bv = smem[word];
+      for (int ks = 0; ks < C::S; ++ks)
 #pragma unroll
-        for (int m = 0; m < MT; ++m)
-          acc[m][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[ks][m], bv, acc[m][i], 0, 0, 0);
-      }
-    const unsigned rslot = resbase + (unsigned)(s % 3) * C::RESW;
+        for (int i = 0; i < C::NV; ++i) {
+          const int qrow = wv * C::NV + i;
+          const int t = qrow / TH, r = qrow % TH;
+          const int word = ((base + t + kdv[ks]) & 7) * C::SLOTW + c * NB * C::PLANEP + koff[ks] + r * C::RW + n;
+          const bf16x8 bv = smem[word];
+#pragma unroll
+          for (int m = 0; m < MT; ++m)
+            acc[m][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[c][ks][m], bv, acc[m][i], 0, 0, 0);
+        }
+    const unsigned rslot = resbase + (unsigned)(s & 1) * C::RESW;
 #pragma unroll
     for (int m = 0; m < MT; ++m) {
       const int co = cob * C::COB + (mtile0 + m) * 16 + 4 * g;
@@ -559,12 +560,6 @@ __global__ __launch_bounds__(kThreads, 2) void conv_bf16_stream_kernel(const Arg
         for (int r = 0; r < 4; ++r) out[r] = (__bf16)v[r];
         *reinterpret_cast<bf16x4*>(a.y + (long long)b * a.ybs + cofs + ((long long)d * HW + h * a.W + w) * 8) = out;
       }
-    }
-    if (resid && s + 2 < s1) load_res(s + 2);
-    else if (resid) {  // keep the per-step count uniform: a dummy residual fetch into slot (s+2) % 3
-      const unsigned rslot2 = resbase + (unsigned)((s + 2) % 3) * C::RESW;
-#pragma unroll
-      for (int t = 0; t < C::RPW; ++t) dma_x4(rrs, 0xFFFFFFF0u, lds0 + 16u * (rslot2 + (unsigned)t * 64u));
     }
     load_plane(2 * s + 5);
     load_plane(2 * s + 6);
@@ -608,12 +603,16 @@ inline Plan plan(int B, int cout, int D, int H, int W, int ks, int cin) {
     p.wc = cobv / 16 / p.mt;
   }
   p.nsplit = 0;
-  if (ks == 3 && cin <= 8 * p.nb && g_variant == 0 && g_override[0] == 0 && D >= 4) {
-    // single-chunk layer: stream along D; column segments so the grid holds >= 6
-    // workgroups per CU, each walking >= 4 steps
+  // (r02 tools/bf16_stream_bench.py: two-chunk layers with 64-cout blocks -- the L2
+  // 32->96 sibling groups -- hold 221 VGPRs of weights and accumulators and run slower
+  // streamed; they stay on the tile kernel)
+  const bool two_chunks_wide = cin > 8 * p.nb && cobv > 32;
+  if (ks == 3 && cin <= 16 * p.nb && !two_chunks_wide && g_variant == 0 && g_override[0] == 0 && D >= 4) {
+    // one or two K chunks (cin <= 32): stream along D; column segments so the grid
+    // holds >= 6 workgroups per CU, each walking >= 4 steps
     p.mt = 1;
     p.wc = cobv / 16;
-    p.th = p.nb == 1 ? 8 : 4;
+    p.th = cin <= 8 ? 8 : 4;
     p.td = 2;
     const long long cols = (long long)((W + 15) / 16) * ((H + p.th - 1) / p.th) * B * ncob;
     const int nst = (D + 1) / 2;
@@ -642,16 +641,16 @@ inline Plan plan(int B, int cout, int D, int H, int W, int ks, int cin) {
   LEA_BF_TH(KS, 1, 1, TD, NB, CV) LEA_BF_TH(KS, 2, 1, TD, NB, CV) LEA_BF_TH(KS, 1, 2, TD, NB, CV) \
   LEA_BF_TH(KS, 2, 2, TD, NB, CV) LEA_BF_TH(KS, 1, 4, TD, NB, CV)
 
-#define LEA_BFS_CASE(WC, TH, NB)                                                              \
-  if (p.wc == WC && p.th == TH && p.nb == NB) {                                               \
+#define LEA_BFS_CASE(WC, TH, NB, NCH)                                                         \
+  if (p.wc == WC && p.th == TH && p.nb == NB && a.nchunks == NCH) {                           \
     a.tiles_w = (a.W + 15) / 16;                                                              \
     a.ntiles = a.tiles_w * ((a.H + TH - 1) / TH);                                             \
     const long long nb_ = (long long)a.ntiles * p.nsplit * B * a.ncob;                        \
     LEA_CHECK_ARG(nb_ < (1LL << 31), "lea_conv3d(bf16 stream): grid too large");              \
     a.nblk = (int)nb_;                                                                        \
-    using S_ = SCfg<1, WC, TH, NB>;                                                           \
+    using S_ = SCfg<1, WC, TH, NB, NCH>;                                                      \
     const size_t lds_ = (size_t)((a.flags & LEA_RESIDUAL) ? S_::LDSW : S_::RINGW) * 16;       \
-    conv_bf16_stream_kernel<1, WC, TH, NB><<<dim3((unsigned)nb_), kThreads, lds_, st>>>(a, p.nsplit); \
+    conv_bf16_stream_kernel<1, WC, TH, NB, NCH><<<dim3((unsigned)nb_), kThreads, lds_, st>>>(a, p.nsplit); \
     return launch_status("lea_conv3d(bf16 stream)");                                         \
   }
 
@@ -659,8 +658,9 @@ int run(const Plan& p, Args a, int B, hipStream_t st, bool cv) {
   if (p.nsplit > 0 && !cv && a.cb1 * 8 == a.cin) {  // (one source: the ring walks one tensor)
     LEA_CHECK_ARG((long long)std::max(a.cin, a.cout + 7) / 8 * a.D * a.H * a.W * 16 < 0xFFFFFFF0LL,
                   "lea_conv3d(bf16 stream): volume too large");
-    LEA_BFS_CASE(1, 8, 1) LEA_BFS_CASE(2, 8, 1) LEA_BFS_CASE(4, 8, 1)
-    LEA_BFS_CASE(1, 4, 2) LEA_BFS_CASE(2, 4, 2) LEA_BFS_CASE(4, 4, 2)
+    LEA_BFS_CASE(1, 8, 1, 1) LEA_BFS_CASE(2, 8, 1, 1) LEA_BFS_CASE(4, 8, 1, 1)
+    LEA_BFS_CASE(1, 4, 2, 1) LEA_BFS_CASE(2, 4, 2, 1) LEA_BFS_CASE(4, 4, 2, 1)
+    LEA_BFS_CASE(1, 4, 2, 2) LEA_BFS_CASE(2, 4, 2, 2)
   }
   if (cv) {
     LEA_BF_MT(3, 2, 2, true)
@@ -755,7 +755,8 @@ extern "C" const char* lea_conv3d_kernel_name_bf16(int B, int cout, int cin, int
   if (B <= 0 || cout <= 0 || cin <= 0 || (k != 1 && k != 3) || D <= 0 || H <= 0 || W <= 0) return nullptr;
   const bf::Plan p = bf::plan(B, cout, D, H, W, k, cin);
   if (p.nsplit > 0 && !costvolume)
-    snprintf(bf::g_bf_name, sizeof(bf::g_bf_name), "conv_bf16_stream_kernel<1, %d, %d, %d>", p.wc, p.th, p.nb);
+    snprintf(bf::g_bf_name, sizeof(bf::g_bf_name), "conv_bf16_stream_kernel<1, %d, %d, %d, %d>", p.wc, p.th,
+             p.nb, (cin / 8 + p.nb - 1) / p.nb);
   else
     snprintf(bf::g_bf_name, sizeof(bf::g_bf_name), "conv_bf16_kernel<%d, %d, %d, %d, %d, %d, %s>",
              p.ks, p.mt, p.wc, p.th, p.td, p.nb, costvolume ? "true" : "false");

@@ -201,10 +201,14 @@ def test_bf16_feature_net_vs_f32():
 @pytest.mark.parametrize("b,cin,cout,shape,mode", [
     (1, 8, 8, (64, 24, 40), "acc"), (2, 8, 8, (9, 13, 37), "res"), (1, 16, 16, (32, 12, 33), "acc"),
     (2, 16, 16, (7, 9, 20), None), (1, 8, 24, (16, 17, 50), None), (1, 16, 48, (12, 9, 40), None),
-    (1, 8, 8, (4, 3, 5), "acc"), (1, 16, 16, (5, 8, 16), "res"), (3, 8, 16, (6, 10, 31), "acc")])
+    (1, 8, 8, (4, 3, 5), "acc"), (1, 16, 16, (5, 8, 16), "res"), (3, 8, 16, (6, 10, 31), "acc"),
+    # two K chunks (cin = 32: stem1, the L2 cells and their sibling groups)
+    (1, 32, 32, (16, 12, 40), "acc"), (2, 32, 16, (9, 13, 37), None), (1, 32, 32, (24, 20, 48), None),
+    (1, 32, 24, (6, 9, 20), "res")])
 def test_stream_kernel_is_the_tile_kernel(b, cin, cout, shape, mode):
     """The streaming kernel (ring of planes along D, weights in registers, residual by
-    LDS-DMA) computes the tile kernel's sums in the same order: bit-identical outputs,
+    LDS-DMA; one or two K chunks) computes the tile kernel's sums in the same order:
+    bit-identical outputs,
     on odd D (a half last step), ragged H/W, column segments along D, every epilogue,
     an output block slice, and vs float64 torch within the bf16 tolerance."""
     from leastereo_amd import _lib

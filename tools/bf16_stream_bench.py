@@ -19,6 +19,9 @@ LAYERS = {  # name: cin, cout, volume, accumulate
     "cell_8to24_L0_s1grp": (8, 24, L0, False),
     "cell_16to16_L1": (16, 16, L1, True),
     "cell_16to48_L1_s1grp": (16, 48, L1, False),
+    "stem1_32to32_L0": (32, 32, L0, False),
+    "cell_32to32_L2": (32, 32, L2, True),
+    "cell_32to96_L2_s1grp": (32, 96, L2, False),
 }
 
 
