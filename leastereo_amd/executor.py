@@ -353,6 +353,22 @@ class _C8Layout:
     def _resample(x, size):
         return kernels.resample_trilinear_bf16(x, size)
 
+    def _downsampled(self, x, size):
+        """Materialised trilinear resample of a c8 tensor, memoised for one reuse: cell i
+        resizes its s1 (skip_model_3d.py:44-48) and cell i+1 resizes the same raw tensor
+        as its s0 to the same size (:49-51) -- stem1 L0->L1, cell1's output and conv1's
+        L1->L2.  The memo holds the source itself (no address reuse while cached) and
+        is dropped at the end of every forward (_fresh)."""
+        memo = getattr(self, "_rs_memo", None)
+        if memo is not None and memo[0] is x and memo[1] == tuple(size):
+            return memo[2]
+        y = kernels.resample_trilinear_bf16(x, size)
+        self._rs_memo = (x, tuple(size), y)
+        return y
+
+    def _fresh(self):
+        self._rs_memo = None
+
     def _conv_c8(self, name, x, out=None, accumulate=False, x2=None, size=None, residual=None):
         p = self.p[name]
         cin = (x.shape[1] + (x2.shape[1] if x2 is not None else 0)) * 8
@@ -365,7 +381,7 @@ class _C8Layout:
             if p.k == 1 and up:  # commuted: 1x1 at the low resolution, resample + BN/ReLU
                 z = kernels.conv3d_bnrelu_bf16(x, p.packed, p.cout, 1, None, None, relu=False)
                 return kernels.resample_trilinear_bf16(z, size, True, out, p.scale, p.shift, p.relu)
-            x = kernels.resample_trilinear_bf16(x, size)
+            x = self._downsampled(x, size)
         if p.kind == "bf16_2d":
             if x2 is not None:
                 raise ValueError(f"{name}: 2D conv takes one input")
@@ -425,9 +441,20 @@ class MatchingExecutorBF16(_C8Layout, MatchingExecutor):
 
     def run(self, x):
         """x: f32 cost volume [B, 64, D3, H3, W3] -> f32 matching cost [B, 1, D3, H3, W3]."""
-        return self._from_stem0(self.conv("stem0", kernels.to_c8(x)))
+        self._fresh()
+        try:
+            return self._from_stem0(self.conv("stem0", kernels.to_c8(x)))
+        finally:
+            self._fresh()
 
     def run_features(self, fl, fr, maxdisp):
+        self._fresh()
+        try:
+            return self._run_features(fl, fr, maxdisp)
+        finally:
+            self._fresh()
+
+    def _run_features(self, fl, fr, maxdisp):
         p = self.p["stem0"]
         cf = fl.shape[1] * (8 if fl.dtype == torch.bfloat16 else 1)
         if cf * 2 != p.cin:
@@ -473,6 +500,13 @@ class FeatureExecutorBF16(_C8Layout, FeatureExecutor):
         return self._conv_c8(name, x, *args, **kw)
 
     def run(self, x):
+        self._fresh()
+        try:
+            return self._run(x)
+        finally:
+            self._fresh()
+
+    def _run(self, x):
         x5 = x.unsqueeze(2)
         stem1 = kernels.to_c8(self.conv("stem1", self.conv("stem0", x5)))
         stem2 = self.conv("stem2", stem1)
