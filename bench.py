@@ -157,6 +157,15 @@ def golden_epe(device, precision="f32"):
     return float(np.abs(got - want).mean())
 
 
+def algorithm_name(kernel: str) -> str:
+    """The convolution algorithm a conv kernel instantiation runs."""
+    if kernel.startswith("conv3d_wino2_kernel<"):
+        return "winograd F(4,3) along W x F(2,3) along D"
+    if kernel.startswith("conv3d_wino_kernel<"):
+        return f"winograd F({kernel.split('<')[1].split(',')[0]},3) along W"
+    return "direct convolution"
+
+
 def _quantile(xs, q):
     """Linear-interpolated quantile of a sorted list."""
     pos = q * (len(xs) - 1)
@@ -284,8 +293,7 @@ def main():
                      "flops_per_launch": flops_per_launch, "ms_per_launch": ms_per_launch,
                      # products the kernel actually issues: Winograd F(2,3) does 4 per 6 of
                      # the direct convolution whose FLOPs define `achieved`
-                     "algorithm": (f"winograd F({dominant.split('<')[1].split(',')[0]},3) along W"
-                                   if "wino" in dominant else "direct convolution"),
+                     "algorithm": algorithm_name(dominant),
                      "mfma_executed": mfma_tflops, "mfma_executed_frac": mfma_tflops / peak},
         "epe_px": None if epe is None else {
             "vs": "reference LEAStereo fp32 disparity (tests/golden e2e b1_h96_w192_md48)",

@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define LEA_ABI_VERSION 6
+#define LEA_ABI_VERSION 7
 
 #define LEA_F32 0
 #define LEA_BF16 1
@@ -273,6 +273,30 @@ int lea_conv3d_wino_set_tile_override(int np, int td, int f);
  * cout tile, 3 = eight waves, 4 = two cout tiles per wave at one wave per SIMD.
  * Per calling thread, like the tile override. */
 int lea_conv3d_wino_set_variant(int variant);
+
+/* ---- Matching-net stem0 over the cost volume, factored (csrc/cv_stem.hip) ----
+ * Replaces retrain/LEAStereo.py:34-48 + skip_model_3d.py:141 like
+ * lea_conv3d_bnrelu_costvolume, without a 3D convolution: every cost-volume plane is
+ * a shifted copy of the feature maps, so with u = w - d
+ *   conv(cost)[o, d, h, w] = sum_{kd: 0 <= d+kd-1 < D3} ( LK[kd][max(kd-u, 0)][o, h, w]
+ *                                                       + Bk[kd][o, h, u-kd+1] )
+ * (LK[kd][t] = 0 for kd - u >= 3; Bk[kd] at column -1 = K2[kd] at column 0; the last
+ * column w = W-1 subtracts K2[kd][o, h, u-kd+2]), where LK, Bk, K2 are 2D 3x3 convs of
+ * the left / right feature maps:
+ *   lea_cv_stem_split_weights: stem0's [cout, 2C, 3, 3, 3] f32 weight ->
+ *     wl [9 cout, C, 3, 3]: wl[(3 kd + t) cout + o][c][kh][kw] = W[o][c][kd][kh][kw] (kw >= t)
+ *     wr [6 cout, C, 3, 3]: wr[kd cout + o] = W[o][C + c][kd]  (Bk)
+ *                           wr[(3 + kd) cout + o][c][kh][1] = W[o][C + c][kd][kh][2]  (K2)
+ *   maps: lea_conv2d_bnrelu (f32) / lea_conv2d_bnrelu_bf16 (c8) of left with wl and of
+ *     right with wr, no BN/ReLU: lmaps [B, 9 cout, H, W], rmaps [B, 6 cout, H, W];
+ *   lea_cv_stem_combine: the sum above, the folded BN and ReLU, written as
+ *     y [B, cout, D3, H, W] (dtype LEA_F32: NCDHW, W % 4 == 0; LEA_BF16: c8 maps in,
+ *     c8 out, cout % 8 == 0).  D3 >= 2.  Equal to the direct conv up to summation
+ *     order (and, at bf16, the maps' rounding). */
+int lea_cv_stem_split_weights(const float* w, float* wl, float* wr, int cout, int C, void* stream);
+int lea_cv_stem_combine(const void* lmaps, int64_t l_bstride, const void* rmaps, int64_t r_bstride,
+                        const float* scale, const float* shift, void* y, int64_t y_bstride, int B,
+                        int cout, int D3, int H, int W, unsigned flags, int dtype, void* stream);
 
 /* ---- host steps either side of forward ---- */
 

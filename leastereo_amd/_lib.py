@@ -12,7 +12,7 @@ LIB_PATH = os.environ.get(
     "LEASTEREO_HIP_LIB",
     os.path.join(os.path.dirname(os.path.abspath(__file__)), "libleastereo_hip.so"))
 
-ABI_VERSION = 6
+ABI_VERSION = 7
 LEA_F32 = 0
 LEA_BF16 = 1
 LEA_RELU = 1
@@ -80,6 +80,10 @@ SIGNATURES = {
     "lea_conv3d_wino_kernel_name": (ctypes.c_char_p, [_i, _i, _i, _i, _i, _i]),
     "lea_conv3d_wino_set_tile_override": (_i, [_i, _i, _i]),
     "lea_conv3d_wino_set_variant": (_i, [_i]),
+    # stem0 over the cost volume, factored through 2D maps
+    "lea_cv_stem_split_weights": (_i, [_p, _p, _p, _i, _i, _p]),
+    "lea_cv_stem_combine": (_i, [_p, _i64, _p, _i64, _p, _p, _p, _i64, _i, _i, _i, _i, _i, _u, _i,
+                                 _p]),
     # host steps either side of forward: predict.py load_data/test_transform, metrics
     "lea_standardize_workspace_bytes": (ctypes.c_size_t, [_i]),
     "lea_standardize_crop_u8": (_i, [_p, _p, _i, _i, _i, _i, _p, _p, _i, _i, _p, _p]),

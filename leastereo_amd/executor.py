@@ -44,6 +44,9 @@ class ConvParams:
 # f32 3x3x3 layers run on the Winograd F(2,3)-along-W engine (2/3 of the direct
 # engine's MFMA work); LEASTEREO_WINOGRAD=0 keeps them on the direct engine.
 WINOGRAD = os.environ.get("LEASTEREO_WINOGRAD", "1") != "0"
+# stem0 over the cost volume through 2D maps (csrc/cv_stem.hip); LEASTEREO_CV_STEM=0
+# runs the 3D conv on the in-place cost volume instead.
+CV_STEM = os.environ.get("LEASTEREO_CV_STEM", "1") != "0"
 
 
 def _conv_params(mod, w=None, folded=None):
@@ -237,6 +240,9 @@ class MatchingExecutor(CellGraphExecutor):
         p = self.p["stem0"]
         if fl.shape[1] * 2 != p.cin:
             raise ValueError(f"stem0 expects {p.cin} cost-volume channels, got 2*{fl.shape[1]}")
+        d3 = int(maxdisp / 3)
+        if self.cv is not None and kernels.cv_stem_supported(p.cout, d3, fl.shape[3], False):
+            return self._from_stem0(self._cv_stem(fl.unsqueeze(2), fr.unsqueeze(2), d3))
         if p.wino is not None and kernels.wino_preferred(fl.shape[0], p.cout, p.cin, int(maxdisp / 3),
                                                          *fl.shape[2:4]):
             stem0 = kernels.conv3d_bnrelu_costvolume_wino(fl, fr, maxdisp, p.wino, p.cout, p.scale,
@@ -245,6 +251,17 @@ class MatchingExecutor(CellGraphExecutor):
             stem0 = kernels.conv3d_bnrelu_costvolume(fl, fr, maxdisp, p.packed, p.cout, p.scale,
                                                      p.shift, p.relu)
         return self._from_stem0(stem0)
+
+    def _cv_stem(self, fl5, fr5, d3):
+        """stem0 = ConvBR3d(cost volume) (LEAStereo.py:34-48, skip_model_3d.py:141) as
+        2D maps of each feature map + lea_cv_stem_combine (csrc/cv_stem.hip)."""
+        p, (wl, wr) = self.p["stem0"], self.cv
+        lm = kernels.conv2d_bnrelu(fl5, wl, 9 * p.cout, None, None, relu=False)
+        rm = kernels.conv2d_bnrelu(fr5, wr, 6 * p.cout, None, None, relu=False)
+        return kernels.cv_stem_combine(lm, rm, p.cout, d3, p.scale, p.shift, p.relu)
+
+    def _cv_stem_pack(self, wl, wr):
+        return kernels.pack_conv2d_weight(wl), kernels.pack_conv2d_weight(wr)
 
     def _from_stem0(self, stem0):
         d, h, w = self._volume(stem0)
@@ -300,6 +317,9 @@ class MatchingExecutor(CellGraphExecutor):
             taps = last3.permute(0, 2, 3, 4, 1).reshape(co * 27, ci, 1, 1, 1)
             self.p["last_3.taps"] = ConvParams(kernels.pack_conv_weight(taps), None, None,
                                                ci, co * 27, 1, False)
+            self.cv = None
+            if CV_STEM:
+                self.cv = self._cv_stem_pack(*kernels.cv_stem_split_weights(matching.stem0.conv.weight))
         self._use_winograd()
 
 
@@ -428,6 +448,16 @@ class MatchingExecutorBF16(_C8Layout, MatchingExecutor):
     def _use_winograd(self):
         """bf16 layers stay on the bf16 engine."""
 
+    def _cv_stem_pack(self, wl, wr):
+        return kernels.pack_conv2d_weight_bf16(wl), kernels.pack_conv2d_weight_bf16(wr)
+
+    def _cv_stem(self, fl8, fr8, d3):
+        p, (wl, wr) = self.p["stem0"], self.cv
+        lm = kernels.conv2d_bnrelu_bf16(fl8, wl, 9 * p.cout, None, None, relu=False)
+        rm = kernels.conv2d_bnrelu_bf16(fr8, wr, 6 * p.cout, None, None, relu=False)
+        return kernels.cv_stem_combine(lm, rm, p.cout, d3, p.scale, p.shift, p.relu,
+                                       name="cv_stem_c8_kernel")
+
     @staticmethod
     def _tapsum(q, p3, full):
         return kernels.tapsum_upsample_bf16(q, p3.cout, full, p3.scale, p3.shift, p3.relu)
@@ -464,6 +494,9 @@ class MatchingExecutorBF16(_C8Layout, MatchingExecutor):
         else:
             f8 = kernels.to_c8(torch.cat((fl, fr), 0))  # [2B, C/8, 1, H, W, 8]
             b = fl.shape[0]
+        d3 = int(maxdisp / 3)
+        if self.cv is not None and kernels.cv_stem_supported(p.cout, d3, f8.shape[4], True):
+            return self._from_stem0(self._cv_stem(f8[:b], f8[b:], d3))
         stem0 = kernels.conv3d_bnrelu_costvolume_bf16(f8[:b], f8[b:], maxdisp, p.packed, p.cout,
                                                       p.scale, p.shift, p.relu)
         return self._from_stem0(stem0)

@@ -606,6 +606,73 @@ def conv2d_bnrelu_bf16(x: torch.Tensor, packed: torch.Tensor, cout: int, scale, 
     return out
 
 
+# ---- stem0 over the cost volume, factored through 2D maps (csrc/cv_stem.hip) ----
+
+def cv_stem_split_weights(w: torch.Tensor):
+    """stem0's [cout, 2C, 3, 3, 3] weight -> (wl [9 cout, C, 3, 3], wr [6 cout, C, 3, 3]),
+    the 2D map weights of lea_cv_stem_split_weights."""
+    _require_cuda(w)
+    w = w.detach().contiguous()
+    if w.dim() != 5 or tuple(w.shape[2:]) != (3, 3, 3) or w.shape[1] % 2:
+        raise ValueError(f"expected a [cout, 2C, 3, 3, 3] weight, got {tuple(w.shape)}")
+    cout, c = w.shape[0], w.shape[1] // 2
+    wl = torch.empty((9 * cout, c, 3, 3), device=w.device, dtype=torch.float32)
+    wr = torch.empty((6 * cout, c, 3, 3), device=w.device, dtype=torch.float32)
+    check(_lib.load().lea_cv_stem_split_weights(w.data_ptr(), wl.data_ptr(), wr.data_ptr(), cout, c,
+                                                _stream()), "lea_cv_stem_split_weights")
+    return wl, wr
+
+
+def cv_stem_supported(cout: int, d3: int, w: int, bf16: bool) -> bool:
+    """Shapes lea_cv_stem_combine takes (f32 stores float4 rows; LDS holds the
+    workgroup's right-half sums over D3 + 63 columns)."""
+    ob = 32 if bf16 else 16
+    lds = 3 * ob * (d3 + 63) * 4
+    return d3 >= 2 and lds <= 160 * 1024 and (cout % 8 == 0 if bf16 else w % 4 == 0)
+
+
+def cv_stem_combine(lmaps: torch.Tensor, rmaps: torch.Tensor, cout: int, d3: int,
+                    scale: torch.Tensor | None, shift: torch.Tensor | None, relu: bool = True,
+                    name: str = "cv_stem_f32_kernel") -> torch.Tensor:
+    """stem0's output from the 2D maps: lmaps [B, 9 cout, 1, H, W] / rmaps [B, 6 cout, 1, H, W]
+    f32 -> [B, cout, D3, H, W] f32, or c8 maps -> c8 [B, cout/8, D3, H, W, 8] bf16."""
+    c8 = lmaps.dtype == torch.bfloat16
+    if c8:
+        _require_c8(lmaps, rmaps)
+        b, _, _, h, w, _ = lmaps.shape
+        lbs, rbs = _check_c8_view(lmaps, "lmaps"), _check_c8_view(rmaps, "rmaps")
+        if lmaps.shape[1] * 8 != 9 * cout or rmaps.shape[1] * 8 != 6 * cout:
+            raise ValueError("cv_stem_combine: map channels must be 9 / 6 x cout")
+        out = torch.empty((b, cout // 8, d3, h, w, 8), device=lmaps.device, dtype=torch.bfloat16)
+        ybs = out.stride(0)
+    else:
+        _require_cuda(lmaps, rmaps)
+        b, _, _, h, w = lmaps.shape
+        lbs, rbs = _check_volume_view(lmaps, "lmaps"), _check_volume_view(rmaps, "rmaps")
+        if lmaps.shape[1] != 9 * cout or rmaps.shape[1] != 6 * cout:
+            raise ValueError("cv_stem_combine: map channels must be 9 / 6 x cout")
+        out = torch.empty((b, cout, d3, h, w), device=lmaps.device, dtype=torch.float32)
+        ybs = out.stride(0)
+    _require_cuda(scale, shift)
+    if tuple(rmaps.shape[0:1]) != (b,) or tuple(rmaps.shape[3:5]) != (h, w):
+        raise ValueError("cv_stem_combine: left/right maps differ in batch or size")
+    rec = None
+    if _probe is not None and (_probe.names is None or name in _probe.names):
+        # algorithmic bytes: the output write (the maps are L2/MALL-resident reads)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        rec = (name, 0.0, float(out.numel() * out.element_size()), e0, e1, 0.0)
+    check(_lib.load().lea_cv_stem_combine(
+        lmaps.data_ptr(), lbs, rmaps.data_ptr(), rbs,
+        scale.data_ptr() if scale is not None else None,
+        shift.data_ptr() if shift is not None else None, out.data_ptr(), ybs, b, cout, d3, h, w,
+        LEA_RELU if relu else 0, _lib.LEA_BF16 if c8 else LEA_F32, _stream()), "lea_cv_stem_combine")
+    if rec is not None:
+        rec[4].record()
+        _probe.records.append(rec)
+    return out
+
+
 # ---- host steps either side of forward (SURVEY.md §8f rank 3) ----
 
 def standardize_crop_u8(left: torch.Tensor, right: torch.Tensor, crop_height: int, crop_width: int):
