@@ -35,7 +35,8 @@ def _want(fl, fr, w, scale, shift, maxdisp):
 
 @pytest.mark.parametrize("b,c,cout,maxdisp,hw", [
     (2, 32, 32, 48, (12, 40)), (1, 4, 16, 27, (5, 8)), (1, 32, 32, 192, (10, 100)),
-    (1, 8, 48, 9, (9, 20)), (1, 8, 16, 6, (3, 4)), (1, 32, 32, 264, (4, 132)), (1, 16, 24, 96, (7, 320))])
+    (1, 8, 48, 9, (9, 20)), (1, 8, 16, 6, (3, 4)), (1, 32, 32, 264, (4, 132)), (1, 16, 24, 96, (7, 320)),
+    (1, 4, 8, 1700, (2, 8))])  # D3 = 566: the planes split over two workgroups
 def test_cv_stem_f32_vs_float64(b, c, cout, maxdisp, hw):
     fl, fr, w, scale, shift = _case(b, c, cout, maxdisp, hw, c + cout + maxdisp)
     d3 = int(maxdisp / 3)
@@ -71,7 +72,8 @@ def _bf(t):
 
 
 @pytest.mark.parametrize("b,c,cout,maxdisp,hw", [(2, 32, 32, 48, (12, 40)), (1, 16, 16, 27, (5, 19)),
-                                                  (1, 32, 32, 192, (6, 70)), (1, 16, 40, 12, (3, 5))])
+                                                  (1, 32, 32, 192, (6, 70)), (1, 16, 40, 12, (3, 5)),
+                                                  (1, 16, 16, 700, (2, 24))])  # D3 = 233: split
 def test_cv_stem_bf16_vs_float64(b, c, cout, maxdisp, hw):
     fl, fr, w, scale, shift = _case(b, c, cout, maxdisp, hw, 7 * c + cout + maxdisp)
     fl, fr, w = _bf(fl), _bf(fr), _bf(w)
