@@ -220,6 +220,11 @@ int lea_resample3d_trilinear_bf16(const void* x, int64_t x_bstride, void* y, int
                                   int align_corners, const float* scale, const float* shift,
                                   unsigned flags, void* stream);
 
+/* Tuning hook (tools/resample_probe.py): output words per thread of the c8 resample,
+ * k in {1, 2, 4}; 0 restores the default (4 when up-sampling, else 1).  Per calling
+ * thread. */
+int lea_resample_bf16_set_batch(int k);
+
 /* Layout converters: f32 NC[D]HW (vol = D*H*W voxels per channel) <-> bf16 c8. */
 int lea_to_c8_bf16(const float* x, int64_t x_bstride, void* y, int64_t y_bstride, int B, int C,
                    int64_t vol, void* stream);
@@ -273,6 +278,14 @@ int lea_conv3d_wino_set_tile_override(int np, int td, int f);
  * cout tile, 3 = eight waves, 4 = two cout tiles per wave at one wave per SIMD.
  * Per calling thread, like the tile override. */
 int lea_conv3d_wino_set_variant(int variant);
+/* Tuning hook: depth pairs each W x D engine workgroup walks (its items = pairs x
+ * 4-channel chunks through one DMA pipeline); 0 restores the planner.  Per calling
+ * thread. */
+int lea_conv3d_wino2_set_walk(int spw);
+/* couts <= 8 on the Winograd entries: 0 (default) = the depth-paired 1-D tile, 1 =
+ * packed and planned as 16-row cout blocks (the W x D engine).  Packing and launches must
+ * use the same mode.  Per calling thread. */
+int lea_conv3d_wino_set_small_cout(int mode);
 
 /* ---- Matching-net stem0 over the cost volume, factored (csrc/cv_stem.hip) ----
  * Replaces retrain/LEAStereo.py:34-48 + skip_model_3d.py:141 like

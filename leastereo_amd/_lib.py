@@ -64,6 +64,7 @@ SIGNATURES = {
     "lea_conv3d_bf16_set_variant": (_i, [_i]),
     "lea_resample3d_trilinear_bf16": (_i, [_p, _i64, _p, _i64, _i, _i, _i, _i, _i, _i, _i, _i,
                                            _i, _p, _p, _u, _p]),
+    "lea_resample_bf16_set_batch": (_i, [_i]),
     "lea_to_c8_bf16": (_i, [_p, _i64, _p, _i64, _i, _i, _i64, _p]),
     "lea_conv2d_packed_elems_bf16": (ctypes.c_size_t, [_i, _i]),
     "lea_conv2d_pack_weights_bf16": (_i, [_p, _p, _i, _i, _p]),
@@ -80,6 +81,8 @@ SIGNATURES = {
     "lea_conv3d_wino_kernel_name": (ctypes.c_char_p, [_i, _i, _i, _i, _i, _i]),
     "lea_conv3d_wino_set_tile_override": (_i, [_i, _i, _i]),
     "lea_conv3d_wino_set_variant": (_i, [_i]),
+    "lea_conv3d_wino2_set_walk": (_i, [_i]),
+    "lea_conv3d_wino_set_small_cout": (_i, [_i]),
     # stem0 over the cost volume, factored through 2D maps
     "lea_cv_stem_split_weights": (_i, [_p, _p, _p, _i, _i, _p]),
     "lea_cv_stem_combine": (_i, [_p, _i64, _p, _i64, _p, _p, _p, _i64, _i, _i, _i, _i, _i, _u, _i,
@@ -116,8 +119,22 @@ def load():
                 fn = getattr(lib, name)
                 fn.restype = res
                 fn.argtypes = args
+            _apply_env_tuning(lib)
             _lib = lib
     return _lib
+
+
+# A/B switches for the planners' tuning hooks (thread-local in the library: they apply
+# to the thread that loads it), e.g. LEASTEREO_WINO2_WALK=1 to disable the depth walk
+TUNING_ENV = {"LEASTEREO_WINO2_WALK": "lea_conv3d_wino2_set_walk",
+              "LEASTEREO_RESAMPLE_K": "lea_resample_bf16_set_batch"}
+
+
+def _apply_env_tuning(lib):
+    for var, fn in TUNING_ENV.items():
+        if os.environ.get(var):
+            if getattr(lib, fn)(int(os.environ[var])) != 0:
+                raise HipKernelError(f"{var}={os.environ[var]}: {lib.lea_last_error().decode()}")
 
 
 def check(rc: int, what: str):

@@ -304,8 +304,14 @@ __global__ void from_c8_kernel(const __bf16* __restrict__ x, long long xbs, floa
 }
 
 // Trilinear resample (aten source-index rule, common.h Axis) of a c8 volume with
-// the optional per-channel relu(scale * . + shift) epilogue; one 16-byte voxel
-// block (8 channels) per thread: 8 corner words, interpolated in f32.
+// the optional per-channel relu(scale * . + shift) epilogue; 16-byte voxel blocks (8
+// channels) per output word: 8 corner words, interpolated in f32.  K output words per
+// thread (grid stride apart), all 8K corner loads issued before the first lerp: K = 1
+// keeps the most loads in flight chip-wide for the read-heavy down-samplings, K = 4
+// cuts the workgroup count of the write-heavy up-samplings (r02: one word per thread
+// launched 123 K workgroups for an L1 -> L0 8-channel up-sampling and ran at 1.9 TB/s,
+// dispatch-bound).
+template <int K>
 __global__ __launch_bounds__(256) void resample_c8_kernel(
     const __bf16* __restrict__ x, long long xbs, __bf16* __restrict__ y, long long ybs, int CB,
     int Di, int Hi, int Wi, int Do, int Ho, int Wo, float rd, float rh, float rw, int ac,
@@ -319,29 +325,53 @@ __global__ __launch_bounds__(256) void resample_c8_kernel(
   const long long HWi = (long long)Hi * Wi;
   const bf16x8* xc = reinterpret_cast<const bf16x8*>(x + (long long)b * xbs) + (long long)cb * Di * HWi;
   bf16x8* yp = reinterpret_cast<bf16x8*>(y + (long long)b * ybs) + ((long long)cb * Do + od) * Ho * Wo;
+  const bf16x8* p0 = xc + ad.i0 * HWi;
+  const bf16x8* p1 = xc + ad.i1 * HWi;
   const bool relu = flags & LEA_RELU;
-  for (int t = blockIdx.x * blockDim.x + threadIdx.x; t < Ho * Wo; t += gridDim.x * blockDim.x) {
-    const int oh = t / Wo, ow = t % Wo;
-    const Axis ah = axis_index(rh, oh, Hi, Ho, ac);
-    const Axis aw = axis_index(rw, ow, Wi, Wo, ac);
-    const bf16x8* p0 = xc + ad.i0 * HWi;
-    const bf16x8* p1 = xc + ad.i1 * HWi;
-    const bf16x8 c000 = p0[(long long)ah.i0 * Wi + aw.i0], c001 = p0[(long long)ah.i0 * Wi + aw.i1];
-    const bf16x8 c010 = p0[(long long)ah.i1 * Wi + aw.i0], c011 = p0[(long long)ah.i1 * Wi + aw.i1];
-    const bf16x8 c100 = p1[(long long)ah.i0 * Wi + aw.i0], c101 = p1[(long long)ah.i0 * Wi + aw.i1];
-    const bf16x8 c110 = p1[(long long)ah.i1 * Wi + aw.i0], c111 = p1[(long long)ah.i1 * Wi + aw.i1];
-    bf16x8 o;
+  float sc[8], sh[8];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      float r = ad.l0 * (ah.l0 * (aw.l0 * (float)c000[j] + aw.l1 * (float)c001[j]) +
-                         ah.l1 * (aw.l0 * (float)c010[j] + aw.l1 * (float)c011[j])) +
-                ad.l1 * (ah.l0 * (aw.l0 * (float)c100[j] + aw.l1 * (float)c101[j]) +
-                         ah.l1 * (aw.l0 * (float)c110[j] + aw.l1 * (float)c111[j]));
-      if (scale) r = r * scale[cb * 8 + j] + shift[cb * 8 + j];
-      if (relu) r = fmaxf(r, 0.f);
-      o[j] = (__bf16)r;
+  for (int j = 0; j < 8; ++j) {
+    sc[j] = scale ? scale[cb * 8 + j] : 1.f;
+    sh[j] = scale ? shift[cb * 8 + j] : 0.f;
+  }
+  const int cells = Ho * Wo, stride = gridDim.x * blockDim.x;
+  for (int t0 = blockIdx.x * blockDim.x + threadIdx.x; t0 < cells; t0 += K * stride) {
+    bf16x8 c[K][8];
+    Axis ah[K], aw[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      const int t = min(t0 + k * stride, cells - 1);
+      const int oh = t / Wo, ow = t % Wo;
+      ah[k] = axis_index(rh, oh, Hi, Ho, ac);
+      aw[k] = axis_index(rw, ow, Wi, Wo, ac);
+      const long long r0 = (long long)ah[k].i0 * Wi, r1 = (long long)ah[k].i1 * Wi;
+      c[k][0] = p0[r0 + aw[k].i0];
+      c[k][1] = p0[r0 + aw[k].i1];
+      c[k][2] = p0[r1 + aw[k].i0];
+      c[k][3] = p0[r1 + aw[k].i1];
+      c[k][4] = p1[r0 + aw[k].i0];
+      c[k][5] = p1[r0 + aw[k].i1];
+      c[k][6] = p1[r1 + aw[k].i0];
+      c[k][7] = p1[r1 + aw[k].i1];
     }
-    yp[t] = o;
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      const int t = t0 + k * stride;
+      if (t >= cells) break;
+      const Axis &h = ah[k], &w = aw[k];
+      bf16x8 o;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        float r = ad.l0 * (h.l0 * (w.l0 * (float)c[k][0][j] + w.l1 * (float)c[k][1][j]) +
+                           h.l1 * (w.l0 * (float)c[k][2][j] + w.l1 * (float)c[k][3][j])) +
+                  ad.l1 * (h.l0 * (w.l0 * (float)c[k][4][j] + w.l1 * (float)c[k][5][j]) +
+                           h.l1 * (w.l0 * (float)c[k][6][j] + w.l1 * (float)c[k][7][j]));
+        if (scale) r = r * sc[j] + sh[j];
+        if (relu) r = fmaxf(r, 0.f);
+        o[j] = (__bf16)r;
+      }
+      yp[t] = o;
+    }
   }
 }
 
@@ -868,6 +898,16 @@ extern "C" int lea_from_c8_bf16(const void* x, int64_t x_bstride, float* y, int6
   return launch_status("lea_from_c8_bf16");
 }
 
+// resample words per thread (lea_resample_bf16_set_batch; 0 = up-sampling 4, else 1)
+static thread_local int g_resample_k = 0;
+
+extern "C" int lea_resample_bf16_set_batch(int k) {
+  clear_error();
+  LEA_CHECK_ARG(k == 0 || k == 1 || k == 2 || k == 4, "lea_resample_bf16_set_batch: k=%d", k);
+  g_resample_k = k;
+  return 0;
+}
+
 extern "C" int lea_resample3d_trilinear_bf16(const void* x, int64_t x_bstride, void* y,
                                              int64_t y_bstride, int B, int C, int Di, int Hi,
                                              int Wi, int Do, int Ho, int Wo, int align_corners,
@@ -882,13 +922,15 @@ extern "C" int lea_resample3d_trilinear_bf16(const void* x, int64_t x_bstride, v
                 "lea_resample3d_trilinear_bf16: bad shape");
   const int ac = align_corners ? 1 : 0;
   const long long cells = (long long)Ho * Wo;
-  // one output word (8 channels) per thread: the 8 corner loads of many threads in
-  // flight hide the gather latency (r01: 64 workgroups per plane looping 4x ran at
-  // ~1.5 TB/s on the B=8 down-sampling)
-  dim3 grid((unsigned)((cells + 255) / 256), B * (C / 8) * Do);
-  bf::resample_c8_kernel<<<grid, 256, 0, as_stream(stream)>>>(
-      (const __bf16*)x, x_bstride, (__bf16*)y, y_bstride, C / 8, Di, Hi, Wi, Do, Ho, Wo,
-      axis_ratio(Di, Do, ac), axis_ratio(Hi, Ho, ac), axis_ratio(Wi, Wo, ac), ac, scale, shift, flags);
+  const int k = g_resample_k > 0 ? g_resample_k : ((long long)Do * Ho * Wo > (long long)Di * Hi * Wi ? 4 : 1);
+  dim3 grid((unsigned)((cells + 256LL * k - 1) / (256LL * k)), B * (C / 8) * Do);
+#define LEA_RS_K(K_)                                                                                \
+  if (k == K_)                                                                                     \
+    bf::resample_c8_kernel<K_><<<grid, 256, 0, as_stream(stream)>>>(                               \
+        (const __bf16*)x, x_bstride, (__bf16*)y, y_bstride, C / 8, Di, Hi, Wi, Do, Ho, Wo,          \
+        axis_ratio(Di, Do, ac), axis_ratio(Hi, Ho, ac), axis_ratio(Wi, Wo, ac), ac, scale, shift, flags);
+  LEA_RS_K(1) LEA_RS_K(2) LEA_RS_K(4)
+#undef LEA_RS_K
   return launch_status("lea_resample3d_trilinear_bf16");
 }
 

@@ -437,11 +437,17 @@ thread_local int g_override[3] = {0, 0, 0};  // np, td, f (lea_conv3d_wino_set_t
 // with the inputs transformed once per chunk into LDS (32-cout blocks; 16-cout blocks
 // keep 2)
 thread_local int g_variant = 0;
+thread_local int g_spw = 0;  // lea_conv3d_wino2_set_walk: depth pairs per workgroup (0 = planner)
+// lea_conv3d_wino_set_small_cout: couts <= 8 packed / planned as 16-row blocks for the
+// W x D engine (1) or depth-paired for the 1-D engine (0, the default: r02 sweep, L0 8->8
+// 175 us depth-paired vs 210 us on the W x D engine's half-empty 16-row block)
+thread_local int g_small16 = 0;
+inline int host_mt(int cout) { return (g_small16 && cout <= 8) ? 1 : mt_of(cout); }
 
 // W x D engine tile for variant v (2..4), or nullptr-equivalent (q = 0) when the
 // layer's cout block has no such tile (couts <= 8 and the 48-row blocks stay 1-D)
 inline Plan2 plan2(int v, int mt, int q) {
-  Plan2 t{0, 0, 0, 0, 0, false};
+  Plan2 t{0, 0, 0, 0, 0, false, 0};
   if (mt != 1 && mt != 2) return t;
   if (v >= 5) {
     t.pv = mt == 2;
@@ -469,7 +475,7 @@ inline Plan make_plan(int B, int cout, int D, int H, int W) {
   // 32-wide row pairs (L1, L2), F(2,3) for the 48-row blocks (their LDS budget);
   // two output planes per workgroup unless the volume is too shallow to fill the chip.
   Plan p;
-  p.mt = mt_of(cout);
+  p.mt = host_mt(cout);
   const long long ncob = (cout + cop_of(p.mt) - 1) / cop_of(p.mt);
   auto fits = [&](int tw) { return (W + tw - 1) / tw * tw * 10 <= W * 11; };  // <= 10 % padding
   p.f = 2;
@@ -509,6 +515,7 @@ inline Plan make_plan(int B, int cout, int D, int H, int W) {
   if (v >= 2) {
     p.p2 = plan2(v, p.mt, fits(64) ? 16 : 8);
     p.d2 = p.p2.q > 0;
+    if (g_spw > 0) p.p2.spw = g_spw;
   }
   return p;
 }
@@ -585,7 +592,7 @@ using namespace lea;
 
 extern "C" size_t lea_conv3d_wino_packed_floats(int cout, int cin) {
   if (cout <= 0 || cin <= 0 || cin % wino::CIN_B != 0) return 0;
-  const int mt = wino::mt_of(cout), cop = wino::cop_of(mt), nstep = mt == 0 ? 12 : 9;
+  const int mt = wino::host_mt(cout), cop = wino::cop_of(mt), nstep = mt == 0 ? 12 : 9;
   // + one 256-float tail: the kernel stages whole 256-float pieces per chunk
   return (size_t)((cout + cop - 1) / cop) * (cin / wino::CIN_B) * nstep * 3 * wino::CIN_B * cop + 256;
 }
@@ -599,7 +606,7 @@ extern "C" int lea_conv3d_wino_pack_weights(const float* w, float* packed, int c
   const long long total = (long long)lea_conv3d_wino_packed_floats(cout, cin);
   const int grid = (int)std::min<long long>((total + 255) / 256, 4096);
   hipStream_t st = as_stream(stream);
-  switch (wino::mt_of(cout)) {
+  switch (wino::host_mt(cout)) {
     case 0: wino::pack_wino_dp_kernel<<<grid, 256, 0, st>>>(w, packed, cout, cin, cin / wino::CIN_B, total); break;
     case 1: wino::pack_wino_kernel<1><<<grid, 256, 0, st>>>(w, packed, cout, cin, cin / wino::CIN_B, total); break;
     case 3: wino::pack_wino_kernel<3><<<grid, 256, 0, st>>>(w, packed, cout, cin, cin / wino::CIN_B, total); break;
@@ -624,6 +631,20 @@ extern "C" int lea_conv3d_wino_set_tile_override(int np, int td, int f) {
   wino::g_override[0] = np;
   wino::g_override[1] = td;
   wino::g_override[2] = f;
+  return 0;
+}
+
+extern "C" int lea_conv3d_wino_set_small_cout(int mode) {
+  clear_error();
+  LEA_CHECK_ARG(mode == 0 || mode == 1, "lea_conv3d_wino_set_small_cout: mode=%d", mode);
+  wino::g_small16 = mode;
+  return 0;
+}
+
+extern "C" int lea_conv3d_wino2_set_walk(int spw) {
+  clear_error();
+  LEA_CHECK_ARG(spw >= 0 && spw <= 64, "lea_conv3d_wino2_set_walk: spw=%d", spw);
+  wino::g_spw = spw;
   return 0;
 }
 

@@ -122,53 +122,75 @@ __global__ __launch_bounds__(NW * 64, OCC) void conv3d_wino2_kernel(const ConvAr
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wc = wave % WC, wr = wave / WC;
   // XCD-aware 1-D order (as the 1-D engine): each XCD walks a contiguous range of
-  // (batch/cout-block, tile, depth pair), depth pair fastest
+  // (batch/cout-block, tile, depth-pair group), depth fastest.  A workgroup walks spw
+  // consecutive depth pairs (items = pairs x chunks through one DMA pipeline): the
+  // small-cin layers (2-4 chunks per pair) otherwise pay a cold first DMA and an
+  // exposed epilogue per two planes
   const int nblk = a.nblk;
   const int xcd = blockIdx.x % 8, idx = blockIdx.x / 8;
   const int q8 = nblk / 8, r8 = nblk % 8;
   const int lin = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + idx;
-  const int dz = lin % a.ndz;
-  const int tile = (lin / a.ndz) % a.ntiles;
-  const int bc = lin / (a.ndz * a.ntiles);
+  const int spw = a.spw > 0 ? a.spw : 1;
+  const int ngz = (a.ndz + spw - 1) / spw;
+  const int gz = lin % ngz;
+  const int tile = (lin / ngz) % a.ntiles;
+  const int bc = lin / (ngz * a.ntiles);
   const int h0 = (tile / a.tiles_w) * C::TH;
   const int w0 = (tile % a.tiles_w) * C::TW;
-  const int d0 = dz * C::TD;
+  const int pz0 = gz * spw, npairs = min(spw, a.ndz - pz0);
   const int b = bc / a.ncob;
   const int cob = bc - b * a.ncob;
   const int co0 = cob * C::COP;
   const int nchunks = a.cin / CIN_B;
+  const int nitems = npairs * nchunks;
   const float* wp = a.wp + (long long)cob * nchunks * C::WS;
   const int HW = a.H * a.W;  // host checks D*H*W*4 < 2^32
   const unsigned nrec = (unsigned)(HW * a.D) * 4u;
 
-  // per-lane byte offsets of this wave's DMA pieces inside one channel volume
-  unsigned voff[XSLOTS_W], voffr[CV ? XSLOTS_W : 1];
+  // per-lane DMA pieces of this wave inside one channel volume: (plane, h, w) of each,
+  // the (h, w) part once (hwo: byte offset in a plane, or OOB), the plane per pair
+  unsigned hwo[XSLOTS_W];
+  int pln[XSLOTS_W], wco[CV ? XSLOTS_W : 1];
 #pragma unroll
   for (int t = 0; t < XSLOTS_W; ++t) {
     const int e = (wave + NW * t) * 64 + lane;
-    unsigned v = 0xFFFFFFF0u, vr = 0xFFFFFFF0u;
+    unsigned v = 0xFFFFFFF0u;
+    int pl = -1000, wc_ = 0;
     if (e < C::IMG) {
       const int p = e / C::PLANE;
       const int r = e - p * C::PLANE;
       const int rr = r / C::RW;
       const int cc = r - rr * C::RW;
-      const int d = d0 + p - 1, h = h0 + rr - 1, w = w0 + cc - 1;
-      if ((unsigned)d < (unsigned)a.D && (unsigned)h < (unsigned)a.H && (unsigned)w < (unsigned)a.W) {
-        if constexpr (CV) {
-          if (w >= d) {
-            v = (unsigned)(h * a.W + w) * 4u;
-            vr = (unsigned)(h * a.W + w - d) * 4u;
-          }
-        } else {
-          v = (unsigned)(d * HW + h * a.W + w) * 4u;
-        }
+      const int h = h0 + rr - 1, w = w0 + cc - 1;
+      if ((unsigned)h < (unsigned)a.H && (unsigned)w < (unsigned)a.W) {
+        v = (unsigned)(h * a.W + w) * 4u;
+        pl = p - 1;
+        wc_ = w;
       }
     }
-    voff[t] = v;
-    if constexpr (CV) voffr[t] = vr;
+    hwo[t] = v;
+    pln[t] = pl;
+    if constexpr (CV) wco[t] = wc_;
   }
+  unsigned voff[XSLOTS_W], voffr[CV ? XSLOTS_W : 1];
+  auto set_pair = [&](int d0) {  // DMA offsets of the pair at output planes d0, d0 + 1
+#pragma unroll
+    for (int t = 0; t < XSLOTS_W; ++t) {
+      const int d = d0 + pln[t];
+      const bool ok = hwo[t] != 0xFFFFFFF0u && (unsigned)d < (unsigned)a.D;
+      if constexpr (CV) {  // planes are the feature maps: left (w >= d) / right shifted by d
+        const bool okc = ok && wco[t] >= d;
+        voff[t] = okc ? hwo[t] : 0xFFFFFFF0u;
+        voffr[t] = okc ? hwo[t] - (unsigned)d * 4u : 0xFFFFFFF0u;
+      } else {
+        voff[t] = ok ? hwo[t] + (unsigned)d * (unsigned)HW * 4u : 0xFFFFFFF0u;
+      }
+    }
+  };
 
-  auto issue = [&](int ch, float* st) {
+  auto issue = [&](int item, float* st) {
+    const int ch = item % nchunks;
+    if (ch == 0) set_pair((pz0 + item / nchunks) * C::TD);
     const float* wsrc = wp + (long long)ch * C::WS;
     float* wdst = st + C::XS;
 #pragma unroll
@@ -231,12 +253,72 @@ __global__ __launch_bounds__(NW * 64, OCC) void conv3d_wino2_kernel(const ConvAr
 #pragma unroll
       for (int m = 0; m < MTE; ++m) acc[x][e][m] = f32x4{0.f, 0.f, 0.f, 0.f};
 
+  // epilogue of one depth pair (output planes d0, d0 + 1): A_W^T per D point, A_D^T
+  // (with G_D's 1/2 factors), folded BN, ReLU, residual; the lane stores 4 outputs
+  // along W for each of the two planes
+  const bool relu = a.flags & LEA_RELU, resid = a.flags & LEA_RESIDUAL;
+  const long long DHW = (long long)HW * a.D;
+  const int w = w0 + F * pq;
+  const int h = h0 + wr * C::RPG + pr;
+  const int nv = min(F, a.W - w);  // valid outputs of this group
+  auto epilogue = [&](int d0) {
+    if (h >= a.H || w >= a.W) return;
+#pragma unroll
+    for (int m = 0; m < MTE; ++m)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int co = co0 + 16 * (wc * MTE + m) + 4 * ci + r;
+        if (co >= a.cout) continue;
+        float n[NE][F];
+#pragma unroll
+        for (int e = 0; e < NE; ++e)
+          aw4(acc[0][e][m][r], acc[1][e][m][r], acc[2][e][m][r], acc[3][e][m][r], acc[4][e][m][r],
+              acc[5][e][m][r], n[e]);
+#pragma unroll
+        for (int t = 0; t < C::TD; ++t) {
+          const int d = d0 + t;
+          if (d >= a.D) break;
+          float y[F];
+#pragma unroll
+          for (int j = 0; j < F; ++j) {
+            const float s = t == 0 ? 0.5f * (n[1][j] + n[2][j]) : 0.5f * (n[1][j] - n[2][j]);
+            y[j] = t == 0 ? n[0][j] + s : s - n[3][j];
+            y[j] = y[j] * sc[m][r] + sh[m][r];
+            if (relu) y[j] = fmaxf(y[j], 0.f);
+          }
+          const long long o = (long long)co * DHW + (long long)d * HW + (long long)h * a.W + w;
+          float* yp = a.y + (long long)b * a.ybs + o;
+          const float* rp = a.res + (long long)b * a.rbs + o;
+          const bool vec = nv == F &&
+              ((reinterpret_cast<uintptr_t>(yp) | (resid ? reinterpret_cast<uintptr_t>(rp) : 0)) & 15) == 0;
+          if (vec) {
+            if (resid) {
+              const float4 rv = *reinterpret_cast<const float4*>(rp);
+              y[0] += rv.x;
+              y[1] += rv.y;
+              y[2] += rv.z;
+              y[3] += rv.w;
+            }
+            *reinterpret_cast<float4*>(yp) = make_float4(y[0], y[1], y[2], y[3]);
+          } else {
+#pragma unroll
+            for (int j = 0; j < F; ++j)
+              if (j < nv) {
+                if (resid) y[j] += rp[j];
+                yp[j] = y[j];
+              }
+          }
+        }
+      }
+  };
+
   issue(0, smem);
-  for (int ch = 0; ch < nchunks; ++ch) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's pieces of chunk ch landed
-    __syncthreads();  // ... and everyone's; chunk ch-1's stage is free
-    if (ch + 1 < nchunks) issue(ch + 1, smem + ((ch + 1) & 1) * C::STAGE);
-    const float* xs = smem + (ch & 1) * C::STAGE;
+  for (int it = 0; it < nitems; ++it) {
+    const int ch = it % nchunks;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's pieces of item it landed
+    __syncthreads();  // ... and everyone's; item it-1's stage is free
+    if (it + 1 < nitems) issue(it + 1, smem + ((it + 1) & 1) * C::STAGE);
+    const float* xs = smem + (it & 1) * C::STAGE;
     const float* ws = xs + C::XS;
     if constexpr (PV) {
       // the workgroup transforms the chunk's halo once: unit (ci, row, group) reads
@@ -362,66 +444,33 @@ __global__ __launch_bounds__(NW * 64, OCC) void conv3d_wino2_kernel(const ConvAr
     xform(raw[0], xf[0]);
     mfmas(xf[1]);
     mfmas(xf[0]);
-  }
-
-  // epilogue: A_W^T per D point, A_D^T (with G_D's 1/2 factors), folded BN, ReLU,
-  // residual; the lane stores 4 outputs along W for each of the two planes
-  const bool relu = a.flags & LEA_RELU, resid = a.flags & LEA_RESIDUAL;
-  const long long DHW = (long long)HW * a.D;
-  const int w = w0 + F * pq;
-  const int h = h0 + wr * C::RPG + pr;
-  if (h >= a.H || w >= a.W) return;
-  const int nv = min(F, a.W - w);  // valid outputs of this group
+    if (ch == nchunks - 1) {  // the pair's last chunk: its epilogue, fresh accumulators
+      epilogue((pz0 + it / nchunks) * C::TD);
 #pragma unroll
-  for (int m = 0; m < MTE; ++m)
+      for (int x = 0; x < NX; ++x)
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int co = co0 + 16 * (wc * MTE + m) + 4 * ci + r;
-      if (co >= a.cout) continue;
-      float n[NE][F];
+        for (int e = 0; e < NE; ++e)
 #pragma unroll
-      for (int e = 0; e < NE; ++e)
-        aw4(acc[0][e][m][r], acc[1][e][m][r], acc[2][e][m][r], acc[3][e][m][r], acc[4][e][m][r],
-            acc[5][e][m][r], n[e]);
-#pragma unroll
-      for (int t = 0; t < C::TD; ++t) {
-        const int d = d0 + t;
-        if (d >= a.D) break;
-        float y[F];
-#pragma unroll
-        for (int j = 0; j < F; ++j) {
-          const float s = t == 0 ? 0.5f * (n[1][j] + n[2][j]) : 0.5f * (n[1][j] - n[2][j]);
-          y[j] = t == 0 ? n[0][j] + s : s - n[3][j];
-          y[j] = y[j] * sc[m][r] + sh[m][r];
-          if (relu) y[j] = fmaxf(y[j], 0.f);
-        }
-        const long long o = (long long)co * DHW + (long long)d * HW + (long long)h * a.W + w;
-        float* yp = a.y + (long long)b * a.ybs + o;
-        const float* rp = a.res + (long long)b * a.rbs + o;
-        const bool vec = nv == F &&
-            ((reinterpret_cast<uintptr_t>(yp) | (resid ? reinterpret_cast<uintptr_t>(rp) : 0)) & 15) == 0;
-        if (vec) {
-          if (resid) {
-            const float4 rv = *reinterpret_cast<const float4*>(rp);
-            y[0] += rv.x;
-            y[1] += rv.y;
-            y[2] += rv.z;
-            y[3] += rv.w;
-          }
-          *reinterpret_cast<float4*>(yp) = make_float4(y[0], y[1], y[2], y[3]);
-        } else {
-#pragma unroll
-          for (int j = 0; j < F; ++j)
-            if (j < nv) {
-              if (resid) y[j] += rp[j];
-              yp[j] = y[j];
-            }
-        }
-      }
+          for (int m = 0; m < MTE; ++m) acc[x][e][m] = f32x4{0.f, 0.f, 0.f, 0.f};
     }
+  }
 }
 
 thread_local char g_name2[96];
+
+// Depth pairs per workgroup when the planner leaves it open (r02 walk sweep,
+// profiles/r02_wino2_walk_sweep.txt): walking 4 pairs gains 4-17 % on the L0 layers
+// (cin 8-32: 2-8 chunks per pair) and 2 on the 16-channel L1 cells, as long as about a
+// full round of workgroups remains (walks that leave the chip half empty lose up to 5x
+// on the small L2 volumes); pairs of 32 chunks (conv1/2) gain nothing from it.
+inline int auto_walk(const ConvArgs& a, int B, int wg_per_cu) {
+  const long long base = (long long)a.ntiles * a.ndz * B * a.ncob;
+  const long long round = 256LL * wg_per_cu;
+  if (a.cin / CIN_B > 16) return 1;
+  int s = 1;
+  while (s < 4 && base / (2 * s) >= round * 15 / 16) s *= 2;
+  return s;
+}
 
 #define LEA_WINO2_CASE(Q, WC, MTE, NW, OCC, PV, CV)                                                \
   if (p.q == Q && p.wc == WC && p.mte == MTE && p.nw == NW && p.occ == OCC && p.pv == PV) {        \
@@ -430,7 +479,8 @@ thread_local char g_name2[96];
     a.tiles_w = (a.W + C_::TW - 1) / C_::TW;                                                       \
     a.ntiles = a.tiles_w * ((a.H + C_::TH - 1) / C_::TH);                                          \
     a.ndz = (a.D + C_::TD - 1) / C_::TD;                                                           \
-    const long long n_ = (long long)a.ntiles * a.ndz * B * a.ncob;                                 \
+    a.spw = std::max(1, std::min(p.spw > 0 ? p.spw : auto_walk(a, B, C_::WG_PER_CU), a.ndz));    \
+    const long long n_ = (long long)a.ntiles * ((a.ndz + a.spw - 1) / a.spw) * B * a.ncob;         \
     LEA_CHECK_ARG(n_ < (1LL << 31), "lea_conv3d(wino2): grid too large");                          \
     a.nblk = (int)n_;                                                                              \
     conv3d_wino2_kernel<Q, WC, MTE, NW, OCC, PV, CV><<<dim3((unsigned)n_), NW * 64, 0, st>>>(a);   \

@@ -72,6 +72,7 @@ __device__ __forceinline__ int a_col(int m, int ci, int n, bool swz) { return ((
 struct Plan2 {
   int q, wc, mte, nw, occ;
   bool pv;  // V transformed once per chunk into LDS by the workgroup
+  int spw;  // depth pairs walked per workgroup
 };
 int run2(const Plan2& p, ConvArgs a, int B, hipStream_t st, bool cv);
 const char* name2(const Plan2& p, bool cv);

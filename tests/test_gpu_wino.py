@@ -125,17 +125,27 @@ def test_wino_matches_the_direct_engine_at_full_size():
     assert err <= 1e-4 * float(a.abs().max()), err
 
 
-def test_depth_paired_tile_matches_the_direct_engine_at_full_size():
-    """The L0 8->8 cell op at config 2 (8 channels, 64x192x320): the depth-paired
-    Winograd tile (couts of two planes per 16-row MFMA tile) vs the direct engine."""
-    assert kernels.wino_kernel_name(1, 8, 64, 192, 320) == "conv3d_wino_kernel<4, 16, 0, 1, 2, false>"
-    g = torch.Generator(device=DEV).manual_seed(4)
-    x = torch.randn((1, 8, 64, 192, 320), device=DEV, generator=g)
-    w = torch.randn(8, 8, 3, 3, 3, device=DEV, generator=g) / np.sqrt(8 * 27)
-    a = kernels.conv3d_bnrelu(x, kernels.pack_conv_weight(w), 8, 3, None, None, relu=False)
-    b = kernels.conv3d_bnrelu_wino(x, kernels.pack_conv_weight_wino(w), 8, None, None, relu=False)
-    err = float((a - b).abs().max())
-    assert err <= 1e-4 * float(a.abs().max()), err
+@pytest.mark.parametrize("mode,name", [
+    (0, "conv3d_wino_kernel<4, 16, 0, 1, 2, false>"),
+    (1, "conv3d_wino2_kernel<16, 1, 1, 4, 2, false, false>")])
+def test_small_cout_tiles_match_the_direct_engine_at_full_size(mode, name):
+    """The L0 8->8 cell op at config 2 (8 channels, 64x192x320) on both small-cout forms
+    of the Winograd entries -- the depth-paired 1-D tile (couts of two planes per 16-row
+    MFMA tile, mode 0, the default) and the W x D engine's 16-row block (mode 1) -- vs
+    the direct engine.  Packing and launch share the mode."""
+    lib = _lib.load()
+    assert lib.lea_conv3d_wino_set_small_cout(mode) == 0
+    try:
+        assert kernels.wino_kernel_name(1, 8, 64, 192, 320) == name
+        g = torch.Generator(device=DEV).manual_seed(4)
+        x = torch.randn((1, 8, 64, 192, 320), device=DEV, generator=g)
+        w = torch.randn(8, 8, 3, 3, 3, device=DEV, generator=g) / np.sqrt(8 * 27)
+        a = kernels.conv3d_bnrelu(x, kernels.pack_conv_weight(w), 8, 3, None, None, relu=False)
+        b = kernels.conv3d_bnrelu_wino(x, kernels.pack_conv_weight_wino(w), 8, None, None, relu=False)
+        err = float((a - b).abs().max())
+        assert err <= 1e-4 * float(a.abs().max()), err
+    finally:
+        lib.lea_conv3d_wino_set_small_cout(0)
 
 
 def test_model_uses_the_winograd_engine():
@@ -146,7 +156,7 @@ def test_model_uses_the_winograd_engine():
     ex = m.matching.executor()
     wino = {n for n, p in ex.p.items() if p.wino is not None}
     assert executor.WINOGRAD and {"stem0", "stem1", "conv1", "conv2"} <= wino
-    # the L0 8-channel cell ops run depth-paired on the same engine
+    # the L0 8-channel cell ops run on the same engine
     assert any(ex.p[n].cout <= 8 and ex.p[n].k == 3 for n in wino)
 
 
@@ -245,9 +255,16 @@ def test_wino2_vs_torch(wino_variant, variant, b, cin, cout, shape, mode):
 
 @pytest.mark.parametrize("variant", [2, 3, 4, 5, 6, 7])
 def test_wino2_keeps_the_1d_engine_where_it_has_no_tile(wino_variant, variant):
-    """couts <= 8 (depth-paired) and 48-row blocks stay on F(4,3) along W."""
+    """48-row blocks, and couts <= 8 in the default (depth-paired) mode, stay on F(4,3)
+    along W; couts <= 8 in mode 1 take the W x D engine's 16-row block."""
     wino_variant(variant)
+    lib = _lib.load()
     assert kernels.wino_kernel_name(1, 8, 64, 192, 320).startswith("conv3d_wino_kernel<")
+    assert lib.lea_conv3d_wino_set_small_cout(1) == 0
+    try:
+        assert kernels.wino_kernel_name(1, 8, 64, 192, 320).startswith("conv3d_wino2_kernel<")
+    finally:
+        lib.lea_conv3d_wino_set_small_cout(0)
     assert kernels.wino_kernel_name(1, 48, 32, 96, 160).startswith("conv3d_wino_kernel<")
 
 
