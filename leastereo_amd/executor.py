@@ -69,6 +69,11 @@ def _conv_params(mod, w=None, folded=None):
 class CellGraphExecutor:
     """Shared machinery: parameter packing, ConvBR dispatch, the searched cell."""
 
+    # fp32: a down-sampled s1 that the next cell reads again as its s0 (same tensor, same
+    # size) feeds one stacked 1x1 conv for both cells (the bf16 executors memoise every
+    # resample instead); LEASTEREO_SHARE_DOWNSAMPLE=0 keeps two passes
+    SHARE_DOWNSAMPLE = os.environ.get("LEASTEREO_SHARE_DOWNSAMPLE", "1") != "0"
+
     def __init__(self, net):
         from .model import ConvBR
         self.m = net
@@ -101,6 +106,20 @@ class CellGraphExecutor:
                 shift = torch.cat([f[1] for f in folded]).contiguous()
                 self.p[f"cells.{i}.s1_group"] = _conv_params(mods[0], w, (scale, shift))
                 self.s1_group[i] = group
+            # a cell that down-samples s1, followed by a same-level cell: the next cell's
+            # s0 is this s1 (Cell.forward returns prev_input, skip_model_3d.py:75) at the
+            # same size, so both 1x1 convs run as one stacked conv over one read of it
+            cells = list(net.cells)
+            for i, (cell, nxt) in enumerate(zip(cells, cells[1:])):
+                if (self.SHARE_DOWNSAMPLE and cell.downup_sample < 0 and nxt.downup_sample == 0
+                        and nxt.c_out == cell.c_out and 2 + cell.steps - cell.block_multiplier == 1
+                        and cell.preprocess.conv.weight.shape[1] == nxt.pre_preprocess.conv.weight.shape[1]):
+                    mods = [nxt.pre_preprocess, cell.preprocess]
+                    folded = [m.folded_bn() for m in mods]
+                    self.p[f"cells.{i}.share"] = _conv_params(
+                        mods[0], torch.cat([m.conv.weight for m in mods], 0),
+                        (torch.cat([f[0] for f in folded]).contiguous(),
+                         torch.cat([f[1] for f in folded]).contiguous()))
 
     def conv(self, name, x, out=None, accumulate=False, x2=None, size=None, residual=None):
         """ConvBR ``name`` on x (or cat(x, x2)); with ``size`` != x's volume the input
@@ -186,17 +205,35 @@ class CellGraphExecutor:
         b = s1.shape[0]
         bm = cell.block_multiplier
         n_states = 2 + cell.steps
-        out = self._empty(b, bm * c, size, s1)
+        memo, self._share_memo = getattr(self, "_share_memo", None), None
+        share = f"cells.{i}.share" in self.p
+        if share:
+            # this cell's s1 preprocess and the next cell's s0 pre_preprocess read the
+            # same down-sampled tensor: one stacked 1x1 conv writes [next s0 | this s1]
+            # into the channels just before and at the start of this cell's output
+            big = self._empty(b, c + bm * c, size, s1)
+            out = self._channels(big, c, c + bm * c)
+        else:
+            out = self._empty(b, bm * c, size, s1)
         slot = {idx: self._channels(out, k * c, (k + 1) * c)
                 for k, idx in enumerate(range(n_states - bm, n_states))}
-        if self._nchannels(s0) != c:
+        if memo is not None and memo[0] is s0 and memo[1] == size:
+            s0 = memo[2]  # computed by the previous cell's stacked conv
+            if 0 in slot:
+                slot[0].copy_(s0)
+        elif self._nchannels(s0) != c:
             s0 = self.conv(f"cells.{i}.pre_preprocess", s0, out=slot.get(0), size=size)
         else:
             if self._volume(s0) != size:
                 s0 = self._resample(s0, size)
             if 0 in slot:
                 slot[0].copy_(s0)
-        s1 = self.conv(f"cells.{i}.preprocess", s1, out=slot.get(1), size=size)
+        if share:
+            self.conv(f"cells.{i}.share", s1, out=self._channels(big, 0, 2 * c), size=size)
+            self._share_memo = (prev_input, size, self._channels(big, 0, c))
+            s1 = self._channels(big, c, 2 * c)
+        else:
+            s1 = self.conv(f"cells.{i}.preprocess", s1, out=slot.get(1), size=size)
         states = [s0, s1]
         group = self.s1_group.get(i, [])
         written = set()
@@ -357,6 +394,8 @@ class FeatureExecutor(CellGraphExecutor):
 class _C8Layout:
     """Activation-layout hooks of the bf16 executors: c8 tensors
     ([B, C/8, D, H, W, 8] bfloat16), channel slices on block boundaries."""
+
+    SHARE_DOWNSAMPLE = False  # _downsampled memoises every resample
 
     def _empty(self, b, c, size, like):
         return torch.empty((b, c // 8) + tuple(size) + (8,), device=like.device, dtype=torch.bfloat16)
