@@ -106,12 +106,14 @@ class CellGraphExecutor:
                 shift = torch.cat([f[1] for f in folded]).contiguous()
                 self.p[f"cells.{i}.s1_group"] = _conv_params(mods[0], w, (scale, shift))
                 self.s1_group[i] = group
-            # a cell that down-samples s1, followed by a same-level cell: the next cell's
-            # s0 is this s1 (Cell.forward returns prev_input, skip_model_3d.py:75) at the
-            # same size, so both 1x1 convs run as one stacked conv over one read of it
+            # a cell that resamples s1, followed by a same-level cell: the next cell's s0
+            # is this s1 (Cell.forward returns prev_input, skip_model_3d.py:75) at the same
+            # size, so both 1x1 convs run as one stacked conv over one read of it (down:
+            # interpolation in the conv's staging; up: one low-resolution conv and one
+            # up-sampling with the stacked BN)
             cells = list(net.cells)
             for i, (cell, nxt) in enumerate(zip(cells, cells[1:])):
-                if (self.SHARE_DOWNSAMPLE and cell.downup_sample < 0 and nxt.downup_sample == 0
+                if (self.SHARE_DOWNSAMPLE and cell.downup_sample != 0 and nxt.downup_sample == 0
                         and nxt.c_out == cell.c_out and 2 + cell.steps - cell.block_multiplier == 1
                         and cell.preprocess.conv.weight.shape[1] == nxt.pre_preprocess.conv.weight.shape[1]):
                     mods = [nxt.pre_preprocess, cell.preprocess]
