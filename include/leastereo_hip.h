@@ -214,6 +214,17 @@ int lea_conv3d_bf16_set_variant(int variant);
 const char* lea_conv3d_kernel_name_bf16(int B, int cout, int cin, int D, int H, int W, int k,
                                         int costvolume);
 
+/* ConvBR 1x1 of a trilinearly resampled c8 input (align_corners=True): the cell
+ * preprocess after a level change, skip_model_3d.py:44-53, without the resampled
+ * tensor -- bit-identical to lea_resample3d_trilinear_bf16 (no epilogue) followed by
+ * lea_conv3d_bnrelu_bf16 (k = 1).  x: [B, cin/8, Di, Hi, Wi, 8]; y: [B, cout/8, D, H, W, 8];
+ * w_packed: the k = 1 packing of lea_conv3d_pack_weights_bf16; cin % 32 == 0 (<= 128),
+ * cout in {16, 32, 64}; flags: LEA_RELU. */
+int lea_conv1x1_resampled_bf16(const void* x, int64_t x_bstride, int Di, int Hi, int Wi,
+                               const void* w_packed, const float* scale, const float* shift,
+                               void* y, int64_t y_bstride, int B, int cin, int cout, int D, int H,
+                               int W, unsigned flags, void* stream);
+
 /* lea_resample3d_trilinear on c8 tensors (same source-index rule and epilogue). */
 int lea_resample3d_trilinear_bf16(const void* x, int64_t x_bstride, void* y, int64_t y_bstride,
                                   int B, int C, int Di, int Hi, int Wi, int Do, int Ho, int Wo,
@@ -286,6 +297,10 @@ int lea_conv3d_wino2_set_walk(int spw);
  * packed and planned as 16-row cout blocks (the W x D engine).  Packing and launches must
  * use the same mode.  Per calling thread. */
 int lea_conv3d_wino_set_small_cout(int mode);
+/* 48k-cout layers (not multiples of 32) on the Winograd entries: 1 (default) = 48-row
+ * blocks of the 1-D engine, 0 = 32-row blocks of the W x D engine (last block padded).
+ * Packing and launches must use the same setting.  Per calling thread. */
+int lea_conv3d_wino_set_block48(int on);
 
 /* ---- Matching-net stem0 over the cost volume, factored (csrc/cv_stem.hip) ----
  * Replaces retrain/LEAStereo.py:34-48 + skip_model_3d.py:141 like

@@ -65,6 +65,8 @@ SIGNATURES = {
     "lea_resample3d_trilinear_bf16": (_i, [_p, _i64, _p, _i64, _i, _i, _i, _i, _i, _i, _i, _i,
                                            _i, _p, _p, _u, _p]),
     "lea_resample_bf16_set_batch": (_i, [_i]),
+    "lea_conv1x1_resampled_bf16": (_i, [_p, _i64, _i, _i, _i, _p, _p, _p, _p, _i64, _i, _i, _i, _i, _i,
+                                        _i, _u, _p]),
     "lea_to_c8_bf16": (_i, [_p, _i64, _p, _i64, _i, _i, _i64, _p]),
     "lea_conv2d_packed_elems_bf16": (ctypes.c_size_t, [_i, _i]),
     "lea_conv2d_pack_weights_bf16": (_i, [_p, _p, _i, _i, _p]),
@@ -83,6 +85,7 @@ SIGNATURES = {
     "lea_conv3d_wino_set_variant": (_i, [_i]),
     "lea_conv3d_wino2_set_walk": (_i, [_i]),
     "lea_conv3d_wino_set_small_cout": (_i, [_i]),
+    "lea_conv3d_wino_set_block48": (_i, [_i]),
     # stem0 over the cost volume, factored through 2D maps
     "lea_cv_stem_split_weights": (_i, [_p, _p, _p, _i, _i, _p]),
     "lea_cv_stem_combine": (_i, [_p, _i64, _p, _i64, _p, _p, _p, _i64, _i, _i, _i, _i, _i, _u, _i,

@@ -375,6 +375,106 @@ __global__ __launch_bounds__(256) void resample_c8_kernel(
   }
 }
 
+// ---- 1x1 conv of a trilinearly resampled c8 input (align_corners=True): the cell
+// preprocess after a level change (skip_model_3d.py:44-53) without materialising the
+// resampled tensor.  A gather-GEMM: lane (g, n) of a wave forms its own B fragment of
+// v_mfma_f32_16x16x32_bf16 -- channel block g of output voxel n, i.e. one 16-byte word
+// of the resampled input -- from the 8 corner words (the resample_c8 expression,
+// rounded to bf16 the same way), so no LDS; the A fragments (the k = 1 packing: one
+// k-step per 32-channel chunk) sit in registers.  Bit-identical to resample_c8 + the
+// 1x1 tile kernel; saves the resampled tensor's write and read.
+template <int MT>
+__global__ __launch_bounds__(256) void conv1x1_rs_c8_kernel(
+    const __bf16* __restrict__ x, long long xbs, int Di, int Hi, int Wi, const bf16x8* __restrict__ wp,
+    const float* __restrict__ scale, const float* __restrict__ shift, __bf16* __restrict__ y,
+    long long ybs, int cin, int cout, int Do, int Ho, int Wo, float rd, float rh, float rw,
+    unsigned flags, int tiles_per_wave) {
+#pragma clang fp contract(off)
+  constexpr int MAXCH = 4;  // cin <= 128 (host)
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int g = lane >> 4, n = lane & 15;
+  const int b = blockIdx.y;
+  const int nch = cin / 32;
+  const long long HWi = (long long)Hi * Wi, vin = HWi * Di;
+  const int HWo = Ho * Wo;
+  const long long vout = (long long)HWo * Do;
+  const bf16x8* xb = reinterpret_cast<const bf16x8*>(x + (long long)b * xbs);
+  // A fragments of every chunk and cout tile (cob block of 16 MT couts: [chunk][s][mtile][g][16])
+  bf16x8 av[MAXCH][MT];
+#pragma unroll
+  for (int c = 0; c < MAXCH; ++c)
+#pragma unroll
+    for (int m = 0; m < MT; ++m) av[c][m] = c < nch ? wp[((c * MT + m) * 4 + g) * 16 + n] : bf16x8{};
+  float sc[MT][4], sh[MT][4];
+#pragma unroll
+  for (int m = 0; m < MT; ++m)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int co = 16 * m + 4 * g + r;
+      sc[m][r] = (scale && co < cout) ? scale[co] : 1.f;
+      sh[m][r] = (scale && co < cout) ? shift[co] : 0.f;
+    }
+  const bool relu = flags & LEA_RELU;
+  const long long tile0 = ((long long)blockIdx.x * 4 + wave) * tiles_per_wave;
+  for (int tt = 0; tt < tiles_per_wave; ++tt) {
+    const long long v0 = (tile0 + tt) * 16;
+    if (v0 >= vout) break;
+    const long long v = min(v0 + n, vout - 1);
+    const int od = (int)(v / HWo), rem = (int)(v - (long long)od * HWo);
+    const int oh = rem / Wo, ow = rem - oh * Wo;
+    const Axis ad = axis_index(rd, od, Di, Do, 1), ah = axis_index(rh, oh, Hi, Ho, 1),
+               aw = axis_index(rw, ow, Wi, Wo, 1);
+    const long long o00 = (long long)ad.i0 * HWi + (long long)ah.i0 * Wi, o01 = (long long)ad.i0 * HWi + (long long)ah.i1 * Wi;
+    const long long o10 = (long long)ad.i1 * HWi + (long long)ah.i0 * Wi, o11 = (long long)ad.i1 * HWi + (long long)ah.i1 * Wi;
+    bf16x8 cw[MAXCH][8];
+#pragma unroll
+    for (int c = 0; c < MAXCH; ++c) {
+      if (c >= nch) break;
+      const bf16x8* xc = xb + (long long)(4 * c + g) * vin;
+      cw[c][0] = xc[o00 + aw.i0];
+      cw[c][1] = xc[o00 + aw.i1];
+      cw[c][2] = xc[o01 + aw.i0];
+      cw[c][3] = xc[o01 + aw.i1];
+      cw[c][4] = xc[o10 + aw.i0];
+      cw[c][5] = xc[o10 + aw.i1];
+      cw[c][6] = xc[o11 + aw.i0];
+      cw[c][7] = xc[o11 + aw.i1];
+    }
+    f32x4 acc[MT];
+#pragma unroll
+    for (int m = 0; m < MT; ++m) acc[m] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int c = 0; c < MAXCH; ++c) {
+      if (c >= nch) break;
+      bf16x8 bv;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float r = ad.l0 * (ah.l0 * (aw.l0 * (float)cw[c][0][j] + aw.l1 * (float)cw[c][1][j]) +
+                                 ah.l1 * (aw.l0 * (float)cw[c][2][j] + aw.l1 * (float)cw[c][3][j])) +
+                        ad.l1 * (ah.l0 * (aw.l0 * (float)cw[c][4][j] + aw.l1 * (float)cw[c][5][j]) +
+                                 ah.l1 * (aw.l0 * (float)cw[c][6][j] + aw.l1 * (float)cw[c][7][j]));
+        bv[j] = (__bf16)r;
+      }
+#pragma unroll
+      for (int m = 0; m < MT; ++m) acc[m] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[c][m], bv, acc[m], 0, 0, 0);
+    }
+    if (v0 + n >= vout) continue;
+#pragma unroll
+    for (int m = 0; m < MT; ++m) {
+      const int co = 16 * m + 4 * g;  // first of the lane's 4 couts
+      if (co >= cout) continue;
+      bf16x4 out;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        float t = acc[m][r] * sc[m][r] + sh[m][r];
+        if (relu) t = fmaxf(t, 0.f);
+        out[r] = (__bf16)t;
+      }
+      *reinterpret_cast<bf16x4*>(y + (long long)b * ybs + ((long long)(co / 8) * vout + v0 + n) * 8 + co % 8) = out;
+    }
+  }
+}
+
 // ---- D-streaming form for the single-chunk 3x3x3 layers (cin <= 16: the whole K is
 // one chunk).  The tile kernel above stages a (TH+2) x 18 x (TD+2) halo per TH x 16 x TD
 // tile and waits for it: r01 counters put these layers' waves 60-78 % parked on that
@@ -736,6 +836,7 @@ thread_local char g_bf_name[96];
 }  // namespace lea
 
 using namespace lea;
+using bf16x8_t = bf::bf16x8;
 
 extern "C" int lea_conv3d_bf16_set_tile_override(int th, int td, int mt) {
   clear_error();
@@ -932,6 +1033,39 @@ extern "C" int lea_resample3d_trilinear_bf16(const void* x, int64_t x_bstride, v
   LEA_RS_K(1) LEA_RS_K(2) LEA_RS_K(4)
 #undef LEA_RS_K
   return launch_status("lea_resample3d_trilinear_bf16");
+}
+
+extern "C" int lea_conv1x1_resampled_bf16(const void* x, int64_t x_bstride, int Di, int Hi, int Wi,
+                                          const void* w_packed, const float* scale, const float* shift,
+                                          void* y, int64_t y_bstride, int B, int cin, int cout, int D,
+                                          int H, int W, unsigned flags, void* stream) {
+  clear_error();
+  LEA_CHECK_ARG(x && w_packed && y && x != y, "lea_conv1x1_resampled_bf16: null or aliased pointer");
+  LEA_CHECK_ARG((scale == nullptr) == (shift == nullptr),
+                "lea_conv1x1_resampled_bf16: scale/shift must both be set or both NULL");
+  LEA_CHECK_ARG(B > 0 && B <= 65535 && Di > 0 && Hi > 0 && Wi > 0 && D > 0 && H > 0 && W > 0,
+                "lea_conv1x1_resampled_bf16: bad shape");
+  LEA_CHECK_ARG(cin % 32 == 0 && cin <= 128 && cout % 16 == 0 && cout <= 64,
+                "lea_conv1x1_resampled_bf16: cin %% 32 (<= 128), cout %% 16 (<= 64) required, got %d/%d",
+                cin, cout);
+  const long long vout = (long long)D * H * W;
+  const int tpw = 2;  // 16-voxel tiles per wave
+  const long long nblk = (vout + 64LL * tpw - 1) / (64LL * tpw);
+  LEA_CHECK_ARG(nblk < (1LL << 31), "lea_conv1x1_resampled_bf16: grid too large");
+  const dim3 grid((unsigned)nblk, B);
+  const float rd = axis_ratio(Di, D, 1), rh = axis_ratio(Hi, H, 1), rw = axis_ratio(Wi, W, 1);
+  // the packed weights are the k = 1 layout of lea_conv3d_pack_weights_bf16 for this cout
+  // (one block of cob_of(cout) couts: cout = 16 MT)
+  LEA_CHECK_ARG(bf::cob_of(cout) == cout, "lea_conv1x1_resampled_bf16: cout %d is not one packing block", cout);
+  const bf16x8_t* wp = reinterpret_cast<const bf16x8_t*>(w_packed);
+#define LEA_RS1(MT_)                                                                                 \
+  if (cout == 16 * MT_)                                                                              \
+    bf::conv1x1_rs_c8_kernel<MT_><<<grid, 256, 0, as_stream(stream)>>>(                              \
+        (const __bf16*)x, x_bstride, Di, Hi, Wi, wp, scale, shift, (__bf16*)y, y_bstride, cin, cout, D, \
+        H, W, rd, rh, rw, flags, tpw);
+  LEA_RS1(1) LEA_RS1(2) LEA_RS1(4)
+#undef LEA_RS1
+  return launch_status("lea_conv1x1_resampled_bf16");
 }
 
 // ---- 2D 3x3 (feature net) on the bf16 engine: the D = 1 case of a (1, 3, 3) kernel

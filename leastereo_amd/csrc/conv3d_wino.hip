@@ -96,48 +96,69 @@ __global__ __launch_bounds__(kConvThreads, 2) void conv3d_wino_kernel(const Conv
   const int xcd = blockIdx.x % 8, idx = blockIdx.x / 8;
   const int q8 = nblk / 8, r8 = nblk % 8;
   const int lin = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + idx;
-  const int dz = lin % a.ndz;
-  const int tile = (lin / a.ndz) % a.ntiles;
-  const int bc = lin / (a.ndz * a.ntiles);
+  // a workgroup walks spw consecutive depth groups of TD planes (items = groups x
+  // chunks through one DMA pipeline), as the W x D engine (conv3d_wino2.hip)
+  const int spw = a.spw > 0 ? a.spw : 1;
+  const int ngz = (a.ndz + spw - 1) / spw;
+  const int gz = lin % ngz;
+  const int tile = (lin / ngz) % a.ntiles;
+  const int bc = lin / (ngz * a.ntiles);
   const int h0 = (tile / a.tiles_w) * C::TH;
   const int w0 = (tile % a.tiles_w) * C::TW;
-  const int d0 = dz * TD;
+  const int dz0 = gz * spw, ngroups = min(spw, a.ndz - dz0);
   const int b = bc / a.ncob;
   const int cob = bc - b * a.ncob;
   const int co0 = cob * C::COP;
   const int nchunks = a.cin / CIN_B;
+  const int nitems = ngroups * nchunks;
   const float* wp = a.wp + (long long)cob * nchunks * C::WS;
   const int HW = a.H * a.W;  // host checks D*H*W*4 < 2^32
   const unsigned nrec = (unsigned)(HW * a.D) * 4u;
 
-  // per-lane byte offsets of this wave's DMA pieces inside one channel volume
-  unsigned voff[XSLOTS_W], voffr[CV ? XSLOTS_W : 1];
+  // per-lane DMA pieces of this wave inside one channel volume: the (h, w) byte offset
+  // once (or OOB), the plane per depth group
+  unsigned hwo[XSLOTS_W];
+  int pln[XSLOTS_W], wco[CV ? XSLOTS_W : 1];
 #pragma unroll
   for (int t = 0; t < XSLOTS_W; ++t) {
     const int e = (wave + kConvWaves * t) * 64 + lane;
-    unsigned v = 0xFFFFFFF0u, vr = 0xFFFFFFF0u;
+    unsigned v = 0xFFFFFFF0u;
+    int pl = -1000, wc_ = 0;
     if (e < C::IMG) {
       const int p = e / C::PLANE;
       const int r = e - p * C::PLANE;
       const int rr = r / C::RW;
       const int cc = r - rr * C::RW;
-      const int d = d0 + p - 1, h = h0 + rr - 1, w = w0 + cc - 1;
-      if ((unsigned)d < (unsigned)a.D && (unsigned)h < (unsigned)a.H && (unsigned)w < (unsigned)a.W) {
-        if constexpr (CV) {
-          if (w >= d) {
-            v = (unsigned)(h * a.W + w) * 4u;
-            vr = (unsigned)(h * a.W + w - d) * 4u;
-          }
-        } else {
-          v = (unsigned)(d * HW + h * a.W + w) * 4u;
-        }
+      const int h = h0 + rr - 1, w = w0 + cc - 1;
+      if ((unsigned)h < (unsigned)a.H && (unsigned)w < (unsigned)a.W) {
+        v = (unsigned)(h * a.W + w) * 4u;
+        pl = p - 1;
+        wc_ = w;
       }
     }
-    voff[t] = v;
-    if constexpr (CV) voffr[t] = vr;
+    hwo[t] = v;
+    pln[t] = pl;
+    if constexpr (CV) wco[t] = wc_;
   }
+  unsigned voff[XSLOTS_W], voffr[CV ? XSLOTS_W : 1];
+  auto set_group = [&](int d0) {  // DMA offsets of the depth group at output planes d0 ..
+#pragma unroll
+    for (int t = 0; t < XSLOTS_W; ++t) {
+      const int d = d0 + pln[t];
+      const bool ok = hwo[t] != 0xFFFFFFF0u && (unsigned)d < (unsigned)a.D;
+      if constexpr (CV) {  // planes are the feature maps: left (w >= d) / right shifted by d
+        const bool okc = ok && wco[t] >= d;
+        voff[t] = okc ? hwo[t] : 0xFFFFFFF0u;
+        voffr[t] = okc ? hwo[t] - (unsigned)d * 4u : 0xFFFFFFF0u;
+      } else {
+        voff[t] = ok ? hwo[t] + (unsigned)d * (unsigned)HW * 4u : 0xFFFFFFF0u;
+      }
+    }
+  };
 
-  auto issue = [&](int ch, float* st) {
+  auto issue = [&](int item, float* st) {
+    const int ch = item % nchunks;
+    if (ch == 0) set_group((dz0 + item / nchunks) * TD);
     const float* wsrc = wp + (long long)ch * C::WS;
     float* wdst = st + C::XS;
 #pragma unroll
@@ -204,12 +225,91 @@ __global__ __launch_bounds__(kConvThreads, 2) void conv3d_wino_kernel(const Conv
 #pragma unroll
         for (int j = 0; j < NP; ++j) acc[x][t][m][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
+  // epilogue of one depth group (output planes d0 ..): A^T, folded BN, ReLU, residual;
+  // lane stores outputs w0 + F p .. + F - 1
+  const bool relu = a.flags & LEA_RELU, resid = a.flags & LEA_RESIDUAL;
+  const long long DHW = (long long)HW * a.D;
+  const int w = w0 + F * pq;
+  auto epilogue = [&](int d0) {
+#pragma unroll
+  for (int t = 0; t < C::TDA; ++t) {
+    const int d = C::DP ? d0 + (ci >> 1) : d0 + t;
+#pragma unroll
+    for (int j = 0; j < NP; ++j) {
+      const int h = h0 + (wave * NP + j) * C::RPG + pr;
+      if (d >= a.D || h >= a.H || w >= a.W) continue;
+      const int nv = min(F, a.W - w);  // valid outputs of this group
+#pragma unroll
+      for (int m = 0; m < C::MTE; ++m)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int co = C::DP ? 4 * (ci & 1) + r : co0 + 16 * m + 4 * ci + r;
+          if (co >= a.cout) continue;
+          float y[F];
+          if constexpr (F == 2) {
+            const float m0 = acc[0][t][m][j][r], m1 = 0.5f * acc[1][t][m][j][r];
+            const float m2 = 0.5f * acc[2][t][m][j][r], m3 = acc[3][t][m][j][r];
+            y[0] = (m0 + m1) + m2;
+            y[1] = (m1 - m2) - m3;
+          } else {
+            const float m0 = 0.25f * acc[0][t][m][j][r];
+            const float m1 = (-1.f / 6.f) * acc[1][t][m][j][r], m2 = (-1.f / 6.f) * acc[2][t][m][j][r];
+            const float m3 = (1.f / 24.f) * acc[3][t][m][j][r], m4 = (1.f / 24.f) * acc[4][t][m][j][r];
+            const float m5 = acc[NX - 1][t][m][j][r];
+            const float sp = m1 + m2, sm = m1 - m2, tp = m3 + m4, tm = m3 - m4;
+            y[0] = (m0 + sp) + tp;
+            y[1] = fmaf(2.f, tm, sm);
+            y[F / 2] = fmaf(4.f, tp, sp);
+            y[F - 1] = fmaf(8.f, tm, sm) + m5;
+          }
+#pragma unroll
+          for (int e = 0; e < F; ++e) {
+            y[e] = y[e] * sc[m][r] + sh[m][r];
+            if (relu) y[e] = fmaxf(y[e], 0.f);
+          }
+          const long long o = (long long)co * DHW + (long long)d * HW + (long long)h * a.W + w;
+          float* yp = a.y + (long long)b * a.ybs + o;
+          const float* rp = a.res + (long long)b * a.rbs + o;
+          const bool vec = nv == F &&
+              ((reinterpret_cast<uintptr_t>(yp) | (resid ? reinterpret_cast<uintptr_t>(rp) : 0)) & (4 * F - 1)) == 0;
+          if (vec) {
+            if constexpr (F == 2) {
+              if (resid) {
+                const float2 rv = *reinterpret_cast<const float2*>(rp);
+                y[0] += rv.x;
+                y[1] += rv.y;
+              }
+              *reinterpret_cast<float2*>(yp) = make_float2(y[0], y[1]);
+            } else {
+              if (resid) {
+                const float4 rv = *reinterpret_cast<const float4*>(rp);
+                y[0] += rv.x;
+                y[1] += rv.y;
+                y[F / 2] += rv.z;
+                y[F - 1] += rv.w;
+              }
+              *reinterpret_cast<float4*>(yp) = make_float4(y[0], y[1], y[F / 2], y[F - 1]);
+            }
+          } else {
+#pragma unroll
+            for (int e = 0; e < F; ++e)
+              if (e < nv) {
+                if (resid) y[e] += rp[e];
+                yp[e] = y[e];
+              }
+          }
+        }
+    }
+  }
+  };
+
   issue(0, smem);
-  for (int ch = 0; ch < nchunks; ++ch) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's pieces of chunk ch landed
-    __syncthreads();  // ... and everyone's; chunk ch-1's stage is free
-    if (ch + 1 < nchunks) issue(ch + 1, smem + ((ch + 1) & 1) * C::STAGE);
-    const float* xs = smem + (ch & 1) * C::STAGE;
+  for (int it = 0; it < nitems; ++it) {
+    const int ch = it % nchunks;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's pieces of item it landed
+    __syncthreads();  // ... and everyone's; item it-1's stage is free
+    if (it + 1 < nitems) issue(it + 1, smem + ((it + 1) & 1) * C::STAGE);
+    const float* xs = smem + (it & 1) * C::STAGE;
     const float* ws = xs + C::XS;
     // one (kd, kh) step: raw inputs (F + 2 per lane as float2s) and weight rows g.
     // Depth-paired, step (p, kh) reads staged plane p once for both output planes.
@@ -301,80 +401,16 @@ __global__ __launch_bounds__(kConvThreads, 2) void conv3d_wino_kernel(const Conv
       if (step + 2 < C::NSTEP) load_step(step + 2, ops[step & 1]);
       mfmas(xf[step & 1]);
     }
-  }
-
-  // epilogue: A^T, folded BN, ReLU, residual; lane stores outputs w0 + F p .. + F - 1
-  const bool relu = a.flags & LEA_RELU, resid = a.flags & LEA_RESIDUAL;
-  const long long DHW = (long long)HW * a.D;
-  const int w = w0 + F * pq;
+    if (ch == nchunks - 1) {  // the depth group's last chunk: its epilogue, fresh accumulators
+      epilogue((dz0 + it / nchunks) * TD);
 #pragma unroll
-  for (int t = 0; t < C::TDA; ++t) {
-    const int d = C::DP ? d0 + (ci >> 1) : d0 + t;
+      for (int x = 0; x < NX; ++x)
 #pragma unroll
-    for (int j = 0; j < NP; ++j) {
-      const int h = h0 + (wave * NP + j) * C::RPG + pr;
-      if (d >= a.D || h >= a.H || w >= a.W) continue;
-      const int nv = min(F, a.W - w);  // valid outputs of this group
+        for (int t = 0; t < C::TDA; ++t)
 #pragma unroll
-      for (int m = 0; m < C::MTE; ++m)
+          for (int m = 0; m < C::MTE; ++m)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int co = C::DP ? 4 * (ci & 1) + r : co0 + 16 * m + 4 * ci + r;
-          if (co >= a.cout) continue;
-          float y[F];
-          if constexpr (F == 2) {
-            const float m0 = acc[0][t][m][j][r], m1 = 0.5f * acc[1][t][m][j][r];
-            const float m2 = 0.5f * acc[2][t][m][j][r], m3 = acc[3][t][m][j][r];
-            y[0] = (m0 + m1) + m2;
-            y[1] = (m1 - m2) - m3;
-          } else {
-            const float m0 = 0.25f * acc[0][t][m][j][r];
-            const float m1 = (-1.f / 6.f) * acc[1][t][m][j][r], m2 = (-1.f / 6.f) * acc[2][t][m][j][r];
-            const float m3 = (1.f / 24.f) * acc[3][t][m][j][r], m4 = (1.f / 24.f) * acc[4][t][m][j][r];
-            const float m5 = acc[NX - 1][t][m][j][r];
-            const float sp = m1 + m2, sm = m1 - m2, tp = m3 + m4, tm = m3 - m4;
-            y[0] = (m0 + sp) + tp;
-            y[1] = fmaf(2.f, tm, sm);
-            y[F / 2] = fmaf(4.f, tp, sp);
-            y[F - 1] = fmaf(8.f, tm, sm) + m5;
-          }
-#pragma unroll
-          for (int e = 0; e < F; ++e) {
-            y[e] = y[e] * sc[m][r] + sh[m][r];
-            if (relu) y[e] = fmaxf(y[e], 0.f);
-          }
-          const long long o = (long long)co * DHW + (long long)d * HW + (long long)h * a.W + w;
-          float* yp = a.y + (long long)b * a.ybs + o;
-          const float* rp = a.res + (long long)b * a.rbs + o;
-          const bool vec = nv == F &&
-              ((reinterpret_cast<uintptr_t>(yp) | (resid ? reinterpret_cast<uintptr_t>(rp) : 0)) & (4 * F - 1)) == 0;
-          if (vec) {
-            if constexpr (F == 2) {
-              if (resid) {
-                const float2 rv = *reinterpret_cast<const float2*>(rp);
-                y[0] += rv.x;
-                y[1] += rv.y;
-              }
-              *reinterpret_cast<float2*>(yp) = make_float2(y[0], y[1]);
-            } else {
-              if (resid) {
-                const float4 rv = *reinterpret_cast<const float4*>(rp);
-                y[0] += rv.x;
-                y[1] += rv.y;
-                y[F / 2] += rv.z;
-                y[F - 1] += rv.w;
-              }
-              *reinterpret_cast<float4*>(yp) = make_float4(y[0], y[1], y[F / 2], y[F - 1]);
-            }
-          } else {
-#pragma unroll
-            for (int e = 0; e < F; ++e)
-              if (e < nv) {
-                if (resid) y[e] += rp[e];
-                yp[e] = y[e];
-              }
-          }
-        }
+            for (int j = 0; j < NP; ++j) acc[x][t][m][j] = f32x4{0.f, 0.f, 0.f, 0.f};
     }
   }
 }
@@ -442,7 +478,14 @@ thread_local int g_spw = 0;  // lea_conv3d_wino2_set_walk: depth pairs per workg
 // W x D engine (1) or depth-paired for the 1-D engine (0, the default: r02 sweep, L0 8->8
 // 175 us depth-paired vs 210 us on the W x D engine's half-empty 16-row block)
 thread_local int g_small16 = 0;
-inline int host_mt(int cout) { return (g_small16 && cout <= 8) ? 1 : mt_of(cout); }
+// lea_conv3d_wino_set_block48: 48k-cout layers as 48-row blocks of the 1-D engine (1) or
+// as 32-row blocks of the W x D engine, the last one padded (0)
+thread_local int g_block48 = 1;
+inline int host_mt(int cout) {
+  if (g_small16 && cout <= 8) return 1;
+  const int mt = mt_of(cout);
+  return (mt == 3 && !g_block48) ? 2 : mt;
+}
 
 // W x D engine tile for variant v (2..4), or nullptr-equivalent (q = 0) when the
 // layer's cout block has no such tile (couts <= 8 and the 48-row blocks stay 1-D)
@@ -526,7 +569,8 @@ inline Plan make_plan(int B, int cout, int D, int H, int W) {
     a.tiles_w = (a.W + C_::TW - 1) / C_::TW;                                                  \
     a.ntiles = a.tiles_w * ((a.H + C_::TH - 1) / C_::TH);                                     \
     a.ndz = (a.D + TD - 1) / TD;                                                              \
-    const long long n_ = (long long)a.ntiles * a.ndz * B * a.ncob;                            \
+    a.spw = std::max(1, std::min(g_spw > 0 ? g_spw : auto_walk(a, B, 2), a.ndz));             \
+    const long long n_ = (long long)a.ntiles * ((a.ndz + a.spw - 1) / a.spw) * B * a.ncob;    \
     LEA_CHECK_ARG(n_ < (1LL << 31), "lea_conv3d(wino): grid too large");                      \
     a.nblk = (int)n_;                                                                         \
     conv3d_wino_kernel<F, Q, MT, NP, TD, CV><<<dim3((unsigned)n_), kConvThreads, 0, st>>>(a); \
@@ -631,6 +675,13 @@ extern "C" int lea_conv3d_wino_set_tile_override(int np, int td, int f) {
   wino::g_override[0] = np;
   wino::g_override[1] = td;
   wino::g_override[2] = f;
+  return 0;
+}
+
+extern "C" int lea_conv3d_wino_set_block48(int on) {
+  clear_error();
+  LEA_CHECK_ARG(on == 0 || on == 1, "lea_conv3d_wino_set_block48: on=%d", on);
+  wino::g_block48 = on;
   return 0;
 }
 

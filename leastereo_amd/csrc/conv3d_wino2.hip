@@ -458,19 +458,6 @@ __global__ __launch_bounds__(NW * 64, OCC) void conv3d_wino2_kernel(const ConvAr
 
 thread_local char g_name2[96];
 
-// Depth pairs per workgroup when the planner leaves it open (r02 walk sweep,
-// profiles/r02_wino2_walk_sweep.txt): walking 4 pairs gains 4-17 % on the L0 layers
-// (cin 8-32: 2-8 chunks per pair) and 2 on the 16-channel L1 cells, as long as about a
-// full round of workgroups remains (walks that leave the chip half empty lose up to 5x
-// on the small L2 volumes); pairs of 32 chunks (conv1/2) gain nothing from it.
-inline int auto_walk(const ConvArgs& a, int B, int wg_per_cu) {
-  const long long base = (long long)a.ntiles * a.ndz * B * a.ncob;
-  const long long round = 256LL * wg_per_cu;
-  if (a.cin / CIN_B > 16) return 1;
-  int s = 1;
-  while (s < 4 && base / (2 * s) >= round * 15 / 16) s *= 2;
-  return s;
-}
 
 #define LEA_WINO2_CASE(Q, WC, MTE, NW, OCC, PV, CV)                                                \
   if (p.q == Q && p.wc == WC && p.mte == MTE && p.nw == NW && p.occ == OCC && p.pv == PV) {        \

@@ -74,6 +74,20 @@ struct Plan2 {
   bool pv;  // V transformed once per chunk into LDS by the workgroup
   int spw;  // depth pairs walked per workgroup
 };
+// Depth groups (pairs) per workgroup when the planner leaves it open (both engines) (r02 walk sweep,
+// profiles/r02_wino2_walk_sweep.txt): walking 4 pairs gains 4-17 % on the L0 layers
+// (cin 8-32: 2-8 chunks per pair) and 2 on the 16-channel L1 cells, as long as about a
+// full round of workgroups remains (walks that leave the chip half empty lose up to 5x
+// on the small L2 volumes); pairs of 32 chunks (conv1/2) gain nothing from it.
+inline int auto_walk(const ConvArgs& a, int B, int wg_per_cu) {
+  const long long base = (long long)a.ntiles * a.ndz * B * a.ncob;
+  const long long round = 256LL * wg_per_cu;
+  if (a.cin / CIN_B > 16) return 1;
+  int s = 1;
+  while (s < 4 && base / (2 * s) >= round * 15 / 16) s *= 2;
+  return s;
+}
+
 int run2(const Plan2& p, ConvArgs a, int B, hipStream_t st, bool cv);
 const char* name2(const Plan2& p, bool cv);
 

@@ -397,7 +397,11 @@ class _C8Layout:
     """Activation-layout hooks of the bf16 executors: c8 tensors
     ([B, C/8, D, H, W, 8] bfloat16), channel slices on block boundaries."""
 
-    SHARE_DOWNSAMPLE = False  # _downsampled memoises every resample
+    # down-sampling 1x1 convs read their input through the interpolating gather-GEMM
+    # (lea_conv1x1_resampled_bf16), so the shared-preprocess stacking applies as in fp32
+    # (LEASTEREO_BF16_FUSED_RS=0: materialise + memoise the resampled tensor instead)
+    FUSED_RS = os.environ.get("LEASTEREO_BF16_FUSED_RS", "1") != "0"
+    SHARE_DOWNSAMPLE = FUSED_RS and CellGraphExecutor.SHARE_DOWNSAMPLE
 
     def _empty(self, b, c, size, like):
         return torch.empty((b, c // 8) + tuple(size) + (8,), device=like.device, dtype=torch.bfloat16)
@@ -413,6 +417,13 @@ class _C8Layout:
     @staticmethod
     def _resample(x, size):
         return kernels.resample_trilinear_bf16(x, size)
+
+    @staticmethod
+    def _share_weight(net, name):
+        """The stacked 1x1 weight of cells.{i}.share: [next cell's pre_preprocess ; this
+        cell's preprocess] (CellGraphExecutor.__init__)."""
+        i = int(name.split(".")[1])
+        return torch.cat([net.cells[i + 1].pre_preprocess.conv.weight, net.cells[i].preprocess.conv.weight], 0)
 
     def _downsampled(self, x, size):
         """Materialised trilinear resample of a c8 tensor, memoised for one reuse: cell i
@@ -442,6 +453,10 @@ class _C8Layout:
             if p.k == 1 and up:  # commuted: 1x1 at the low resolution, resample + BN/ReLU
                 z = kernels.conv3d_bnrelu_bf16(x, p.packed, p.cout, 1, None, None, relu=False)
                 return kernels.resample_trilinear_bf16(z, size, True, out, p.scale, p.shift, p.relu)
+            if (self.FUSED_RS and p.k == 1 and p.kind == "bf16" and p.cin % 32 == 0 and p.cin <= 128
+                    and p.cout in (16, 32, 64)):
+                return kernels.conv1x1_resampled_bf16(x, size, p.packed, p.cout, p.scale, p.shift,
+                                                      p.relu, out)
             x = self._downsampled(x, size)
         if p.kind == "bf16_2d":
             if x2 is not None:
@@ -479,6 +494,8 @@ class MatchingExecutorBF16(_C8Layout, MatchingExecutor):
                     i = int(name.split(".")[1])
                     mods = [matching.cells[i]._ops[op] for _, op in self.s1_group[i]]
                     w = torch.cat([m.conv.weight for m in mods], 0)
+                elif name.endswith(".share"):
+                    w = self._share_weight(matching, name)
                 else:
                     mod = matching.get_submodule(name)
                     assert isinstance(mod, ConvBR)
@@ -558,6 +575,8 @@ class FeatureExecutorBF16(_C8Layout, FeatureExecutor):
                 if name.endswith(".s1_group"):
                     i = int(name.split(".")[1])
                     w = torch.cat([feature.cells[i]._ops[op].conv.weight for _, op in self.s1_group[i]], 0)
+                elif name.endswith(".share"):
+                    w = self._share_weight(feature, name)
                 else:
                     w = feature.get_submodule(name).conv.weight
                 if p.kind == "2d":

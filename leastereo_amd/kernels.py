@@ -489,6 +489,32 @@ def conv3d_bnrelu_bf16(x: torch.Tensor, packed: torch.Tensor, cout: int, k: int,
     return out
 
 
+def conv1x1_resampled_bf16(x: torch.Tensor, size, packed: torch.Tensor, cout: int, scale, shift,
+                           relu: bool = True, out: torch.Tensor | None = None) -> torch.Tensor:
+    """ConvBR 1x1 of interp(x, size, align_corners=True) on c8 tensors, the resampled
+    input never materialised (lea_conv1x1_resampled_bf16)."""
+    _require_c8(x, out)
+    _require_cuda(scale, shift)
+    b, cb, di, hi, wi, _ = x.shape
+    d, h, w = (int(t) for t in size)
+    xbs = _check_c8_view(x, "x")
+    shape = (b, cout // 8, d, h, w, 8)
+    if out is None:
+        out = torch.empty(shape, device=x.device, dtype=torch.bfloat16)
+    if tuple(out.shape) != shape:
+        raise ValueError(f"out shape {tuple(out.shape)} != {shape}")
+    ybs = _check_c8_view(out, "out")
+    name = "conv1x1_rs_c8_kernel"
+    rec = _probe_begin(b, cb * 8, cout, d, h, w, 1, False, b * di * hi * wi, True, name=name, esz=2)
+    check(_lib.load().lea_conv1x1_resampled_bf16(
+        x.data_ptr(), xbs, di, hi, wi, packed.data_ptr(),
+        scale.data_ptr() if scale is not None else None,
+        shift.data_ptr() if shift is not None else None, out.data_ptr(), ybs, b, cb * 8, cout, d, h,
+        w, LEA_RELU if relu else 0, _stream()), "lea_conv1x1_resampled_bf16")
+    _probe_end(rec)
+    return out
+
+
 def conv3d_bnrelu_costvolume_bf16(fl: torch.Tensor, fr: torch.Tensor, maxdisp: int,
                                   packed: torch.Tensor, cout: int, scale, shift,
                                   relu: bool = True) -> torch.Tensor:

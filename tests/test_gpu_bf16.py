@@ -245,3 +245,27 @@ def test_stream_kernel_is_the_tile_kernel(b, cin, cout, shape, mode):
     if mode:
         want = want + r.double()
     _close(kernels.from_c8(outs[0]), want)
+
+
+@pytest.mark.parametrize("b,cin,cout,src,dst", [
+    (2, 32, 16, (8, 12, 20), (4, 6, 10)), (1, 64, 64, (9, 13, 17), (5, 7, 9)),
+    (1, 128, 32, (6, 10, 14), (3, 5, 7)), (3, 32, 32, (1, 12, 40), (1, 6, 20)),
+    (1, 64, 16, (7, 9, 11), (7, 9, 11))])
+def test_conv1x1_resampled_is_resample_then_conv(b, cin, cout, src, dst):
+    """lea_conv1x1_resampled_bf16 == lea_resample3d_trilinear_bf16 + the k = 1 tile
+    kernel, bit for bit (the same bf16 rounding of the interpolated words, the same
+    MFMA chunk order); the same-size case is the plain 1x1."""
+    g = torch.Generator().manual_seed(cin + cout + src[0])
+    x = kernels.to_c8(torch.randn((b, cin) + src, generator=g).to(DEV))
+    w = (torch.randn(cout, cin, 1, 1, 1, generator=g) / np.sqrt(cin)).to(DEV)
+    scale = (torch.rand(cout, generator=g) + 0.5).to(DEV)
+    shift = (torch.randn(cout, generator=g) * 0.1).to(DEV)
+    packed = kernels.pack_conv_weight_bf16(w)
+    want = kernels.conv3d_bnrelu_bf16(kernels.resample_trilinear_bf16(x, dst, True), packed, cout, 1,
+                                      scale, shift, relu=True)
+    got = kernels.conv1x1_resampled_bf16(x, dst, packed, cout, scale, shift, relu=True)
+    assert torch.equal(got, want)
+    big = torch.zeros((b, cout // 8 + 2) + tuple(dst) + (8,), device=DEV, dtype=torch.bfloat16)
+    kernels.conv1x1_resampled_bf16(x, dst, packed, cout, scale, shift, relu=True, out=big[:, 1:1 + cout // 8])
+    assert torch.equal(big[:, 1:1 + cout // 8], want)
+    assert float(big[:, 0].float().abs().sum()) == 0 and float(big[:, -1].float().abs().sum()) == 0

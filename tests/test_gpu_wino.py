@@ -309,3 +309,39 @@ def test_wino2_matches_the_direct_engine_at_full_size(wino_variant, variant):
         b = kernels.conv3d_bnrelu_wino(x, kernels.pack_conv_weight_wino(w), cout, None, None, relu=False)
         err = float((a - b).abs().max())
         assert err <= 1e-4 * float(a.abs().max()), (cin, cout, err)
+
+
+@pytest.mark.parametrize("b,cin,cout,shape,small", [
+    (1, 16, 16, (11, 20, 40), 0),   # W x D engine, 16-row blocks; 6 depth pairs
+    (2, 8, 24, (9, 8, 70), 0),      # W x D engine with the transform pass (32-row block)
+    (1, 16, 48, (7, 12, 33), 0),    # 1-D engine, 48-row block, one plane per group
+    (1, 8, 8, (13, 10, 64), 0),     # 1-D engine, depth-paired
+    (1, 8, 8, (5, 6, 40), 1)])      # W x D engine with an 8-cout block (small-cout mode 1)
+def test_depth_walk_is_bit_identical(b, cin, cout, shape, small):
+    """Workgroups walking 1, 2, 3 or 4 depth groups (lea_conv3d_wino2_set_walk) run the
+    same per-group arithmetic: outputs identical bit for bit, accumulate mode included,
+    for walks that do and do not divide the number of groups."""
+    lib = _lib.load()
+    g = torch.Generator(device=DEV).manual_seed(cin * 7 + cout)
+    x = torch.randn((b, cin) + shape, device=DEV, generator=g)
+    w = torch.randn(cout, cin, 3, 3, 3, device=DEV, generator=g) / np.sqrt(cin * 27)
+    scale = torch.rand(cout, device=DEV, generator=g) + 0.5
+    shift = torch.randn(cout, device=DEV, generator=g) * 0.1
+    r = torch.randn((b, cout) + shape, device=DEV, generator=g)
+    assert lib.lea_conv3d_wino_set_small_cout(small) == 0
+    try:
+        pw = kernels.pack_conv_weight_wino(w)
+        outs = []
+        for walk in (1, 2, 3, 4):
+            assert lib.lea_conv3d_wino2_set_walk(walk) == 0
+            y = r.clone()
+            kernels.conv3d_bnrelu_wino(x, pw, cout, scale, shift, True, y, True)
+            outs.append(y)
+    finally:
+        lib.lea_conv3d_wino2_set_walk(0)
+        lib.lea_conv3d_wino_set_small_cout(0)
+    for y in outs[1:]:
+        assert torch.equal(y, outs[0])
+    want = F.conv3d(x.double(), w.double(), None, 1, 1)
+    want = torch.relu(want * scale.double().view(1, -1, 1, 1, 1) + shift.double().view(1, -1, 1, 1, 1)) + r.double()
+    np.testing.assert_allclose(outs[0].cpu().double().numpy(), want.cpu().numpy(), rtol=1e-4, atol=1e-4)

@@ -26,6 +26,7 @@ def main():
     ap.add_argument("--variants", default="1,2,3,4")
     ap.add_argument("--walks", default="0", help="W x D engine depth pairs per workgroup (0 = planner)")
     ap.add_argument("--small", default="0", help="couts <= 8: 1 = 16-row blocks (W x D), 0 = depth-paired")
+    ap.add_argument("--block48", default="1", help="48k couts: 1 = 48-row 1-D blocks, 0 = padded W x D")
     a = ap.parse_args()
     lib = _lib.load()
     dev = "cuda"
@@ -43,14 +44,16 @@ def main():
         flops = 2.0 * a.batch * d * h * w * cin * cout * 27
         pw = kernels.pack_conv_weight_wino(wt)
         res, ref = {}, None
-        for v, walk, sm in [(int(s), int(t), int(u)) for s in a.variants.split(",")
-                            for t in a.walks.split(",") for u in a.small.split(",")]:
+        for v, walk, sm, b48 in [(int(s), int(t), int(u), int(x)) for s in a.variants.split(",")
+                                 for t in a.walks.split(",") for u in a.small.split(",")
+                                 for x in a.block48.split(",")]:
             assert lib.lea_conv3d_wino_set_small_cout(sm) == 0
+            assert lib.lea_conv3d_wino_set_block48(b48) == 0
             pw = kernels.pack_conv_weight_wino(wt)
             assert lib.lea_conv3d_wino_set_variant(v) == 0
             assert lib.lea_conv3d_wino2_set_walk(walk) == 0
             kname = kernels.wino_kernel_name(a.batch, cout, d, h, w) + (f" spw{walk}" if walk else "") + \
-                ("" if cout > 8 else f" small{sm}")
+                ("" if cout > 8 else f" small{sm}") + ("" if cout % 48 or cout % 32 == 0 else f" b48={b48}")
             y = r.clone()
             kernels.conv3d_bnrelu_wino(x, pw, cout, scale, shift, True, y, acc)
             torch.cuda.synchronize()
@@ -59,12 +62,13 @@ def main():
             err = float((y - ref).abs().max() / (ref.abs().max() + 1e-30))
             yy = torch.zeros_like(r)
             ms = timed(lambda: kernels.conv3d_bnrelu_wino(x, pw, cout, scale, shift, True, yy, acc), a.iters)
-            res[f"{v}/{walk}/{sm}"] = {"kernel": kname, "ms": ms, "tflops": flops / ms / 1e9, "max_rel_diff_vs_v1": err}
+            res[f"{v}/{walk}/{sm}/{b48}"] = {"kernel": kname, "ms": ms, "tflops": flops / ms / 1e9, "max_rel_diff_vs_v1": err}
             print(f"{name:26s} v{v} {kname:44s} {ms * 1e3:8.1f} us  {flops / ms / 1e9:6.1f} TF/s  "
                   f"x{count}  diff {err:.2e}", flush=True)
         lib.lea_conv3d_wino_set_variant(0)
         lib.lea_conv3d_wino2_set_walk(0)
         lib.lea_conv3d_wino_set_small_cout(0)
+        lib.lea_conv3d_wino_set_block48(1)
         out[name] = {"count": count, "variants": res}
     print(json.dumps(out))
 
