@@ -447,3 +447,24 @@ def test_full_size_c2_vs_torch_oracle():
     assert torch.isfinite(disp).all()
     assert float(disp.min()) >= 0.0 and float(disp.max()) <= 191.0
     assert ref.epe(disp.cpu(), want.cpu()) < 1e-3
+
+
+@pytest.mark.parametrize("precision,bound", [("f32", 1e-3), ("bf16", 0.25)])
+def test_stem0_fallback_shape_vs_torch_oracle(precision, bound):
+    """W3 = 66 (W = 198, legal: 66 -> 33 -> 17 -> 33 -> 66) is not a multiple of 4, so the
+    f32 executor runs stem0 as the 3D conv on the in-place cost volume instead of the
+    factored form (float4 rows); bf16 keeps the factored form.  Both vs the oracle at the
+    f32 bar / the bf16 e2e bar (test_bf16_e2e_vs_reference_fixture)."""
+    from leastereo_amd import executor
+    assert not kernels.cv_stem_supported(32, 8, 66, False) and kernels.cv_stem_supported(32, 8, 66, True)
+    m = LEAStereo(default_arch_args(LEAStereoArgs(maxdisp=24)), DEV, precision=precision)
+    m.load_state_dict(state_dict(), strict=True)
+    m = m.to(DEV).eval()
+    left = normal(5151, (1, 3, 48, 198))
+    right = normal(5152, (1, 3, 48, 198))
+    with torch.no_grad():
+        disp = m(left.to(DEV), right.to(DEV)).cpu()
+        want = ref.leastereo_forward(state_dict(), left, right, 24, arch())
+    # (the reference's feature net returns 65 of the 66 columns here: its output is 195 wide)
+    assert executor.CV_STEM and disp.shape == want.shape and torch.isfinite(disp).all()
+    assert ref.epe(disp, want) < bound
