@@ -133,6 +133,17 @@ int lea_conv2d_s3_bnrelu(const void* x, int64_t x_bstride, const float* w, const
                          const float* shift, void* y, int64_t y_bstride, int B, int cin, int cout,
                          int Hi, int Wi, unsigned flags, int dtype, void* stream);
 
+/* Feature-net stems 0 + 1 fused (retrain/new_model_2d.py:93-94): ConvBR2d 3x3 s1 p1
+ * (cin -> c0) then ConvBR2d 3x3 s3 p1 (c0 -> c1), both with folded BN and ReLU, without
+ * writing stem0's full-resolution output (stride 3 tiles it: each stem0 pixel feeds one
+ * stem1 pixel).  w0: [c0, cin, 3, 3], w1: [c1, c0, 3, 3] raw f32.  x: [B, cin, Hi, Wi] f32;
+ * y: [B, c1, Ho, Wo] f32 (dtype LEA_F32) or c8 [B, c1/8, 1, Ho, Wo, 8] bf16 (LEA_BF16),
+ * Ho = (Hi - 1) / 3 + 1.  Instantiated for 3 -> 16 -> 32 (the searched feature net). */
+int lea_feature_stem_bnrelu(const float* x, int64_t x_bstride, const float* w0, const float* scale0,
+                            const float* shift0, const float* w1, const float* scale1,
+                            const float* shift1, void* y, int64_t y_bstride, int B, int cin, int c0,
+                            int c1, int Hi, int Wi, int dtype, void* stream);
+
 /* Tuning hook: force the (NT, TW, TD) tile of the k=3 DMA engine for later convs on
  * the calling thread (nt <= 0 restores the built-in planner).  A tile that is not
  * instantiated for the conv's cout block makes the conv return LEA_E_UNSUPPORTED.

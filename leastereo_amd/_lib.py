@@ -46,6 +46,8 @@ SIGNATURES = {
                                _i, _p]),
     "lea_conv2d_kernel_name": (ctypes.c_char_p, [_i, _i, _i, _i]),
     "lea_conv2d_s3_bnrelu": (_i, [_p, _i64, _p, _p, _p, _p, _i64, _i, _i, _i, _i, _i, _u, _i, _p]),
+    "lea_feature_stem_bnrelu": (_i, [_p, _i64, _p, _p, _p, _p, _p, _p, _p, _i64, _i, _i, _i, _i, _i, _i,
+                                     _i, _p]),
     "lea_resample3d_trilinear": (_i, [_p, _i64, _p, _i64, _i, _i, _i, _i, _i, _i, _i, _i,
                                       _i, _p, _p, _u, _i, _p]),
     "lea_tapsum_workspace_bytes": (ctypes.c_size_t, [_i, _i, _i, _i, _i]),

@@ -363,10 +363,23 @@ class MatchingExecutor(CellGraphExecutor):
 
 
 class FeatureExecutor(CellGraphExecutor):
+    # stems 0 and 1 as one kernel (csrc/feature_stem.hip); LEASTEREO_FEATURE_STEM=0 runs
+    # them as two convs
+    FUSED_STEM = os.environ.get("LEASTEREO_FEATURE_STEM", "1") != "0"
+
+    def _stems(self, x, c8=False):
+        """new_model_2d.py:93-94 (stem1(stem0(x))), fused where the kernel is instantiated."""
+        p0, p1 = self.p["stem0"], self.p["stem1"]
+        if (self.FUSED_STEM and p0.relu and p1.relu and (p0.cin, p0.cout, p1.cout) == (3, 16, 32)
+                and p1.kind == "s3"):
+            return kernels.feature_stem(x, self.m.stem0.conv.weight, p0.scale, p0.shift, p1.packed,
+                                        p1.scale, p1.shift, c8)
+        stem1 = self.conv("stem1", self.conv("stem0", x.unsqueeze(2)))
+        return kernels.to_c8(stem1) if c8 else stem1
+
     def run(self, x):
         """newFeature.forward (new_model_2d.py:140-165): [N,3,H,W] -> [N,32,H/3,W/3]."""
-        x5 = x.unsqueeze(2)
-        stem1 = self.conv("stem1", self.conv("stem0", x5))
+        stem1 = self._stems(x)
         stem2 = self.conv("stem2", stem1)
         out = (stem1, stem2)
         for i in range(len(self.m.cells)):
@@ -600,8 +613,7 @@ class FeatureExecutorBF16(_C8Layout, FeatureExecutor):
             self._fresh()
 
     def _run(self, x):
-        x5 = x.unsqueeze(2)
-        stem1 = kernels.to_c8(self.conv("stem1", self.conv("stem0", x5)))
+        stem1 = self._stems(x, c8=True)
         stem2 = self.conv("stem2", stem1)
         out = (stem1, stem2)
         for i in range(len(self.m.cells)):

@@ -297,6 +297,31 @@ def conv2d_bnrelu(x: torch.Tensor, packed: torch.Tensor, cout: int,
     return out
 
 
+def feature_stem(x: torch.Tensor, w0: torch.Tensor, scale0, shift0, w1: torch.Tensor, scale1, shift1,
+                 c8: bool = False) -> torch.Tensor:
+    """new_model_2d.py:93-94 fused (ConvBR 3x3 s1 then ConvBR 3x3 s3, BN + ReLU each):
+    x [B, cin, H, W] f32 -> [B, c1, 1, Ho, Wo] f32, or c8 [B, c1/8, 1, Ho, Wo, 8] bf16."""
+    _require_cuda(x, scale0, shift0, scale1, shift1)
+    w0, w1 = w0.detach().contiguous(), w1.detach().contiguous()
+    _require_cuda(w0, w1)
+    x = x.contiguous()
+    b, cin, hi, wi = x.shape
+    c0, c1 = w0.shape[0], w1.shape[0]
+    if tuple(w0.shape) != (c0, cin, 3, 3) or tuple(w1.shape) != (c1, c0, 3, 3):
+        raise ValueError(f"feature_stem: weights {tuple(w0.shape)} / {tuple(w1.shape)} do not chain")
+    ho, wo = (hi - 1) // 3 + 1, (wi - 1) // 3 + 1
+    if c8:
+        out = torch.empty((b, c1 // 8, 1, ho, wo, 8), device=x.device, dtype=torch.bfloat16)
+    else:
+        out = torch.empty((b, c1, 1, ho, wo), device=x.device, dtype=torch.float32)
+    ptr = lambda t: t.data_ptr() if t is not None else None  # noqa: E731
+    check(_lib.load().lea_feature_stem_bnrelu(
+        x.data_ptr(), x.stride(0), w0.data_ptr(), ptr(scale0), ptr(shift0), w1.data_ptr(), ptr(scale1),
+        ptr(shift1), out.data_ptr(), out.stride(0), b, cin, c0, c1, hi, wi,
+        _lib.LEA_BF16 if c8 else LEA_F32, _stream()), "lea_feature_stem_bnrelu")
+    return out
+
+
 def conv2d_s3_bnrelu(x: torch.Tensor, w: torch.Tensor, scale: torch.Tensor | None,
                      shift: torch.Tensor | None, relu: bool = True) -> torch.Tensor:
     """ConvBR2d 3x3, stride 3, pad 1 (new_model_2d.py:94) on x [B, cin, 1, H, W]."""

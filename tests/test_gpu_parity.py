@@ -468,3 +468,27 @@ def test_stem0_fallback_shape_vs_torch_oracle(precision, bound):
     # (the reference's feature net returns 65 of the 66 columns here: its output is 195 wide)
     assert executor.CV_STEM and disp.shape == want.shape and torch.isfinite(disp).all()
     assert ref.epe(disp, want) < bound
+
+
+@pytest.mark.parametrize("c8", [False, True])
+def test_fused_feature_stems_vs_torch(c8):
+    """lea_feature_stem_bnrelu (new_model_2d.py:93-94 fused) vs float64 torch of
+    ConvBR(3->16, s1) then ConvBR(16->32, s3), edge rows / columns included (H, W not
+    multiples of 3); c8: the bf16 output of the same f32 values."""
+    g = torch.Generator().manual_seed(77)
+    x = torch.randn(2, 3, 50, 131, generator=g)
+    w0 = torch.randn(16, 3, 3, 3, generator=g) / np.sqrt(27)
+    w1 = torch.randn(32, 16, 3, 3, generator=g) / np.sqrt(144)
+    s0, t0 = torch.rand(16, generator=g) + 0.5, torch.randn(16, generator=g) * 0.1
+    s1, t1 = torch.rand(32, generator=g) + 0.5, torch.randn(32, generator=g) * 0.1
+    a = torch.relu(F.conv2d(x.double(), w0.double(), None, 1, 1) * s0.double().view(1, -1, 1, 1)
+                   + t0.double().view(1, -1, 1, 1))
+    want = torch.relu(F.conv2d(a, w1.double(), None, 3, 1) * s1.double().view(1, -1, 1, 1)
+                      + t1.double().view(1, -1, 1, 1))
+    got = kernels.feature_stem(x.to(DEV), w0.to(DEV), s0.to(DEV), t0.to(DEV), w1.to(DEV), s1.to(DEV),
+                               t1.to(DEV), c8)
+    if c8:
+        got = kernels.from_c8(got)
+        np.testing.assert_allclose(got[:, :, 0].cpu().double().numpy(), want.numpy(), rtol=1e-2, atol=1e-2)
+    else:
+        np.testing.assert_allclose(got[:, :, 0].cpu().double().numpy(), want.numpy(), rtol=1e-4, atol=1e-4)
