@@ -334,13 +334,22 @@ __global__ __launch_bounds__(256) void resample_c8_kernel(
     sc[j] = scale ? scale[cb * 8 + j] : 1.f;
     sh[j] = scale ? shift[cb * 8 + j] : 0.f;
   }
-  const int cells = Ho * Wo, stride = gridDim.x * blockDim.x;
-  for (int t0 = blockIdx.x * blockDim.x + threadIdx.x; t0 < cells; t0 += K * stride) {
+  // XCD-aware order of the plane's workgroups (dispatch round-robins blockIdx over the
+  // 8 XCDs): XCD x takes the contiguous x-th eighth of the rows, so its L2 holds only
+  // that eighth of the source rows (r02: 3.4x fetch amplification on the up-samplings
+  // with the plain order)
+  const int nbx = gridDim.x;
+  const int q8 = nbx / 8, r8 = nbx % 8, xcd = blockIdx.x % 8, idx = blockIdx.x / 8;
+  const int bx = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + idx;
+  const int cells = Ho * Wo;
+  const int span = (cells + nbx - 1) / nbx;  // contiguous outputs per workgroup
+  const int tend = min(cells, (bx + 1) * span);
+  for (int t0 = bx * span + threadIdx.x; t0 < tend; t0 += K * (int)blockDim.x) {
     bf16x8 c[K][8];
     Axis ah[K], aw[K];
 #pragma unroll
     for (int k = 0; k < K; ++k) {
-      const int t = min(t0 + k * stride, cells - 1);
+      const int t = min(t0 + k * (int)blockDim.x, tend - 1);
       const int oh = t / Wo, ow = t % Wo;
       ah[k] = axis_index(rh, oh, Hi, Ho, ac);
       aw[k] = axis_index(rw, ow, Wi, Wo, ac);
@@ -356,8 +365,8 @@ __global__ __launch_bounds__(256) void resample_c8_kernel(
     }
 #pragma unroll
     for (int k = 0; k < K; ++k) {
-      const int t = t0 + k * stride;
-      if (t >= cells) break;
+      const int t = t0 + k * (int)blockDim.x;
+      if (t >= tend) break;
       const Axis &h = ah[k], &w = aw[k];
       bf16x8 o;
 #pragma unroll
