@@ -304,6 +304,11 @@ int lea_conv3d_wino_set_variant(int variant);
  * 4-channel chunks through one DMA pipeline); 0 restores the planner.  Per calling
  * thread. */
 int lea_conv3d_wino2_set_walk(int spw);
+/* Tuning hook: 1 (default) = the Winograd engines' buffer-addressed epilogue where the
+ * shape allows it (W % 4 == 0, 16-B aligned output / residual; residual loads issued
+ * together, the next chunk's DMA waited for without the stores), 0 = the per-group
+ * epilogue.  Per calling thread. */
+int lea_conv3d_wino_set_epi_buf(int on);
 /* couts <= 8 on the Winograd entries: 0 (default) = the depth-paired 1-D tile, 1 =
  * packed and planned as 16-row cout blocks (the W x D engine).  Packing and launches must
  * use the same mode.  Per calling thread. */

@@ -86,6 +86,7 @@ SIGNATURES = {
     "lea_conv3d_wino_set_tile_override": (_i, [_i, _i, _i]),
     "lea_conv3d_wino_set_variant": (_i, [_i]),
     "lea_conv3d_wino2_set_walk": (_i, [_i]),
+    "lea_conv3d_wino_set_epi_buf": (_i, [_i]),
     "lea_conv3d_wino_set_small_cout": (_i, [_i]),
     "lea_conv3d_wino_set_block48": (_i, [_i]),
     # stem0 over the cost volume, factored through 2D maps
@@ -132,6 +133,7 @@ def load():
 # A/B switches for the planners' tuning hooks (thread-local in the library: they apply
 # to the thread that loads it), e.g. LEASTEREO_WINO2_WALK=1 to disable the depth walk
 TUNING_ENV = {"LEASTEREO_WINO2_WALK": "lea_conv3d_wino2_set_walk",
+              "LEASTEREO_EPI_BUF": "lea_conv3d_wino_set_epi_buf",
               "LEASTEREO_RESAMPLE_K": "lea_resample_bf16_set_batch"}
 
 

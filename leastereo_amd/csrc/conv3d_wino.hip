@@ -227,9 +227,76 @@ __global__ __launch_bounds__(kConvThreads, 2) void conv3d_wino_kernel(const Conv
 
   // epilogue of one depth group (output planes d0 ..): A^T, folded BN, ReLU, residual;
   // lane stores outputs w0 + F p .. + F - 1
+#ifdef LEA_EXP_NORES  // timing experiments (tools/build_variants.sh): no residual read
+  const bool relu = a.flags & LEA_RELU, resid = false;
+#else
   const bool relu = a.flags & LEA_RELU, resid = a.flags & LEA_RESIDUAL;
+#endif
   const long long DHW = (long long)HW * a.D;
   const int w = w0 + F * pq;
+  // the buffer-addressed form (wino_common.h, F = 4): residual loads all issued first,
+  // every lane the same NST float4 stores (invalid ones out of range: dropped)
+  const bool ebuf = F == 4 && (a.flags & kEpiBuf);
+  constexpr int NST = C::TDA * NP * C::MTE * 4;
+  const int nco = C::DP ? a.cout : min(C::COP, a.cout - co0);
+  const __amdgpu_buffer_rsrc_t yrs = block_rsrc(a.y + (long long)b * a.ybs + (long long)co0 * DHW, nco * DHW * 4);
+  const __amdgpu_buffer_rsrc_t rrs =
+      block_rsrc((resid ? a.res : a.y) + (long long)b * (resid ? a.rbs : a.ybs) + (long long)co0 * DHW, nco * DHW * 4);
+  auto epilogue_buf = [&](int d0) {
+    unsigned off[C::TDA][NP][C::MTE][4];
+#pragma unroll
+    for (int t = 0; t < C::TDA; ++t)
+#pragma unroll
+      for (int j = 0; j < NP; ++j)
+#pragma unroll
+        for (int m = 0; m < C::MTE; ++m)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int d = C::DP ? d0 + (ci >> 1) : d0 + t;
+            const int h = h0 + (wave * NP + j) * C::RPG + pr;
+            const int cr = C::DP ? 4 * (ci & 1) + r : 16 * m + 4 * ci + r;
+            off[t][j][m][r] = (d < a.D && h < a.H && w < a.W && cr < nco)
+                                  ? (unsigned)(cr * DHW + (long long)d * HW + h * a.W + w) * 4u
+                                  : kEpiOob;
+          }
+    f32x4 rv[C::TDA][NP][C::MTE][4];
+    if (resid) {
+#pragma unroll
+      for (int t = 0; t < C::TDA; ++t)
+#pragma unroll
+        for (int j = 0; j < NP; ++j)
+#pragma unroll
+          for (int m = 0; m < C::MTE; ++m)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) rv[t][j][m][r] = buf_load4(rrs, off[t][j][m][r]);
+    }
+#pragma unroll
+    for (int t = 0; t < C::TDA; ++t)
+#pragma unroll
+      for (int j = 0; j < NP; ++j)
+#pragma unroll
+        for (int m = 0; m < C::MTE; ++m)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const float m0 = 0.25f * acc[0][t][m][j][r];
+            const float m1 = (-1.f / 6.f) * acc[1][t][m][j][r], m2 = (-1.f / 6.f) * acc[2][t][m][j][r];
+            const float m3 = (1.f / 24.f) * acc[3][t][m][j][r], m4 = (1.f / 24.f) * acc[4][t][m][j][r];
+            const float m5 = acc[NX - 1][t][m][j][r];
+            const float sp = m1 + m2, sm = m1 - m2, tp = m3 + m4, tm = m3 - m4;
+            f32x4 y;
+            y[0] = (m0 + sp) + tp;
+            y[1] = fmaf(2.f, tm, sm);
+            y[2] = fmaf(4.f, tp, sp);
+            y[3] = fmaf(8.f, tm, sm) + m5;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              float v = y[e] * sc[m][r] + sh[m][r];
+              if (relu) v = fmaxf(v, 0.f);
+              y[e] = resid ? v + rv[t][j][m][r][e] : v;
+            }
+            buf_store4(yrs, off[t][j][m][r], y);
+          }
+  };
   auto epilogue = [&](int d0) {
 #pragma unroll
   for (int t = 0; t < C::TDA; ++t) {
@@ -272,7 +339,13 @@ __global__ __launch_bounds__(kConvThreads, 2) void conv3d_wino_kernel(const Conv
           const float* rp = a.res + (long long)b * a.rbs + o;
           const bool vec = nv == F &&
               ((reinterpret_cast<uintptr_t>(yp) | (resid ? reinterpret_cast<uintptr_t>(rp) : 0)) & (4 * F - 1)) == 0;
+#ifdef LEA_EXP_NOSTORE  // timing experiments: keep the epilogue math, drop the stores
+          if (y[0] == 1234.5f) *yp = y[F - 1];
+          else if (true) {
+          } else if (vec) {
+#else
           if (vec) {
+#endif
             if constexpr (F == 2) {
               if (resid) {
                 const float2 rv = *reinterpret_cast<const float2*>(rp);
@@ -306,7 +379,7 @@ __global__ __launch_bounds__(kConvThreads, 2) void conv3d_wino_kernel(const Conv
   issue(0, smem);
   for (int it = 0; it < nitems; ++it) {
     const int ch = it % nchunks;
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's pieces of item it landed
+    wait_item<NST>(ebuf && ch == 0 && it > 0);  // this wave's pieces of item it landed
     __syncthreads();  // ... and everyone's; item it-1's stage is free
     if (it + 1 < nitems) issue(it + 1, smem + ((it + 1) & 1) * C::STAGE);
     const float* xs = smem + (it & 1) * C::STAGE;
@@ -402,7 +475,10 @@ __global__ __launch_bounds__(kConvThreads, 2) void conv3d_wino_kernel(const Conv
       mfmas(xf[step & 1]);
     }
     if (ch == nchunks - 1) {  // the depth group's last chunk: its epilogue, fresh accumulators
-      epilogue((dz0 + it / nchunks) * TD);
+      if (ebuf)
+        epilogue_buf((dz0 + it / nchunks) * TD);
+      else
+        epilogue((dz0 + it / nchunks) * TD);
 #pragma unroll
       for (int x = 0; x < NX; ++x)
 #pragma unroll
@@ -481,6 +557,7 @@ thread_local int g_small16 = 0;
 // lea_conv3d_wino_set_block48: 48k-cout layers as 48-row blocks of the 1-D engine (1) or
 // as 32-row blocks of the W x D engine, the last one padded (0)
 thread_local int g_block48 = 1;
+thread_local int g_epibuf = 1;  // lea_conv3d_wino_set_epi_buf
 inline int host_mt(int cout) {
   if (g_small16 && cout <= 8) return 1;
   const int mt = mt_of(cout);
@@ -626,6 +703,7 @@ int common(ConvArgs& a, int B, bool cv, int dtype, void* stream) {
     return LEA_E_UNSUPPORTED;
   }
   const Plan p = make_plan(B, a.cout, a.D, a.H, a.W);
+  if (g_epibuf && epi_buf_ok(a)) a.flags |= kEpiBuf;
   return run(p, a, B, as_stream(stream), cv);
 }
 
@@ -682,6 +760,13 @@ extern "C" int lea_conv3d_wino_set_block48(int on) {
   clear_error();
   LEA_CHECK_ARG(on == 0 || on == 1, "lea_conv3d_wino_set_block48: on=%d", on);
   wino::g_block48 = on;
+  return 0;
+}
+
+extern "C" int lea_conv3d_wino_set_epi_buf(int on) {
+  clear_error();
+  LEA_CHECK_ARG(on == 0 || on == 1, "lea_conv3d_wino_set_epi_buf: on=%d", on);
+  wino::g_epibuf = on;
   return 0;
 }
 

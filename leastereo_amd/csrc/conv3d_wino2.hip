@@ -256,11 +256,70 @@ __global__ __launch_bounds__(NW * 64, OCC) void conv3d_wino2_kernel(const ConvAr
   // epilogue of one depth pair (output planes d0, d0 + 1): A_W^T per D point, A_D^T
   // (with G_D's 1/2 factors), folded BN, ReLU, residual; the lane stores 4 outputs
   // along W for each of the two planes
+#ifdef LEA_EXP_NORES  // timing experiments (tools/build_variants.sh): no residual read
+  const bool relu = a.flags & LEA_RELU, resid = false;
+#else
   const bool relu = a.flags & LEA_RELU, resid = a.flags & LEA_RESIDUAL;
+#endif
   const long long DHW = (long long)HW * a.D;
   const int w = w0 + F * pq;
   const int h = h0 + wr * C::RPG + pr;
   const int nv = min(F, a.W - w);  // valid outputs of this group
+  const bool ebuf = a.flags & kEpiBuf;
+  constexpr int NST = MTE * 4 * C::TD;  // buffer stores per epilogue
+  // the buffer-addressed form (wino_common.h): residual loads all issued first, every
+  // lane the same NST float4 stores (invalid ones out of range: dropped)
+  const int nco = min(C::COP, a.cout - co0);
+  const __amdgpu_buffer_rsrc_t yrs = block_rsrc(a.y + (long long)b * a.ybs + (long long)co0 * DHW, nco * DHW * 4);
+  const __amdgpu_buffer_rsrc_t rrs =
+      block_rsrc((resid ? a.res : a.y) + (long long)b * (resid ? a.rbs : a.ybs) + (long long)co0 * DHW, nco * DHW * 4);
+  auto epilogue_buf = [&](int d0) {
+    const bool lv = h < a.H && w < a.W;
+    unsigned off[MTE][4][C::TD];
+#pragma unroll
+    for (int m = 0; m < MTE; ++m)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int t = 0; t < C::TD; ++t) {
+          const int cr = 16 * (wc * MTE + m) + 4 * ci + r, d = d0 + t;
+          off[m][r][t] = (lv && cr < nco && d < a.D)
+                             ? (unsigned)(cr * DHW + (long long)d * HW + h * a.W + w) * 4u
+                             : kEpiOob;
+        }
+    f32x4 rv[MTE][4][C::TD];
+    if (resid) {
+#pragma unroll
+      for (int m = 0; m < MTE; ++m)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+#pragma unroll
+          for (int t = 0; t < C::TD; ++t) rv[m][r][t] = buf_load4(rrs, off[m][r][t]);
+    }
+#pragma unroll
+    for (int m = 0; m < MTE; ++m)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        float n[NE][F];
+#pragma unroll
+        for (int e = 0; e < NE; ++e)
+          aw4(acc[0][e][m][r], acc[1][e][m][r], acc[2][e][m][r], acc[3][e][m][r], acc[4][e][m][r],
+              acc[5][e][m][r], n[e]);
+#pragma unroll
+        for (int t = 0; t < C::TD; ++t) {
+          f32x4 y;
+#pragma unroll
+          for (int j = 0; j < F; ++j) {
+            const float s = t == 0 ? 0.5f * (n[1][j] + n[2][j]) : 0.5f * (n[1][j] - n[2][j]);
+            float v = t == 0 ? n[0][j] + s : s - n[3][j];
+            v = v * sc[m][r] + sh[m][r];
+            if (relu) v = fmaxf(v, 0.f);
+            y[j] = resid ? v + rv[m][r][t][j] : v;
+          }
+          buf_store4(yrs, off[m][r][t], y);
+        }
+      }
+  };
   auto epilogue = [&](int d0) {
     if (h >= a.H || w >= a.W) return;
 #pragma unroll
@@ -291,7 +350,13 @@ __global__ __launch_bounds__(NW * 64, OCC) void conv3d_wino2_kernel(const ConvAr
           const float* rp = a.res + (long long)b * a.rbs + o;
           const bool vec = nv == F &&
               ((reinterpret_cast<uintptr_t>(yp) | (resid ? reinterpret_cast<uintptr_t>(rp) : 0)) & 15) == 0;
+#ifdef LEA_EXP_NOSTORE  // timing experiments: keep the epilogue math, drop the stores
+          if (y[0] == 1234.5f) *yp = y[F - 1];
+          else if (true) {
+          } else if (vec) {
+#else
           if (vec) {
+#endif
             if (resid) {
               const float4 rv = *reinterpret_cast<const float4*>(rp);
               y[0] += rv.x;
@@ -315,7 +380,7 @@ __global__ __launch_bounds__(NW * 64, OCC) void conv3d_wino2_kernel(const ConvAr
   issue(0, smem);
   for (int it = 0; it < nitems; ++it) {
     const int ch = it % nchunks;
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's pieces of item it landed
+    wait_item<NST>(ebuf && ch == 0 && it > 0);  // this wave's pieces of item it landed
     __syncthreads();  // ... and everyone's; item it-1's stage is free
     if (it + 1 < nitems) issue(it + 1, smem + ((it + 1) & 1) * C::STAGE);
     const float* xs = smem + (it & 1) * C::STAGE;
@@ -445,7 +510,10 @@ __global__ __launch_bounds__(NW * 64, OCC) void conv3d_wino2_kernel(const ConvAr
     mfmas(xf[1]);
     mfmas(xf[0]);
     if (ch == nchunks - 1) {  // the pair's last chunk: its epilogue, fresh accumulators
-      epilogue((pz0 + it / nchunks) * C::TD);
+      if (ebuf)
+        epilogue_buf((pz0 + it / nchunks) * C::TD);
+      else
+        epilogue((pz0 + it / nchunks) * C::TD);
 #pragma unroll
       for (int x = 0; x < NX; ++x)
 #pragma unroll

@@ -65,6 +65,45 @@ __device__ __forceinline__ void dma_dwordx4(const float* src, unsigned lds) {
 
 __device__ __forceinline__ int a_col(int m, int ci, int n, bool swz) { return ((swz ? (m ^ (ci & 1)) : m) * 16) + n; }
 
+// Buffer-addressed epilogue (host sets kEpiBuf, `epi_buf_ok`): every lane issues the
+// same residual loads and output stores whatever its validity -- an invalid lane's
+// offset is out of the block's range, so its load reads 0 and its store is dropped.
+// The loads go out together (one latency instead of one round trip per store), and the
+// count of stores per epilogue is a compile-time constant, so the next chunk head can
+// wait for its DMA with vmcnt(stores) -- loads, stores and LDS-DMA retire in issue
+// order (MI355X_MICROARCH.md, s_waitcnt) -- instead of for the stores as well.
+constexpr unsigned kEpiBuf = 1u << 16;  // internal ConvArgs::flags bit
+constexpr unsigned kEpiOob = 0xFFFFFF00u;
+typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t block_rsrc(const float* base, long long bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc((void*)base, 0, (int)(unsigned)bytes, 0x00020000);
+}
+__device__ __forceinline__ f32x4 buf_load4(__amdgpu_buffer_rsrc_t rs, unsigned off) {
+  return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0));
+}
+__device__ __forceinline__ void buf_store4(__amdgpu_buffer_rsrc_t rs, unsigned off, f32x4 v) {
+  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, v), rs, off, 0, 0);
+}
+// chunk head: this wave's DMA of the coming item landed; after an epilogue of nst
+// buffer stores (issued after that DMA) those may stay in flight
+template <int NST>
+__device__ __forceinline__ void wait_item(bool after_epilogue) {
+  static_assert(NST > 0 && NST < 64, "vmcnt immediate");
+  if (after_epilogue)
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NST) : "memory");
+  else
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+// host: whole float4 output groups, 16-B aligned blocks, a cout block (<= 48 channels)
+// addressable by 32-bit byte offsets below kEpiOob
+inline bool epi_buf_ok(const ConvArgs& a) {
+  const long long dhw = (long long)a.D * a.H * a.W;
+  bool ok = a.W % 4 == 0 && dhw % 4 == 0 && ((uintptr_t)a.y & 15) == 0 && a.ybs % 4 == 0 &&
+            48LL * dhw * 4 < (long long)kEpiOob;
+  if (a.flags & LEA_RESIDUAL) ok = ok && ((uintptr_t)a.res & 15) == 0 && a.rbs % 4 == 0;
+  return ok;
+}
+
 // Two-dimensional engine (conv3d_wino2.hip): Q output groups of 4 per tile row,
 // WC cout tiles x (NW / WC) row sets of waves, MTE 16-row cout tiles per wave, OCC
 // waves per SIMD (launch bound), PV = inputs transformed once per chunk into LDS; the packed weights are the 1-D engine's for the

@@ -27,7 +27,7 @@ class KernelProbe:
 
     def __init__(self, names=None):
         self.names = None if names is None else set(names)
-        self.records = []  # (name, flops, bytes, start_event, end_event, mfma_flops)
+        self.records = []  # (name, flops, bytes, start_event, end_event, mfma_flops, shape)
 
     def __enter__(self):
         global _probe
@@ -41,7 +41,7 @@ class KernelProbe:
     def summary(self):
         torch.cuda.synchronize()
         out = {}
-        for name, flops, nbytes, e0, e1, mfma in self.records:
+        for name, flops, nbytes, e0, e1, mfma, _ in self.records:
             d = out.setdefault(name, {"launches": 0, "flops": 0.0, "bytes": 0.0, "ms": 0.0,
                                       "mfma_flops": 0.0})
             d["launches"] += 1
@@ -126,15 +126,15 @@ def _probe_begin(b, cin, cout, d, h, w, k, accumulate, in_vox, resampled, name=N
     nbytes = esz * (in_vox * cin + vox * cout * (2 if accumulate else 1)) + 4.0 * cout * cin * k ** 3
     e0 = torch.cuda.Event(enable_timing=True)
     e0.record()
-    return probe, name, flops, nbytes, e0, flops * mfma_scale
+    return probe, name, flops, nbytes, e0, flops * mfma_scale, (b, cin, cout, d, h, w, k)
 
 
 def _probe_end(rec):
     if rec is not None:
-        probe, name, flops, nbytes, e0, mfma = rec
+        probe, name, flops, nbytes, e0, mfma, shape = rec
         e1 = torch.cuda.Event(enable_timing=True)
         e1.record()
-        probe.records.append((name, flops, nbytes, e0, e1, mfma))
+        probe.records.append((name, flops, nbytes, e0, e1, mfma, shape))
 
 
 def _conv_out(x_shape5, cout, spatial, out, accumulate, device, dtype):
@@ -710,7 +710,7 @@ def cv_stem_combine(lmaps: torch.Tensor, rmaps: torch.Tensor, cout: int, d3: int
         # algorithmic bytes: the output write (the maps are L2/MALL-resident reads)
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record()
-        rec = (name, 0.0, float(out.numel() * out.element_size()), e0, e1, 0.0)
+        rec = (name, 0.0, float(out.numel() * out.element_size()), e0, e1, 0.0, (b, 0, cout, d3, h, w, 0))
     check(_lib.load().lea_cv_stem_combine(
         lmaps.data_ptr(), lbs, rmaps.data_ptr(), rbs,
         scale.data_ptr() if scale is not None else None,
