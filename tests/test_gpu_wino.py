@@ -345,3 +345,44 @@ def test_depth_walk_is_bit_identical(b, cin, cout, shape, small):
     want = F.conv3d(x.double(), w.double(), None, 1, 1)
     want = torch.relu(want * scale.double().view(1, -1, 1, 1, 1) + shift.double().view(1, -1, 1, 1, 1)) + r.double()
     np.testing.assert_allclose(outs[0].cpu().double().numpy(), want.cpu().numpy(), rtol=1e-4, atol=1e-4)
+
+
+@pytest.mark.parametrize("b,cin,cout,shape,small,variant", [
+    (1, 16, 16, (11, 20, 40), 0, 0),   # W x D engine, 16-row blocks, partial row tiles
+    (2, 8, 24, (9, 8, 68), 0, 0),      # W x D engine with the transform pass, 24 of 32 couts
+    (1, 16, 48, (7, 12, 36), 0, 0),    # 1-D engine, 48-row block
+    (1, 8, 8, (13, 10, 64), 0, 0),     # 1-D engine, depth-paired, odd depth
+    (1, 32, 32, (5, 10, 20), 0, 1),    # 1-D engine, 32-row block, two planes
+    (1, 8, 8, (5, 6, 40), 1, 0)])      # W x D engine with an 8-cout block (small-cout mode 1)
+def test_buffer_epilogue_is_bit_identical(b, cin, cout, shape, small, variant):
+    """The buffer-addressed epilogue (out-of-range lanes dropped, residual loads issued
+    together; lea_conv3d_wino_set_epi_buf) stores exactly what the per-group epilogue
+    stores, into a channel slice of a larger buffer, with and without the residual."""
+    lib = _lib.load()
+    g = torch.Generator(device=DEV).manual_seed(cin * 5 + cout + shape[2])
+    x = torch.randn((b, cin) + shape, device=DEV, generator=g)
+    w = torch.randn(cout, cin, 3, 3, 3, device=DEV, generator=g) / np.sqrt(cin * 27)
+    scale = torch.rand(cout, device=DEV, generator=g) + 0.5
+    shift = torch.randn(cout, device=DEV, generator=g) * 0.1
+    r = torch.randn((b, cout + 8) + shape, device=DEV, generator=g)
+    assert lib.lea_conv3d_wino_set_small_cout(small) == 0
+    assert lib.lea_conv3d_wino_set_variant(variant) == 0
+    try:
+        pw = kernels.pack_conv_weight_wino(w)
+        outs = []
+        for on in (0, 1):
+            assert lib.lea_conv3d_wino_set_epi_buf(on) == 0
+            for acc in (False, True):
+                y = r.clone()
+                kernels.conv3d_bnrelu_wino(x, pw, cout, scale, shift, True, y[:, 4:4 + cout], acc)
+                outs.append(y)
+    finally:
+        lib.lea_conv3d_wino_set_epi_buf(1)
+        lib.lea_conv3d_wino_set_variant(0)
+        lib.lea_conv3d_wino_set_small_cout(0)
+    assert torch.equal(outs[0], outs[2]) and torch.equal(outs[1], outs[3])
+    assert torch.equal(outs[3][:, :4], r[:, :4]) and torch.equal(outs[3][:, 4 + cout:], r[:, 4 + cout:])
+    want = F.conv3d(x.double(), w.double(), None, 1, 1)
+    want = torch.relu(want * scale.double().view(1, -1, 1, 1, 1) + shift.double().view(1, -1, 1, 1, 1))
+    np.testing.assert_allclose(outs[3][:, 4:4 + cout].cpu().double().numpy(),
+                               (want + r[:, 4:4 + cout].double()).cpu().numpy(), rtol=1e-4, atol=1e-4)
