@@ -304,6 +304,11 @@ int lea_conv3d_wino_set_variant(int variant);
  * 4-channel chunks through one DMA pipeline); 0 restores the planner.  Per calling
  * thread. */
 int lea_conv3d_wino2_set_walk(int spw);
+/* Tuning hook: 1 (default) = lea_conv3d_bnrelu_resampled with k = 1 and at most 131072
+ * output voxels (B x D x H x W) on the gather-GEMM (each lane interpolates its own MFMA
+ * operand from the 8 corners, no staging), 0 = always the register-staged engine.
+ * Per calling thread. */
+int lea_conv3d_set_rs_gather(int on);
 /* Tuning hook: 1 (default) = the Winograd engines' buffer-addressed epilogue where the
  * shape allows it (W % 4 == 0, 16-B aligned output / residual; residual loads issued
  * together, the next chunk's DMA waited for without the stores), 0 = the per-group

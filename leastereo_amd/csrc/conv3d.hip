@@ -111,6 +111,111 @@ __global__ __launch_bounds__(kConvThreads, 2) void conv3d_reg_kernel(const ConvA
   epilogue<KS, MT, NT, TW, 1>(a, acc, b, co0, d0, h0, w0, wave, lane);
 }
 
+// ------------------------------------- 1x1 of a trilinearly resampled input, gather-GEMM
+// The cell preprocess after a level change (skip_model_3d.py:44-53: trilinear
+// align_corners=True, then the 1x1 ConvBR) without the resampled tensor and without
+// staging: lane (g, n) of a wave forms its own B fragment of v_mfma_f32_16x16x4_f32 --
+// input channel 4 s + g of output voxel v0 + n -- from the 8 corners of aten's
+// trilinear expression (trilerp: same operands, same order as the register-staged
+// engine; the MFMA sums may associate differently), read by buffer loads (padding channels out of range read
+// 0).  The A fragments (the k = 1 packing of this cout block) sit in LDS.  A wave walks
+// `tpw` consecutive 16-voxel tiles of the flat output run; every k-step's loads of a
+// 32-channel chunk are issued before its MFMAs.  HBM-bound: the input is read once.
+constexpr int kRsMaxCin = 128;
+template <int MT>
+__global__ __launch_bounds__(256) void conv1x1_rs_f32_kernel(const ConvArgs a, int tpw) {
+#pragma clang fp contract(off)
+  constexpr int COP = 16 * MT;
+  constexpr bool SWZ = (COP % 32) == 0;
+  __shared__ __attribute__((aligned(16))) float ws[kRsMaxCin * COP];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int g = lane >> 4, n = lane & 15;
+  const int b = blockIdx.y / a.ncob, cob = blockIdx.y - b * a.ncob;
+  const int co0 = cob * COP;
+  const int nch = (a.cin + 31) / 32;  // 32-channel chunks of the packing
+  {
+    const float4* src = reinterpret_cast<const float4*>(a.wp + (long long)cob * nch * 32 * COP);
+    float4* dst = reinterpret_cast<float4*>(ws);
+    for (int i = threadIdx.x; i < nch * 32 * COP / 4; i += 256) dst[i] = src[i];
+  }
+  float sc[MT][4], sh[MT][4];
+#pragma unroll
+  for (int m = 0; m < MT; ++m)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int co = co0 + 16 * m + 4 * g + r;
+      sc[m][r] = (a.scale && co < a.cout) ? a.scale[co] : 1.f;
+      sh[m][r] = (a.scale && co < a.cout) ? a.shift[co] : 0.f;
+    }
+  __syncthreads();
+  const bool relu = a.flags & LEA_RELU, resid = a.flags & LEA_RESIDUAL;
+  const int HWo = a.H * a.W;
+  const long long vout = (long long)HWo * a.D;
+  const unsigned HWi = (unsigned)(a.Hi * a.Wi), vin = HWi * (unsigned)a.Di;  // host: cin * vin * 4 < 2^32
+  const __amdgpu_buffer_rsrc_t xrs =
+      __builtin_amdgcn_make_buffer_rsrc((void*)(a.x + (long long)b * a.xbs), 0, (int)(unsigned)((long long)a.cin * vin * 4), 0x00020000);
+  const long long t0 = ((long long)blockIdx.x * 4 + wave) * tpw;
+  for (int tt = 0; tt < tpw; ++tt) {
+    const long long v0 = (t0 + tt) * 16;
+    if (v0 >= vout) break;
+    const long long v = min(v0 + n, vout - 1);
+    const int od = (int)(v / HWo), rem = (int)(v - (long long)od * HWo);
+    const int oh = rem / a.W, ow = rem - oh * a.W;
+    const Axis ad = axis_index(a.rd, od, a.Di, a.D, 1), ah = axis_index(a.rh, oh, a.Hi, a.H, 1),
+               aw = axis_index(a.rw, ow, a.Wi, a.W, 1);
+    const unsigned r00 = ((unsigned)ad.i0 * HWi + (unsigned)(ah.i0 * a.Wi)) * 4u;
+    const unsigned r01 = ((unsigned)ad.i0 * HWi + (unsigned)(ah.i1 * a.Wi)) * 4u;
+    const unsigned r10 = ((unsigned)ad.i1 * HWi + (unsigned)(ah.i0 * a.Wi)) * 4u;
+    const unsigned r11 = ((unsigned)ad.i1 * HWi + (unsigned)(ah.i1 * a.Wi)) * 4u;
+    const unsigned w0 = (unsigned)aw.i0 * 4u, w1 = (unsigned)aw.i1 * 4u;
+    f32x4 acc[MT];
+#pragma unroll
+    for (int m = 0; m < MT; ++m) acc[m] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int ch = 0; ch < nch; ++ch) {
+      float c[8][8];
+#pragma unroll
+      for (int s = 0; s < 8; ++s) {
+        const int ci = ch * 32 + 4 * s + g;
+        const unsigned co = ci < a.cin ? (unsigned)ci * vin * 4u : 0xFFFFFF00u;  // padding channels read 0
+        const unsigned rr[4] = {r00, r01, r10, r11};
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          c[s][2 * q] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(xrs, co + rr[q] + w0, 0, 0));
+          c[s][2 * q + 1] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(xrs, co + rr[q] + w1, 0, 0));
+        }
+      }
+#pragma unroll
+      for (int s = 0; s < 8; ++s) {
+        const float* e = c[s];
+        const float bv = ad.l0 * (ah.l0 * (aw.l0 * e[0] + aw.l1 * e[1]) + ah.l1 * (aw.l0 * e[2] + aw.l1 * e[3])) +
+                         ad.l1 * (ah.l0 * (aw.l0 * e[4] + aw.l1 * e[5]) + ah.l1 * (aw.l0 * e[6] + aw.l1 * e[7]));
+        const int ci = ch * 32 + 4 * s + g;
+#pragma unroll
+        for (int m = 0; m < MT; ++m) {
+          const int col = 16 * m + n;
+          const float av = ws[ci * COP + ((SWZ && (ci & 1)) ? (col ^ 16) : col)];
+          acc[m] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bv, acc[m], 0, 0, 0);
+        }
+      }
+    }
+    // D (lane, r) = out[co0 + 16 m + 4 g + r][v0 + n]
+    if (v0 + n < vout) {
+#pragma unroll
+      for (int m = 0; m < MT; ++m)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int co = co0 + 16 * m + 4 * g + r;
+          if (co >= a.cout) continue;
+          float y = acc[m][r] * sc[m][r] + sh[m][r];
+          if (relu) y = fmaxf(y, 0.f);
+          const long long o = (long long)co * vout + v0 + n;
+          if (resid) y += a.res[(long long)b * a.rbs + o];
+          a.y[(long long)b * a.ybs + o] = y;
+        }
+    }
+  }
+}
+
 // ---------------------------------------------------------- 1x1x1 streaming engine
 // A 1x1 ConvBR is a [cout x cin] x [cin x voxels] GEMM that reads every input
 // element exactly once: HBM-bound.  No LDS for X: each lane's B fragment
@@ -421,10 +526,23 @@ inline bool prefer_tw64(int W) {
   return (w64 - W) <= (w32 - W) || W >= 1024;
 }
 
+// lea_conv3d_set_rs_gather: 1 (default) = the resampled 1x1 convs on the gather-GEMM
+// (conv1x1_rs_f32_kernel), 0 = the register-staged engine
+thread_local int g_rs_gather = 1;
+
 inline Plan make_plan(int B, int cout, int D, int H, int W, int k, bool resample) {
   Plan p;
   p.td = 1;
   p.mt = mt_for(cout);
+  // same-box sweep (r02): the gather-GEMM wins on the L1 -> L2 preprocess (64 channels,
+  // 61 K output voxels: 35 -> 29.5 us) and loses on the L0 -> L1 ones (32 channels, 491 K:
+  // 122 -> 136 us: twice the load instructions of the staged engine's row gathers)
+  if (k == 1 && resample && g_rs_gather && (long long)B * D * H * W <= 131072) {
+    p.engine = 5;
+    p.nt = 0;
+    p.tw = 0;
+    return p;
+  }
   if (k == 1 && !resample) {
     p.engine = 1;
     p.nt = 4;
@@ -518,8 +636,34 @@ int run_1x1(const Plan& p, const ConvArgs& a, int B, hipStream_t st) {
   return p.nt == 4 ? launch_1x1<4, 4>(a, B, st) : launch_1x1<4, 2>(a, B, st);
 }
 
+template <int MT>
+int launch_rs_gather(ConvArgs a, int B, hipStream_t st) {
+  const long long vout = (long long)a.D * a.H * a.W;
+  const long long tiles = (vout + 15) / 16;
+  // about 8192 waves over the batch and cout blocks, each walking tpw tiles
+  const long long tpw = std::max(1LL, (tiles * B * a.ncob + 8191) / 8192);
+  const long long gx = (tiles + 4 * tpw - 1) / (4 * tpw);
+  LEA_CHECK_ARG(gx < (1LL << 31) && (long long)B * a.ncob <= 65535, "lea_conv3d: grid too large");
+  conv1x1_rs_f32_kernel<MT><<<dim3((unsigned)gx, B * a.ncob), 256, 0, st>>>(a, (int)tpw);
+  return launch_status("lea_conv3d(rs gather)");
+}
+
 int run_plan(const Plan& p, ConvArgs a, int B, int k, hipStream_t st) {
   a.ncob = (a.cout + p.mt * 16 - 1) / (p.mt * 16);
+  if (p.engine == 5) {
+    const long long xbytes = (long long)a.cin * a.Di * a.Hi * a.Wi * 4;
+    if (a.cin <= kRsMaxCin && a.cin1 == a.cin && xbytes < 0xFFFFFF00LL) {
+      if (p.mt == 1) return launch_rs_gather<1>(a, B, st);
+      if (p.mt == 2) return launch_rs_gather<2>(a, B, st);
+      if (p.mt == 3) return launch_rs_gather<3>(a, B, st);
+      return launch_rs_gather<4>(a, B, st);
+    }
+    // wider inputs than the LDS weight block holds: the register-staged engine
+    if (p.mt == 1) return run_rs<1, 1, 2>(a, prefer_tw64(a.W) ? 64 : 32, B, st);
+    if (p.mt == 2) return run_rs<1, 2, 1>(a, prefer_tw64(a.W) ? 64 : 32, B, st);
+    if (p.mt == 3) return run_rs<1, 3, 1>(a, prefer_tw64(a.W) ? 64 : 32, B, st);
+    return run_rs<1, 4, 1>(a, prefer_tw64(a.W) ? 64 : 32, B, st);
+  }
   if (p.engine == 3) {
     if (a.cout == 1) return launch(conv3d_valu_kernel<1>, a, 8, 64, B, st);
     return launch(conv3d_valu_kernel<2>, a, 8, 64, B, st);
@@ -550,7 +694,9 @@ int run_plan(const Plan& p, ConvArgs a, int B, int k, hipStream_t st) {
 thread_local char g_name[96];
 
 const char* plan_name(const Plan& p, int k) {
-  if (p.engine == 3)
+  if (p.engine == 5)
+    snprintf(g_name, sizeof(g_name), "conv1x1_rs_f32_kernel<%d>", p.mt);
+  else if (p.engine == 3)
     snprintf(g_name, sizeof(g_name), "conv3d_valu_kernel<%d>", p.mt == 1 ? 1 : 2);
   else if (p.engine == 0)
     snprintf(g_name, sizeof(g_name), "conv3d_dma_kernel<%d, %d, %d, %d, %d, false>", p.mt, p.nt,
@@ -624,6 +770,13 @@ extern "C" const char* lea_conv3d_kernel_name(int B, int cout, int D, int H, int
                                               int resample) {
   if (B <= 0 || cout <= 0 || (k != 1 && k != 3) || D <= 0 || H <= 0 || W <= 0) return nullptr;
   return lea::plan_name(lea::make_plan(B, cout, D, H, W, k, resample != 0), k);
+}
+
+extern "C" int lea_conv3d_set_rs_gather(int on) {
+  lea::clear_error();
+  LEA_CHECK_ARG(on == 0 || on == 1, "lea_conv3d_set_rs_gather: on=%d", on);
+  lea::g_rs_gather = on;
+  return 0;
 }
 
 extern "C" int lea_conv3d_set_tile_override(int nt, int tw, int td) {

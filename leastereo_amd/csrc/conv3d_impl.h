@@ -475,7 +475,8 @@ __global__ __launch_bounds__(kConvThreads, 2) void conv3d_dma_kernel(const ConvA
 
 // A launch plan: which instantiation runs a given shape (also reported by name).
 struct Plan {
-  int engine;  // 0 = dma (k3), 1 = 1x1 streaming, 2 = reg resample, 3 = valu (k3, cout <= 2)
+  int engine;  // 0 = dma (k3), 1 = 1x1 streaming, 2 = reg resample, 3 = valu (k3, cout <= 2),
+               // 4 = dma depth-paired, 5 = resampled 1x1 gather-GEMM
   int mt, nt, tw, td;
 };
 

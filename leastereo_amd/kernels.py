@@ -7,6 +7,8 @@ tensor or a missing library raises.
 """
 from __future__ import annotations
 
+import os
+
 import torch
 
 from . import _lib
@@ -793,7 +795,9 @@ def wino_eligible(cout: int, cin: int, k: int) -> bool:
     return k == 3 and cin % 4 == 0
 
 
-WINO_MIN_VOXELS = 200_000  # below this the direct engine's smaller tiles fill the chip better
+# below this the direct engine's smaller tiles fill the chip better (A/B override:
+# LEASTEREO_WINO_MIN_VOXELS)
+WINO_MIN_VOXELS = int(os.environ.get("LEASTEREO_WINO_MIN_VOXELS", "200000"))
 
 
 def wino_preferred(b, cout, cin, d, h, w) -> bool:

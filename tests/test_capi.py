@@ -60,7 +60,12 @@ def test_invalid_arguments_are_rejected_before_launch():
     assert lib.lea_conv3d_set_tile_override(0, 0, 0) == 0
     assert lib.lea_conv3d_kernel_name(1, 32, 64, 192, 320, 3, 0) == b"conv3d_dma_kernel<2, 2, 16, 2, 3, false>"
     assert lib.lea_conv3d_set_tile_override(3, 16, 2) == 1001
-    assert lib.lea_conv3d_kernel_name(1, 8, 64, 192, 320, 1, 1).startswith(b"conv3d_reg_kernel<1, 1")
+    assert lib.lea_conv3d_kernel_name(1, 8, 16, 48, 80, 1, 1) == b"conv1x1_rs_f32_kernel<1>"
+    assert lib.lea_conv3d_set_rs_gather(0) == 0
+    try:
+        assert lib.lea_conv3d_kernel_name(1, 8, 64, 192, 320, 1, 1).startswith(b"conv3d_reg_kernel<1, 1")
+    finally:
+        lib.lea_conv3d_set_rs_gather(1)
     assert lib.lea_conv3d_kernel_name(1, 8, 32, 96, 160, 1, 0) == b"conv1x1_kernel<1, 4>"
     # unsupported dtype is reported as such
     assert lib.lea_disparity_regression(x, x, 1, 1, 1, 1, 1, 7, None) == 1002

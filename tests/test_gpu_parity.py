@@ -15,7 +15,7 @@ import pytest
 import torch
 import torch.nn.functional as F
 
-from leastereo_amd import kernels
+from leastereo_amd import _lib, kernels
 from leastereo_amd.config import LEAStereoArgs, default_arch_args
 from leastereo_amd.model import LEAStereo
 from oracle import torch_ref as ref
@@ -173,6 +173,44 @@ def test_conv_resampled_vs_torch(k, cin, cout, src, dst):
     y = kernels.conv3d_bnrelu_resampled(x.to(DEV), dst, kernels.pack_conv_weight(w.to(DEV)), cout, k,
                                         scale.to(DEV), shift.to(DEV), relu=True)
     np.testing.assert_allclose(y.cpu().double().numpy(), refy.numpy(), rtol=1e-4, atol=1e-4)
+
+
+@pytest.mark.parametrize("cin,cout,src,dst", [
+    (32, 32, (8, 12, 20), (4, 6, 10)),      # L0 -> L1 stacked share conv
+    (64, 64, (5, 9, 17), (3, 5, 9)),        # L1 -> L2 stacked, odd sizes
+    (24, 48, (6, 10, 14), (3, 5, 7)),       # padded 32-channel chunk, 48-row block
+    (128, 16, (3, 5, 9), (5, 9, 17)),       # up-sampling, four chunks
+    (8, 16, (4, 3, 1), (7, 5, 6))])         # width 1 -> 6 (the W pair clamps to one word)
+def test_resampled_1x1_gather_matches_staged_engine(cin, cout, src, dst):
+    """The gather-GEMM (lea_conv3d_set_rs_gather(1), the default for resampled 1x1 convs)
+    stores what the register-staged engine stores (up to the MFMA summation order), into
+    a channel slice, with and without the accumulate epilogue."""
+    lib = _lib.load()
+    g = torch.Generator(device=DEV).manual_seed(cin + cout)
+    x = torch.randn((2, cin) + src, device=DEV, generator=g)
+    w = torch.randn(cout, cin, 1, 1, 1, device=DEV, generator=g) / np.sqrt(cin)
+    scale = torch.rand(cout, device=DEV, generator=g) + 0.5
+    shift = torch.randn(cout, device=DEV, generator=g) * 0.1
+    r = torch.randn((2, cout + 8) + dst, device=DEV, generator=g)
+    pw = kernels.pack_conv_weight(w)
+    outs = []
+    try:
+        for on in (0, 1):
+            assert lib.lea_conv3d_set_rs_gather(on) == 0
+            for acc in (False, True):
+                y = r.clone()
+                kernels.conv3d_bnrelu_resampled(x, dst, pw, cout, 1, scale, shift, True, y[:, 3:3 + cout], acc)
+                outs.append(y)
+    finally:
+        lib.lea_conv3d_set_rs_gather(1)
+    for a, b in ((outs[0], outs[2]), (outs[1], outs[3])):
+        np.testing.assert_allclose(b.cpu().numpy(), a.cpu().numpy(), rtol=1e-5, atol=1e-5)
+    xi = F.interpolate(x.double(), dst, mode="trilinear", align_corners=True)
+    want = torch.relu(F.conv3d(xi, w.double()) * scale.double().view(1, -1, 1, 1, 1)
+                      + shift.double().view(1, -1, 1, 1, 1)) + r[:, 3:3 + cout].double()
+    np.testing.assert_allclose(outs[3][:, 3:3 + cout].cpu().double().numpy(), want.cpu().numpy(),
+                               rtol=1e-4, atol=1e-4)
+    assert torch.equal(outs[3][:, :3], r[:, :3]) and torch.equal(outs[3][:, 3 + cout:], r[:, 3 + cout:])
 
 
 @pytest.mark.parametrize("cout,cin,shape", [(1, 32, (6, 20, 130)), (2, 12, (3, 9, 64)),
