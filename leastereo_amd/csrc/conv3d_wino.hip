@@ -278,9 +278,10 @@ __global__ __launch_bounds__(kConvThreads, 2) void conv3d_wino_kernel(const Conv
         for (int m = 0; m < C::MTE; ++m)
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
+            constexpr int X3 = NX > 4 ? 3 : 0, X4 = NX > 4 ? 4 : 0;  // F = 2 never takes this path
             const float m0 = 0.25f * acc[0][t][m][j][r];
             const float m1 = (-1.f / 6.f) * acc[1][t][m][j][r], m2 = (-1.f / 6.f) * acc[2][t][m][j][r];
-            const float m3 = (1.f / 24.f) * acc[3][t][m][j][r], m4 = (1.f / 24.f) * acc[4][t][m][j][r];
+            const float m3 = (1.f / 24.f) * acc[X3][t][m][j][r], m4 = (1.f / 24.f) * acc[X4][t][m][j][r];
             const float m5 = acc[NX - 1][t][m][j][r];
             const float sp = m1 + m2, sm = m1 - m2, tp = m3 + m4, tm = m3 - m4;
             f32x4 y;
