@@ -466,6 +466,9 @@ __global__ __launch_bounds__(kConvThreads, 2) void conv3d_wino_kernel(const Conv
     // step ahead, so a step's VALU runs under the previous step's MFMAs
     StepOps ops[2];
     Xf xf[2];
+    // scheduler hint: interleave the step's LDS reads / VALU transforms with the MFMAs
+    // (same-box sweep r02: -1 to -4 % per layer; iglp_opt(1) and s_setprio gained less)
+    __builtin_amdgcn_iglp_opt(0);
     load_step(0, ops[0]);
     load_step(1, ops[1]);
     xform(ops[0], xf[0]);

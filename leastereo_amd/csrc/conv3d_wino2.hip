@@ -500,6 +500,9 @@ __global__ __launch_bounds__(NW * 64, OCC) void conv3d_wino2_kernel(const ConvAr
     // 3 kh steps: LDS reads two steps ahead, transforms one step ahead
     Raw raw[2];
     Xf xf[2];
+    // scheduler hint: interleave the step's LDS reads / VALU transforms with the MFMAs
+    // (same-box sweep r02: -1 to -4 % per layer; iglp_opt(1) and s_setprio gained less)
+    __builtin_amdgcn_iglp_opt(0);
     load_step(0, raw[0]);
     load_step(1, raw[1]);
     xform(raw[0], xf[0]);
