@@ -367,19 +367,24 @@ class FeatureExecutor(CellGraphExecutor):
     # them as two convs
     FUSED_STEM = os.environ.get("LEASTEREO_FEATURE_STEM", "1") != "0"
 
-    def _stems(self, x, c8=False):
-        """new_model_2d.py:93-94 (stem1(stem0(x))), fused where the kernel is instantiated."""
+    def _stems(self, x, c8=False, x2=None):
+        """new_model_2d.py:93-94 (stem1(stem0(x))), fused where the kernel is instantiated;
+        with x2 the images of x then x2 as one batch (the fused stem reads both sources,
+        no concatenated copy)."""
         p0, p1 = self.p["stem0"], self.p["stem1"]
         if (self.FUSED_STEM and p0.relu and p1.relu and (p0.cin, p0.cout, p1.cout) == (3, 16, 32)
                 and p1.kind == "s3"):
             return kernels.feature_stem(x, self.m.stem0.conv.weight, p0.scale, p0.shift, p1.packed,
-                                        p1.scale, p1.shift, c8)
+                                        p1.scale, p1.shift, c8, x2)
+        if x2 is not None:
+            x = torch.cat((x, x2), 0)
         stem1 = self.conv("stem1", self.conv("stem0", x.unsqueeze(2)))
         return kernels.to_c8(stem1) if c8 else stem1
 
-    def run(self, x):
-        """newFeature.forward (new_model_2d.py:140-165): [N,3,H,W] -> [N,32,H/3,W/3]."""
-        stem1 = self._stems(x)
+    def run(self, x, x2=None):
+        """newFeature.forward (new_model_2d.py:140-165): [N,3,H,W] -> [N,32,H/3,W/3]
+        (with x2: the stacked features of x then x2)."""
+        stem1 = self._stems(x, x2=x2)
         stem2 = self.conv("stem2", stem1)
         out = (stem1, stem2)
         for i in range(len(self.m.cells)):
@@ -605,15 +610,15 @@ class FeatureExecutorBF16(_C8Layout, FeatureExecutor):
             return CellGraphExecutor.conv(self, name, x, *args, **kw)
         return self._conv_c8(name, x, *args, **kw)
 
-    def run(self, x):
+    def run(self, x, x2=None):
         self._fresh()
         try:
-            return self._run(x)
+            return self._run(x, x2)
         finally:
             self._fresh()
 
-    def _run(self, x):
-        stem1 = self._stems(x, c8=True)
+    def _run(self, x, x2=None):
+        stem1 = self._stems(x, c8=True, x2=x2)
         stem2 = self.conv("stem2", stem1)
         out = (stem1, stem2)
         for i in range(len(self.m.cells)):

@@ -300,27 +300,36 @@ def conv2d_bnrelu(x: torch.Tensor, packed: torch.Tensor, cout: int,
 
 
 def feature_stem(x: torch.Tensor, w0: torch.Tensor, scale0, shift0, w1: torch.Tensor, scale1, shift1,
-                 c8: bool = False) -> torch.Tensor:
+                 c8: bool = False, x2: torch.Tensor | None = None) -> torch.Tensor:
     """new_model_2d.py:93-94 fused (ConvBR 3x3 s1 then ConvBR 3x3 s3, BN + ReLU each):
-    x [B, cin, H, W] f32 -> [B, c1, 1, Ho, Wo] f32, or c8 [B, c1/8, 1, Ho, Wo, 8] bf16."""
-    _require_cuda(x, scale0, shift0, scale1, shift1)
+    x [B, cin, H, W] f32 -> [B, c1, 1, Ho, Wo] f32, or c8 [B, c1/8, 1, Ho, Wo, 8] bf16.
+    With ``x2`` (same shape) the output stacks both, [x; x2] along the batch, without
+    a concatenated copy of the images (one launch per source)."""
+    _require_cuda(x, x2, scale0, shift0, scale1, shift1)
     w0, w1 = w0.detach().contiguous(), w1.detach().contiguous()
     _require_cuda(w0, w1)
     x = x.contiguous()
+    srcs = [x]
+    if x2 is not None:
+        if tuple(x2.shape) != tuple(x.shape):
+            raise ValueError(f"feature_stem: x2 {tuple(x2.shape)} differs from x {tuple(x.shape)}")
+        srcs.append(x2.contiguous())
     b, cin, hi, wi = x.shape
     c0, c1 = w0.shape[0], w1.shape[0]
     if tuple(w0.shape) != (c0, cin, 3, 3) or tuple(w1.shape) != (c1, c0, 3, 3):
         raise ValueError(f"feature_stem: weights {tuple(w0.shape)} / {tuple(w1.shape)} do not chain")
     ho, wo = (hi - 1) // 3 + 1, (wi - 1) // 3 + 1
+    nb = b * len(srcs)
     if c8:
-        out = torch.empty((b, c1 // 8, 1, ho, wo, 8), device=x.device, dtype=torch.bfloat16)
+        out = torch.empty((nb, c1 // 8, 1, ho, wo, 8), device=x.device, dtype=torch.bfloat16)
     else:
-        out = torch.empty((b, c1, 1, ho, wo), device=x.device, dtype=torch.float32)
+        out = torch.empty((nb, c1, 1, ho, wo), device=x.device, dtype=torch.float32)
     ptr = lambda t: t.data_ptr() if t is not None else None  # noqa: E731
-    check(_lib.load().lea_feature_stem_bnrelu(
-        x.data_ptr(), x.stride(0), w0.data_ptr(), ptr(scale0), ptr(shift0), w1.data_ptr(), ptr(scale1),
-        ptr(shift1), out.data_ptr(), out.stride(0), b, cin, c0, c1, hi, wi,
-        _lib.LEA_BF16 if c8 else LEA_F32, _stream()), "lea_feature_stem_bnrelu")
+    for i, src in enumerate(srcs):
+        check(_lib.load().lea_feature_stem_bnrelu(
+            src.data_ptr(), src.stride(0), w0.data_ptr(), ptr(scale0), ptr(shift0), w1.data_ptr(),
+            ptr(scale1), ptr(shift1), out[i * b:].data_ptr(), out.stride(0), b, cin, c0, c1, hi, wi,
+            _lib.LEA_BF16 if c8 else LEA_F32, _stream()), "lea_feature_stem_bnrelu")
     return out
 
 

@@ -139,10 +139,11 @@ class NewFeature(_ExecutorCache, nn.Module):
         _head_modules(self, initial_fm, 2, False)
         self._executor = None
 
-    def forward(self, x):
+    def forward(self, x, y=None):
+        """newFeature.forward(x); with y, the features of x then y as one batch."""
         if not x.is_cuda:
             raise RuntimeError("leastereo_amd feature net runs on a ROCm device only")
-        return self.executor().run(x)
+        return self.executor().run(x, y)
 
 
 class NewMatching(_ExecutorCache, nn.Module):
@@ -224,8 +225,9 @@ class LEAStereo(nn.Module):
             raise RuntimeError("leastereo_amd.LEAStereo runs the matching net on a ROCm device only")
         self.check_shape(x.shape[2], x.shape[3])
         # LEAStereo.py:31-32 runs the feature net twice; every layer is per-sample
-        # (eval-mode BN), so one call on the stacked pair halves the launch count.
-        f = self.feature(torch.cat((x, y), 0))
+        # (eval-mode BN), so one call on the stacked pair halves the launch count (the
+        # fused stem reads x and y directly into the stacked stem1 maps)
+        f = self.feature(x, y)
         fx, fy = f[: x.shape[0]], f[x.shape[0]:]
         # cost volume (:34-48) + matching (:50): stem0 reads the volume in place
         cost = self.matching.executor().run_features(fx, fy, self.maxdisp)

@@ -530,3 +530,10 @@ def test_fused_feature_stems_vs_torch(c8):
         np.testing.assert_allclose(got[:, :, 0].cpu().double().numpy(), want.numpy(), rtol=1e-2, atol=1e-2)
     else:
         np.testing.assert_allclose(got[:, :, 0].cpu().double().numpy(), want.numpy(), rtol=1e-4, atol=1e-4)
+    # two sources: [x; x2] stacked without a concatenated copy, bit for bit
+    x2 = torch.randn(2, 3, 50, 131, generator=g)
+    both = kernels.feature_stem(x.to(DEV), w0.to(DEV), s0.to(DEV), t0.to(DEV), w1.to(DEV), s1.to(DEV),
+                                t1.to(DEV), c8, x2.to(DEV))
+    cat = kernels.feature_stem(torch.cat((x, x2), 0).to(DEV), w0.to(DEV), s0.to(DEV), t0.to(DEV),
+                               w1.to(DEV), s1.to(DEV), t1.to(DEV), c8)
+    assert torch.equal(both, cat)
