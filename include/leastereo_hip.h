@@ -309,6 +309,10 @@ int lea_conv3d_wino2_set_walk(int spw);
  * operand from the 8 corners, no staging), 0 = always the register-staged engine.
  * Per calling thread. */
 int lea_conv3d_set_rs_gather(int on);
+/* Tuning hook: 1 (default) = lea_conv3d_bnrelu_bf16 with k = 1 and cin <= 128 on the
+ * streamed 1x1 kernel (each lane loads its own 16-byte B word, weights in registers, no
+ * staging; bit-identical to the tile kernel), 0 = the tile kernel.  Per calling thread. */
+int lea_conv3d_bf16_set_stream1x1(int on);
 /* Tuning hook: 1 (default) = the Winograd engines' buffer-addressed epilogue where the
  * shape allows it (W % 4 == 0, 16-B aligned output / residual; residual loads issued
  * together, the next chunk's DMA waited for without the stores), 0 = the per-group

@@ -88,6 +88,7 @@ SIGNATURES = {
     "lea_conv3d_wino2_set_walk": (_i, [_i]),
     "lea_conv3d_wino_set_epi_buf": (_i, [_i]),
     "lea_conv3d_set_rs_gather": (_i, [_i]),
+    "lea_conv3d_bf16_set_stream1x1": (_i, [_i]),
     "lea_conv3d_wino_set_small_cout": (_i, [_i]),
     "lea_conv3d_wino_set_block48": (_i, [_i]),
     # stem0 over the cost volume, factored through 2D maps
@@ -136,6 +137,7 @@ def load():
 TUNING_ENV = {"LEASTEREO_WINO2_WALK": "lea_conv3d_wino2_set_walk",
               "LEASTEREO_EPI_BUF": "lea_conv3d_wino_set_epi_buf",
               "LEASTEREO_RS_GATHER": "lea_conv3d_set_rs_gather",
+              "LEASTEREO_BF16_1X1": "lea_conv3d_bf16_set_stream1x1",
               "LEASTEREO_RESAMPLE_K": "lea_resample_bf16_set_batch"}
 
 

@@ -484,6 +484,96 @@ __global__ __launch_bounds__(256) void conv1x1_rs_c8_kernel(
   }
 }
 
+// ---- 1x1 ConvBR on c8 tensors, streamed (conv1x1_rs_c8_kernel without the resample): a
+// 1x1 conv reads every input word once, so nothing is staged -- lane (g, n) loads its own
+// B fragment (channel block 4 c + g of voxel v0 + n, one 16-byte word) straight into
+// registers, the A fragments (the k = 1 packing) sit in registers, and a wave issues the
+// words of TU tiles before their MFMAs so TU * nch loads per lane are in flight.  Same
+// operands, order and epilogue as the tile kernel's k = 1 path: bit-identical.
+template <int MT>
+__global__ __launch_bounds__(256) void conv1x1_c8_kernel(const Args a, int tpw) {
+  constexpr int MAXCH = 4, TU = 4;  // cin <= 128 (host); tiles per load group
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int g = lane >> 4, n = lane & 15;
+  const int b = blockIdx.y / a.ncob, cob = blockIdx.y - b * a.ncob;
+  const int nch = (a.cin / 8 + 3) / 4;
+  const long long vox = (long long)a.D * a.H * a.W;
+  const bf16x8* wp = reinterpret_cast<const bf16x8*>(a.wp);
+  bf16x8 av[MAXCH][MT];
+#pragma unroll
+  for (int c = 0; c < MAXCH; ++c)
+#pragma unroll
+    for (int m = 0; m < MT; ++m)
+      av[c][m] = c < nch ? wp[((((long long)cob * nch + c) * MT + m) * 4 + g) * 16 + n] : bf16x8{};
+  const int co0 = cob * 16 * MT;
+  float sc[MT][4], sh[MT][4];
+#pragma unroll
+  for (int m = 0; m < MT; ++m)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int co = co0 + 16 * m + 4 * g + r;
+      sc[m][r] = (a.scale && co < a.cout) ? a.scale[co] : 1.f;
+      sh[m][r] = (a.shift && co < a.cout) ? a.shift[co] : 0.f;
+    }
+  const bool relu = a.flags & LEA_RELU, resid = a.flags & LEA_RESIDUAL;
+  // this lane's channel block of chunk c: source pointer (x or the cat's second tensor)
+  const bf16x8* src[MAXCH];
+  bool live[MAXCH];
+#pragma unroll
+  for (int c = 0; c < MAXCH; ++c) {
+    const int blk = 4 * c + g;
+    live[c] = c < nch && blk < a.cin / 8;
+    src[c] = blk < a.cb1 ? reinterpret_cast<const bf16x8*>(a.x + (long long)b * a.xbs) + (long long)blk * vox
+                         : reinterpret_cast<const bf16x8*>(a.x2 + (long long)b * a.x2bs) + (long long)(blk - a.cb1) * vox;
+  }
+  const long long t0 = ((long long)blockIdx.x * 4 + wave) * tpw;
+  for (int tt = 0; tt < tpw; tt += TU) {
+    bf16x8 bw[TU][MAXCH];
+#pragma unroll
+    for (int u = 0; u < TU; ++u) {
+      const long long v = min((t0 + tt + u) * 16 + n, vox - 1);
+#pragma unroll
+      for (int c = 0; c < MAXCH; ++c) bw[u][c] = (live[c] && tt + u < tpw) ? src[c][v] : bf16x8{};
+    }
+#pragma unroll
+    for (int u = 0; u < TU; ++u) {
+      const long long v0 = (t0 + tt + u) * 16;
+      if (tt + u >= tpw || v0 >= vox) break;
+      f32x4 acc[MT];
+#pragma unroll
+      for (int m = 0; m < MT; ++m) acc[m] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int c = 0; c < MAXCH; ++c) {
+        if (c >= nch) break;
+#pragma unroll
+        for (int m = 0; m < MT; ++m) acc[m] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[c][m], bw[u][c], acc[m], 0, 0, 0);
+      }
+      if (v0 + n >= vox) continue;
+#pragma unroll
+      for (int m = 0; m < MT; ++m) {
+        const int co = co0 + 16 * m + 4 * g;  // first of the lane's 4 couts
+        if (co >= a.cout) continue;
+        const long long o = ((long long)(co / 8) * vox + v0 + n) * 8 + co % 8;
+        float v[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          v[r] = acc[m][r] * sc[m][r] + sh[m][r];
+          if (relu) v[r] = fmaxf(v[r], 0.f);
+        }
+        if (resid) {
+          const bf16x4 rv = *reinterpret_cast<const bf16x4*>(a.res + (long long)b * a.rbs + o);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) v[r] += (float)rv[r];
+        }
+        bf16x4 out;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) out[r] = (__bf16)v[r];
+        *reinterpret_cast<bf16x4*>(a.y + (long long)b * a.ybs + o) = out;
+      }
+    }
+  }
+}
+
 // ---- D-streaming form for the single-chunk 3x3x3 layers (cin <= 16: the whole K is
 // one chunk).  The tile kernel above stages a (TH+2) x 18 x (TD+2) halo per TH x 16 x TD
 // tile and waits for it: r01 counters put these layers' waves 60-78 % parked on that
@@ -709,10 +799,12 @@ __global__ __launch_bounds__(kThreads, 2) void conv_bf16_stream_kernel(const Arg
 struct Plan {
   int ks, mt, wc, th, td, nb;
   int nsplit;  // > 0: the D-streaming kernel with nsplit column segments along D
+  bool s1x1;   // the streamed 1x1 (conv1x1_c8_kernel)
 };
 
 thread_local int g_override[3] = {0, 0, 0};  // th, td, mt (lea_conv3d_bf16_set_tile_override)
 thread_local int g_variant = 0;              // lea_conv3d_bf16_set_variant: 0 planner, 1 tile kernel only
+thread_local int g_stream1x1 = 1;            // lea_conv3d_bf16_set_stream1x1
 
 inline Plan plan(int B, int cout, int D, int H, int W, int ks, int cin) {
   // r01 sweep (tools/conv_sweep.py --bf16, profiles/r01_conv_sweep_bf16.txt): one
@@ -742,6 +834,7 @@ inline Plan plan(int B, int cout, int D, int H, int W, int ks, int cin) {
     p.wc = cobv / 16 / p.mt;
   }
   p.nsplit = 0;
+  p.s1x1 = ks == 1 && cin <= 128 && g_stream1x1 && g_variant == 0 && g_override[0] == 0;
   // (r02 tools/bf16_stream_bench.py: two-chunk layers with 64-cout blocks -- the L2
   // 32->96 sibling groups -- hold 221 VGPRs of weights and accumulators and run slower
   // streamed; they stay on the tile kernel)
@@ -794,6 +887,19 @@ inline Plan plan(int B, int cout, int D, int H, int W, int ks, int cin) {
   }
 
 int run(const Plan& p, Args a, int B, hipStream_t st, bool cv) {
+  if (p.s1x1 && !cv) {
+    const long long vox = (long long)a.D * a.H * a.W;
+    const long long tiles = (vox + 15) / 16;
+    // about 8192 waves over the batch and cout blocks, each walking tpw tiles
+    const long long tpw = std::max(1LL, (tiles * B * a.ncob + 8191) / 8192);
+    const long long gx = (tiles + 4 * tpw - 1) / (4 * tpw);
+    LEA_CHECK_ARG(gx < (1LL << 31) && (long long)B * a.ncob <= 65535, "lea_conv3d(bf16 1x1): grid too large");
+    const dim3 grid((unsigned)gx, B * a.ncob);
+    if (p.wc == 1) conv1x1_c8_kernel<1><<<grid, 256, 0, st>>>(a, (int)tpw);
+    else if (p.wc == 2) conv1x1_c8_kernel<2><<<grid, 256, 0, st>>>(a, (int)tpw);
+    else conv1x1_c8_kernel<4><<<grid, 256, 0, st>>>(a, (int)tpw);
+    return launch_status("lea_conv3d(bf16 1x1)");
+  }
   if (p.nsplit > 0 && !cv && a.cb1 * 8 == a.cin) {  // (one source: the ring walks one tensor)
     LEA_CHECK_ARG((long long)std::max(a.cin, a.cout + 7) / 8 * a.D * a.H * a.W * 16 < 0xFFFFFFF0LL,
                   "lea_conv3d(bf16 stream): volume too large");
@@ -861,6 +967,13 @@ extern "C" int lea_conv3d_bf16_set_tile_override(int th, int td, int mt) {
   return 0;
 }
 
+extern "C" int lea_conv3d_bf16_set_stream1x1(int on) {
+  clear_error();
+  LEA_CHECK_ARG(on == 0 || on == 1, "lea_conv3d_bf16_set_stream1x1: on=%d", on);
+  bf::g_stream1x1 = on;
+  return 0;
+}
+
 extern "C" int lea_conv3d_bf16_set_variant(int variant) {
   clear_error();
   LEA_CHECK_ARG(variant == 0 || variant == 1, "lea_conv3d_bf16_set_variant: bad variant %d", variant);
@@ -894,7 +1007,9 @@ extern "C" const char* lea_conv3d_kernel_name_bf16(int B, int cout, int cin, int
                                                    int k, int costvolume) {
   if (B <= 0 || cout <= 0 || cin <= 0 || (k != 1 && k != 3) || D <= 0 || H <= 0 || W <= 0) return nullptr;
   const bf::Plan p = bf::plan(B, cout, D, H, W, k, cin);
-  if (p.nsplit > 0 && !costvolume)
+  if (p.s1x1 && !costvolume)
+    snprintf(bf::g_bf_name, sizeof(bf::g_bf_name), "conv1x1_c8_kernel<%d>", p.wc);
+  else if (p.nsplit > 0 && !costvolume)
     snprintf(bf::g_bf_name, sizeof(bf::g_bf_name), "conv_bf16_stream_kernel<1, %d, %d, %d, %d>", p.wc, p.th,
              p.nb, (cin / 8 + p.nb - 1) / p.nb);
   else

@@ -269,3 +269,47 @@ def test_conv1x1_resampled_is_resample_then_conv(b, cin, cout, src, dst):
     kernels.conv1x1_resampled_bf16(x, dst, packed, cout, scale, shift, relu=True, out=big[:, 1:1 + cout // 8])
     assert torch.equal(big[:, 1:1 + cout // 8], want)
     assert float(big[:, 0].float().abs().sum()) == 0 and float(big[:, -1].float().abs().sum()) == 0
+
+
+@pytest.mark.parametrize("b,cin,cout,shape,mode,cin2", [
+    (1, 32, 16, (8, 12, 20), None, 0), (2, 64, 32, (5, 9, 17), "acc", 0), (1, 128, 64, (4, 6, 10), None, 0),
+    (3, 24, 8, (3, 5, 7), "res", 0), (1, 64, 96, (2, 8, 9), None, 0), (2, 8, 24, (6, 7, 5), "acc", 0),
+    (1, 64, 32, (4, 12, 16), None, 32), (2, 48, 16, (3, 4, 33), "res", 16)])
+def test_stream_1x1_is_the_tile_kernel(b, cin, cout, shape, mode, cin2):
+    """The streamed 1x1 (conv1x1_c8_kernel: B words loaded per lane, no staging) stores
+    what the k = 1 tile kernel stores, bit for bit: padded chunks (cin % 32 != 0), several
+    cout blocks, two sources (a block-slice cat), residual and accumulate epilogues, an
+    output block slice; and matches float64 torch within the bf16 tolerance."""
+    from leastereo_amd import _lib
+    lib = _lib.load()
+    g = torch.Generator().manual_seed(cin * 3 + cout + b)
+    x = _bf(torch.randn((b, cin) + shape, generator=g))
+    wt = _bf(torch.randn(cout, cin, 1, 1, 1, generator=g) / np.sqrt(cin))
+    scale = torch.rand(cout, generator=g) + 0.5
+    shift = torch.randn(cout, generator=g) * 0.1
+    r = _bf(torch.randn((b, cout) + shape, generator=g))
+    xc, rc = kernels.to_c8(x.to(DEV)), kernels.to_c8(r.to(DEV))
+    x1, x2 = (xc[:, : (cin - cin2) // 8], xc[:, (cin - cin2) // 8:]) if cin2 else (xc, None)
+    packed = kernels.pack_conv_weight_bf16(wt.to(DEV))
+    outs = []
+    for on in (1, 0):
+        assert lib.lea_conv3d_bf16_set_stream1x1(on) == 0
+        try:
+            name = kernels.conv_kernel_name_bf16(b, cout, cin, *shape, 1)
+            assert name.startswith("conv1x1_c8_kernel<" if on else "conv_bf16_kernel<1,"), name
+            big = torch.zeros((b, cout // 8 + 2) + shape + (8,), device=DEV, dtype=torch.bfloat16)
+            big[:, 1:1 + cout // 8] = rc
+            out = big[:, 1:1 + cout // 8]
+            kernels.conv3d_bnrelu_bf16(x1, packed, cout, 1, scale.to(DEV), shift.to(DEV), relu=True, out=out,
+                                       accumulate=mode == "acc", x2=x2, residual=rc if mode == "res" else None)
+            torch.cuda.synchronize()
+            assert float(big[:, 0].float().abs().sum()) == 0 and float(big[:, -1].float().abs().sum()) == 0
+            outs.append(out.clone())
+        finally:
+            lib.lea_conv3d_bf16_set_stream1x1(1)
+    assert torch.equal(outs[0], outs[1])
+    want = F.conv3d(x.double(), wt.double())
+    want = torch.relu(want * scale.double().view(1, -1, 1, 1, 1) + shift.double().view(1, -1, 1, 1, 1))
+    if mode:
+        want = want + r.double()
+    _close(kernels.from_c8(outs[0]), want)
