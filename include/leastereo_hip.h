@@ -138,7 +138,9 @@ int lea_conv2d_s3_bnrelu(const void* x, int64_t x_bstride, const float* w, const
  * writing stem0's full-resolution output (stride 3 tiles it: each stem0 pixel feeds one
  * stem1 pixel).  w0: [c0, cin, 3, 3], w1: [c1, c0, 3, 3] raw f32.  x: [B, cin, Hi, Wi] f32;
  * y: [B, c1, Ho, Wo] f32 (dtype LEA_F32) or c8 [B, c1/8, 1, Ho, Wo, 8] bf16 (LEA_BF16),
- * Ho = (Hi - 1) / 3 + 1.  Instantiated for 3 -> 16 -> 32 (the searched feature net). */
+ * Ho = (Hi - 1) / 3 + 1.  Instantiated for 3 -> 16 -> 32 (the searched feature net).
+ * Image b is read at x + b * x_bstride (elements, any sign): two separately allocated
+ * images (the left / right pair) run as one B = 2 launch with x_bstride = right - left. */
 int lea_feature_stem_bnrelu(const float* x, int64_t x_bstride, const float* w0, const float* scale0,
                             const float* shift0, const float* w1, const float* scale1,
                             const float* shift1, void* y, int64_t y_bstride, int B, int cin, int c0,

@@ -304,7 +304,8 @@ def feature_stem(x: torch.Tensor, w0: torch.Tensor, scale0, shift0, w1: torch.Te
     """new_model_2d.py:93-94 fused (ConvBR 3x3 s1 then ConvBR 3x3 s3, BN + ReLU each):
     x [B, cin, H, W] f32 -> [B, c1, 1, Ho, Wo] f32, or c8 [B, c1/8, 1, Ho, Wo, 8] bf16.
     With ``x2`` (same shape) the output stacks both, [x; x2] along the batch, without
-    a concatenated copy of the images (one launch per source)."""
+    a concatenated copy of the images: one launch per source, or for one image each a
+    single launch whose batch stride is the distance between the two images."""
     _require_cuda(x, x2, scale0, shift0, scale1, shift1)
     w0, w1 = w0.detach().contiguous(), w1.detach().contiguous()
     _require_cuda(w0, w1)
@@ -325,9 +326,14 @@ def feature_stem(x: torch.Tensor, w0: torch.Tensor, scale0, shift0, w1: torch.Te
     else:
         out = torch.empty((nb, c1, 1, ho, wo), device=x.device, dtype=torch.float32)
     ptr = lambda t: t.data_ptr() if t is not None else None  # noqa: E731
+    if len(srcs) == 2 and b == 1:
+        # one image per source: one launch whose batch stride is the distance between them
+        srcs, b, xbs = [x], 2, (x2.data_ptr() - x.data_ptr()) // x.element_size()
+    else:
+        xbs = x.stride(0)
     for i, src in enumerate(srcs):
         check(_lib.load().lea_feature_stem_bnrelu(
-            src.data_ptr(), src.stride(0), w0.data_ptr(), ptr(scale0), ptr(shift0), w1.data_ptr(),
+            src.data_ptr(), xbs, w0.data_ptr(), ptr(scale0), ptr(shift0), w1.data_ptr(),
             ptr(scale1), ptr(shift1), out[i * b:].data_ptr(), out.stride(0), b, cin, c0, c1, hi, wi,
             _lib.LEA_BF16 if c8 else LEA_F32, _stream()), "lea_feature_stem_bnrelu")
     return out

@@ -13,9 +13,15 @@ path: forward on a non-ROCm device raises.
 """
 from __future__ import annotations
 
+import os
+
 import numpy as np
 import torch
 import torch.nn as nn
+
+# the fused feature stem reads left and right directly (two launches, no concatenated
+# copy); LEASTEREO_STEM_PAIR=0 stacks the images first (one launch + a torch copy)
+STEM_PAIR = os.environ.get("LEASTEREO_STEM_PAIR", "1") != "0"
 
 from . import kernels
 from .arch import (PRIMITIVES_2D, PRIMITIVES_3D, cell_specs, check_matching_shape,
@@ -227,7 +233,7 @@ class LEAStereo(nn.Module):
         # LEAStereo.py:31-32 runs the feature net twice; every layer is per-sample
         # (eval-mode BN), so one call on the stacked pair halves the launch count (the
         # fused stem reads x and y directly into the stacked stem1 maps)
-        f = self.feature(x, y)
+        f = self.feature(x, y) if STEM_PAIR else self.feature(torch.cat((x, y), 0))
         fx, fy = f[: x.shape[0]], f[x.shape[0]:]
         # cost volume (:34-48) + matching (:50): stem0 reads the volume in place
         cost = self.matching.executor().run_features(fx, fy, self.maxdisp)

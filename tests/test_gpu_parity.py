@@ -537,3 +537,7 @@ def test_fused_feature_stems_vs_torch(c8):
     cat = kernels.feature_stem(torch.cat((x, x2), 0).to(DEV), w0.to(DEV), s0.to(DEV), t0.to(DEV),
                                w1.to(DEV), s1.to(DEV), t1.to(DEV), c8)
     assert torch.equal(both, cat)
+    # one image per source: a single launch striding from x to x2
+    one = kernels.feature_stem(x[:1].to(DEV), w0.to(DEV), s0.to(DEV), t0.to(DEV), w1.to(DEV), s1.to(DEV),
+                               t1.to(DEV), c8, x2[1:].to(DEV))
+    assert torch.equal(one, cat[[0, 3]])
