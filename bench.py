@@ -2,23 +2,37 @@
 """Benchmark: LEAStereo inference (feature net -> cost volume -> matching net ->
 disparity regression) on synthetic stereo pairs, one process per GPU.
 
-Contract (driver): ``python bench.py --gpus N --steps K --warmup W``; for N>1 it
-is launched by torch.distributed.run (one rank per GPU, RCCL).  A step is one
-forward of ``--batch`` pairs per rank with inputs already resident in HBM.
-Rank 0 prints one JSON line.
+Contract (driver): ``python bench.py --gpus N --steps K --warmup W``.  For N > 1 the
+driver launches it under torch.distributed.run (one rank per GPU, RCCL); started
+directly with ``--gpus N > 1`` and no WORLD_SIZE in the environment, bench.py starts
+that launcher itself as a child process (before anything touches a GPU) and exits
+with its status.  A rank whose world size differs from ``--gpus`` refuses to run.
+A step is one forward of ``--batch`` pairs per rank with inputs already resident in
+HBM.  Rank 0 prints one JSON line.
 
-Workload (BASELINE.json configs[1]): SceneFlow 576x960, maxdisp 192, fp32,
-batch 1 per GPU; random-init weights of the reference architecture
-(leastereo_amd.weights recipe; no checkpoints exist upstream) and synthetic
-N(0,1) images (the post-standardisation statistics of predict.py:162-184).
+Workload (BASELINE.json configs[1]): SceneFlow 576x960, maxdisp 192, fp32, batch 1
+per GPU; random-init weights of the reference architecture (leastereo_amd.weights
+recipe; no checkpoints exist upstream) and synthetic N(0,1) images (the
+post-standardisation statistics of predict.py:162-184).  ``--config c3|c4|c5`` picks
+the other BASELINE configs (c4 = 8 pairs per GPU of the 64-pair global batch).
 
 Extras in the JSON line:
-  roofline      the dominant conv kernel instantiation timed with HIP events
-                inside the timed region (algorithmic FLOPs / event time)
-  cpu_baseline  the CPU oracle (oracle/torch_ref.py, a restatement of the
-                reference's exact aten op sequence) on the host cores, rank 0, N=1
-  epe_px        per rank: HIP disparity vs the reference's own fp32 output on the
-                golden e2e case, all-gathered over ranks (one RCCL all-gather)
+  roofline       the dominant conv kernel instantiation timed with HIP events inside
+                 the timed region; ``achieved`` counts the MFMA products the kernel
+                 issues (Winograd products, padded cout blocks), so ``frac`` is the
+                 matrix-core utilisation; the direct-convolution equivalent is a
+                 separate key
+  path_roofline  sum over every launch of one forward of max(issued MFMA FLOP / peak,
+                 VALU FLOP / peak, algorithmic bytes / 8 TB/s), for the algorithms
+                 actually run, over the measured step time; plus the HBM-only fraction
+  pair_epe_px    per pair of every rank's shard: |HIP - an independent HIP path|
+                 (f32: the direct-conv engine over the in-place cost volume; bf16: the
+                 f32 path), all-gathered over ranks (the data path's one collective)
+  epe_px         per rank: HIP vs the reference's own fp32 output (golden e2e case)
+  cpu_baseline   the CPU oracle (oracle/torch_ref.py, the reference's aten op sequence
+                 restated) on the host's physical cores, rank 0, N = 1: C2 (this
+                 workload's first pair) and C1 (the SceneFlow sample pair), 1 warm-up +
+                 3 timed each, HIP-vs-CPU and HIP-vs-fp64 EPE
 """
 from __future__ import annotations
 
@@ -26,6 +40,8 @@ import argparse
 import json
 import os
 import platform
+import socket
+import subprocess
 import sys
 import time
 
@@ -40,9 +56,9 @@ from leastereo_amd.model import LEAStereo  # noqa: E402
 from leastereo_amd.weights import synthetic_state_dict  # noqa: E402
 
 METRIC = "stereo pairs/s at 576×960 D=192, 1/2/4/8 GPU; EPE vs reference"
-FP32_MFMA_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md, fp32 (vector = MFMA) dense
+FP32_PEAK_TFLOPS = 157.3        # MI355X_MICROARCH.md: fp32 matrix = fp32 vector, dense
+BF16_MFMA_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md, bf16 dense (no sparsity)
 HBM_PEAK_GBS = 8000.0           # MI355X_MICROARCH.md, spec
-
 
 # BASELINE.json configs: c2 is the headline workload (defaults);
 # c3/c4 are the bf16 ones (c4 = 8 pairs per GPU of the 64-pair global batch)
@@ -52,13 +68,16 @@ CONFIGS = {
     "c4": dict(height=576, width=960, maxdisp=192, batch=8, precision="bf16"),
     "c5": dict(height=1008, width=1512, maxdisp=264, batch=1, precision="f32"),
 }
-BF16_MFMA_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md, bf16 dense (no sparsity)
-# Whole-path roofline time per step, SURVEY.md §8d (sum over the matching net's
-# layers of max(FLOP/peak, bytes/8 TB/s), reference op accounting), per config
-T_ROOF_MS = {("c2", 1): 11.36, ("c3", 8): 10.91, ("c4", 8): 12.59, ("c5", 1): 43.1}
+# SURVEY.md §8d's roofline of the reference algorithm (direct convolutions, a
+# materialised cost volume): kept for comparison beside the issued-work roofline
+T_ROOF_REFERENCE_MS = {("c2", 1): 11.36, ("c3", 8): 10.91, ("c4", 8): 12.59, ("c5", 1): 43.1}
+WORKLOADS = {"c2": "SceneFlow 576x960 D=192 fp32, batch 1 per GPU (BASELINE configs[1])",
+             "c3": "KITTI2015 384x1248 D=192 bf16, batch 8 (BASELINE configs[2])",
+             "c4": "SceneFlow 576x960 D=192 bf16, 8 pairs per GPU (BASELINE configs[3])",
+             "c5": "Middlebury 1008x1512 D=264 fp32, batch 1 (BASELINE configs[4], D256 is illegal)"}
 
 
-def parse():
+def parse(argv=None):
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=20)
@@ -68,16 +87,21 @@ def parse():
     p.add_argument("--width", type=int, default=960)
     p.add_argument("--maxdisp", type=int, default=192)
     p.add_argument("--cpu-baseline", type=int, default=1, help="time the CPU oracle (rank 0, N=1)")
-    p.add_argument("--cpu-steps", type=int, default=2)
+    p.add_argument("--cpu-timed", type=int, default=3, help="timed CPU forwards per config (+1 warm-up)")
+    p.add_argument("--cpu-configs", default="c2,c1", help="CPU baseline configs (c2 = this workload)")
+    p.add_argument("--cpu-fp64", type=int, default=1, help="HIP vs a float64 CPU forward at C2")
     p.add_argument("--epe", type=int, default=1, help="check EPE vs the reference golden disparity")
-    p.add_argument("--breakdown", type=int, default=0, help="print per-kernel conv times to stderr")
+    p.add_argument("--pair-check", type=int, default=1,
+                   help="per-pair EPE of every rank's shard vs an independent HIP path, all-gathered")
+    p.add_argument("--breakdown", type=int, default=0, help="print per-kernel times to stderr")
     p.add_argument("--graph", type=int, default=0,
                    help="time a HIP-graph replay of the forward (LEAStereo.graphed) instead of eager launches")
     p.add_argument("--precision", choices=("f32", "bf16"), default="f32",
                    help="matching-net arithmetic (bf16 = BASELINE configs 3/4)")
     p.add_argument("--config", choices=sorted(CONFIGS), default=None,
                    help="preset: c2 (default workload) / c3 / c4 (per GPU) / c5 of BASELINE.json")
-    a = p.parse_args()
+    p.add_argument("--stub", type=int, default=0, help=argparse.SUPPRESS)  # tests: no GPU, gloo
+    a = p.parse_args(argv)
     if a.config:
         for k, v in CONFIGS[a.config].items():
             setattr(a, k, v)
@@ -88,6 +112,26 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
+# ------------------------------------------------------------------------ launcher
+def _free_port() -> int:
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch(n: int, argv) -> int:
+    """Start ``n`` ranks of this script under torch.distributed.run (one process per
+    GPU, rendezvous on 127.0.0.1) as a child process and return its exit status.
+    Runs before anything in this process touches a GPU (no exec from here)."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+           os.path.abspath(__file__)] + list(argv)
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.call(cmd, env=env)
+
+
+# ------------------------------------------------------------------------ models
 def build_model(maxdisp, device, precision="f32"):
     args = default_arch_args(LEAStereoArgs(maxdisp=maxdisp))
     model = LEAStereo(args, device, precision=precision)
@@ -96,39 +140,8 @@ def build_model(maxdisp, device, precision="f32"):
     return model.to(device).eval()
 
 
-def cpu_baseline(args, model, left0, right0, disp0):
-    """CPU leg: the oracle (oracle/torch_ref.py, the reference's aten op sequence
-    restated) on the host cores, on a bounded sample of the same workload: the
-    benchmark's own first pair, ``--cpu-steps`` times.  Its output doubles as
-    the parity check of the HIP disparity for that pair (EPE reported)."""
-    from oracle import torch_ref as ref
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
-    torch.set_num_threads(threads)
-    sd = {k: v.detach().cpu() for k, v in model.state_dict().items()}
-    a = arch_arrays()
-    left, right = left0.cpu(), right0.cpu()
-    with torch.no_grad():
-        ref.leastereo_forward(sd, left[..., :96, :192].contiguous(), right[..., :96, :192].contiguous(),
-                              48, a)  # warm the CPU kernels on a small case
-        t0 = time.perf_counter()
-        for _ in range(args.cpu_steps):
-            want = ref.leastereo_forward(sd, left, right, args.maxdisp, a)
-        dt = time.perf_counter() - t0
-    cpu_model = platform.processor() or platform.machine()
-    try:
-        with open("/proc/cpuinfo") as f:
-            for line in f:
-                if line.startswith("model name"):
-                    cpu_model = line.split(":", 1)[1].strip()
-                    break
-    except OSError:
-        pass
-    return {"value": args.cpu_steps / dt, "unit": "pairs/s", "cores": threads, "kind": "port",
-            "sample": f"{args.cpu_steps} forward(s) of the benchmark's first pair at "
-                      f"{args.height}x{args.width} D={args.maxdisp} fp32 (oracle/torch_ref.py on "
-                      f"torch CPU, {cpu_model})",
-            "s_per_pair": dt / args.cpu_steps,
-            "epe_px_hip_vs_this": float((disp0.cpu().double() - want.double()).abs().mean())}
+def config_name(args):
+    return next((k for k, v in CONFIGS.items() if all(getattr(args, f) == x for f, x in v.items())), None)
 
 
 def arch_arrays():
@@ -157,6 +170,115 @@ def golden_epe(device, precision="f32"):
     return float(np.abs(got - want).mean())
 
 
+# ------------------------------------------------------------------------ CPU baseline
+def host_cores():
+    """Physical cores this process may use: the distinct (package, core) pairs of the
+    CPUs in its affinity mask, capped by the cgroup CPU quota (a container's share of
+    a large host), plus the CPU model (lscpu's "Model name")."""
+    aff = sorted(os.sched_getaffinity(0))
+    phys = set()
+    for c in aff:
+        try:
+            base = f"/sys/devices/system/cpu/cpu{c}/topology/"
+            with open(base + "physical_package_id") as f:
+                pkg = f.read().strip()
+            with open(base + "core_id") as f:
+                phys.add((pkg, f.read().strip()))
+        except OSError:
+            phys.add(("?", str(c)))
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, period = f.read().split()
+            if q != "max":
+                quota = max(1, int(int(q) / int(period)))
+    except (OSError, ValueError):
+        pass
+    model = platform.processor() or platform.machine()
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    use = len(phys) if quota is None else min(len(phys), quota)
+    return {"threads": use, "physical_cores_in_affinity": len(phys), "logical_cpus_in_affinity": len(aff),
+            "cgroup_cpu_quota": quota, "model": model}
+
+
+def _time_cpu(fn, timed):
+    fn()  # warm-up
+    t0 = time.perf_counter()
+    for _ in range(timed):
+        out = fn()
+    return (time.perf_counter() - t0) / timed, out
+
+
+def _time_hip(model, left, right, n=20):
+    with torch.no_grad():
+        for _ in range(3):
+            model(left, right)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(n):
+            out = model(left, right)
+        torch.cuda.synchronize()
+    return (time.perf_counter() - t0) / n, out
+
+
+def cpu_baseline(args, model, left0, right0, disp0, hip_step_s, device):
+    """CPU leg: the oracle (oracle/torch_ref.py, the reference's aten
+    op sequence restated) on the host's physical cores, 1 warm-up + ``--cpu-timed``
+    forwards per config, fp32, B = 1, beside the HIP path on the same inputs.  C2 is
+    this benchmark's first pair; C1 is predict.py's preprocessing of the reference's
+    SceneFlow sample pair (tests/golden/c1_sceneflow.npz) at 288x576 D96."""
+    from oracle import torch_ref as ref
+    cores = host_cores()
+    torch.set_num_threads(cores["threads"])
+    sd = {k: v.detach().cpu() for k, v in model.state_dict().items()}
+    a = arch_arrays()
+    res = {"kind": "port", "unit": "pairs/s", "cores": cores["threads"], "host": cores, "configs": {}}
+    cfgs = [c for c in args.cpu_configs.split(",") if c]
+    with torch.no_grad():
+        for cfg in cfgs:
+            if cfg == "c2" or cfg == config_name(args):
+                l, r, md = left0.cpu(), right0.cpu(), args.maxdisp
+                hip_out, hip_s = disp0.cpu(), hip_step_s / args.batch
+                tag = f"{args.height}x{args.width} D={args.maxdisp}"
+            elif cfg == "c1":
+                from tests.golden_util import c1_inputs
+                l, r = c1_inputs()
+                md = 96
+                m1 = build_model(md, device, "f32")
+                hip_s, hip_out = _time_hip(m1, l.to(device), r.to(device))
+                hip_out = hip_out.cpu()
+                tag = "SceneFlow sample pair 0001 (predict.py preprocessing), 288x576 D=96"
+            else:
+                raise ValueError(f"unknown CPU baseline config {cfg}")
+            s_pair, want = _time_cpu(lambda: ref.leastereo_forward(sd, l, r, md, a), args.cpu_timed)
+            entry = {"workload": tag, "cpu_s_per_pair": s_pair, "cpu_pairs_s": 1.0 / s_pair,
+                     "hip_pairs_s": 1.0 / hip_s, "hip_vs_cpu_speedup": s_pair / hip_s,
+                     "epe_px_hip_vs_cpu_f32": ref.epe(hip_out, want),
+                     "timing": f"1 warm-up + {args.cpu_timed} timed forwards, B=1 fp32"}
+            if args.cpu_fp64 and cfg == "c2":
+                sd64 = {k: (v.double() if v.is_floating_point() else v) for k, v in sd.items()}
+                t0 = time.perf_counter()
+                want64 = ref.leastereo_forward(sd64, l.double(), r.double(), md, a)
+                entry["fp64_s"] = time.perf_counter() - t0
+                entry["epe_px_hip_vs_fp64"] = ref.epe(hip_out, want64)
+                entry["epe_px_cpu_f32_vs_fp64"] = ref.epe(want, want64)
+            res["configs"][cfg] = entry
+    head = res["configs"].get("c2") or next(iter(res["configs"].values()))
+    res["value"] = head["cpu_pairs_s"]
+    res["sample"] = (f"oracle/torch_ref.py on torch CPU ({cores['model']}, {cores['threads']} threads = "
+                     f"physical cores available to the process), {head['timing']}: "
+                     + "; ".join(f"{k}: {v['workload']}" for k, v in res["configs"].items()))
+    return res
+
+
+# ------------------------------------------------------------------------ roofline
 def algorithm_name(kernel: str) -> str:
     """The convolution algorithm a conv kernel instantiation runs."""
     if kernel.startswith("conv3d_wino2_kernel<"):
@@ -164,6 +286,24 @@ def algorithm_name(kernel: str) -> str:
     if kernel.startswith("conv3d_wino_kernel<"):
         return f"winograd F({kernel.split('<')[1].split(',')[0]},3) along W"
     return "direct convolution"
+
+
+def _matrix_peak(name: str) -> float:
+    return BF16_MFMA_PEAK_TFLOPS if ("bf16" in name or "c8" in name) else FP32_PEAK_TFLOPS
+
+
+def path_roofline(records):
+    """T_roof of one forward for the algorithms it runs: per launch max(issued MFMA FLOP
+    / matrix peak, VALU FLOP / fp32 peak, algorithmic bytes / HBM peak), summed; and
+    the HBM-only time (sum of bytes / HBM peak)."""
+    t_roof = t_hbm = t_mat = 0.0
+    for name, flops, nbytes, _e0, _e1, mfma, _shape in records:
+        t_m = mfma / (_matrix_peak(name) * 1e12) if mfma else flops / (FP32_PEAK_TFLOPS * 1e12)
+        t_b = nbytes / (HBM_PEAK_GBS * 1e9)
+        t_roof += max(t_m, t_b)
+        t_hbm += t_b
+        t_mat += t_m
+    return t_roof * 1e3, t_hbm * 1e3, t_mat * 1e3, len(records)
 
 
 def _quantile(xs, q):
@@ -174,9 +314,30 @@ def _quantile(xs, q):
     return xs[i] + (xs[j] - xs[i]) * (pos - i)
 
 
-def main():
-    args = parse()
-    info = parallel.rank_info()
+# ------------------------------------------------------------------------ ranks
+def run_stub(args, info):
+    """Launcher / sharding / gather plumbing with a CPU step (tests, gloo): each rank
+    'processes' its shard of world*batch pairs and reports pair index * 1e-3 as its
+    per-pair value, so the gathered vector shows the order the ranks' shards land in."""
+    parallel.init("gloo", info, None)
+    shard = parallel.shard(info.world * args.batch, info)
+    parallel.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        torch.zeros(args.batch, 8, 8).add_(1.0)
+    parallel.barrier()
+    elapsed = parallel.max_over_ranks(time.perf_counter() - t0, torch.device("cpu"))
+    per_pair = parallel.gather_per_pair(torch.tensor([i * 1e-3 for i in shard], dtype=torch.float32))
+    shards = parallel.gather_per_pair(torch.tensor([shard.start, shard.stop], dtype=torch.int64))
+    if info.is_main:
+        print(json.dumps({"metric": METRIC, "value": info.world * args.batch * args.steps / max(elapsed, 1e-9),
+                          "unit": "pairs/s", "n_gpus": info.world, "steps": args.steps, "stub": True,
+                          "shards": shards.view(-1, 2).tolist(),
+                          "pair_epe_px": {"per_pair": [float(v) for v in per_pair]}}), flush=True)
+    parallel.finalize()
+
+
+def run(args, info):
     world, rank = info.world, info.rank
     device = torch.device("cuda", info.local_rank)
     if world > 1:
@@ -187,8 +348,10 @@ def main():
 
     model = build_model(args.maxdisp, device, args.precision)
     model.check_shape(args.height, args.width)
-    # weak scaling: every rank owns args.batch pairs of the global batch (shard of
-    # world*batch pairs), generated on its own device from a rank-seeded stream
+    # weak scaling: rank r owns pairs shard(r) of the world*batch global batch, generated
+    # on its own device from a rank-seeded stream
+    shard = parallel.shard(world * args.batch, info)
+    assert len(shard) == args.batch
     g = torch.Generator(device=device).manual_seed(1234 + rank)
     left = torch.randn(args.batch, 3, args.height, args.width, device=device, generator=g)
     right = torch.randn(args.batch, 3, args.height, args.width, device=device, generator=g)
@@ -208,15 +371,19 @@ def main():
     with torch.no_grad():
         for _ in range(max(args.warmup, 1)):
             out = step()
-        # find the dominant conv kernel instantiation (untimed eager pass)
+        # every launch of one (untimed) eager forward: the path roofline, and the
+        # dominant conv kernel instantiation
         with kernels.KernelProbe() as probe:
             model(left, right)
         per_kernel = probe.summary()
-        dominant = max(per_kernel, key=lambda n: per_kernel[n]["ms"])
+        t_roof_ms, t_hbm_ms, t_mat_ms, n_launch = path_roofline(probe.records)
+        convs = {n: d for n, d in per_kernel.items() if d["mfma_flops"] > 0}
+        dominant = max(convs, key=lambda n: convs[n]["ms"])
         if args.breakdown and info.is_main:
             for n, d in sorted(per_kernel.items(), key=lambda kv: -kv[1]["ms"]):
-                log(f"{n:40s} launches {d['launches']:3d}  {d['ms']:8.3f} ms  "
-                    f"{d['flops'] / d['ms'] / 1e9:8.1f} TFLOP/s  {d['bytes'] / d['ms'] / 1e6:8.1f} GB/s")
+                log(f"{n:48s} launches {d['launches']:3d}  {d['ms']:8.3f} ms  "
+                    f"{d['mfma_flops'] / d['ms'] / 1e9:8.1f} TFLOP/s issued  "
+                    f"{d['bytes'] / d['ms'] / 1e6:8.1f} GB/s")
 
         parallel.barrier()
         torch.cuda.synchronize()
@@ -239,32 +406,43 @@ def main():
         step_ms = sorted(ev[i].elapsed_time(ev[i + 1]) for i in range(args.steps))
     elapsed = parallel.max_over_ranks(elapsed, device)
 
+    # after the timed region: the per-pair check of this rank's shard against an
+    # independent HIP path, then the data path's one collective (all-gather over ranks)
+    pair = None
+    if args.pair_check:
+        ref_prec = "f32_direct" if args.precision == "f32" else "f32"
+        with torch.no_grad():
+            check = build_model(args.maxdisp, device, ref_prec)(left, right)
+            e = (out.double() - check.double()).abs().mean(dim=(1, 2)).float()
+        del check
+        per_pair = [float(v) for v in parallel.gather_per_pair(e).cpu()]
+        pair = {"vs": ("HIP f32 on the direct-conv engine over the in-place cost volume (no Winograd, "
+                       "no factored stem0)" if args.precision == "f32" else "HIP f32 path, same weights"),
+                "pairs": world * args.batch, "max": max(per_pair), "mean": sum(per_pair) / len(per_pair),
+                "per_pair": per_pair}
     epe = None
-    if args.epe:  # after the timed region: one all-gather of the per-rank parity check
+    if args.epe:
         e = torch.tensor([golden_epe(device, args.precision)], device=device, dtype=torch.float32)
         epe = [float(v) for v in parallel.gather_per_pair(e).cpu()]
 
-    flops_per_launch = dom["flops"] / dom["launches"]
-    ms_per_launch = dom["ms"] / dom["launches"]
-    achieved = flops_per_launch / (ms_per_launch * 1e-3) / 1e12
-    mfma_tflops = dom["mfma_flops"] / dom["launches"] / (ms_per_launch * 1e-3) / 1e12
+    launches = dom["launches"]
+    ms_per_launch = dom["ms"] / launches
+    issued = dom["mfma_flops"] / launches
+    direct = dom["flops"] / launches
+    bf16 = args.precision == "bf16"
+    peak = BF16_MFMA_PEAK_TFLOPS if bf16 else FP32_PEAK_TFLOPS
+    achieved = issued / (ms_per_launch * 1e-3) / 1e12
     traffic = None
+    cfg = config_name(args)
     tf_file = os.path.join(REPO, "profiles", "hbm_traffic.json")
     if os.path.exists(tf_file):
         with open(tf_file) as f:
             tf = json.load(f)
         # per-config entries (tools/traffic_merge.py) first: bytes per launch depend on shapes
-        cfg_name = next((k for k, v in CONFIGS.items() if all(getattr(args, f) == x for f, x in v.items())), None)
-        traffic = (tf.get(f"{dominant}@{cfg_name}") or tf.get(dominant, {})).get("bytes_per_launch")
-
-    bf16 = args.precision == "bf16"
-    peak = BF16_MFMA_PEAK_TFLOPS if bf16 else FP32_MFMA_PEAK_TFLOPS
-    workload = {(576, 960, 192, 1, "f32"): "SceneFlow 576x960 D=192 fp32, batch 1 per GPU (BASELINE configs[1])",
-                (384, 1248, 192, 8, "bf16"): "KITTI2015 384x1248 D=192 bf16, batch 8 (BASELINE configs[2])",
-                (576, 960, 192, 8, "bf16"): "SceneFlow 576x960 D=192 bf16, 8 pairs per GPU (BASELINE configs[3])",
-                (1008, 1512, 264, 1, "f32"): "Middlebury 1008x1512 D=264 fp32, batch 1 (BASELINE configs[4], D256 is illegal)",
-                }.get((args.height, args.width, args.maxdisp, args.batch, args.precision),
-                      f"{args.height}x{args.width} D={args.maxdisp} {args.precision}, batch {args.batch} per GPU")
+        traffic = (tf.get(f"{dominant}@{cfg}") or tf.get(dominant, {})).get("bytes_per_launch")
+    ms_step = elapsed / args.steps * 1e3
+    workload = WORKLOADS.get(cfg, f"{args.height}x{args.width} D={args.maxdisp} {args.precision}, "
+                                  f"batch {args.batch} per GPU")
     result = {
         "metric": METRIC,
         "value": world * args.batch * args.steps / elapsed,
@@ -272,7 +450,7 @@ def main():
         "n_gpus": world,
         "steps": args.steps,
         "warmup": args.warmup,
-        "ms_per_step": elapsed / args.steps * 1e3,
+        "ms_per_step": ms_step,
         "step_ms": {"median": _quantile(step_ms, 0.5), "p10": _quantile(step_ms, 0.1),
                     "p90": _quantile(step_ms, 0.9), "source": "HIP events between steps, this rank"},
         "higher_is_better": True,
@@ -284,34 +462,49 @@ def main():
         "config": {"workload": workload,
                    "height": args.height, "width": args.width, "maxdisp": args.maxdisp,
                    "global_batch": world * args.batch,
-                   "parallelism": f"dp{world} (independent pairs per rank, no collective in the step)",
+                   "parallelism": f"dp{world} (pairs sharded over ranks, no collective in the step)",
                    "launch": "hip graph replay" if args.graph else "eager"},
-        "roofline": {"bound": "mfma", "kernel": dominant, "achieved": achieved,
-                     "peak": peak, "unit": "TFLOP/s",
-                     "frac": achieved / peak, "traffic": traffic,
-                     "launches_per_step": dom["launches"] / args.steps,
-                     "flops_per_launch": flops_per_launch, "ms_per_launch": ms_per_launch,
-                     # products the kernel actually issues: Winograd F(2,3) does 4 per 6 of
-                     # the direct convolution whose FLOPs define `achieved`
-                     "algorithm": algorithm_name(dominant),
-                     "mfma_executed": mfma_tflops, "mfma_executed_frac": mfma_tflops / peak},
+        "roofline": {"bound": "mfma", "kernel": dominant, "algorithm": algorithm_name(dominant),
+                     "achieved": achieved, "peak": peak, "unit": "TFLOP/s", "frac": achieved / peak,
+                     "traffic": traffic,
+                     "work": "MFMA FLOPs the kernel issues per launch (Winograd products, cout "
+                             "padded to its blocks); DESIGN.md §4 gives the per-launch formula",
+                     "flops_per_launch": issued, "ms_per_launch": ms_per_launch,
+                     "launches_per_step": launches / args.steps,
+                     "direct_equivalent": {"flops_per_launch": direct,
+                                           "achieved": direct / (ms_per_launch * 1e-3) / 1e12,
+                                           "note": "the reference algorithm's (direct convolution's) "
+                                                   "FLOPs for the same outputs; not a utilisation"}},
+        "path_roofline": {"t_roof_ms": t_roof_ms, "frac": t_roof_ms / ms_step,
+                          "hbm_only_ms": t_hbm_ms, "hbm_frac": t_hbm_ms / ms_step,
+                          "matrix_only_ms": t_mat_ms, "launches": n_launch,
+                          "source": "one eager forward: sum over its launches of max(issued MFMA FLOP / "
+                                    "peak, VALU FLOP / fp32 peak, algorithmic bytes / 8 TB/s)",
+                          "reference_algorithm_t_roof_ms": T_ROOF_REFERENCE_MS.get((cfg, args.batch))},
+        "pair_epe_px": pair,
         "epe_px": None if epe is None else {
-            "vs": "reference LEAStereo fp32 disparity (tests/golden e2e b1_h96_w192_md48)",
+            "vs": "reference LEAStereo fp32 disparity (tests/golden e2e b1_h96_w192_md48)"
+                  + (" (bf16 matching net: no upstream tolerance; see DESIGN.md)" if bf16 else ""),
             "max_over_ranks": max(epe), "per_rank": epe},
     }
-    cfg = next((k for k, v in CONFIGS.items() if all(getattr(args, f) == x for f, x in v.items())), None)
-    t_roof = T_ROOF_MS.get((cfg, args.batch))
-    if t_roof is not None:
-        result["path_roofline"] = {"t_roof_ms": t_roof, "frac": t_roof / result["ms_per_step"],
-                                   "source": "SURVEY.md §8d: sum over matching-net layers of "
-                                             "max(FLOP / MFMA peak, bytes / 8 TB/s)"}
-    if bf16 and result["epe_px"] is not None:
-        result["epe_px"]["vs"] += " (bf16 matching net: no upstream tolerance; see DESIGN.md)"
     if info.is_main and world == 1 and args.cpu_baseline:
-        result["cpu_baseline"] = cpu_baseline(args, model, left[:1], right[:1], out[:1])
+        result["cpu_baseline"] = cpu_baseline(args, model, left[:1], right[:1], out[:1],
+                                              float(_quantile(step_ms, 0.5)) * 1e-3, device)
     if info.is_main:
         print(json.dumps(result), flush=True)
     parallel.finalize()
+
+
+def main(argv=None):
+    argv = sys.argv[1:] if argv is None else argv
+    args = parse(argv)
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(launch(args.gpus, argv))
+    info = parallel.rank_info()
+    if info.world != args.gpus:
+        log(f"bench.py: --gpus {args.gpus} but the launcher started {info.world} rank(s)")
+        sys.exit(2)
+    (run_stub if args.stub else run)(args, info)
 
 
 if __name__ == "__main__":

@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define LEA_ABI_VERSION 7
+#define LEA_ABI_VERSION 8
 
 #define LEA_F32 0
 #define LEA_BF16 1
@@ -146,11 +146,6 @@ int lea_feature_stem_bnrelu(const float* x, int64_t x_bstride, const float* w0, 
                             const float* shift1, void* y, int64_t y_bstride, int B, int cin, int c0,
                             int c1, int Hi, int Wi, int dtype, void* stream);
 
-/* Tuning hook: force the (NT, TW, TD) tile of the k=3 DMA engine for later convs on
- * the calling thread (nt <= 0 restores the built-in planner).  A tile that is not
- * instantiated for the conv's cout block makes the conv return LEA_E_UNSUPPORTED.
- * Used by tools/conv_sweep.py; callers never need it. */
-int lea_conv3d_set_tile_override(int nt, int tw, int td);
 
 /* Trilinear resample.  Replaces F.interpolate(mode='trilinear') at
  * skip_model_3d.py:48,50 and nn.Upsample at :162-164 (align_corners=1), with
@@ -214,14 +209,6 @@ int lea_conv3d_bnrelu_costvolume_bf16(const void* left, const void* right, int64
                                       void* y, int64_t y_bstride, int B, int C, int cout, int D3,
                                       int H, int W, unsigned flags, void* stream);
 
-/* Tuning hook (tools/conv_sweep.py --bf16): force the bf16 conv tile -- th rows,
- * td planes, mt 16-row tiles per wave -- on the calling thread; th <= 0 restores
- * the planner. */
-int lea_conv3d_bf16_set_tile_override(int th, int td, int mt);
-/* bf16 engine variant: 0 = the planner's choice (single-chunk 3x3x3 layers, cin <= 16,
- * stream along D: "conv_bf16_stream_kernel<MT, WC, TH, NB>"), 1 = the tile kernel for
- * every layer.  Per calling thread. */
-int lea_conv3d_bf16_set_variant(int variant);
 
 /* Kernel instantiation the bf16 conv of this shape launches. */
 const char* lea_conv3d_kernel_name_bf16(int B, int cout, int cin, int D, int H, int W, int k,
@@ -244,10 +231,6 @@ int lea_resample3d_trilinear_bf16(const void* x, int64_t x_bstride, void* y, int
                                   int align_corners, const float* scale, const float* shift,
                                   unsigned flags, void* stream);
 
-/* Tuning hook (tools/resample_probe.py): output words per thread of the c8 resample,
- * k in {1, 2, 4}; 0 restores the default (4 when up-sampling, else 1).  Per calling
- * thread. */
-int lea_resample_bf16_set_batch(int k);
 
 /* Layout converters: f32 NC[D]HW (vol = D*H*W voxels per channel) <-> bf16 c8. */
 int lea_to_c8_bf16(const float* x, int64_t x_bstride, void* y, int64_t y_bstride, int B, int C,
@@ -289,45 +272,10 @@ int lea_conv3d_bnrelu_costvolume_wino(const void* left, const void* right, int64
                                       int cout, int D3, int H, int W, unsigned flags, int dtype,
                                       void* stream);
 /* Kernel instantiation the Winograd entries launch for this shape
- * ("conv3d_wino_kernel<F, Q, MT, NP, TD, CV>"); tile override for the tuning tools
- * (np in {1, 2} tile rows per wave, td in {1, 2} planes, f in {0 = planner, 2, 4,
- * 8 = F(4,3) on 32-wide row pairs}; np = 0 resets; depth-paired shapes keep np = 1,
- * td = 2 and F(4,3)). */
+ * ("conv3d_wino_kernel<F, Q, MT, NP, TD, CV>", or on the W x D engine
+ * "conv3d_wino2_kernel<Q, WC, MTE, NW, OCC, PV, CV>").  The engines' tuning hooks are
+ * in leastereo_hip_tuning.h. */
 const char* lea_conv3d_wino_kernel_name(int B, int cout, int D, int H, int W, int costvolume);
-int lea_conv3d_wino_set_tile_override(int np, int td, int f);
-/* Engine variant for the Winograd entries (same packed weights): 0 = the planner's
- * choice, 1 = F(4,3) along W only, 2..4 = F(4,3) along W x F(2,3) along D
- * (csrc/conv3d_wino2.hip: "conv3d_wino2_kernel<Q, WC, MTE, NW, OCC, CV>") where the
- * cout block allows it (16 or 32 couts per block): 2 = four waves of one 16-row
- * cout tile, 3 = eight waves, 4 = two cout tiles per wave at one wave per SIMD.
- * Per calling thread, like the tile override. */
-int lea_conv3d_wino_set_variant(int variant);
-/* Tuning hook: depth pairs each W x D engine workgroup walks (its items = pairs x
- * 4-channel chunks through one DMA pipeline); 0 restores the planner.  Per calling
- * thread. */
-int lea_conv3d_wino2_set_walk(int spw);
-/* Tuning hook: 1 (default) = lea_conv3d_bnrelu_resampled with k = 1 and at most 131072
- * output voxels (B x D x H x W) on the gather-GEMM (each lane interpolates its own MFMA
- * operand from the 8 corners, no staging), 0 = always the register-staged engine.
- * Per calling thread. */
-int lea_conv3d_set_rs_gather(int on);
-/* Tuning hook: 1 (default) = lea_conv3d_bnrelu_bf16 with k = 1 and cin <= 128 on the
- * streamed 1x1 kernel (each lane loads its own 16-byte B word, weights in registers, no
- * staging; bit-identical to the tile kernel), 0 = the tile kernel.  Per calling thread. */
-int lea_conv3d_bf16_set_stream1x1(int on);
-/* Tuning hook: 1 (default) = the Winograd engines' buffer-addressed epilogue where the
- * shape allows it (W % 4 == 0, 16-B aligned output / residual; residual loads issued
- * together, the next chunk's DMA waited for without the stores), 0 = the per-group
- * epilogue.  Per calling thread. */
-int lea_conv3d_wino_set_epi_buf(int on);
-/* couts <= 8 on the Winograd entries: 0 (default) = the depth-paired 1-D tile, 1 =
- * packed and planned as 16-row cout blocks (the W x D engine).  Packing and launches must
- * use the same mode.  Per calling thread. */
-int lea_conv3d_wino_set_small_cout(int mode);
-/* 48k-cout layers (not multiples of 32) on the Winograd entries: 1 (default) = 48-row
- * blocks of the 1-D engine, 0 = 32-row blocks of the W x D engine (last block padded).
- * Packing and launches must use the same setting.  Per calling thread. */
-int lea_conv3d_wino_set_block48(int on);
 
 /* ---- Matching-net stem0 over the cost volume, factored (csrc/cv_stem.hip) ----
  * Replaces retrain/LEAStereo.py:34-48 + skip_model_3d.py:141 like

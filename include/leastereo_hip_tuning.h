@@ -1,0 +1,81 @@
+/*
+ * leastereo_hip_tuning.h -- tuning hooks of libleastereo_hip.so (not part of the
+ * drop-in contract in leastereo_hip.h).
+ *
+ * Each hook overrides a planner choice of one engine for A/B measurements and the
+ * sweep tools under tools/ (conv_sweep.py, wino_sweep.py, wino2_sweep.py,
+ * resample_probe.py, gpu_ab.sh via the LEASTEREO_* variables of _lib.py).  The
+ * settings are process-wide (every host thread sees them) and take effect on the
+ * next launch; callers of the hot path never need them.  Each returns 0, or
+ * LEA_E_INVALID for an out-of-range value (nothing changed).
+ */
+#ifndef LEASTEREO_HIP_TUNING_H
+#define LEASTEREO_HIP_TUNING_H
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Direct k = 3 engine: force the (NT, TW, TD) tile (nt <= 0 restores the planner).
+ * A tile not instantiated for the conv's cout block makes the conv return
+ * LEA_E_UNSUPPORTED (tools/conv_sweep.py). */
+int lea_conv3d_set_tile_override(int nt, int tw, int td);
+
+/* 1 (default) = lea_conv3d_bnrelu_resampled with k = 1 and at most 131072 output
+ * voxels (B x D x H x W) on the gather-GEMM (each lane interpolates its own MFMA
+ * operand from the 8 corners, no staging), 0 = always the register-staged engine. */
+int lea_conv3d_set_rs_gather(int on);
+
+/* bf16 engine: force the conv tile -- th rows, td planes, mt 16-row tiles per wave
+ * (th <= 0 restores the planner; tools/conv_sweep.py --bf16). */
+int lea_conv3d_bf16_set_tile_override(int th, int td, int mt);
+
+/* bf16 engine variant: 0 = the planner's choice (single-chunk 3x3x3 layers, cin <= 16,
+ * stream along D: "conv_bf16_stream_kernel<MT, WC, TH, NB>"), 1 = the tile kernel for
+ * every layer. */
+int lea_conv3d_bf16_set_variant(int variant);
+
+/* 1 (default) = lea_conv3d_bnrelu_bf16 with k = 1 and cin <= 128 on the streamed 1x1
+ * kernel (each lane loads its own 16-byte B word, weights in registers, no staging;
+ * bit-identical to the tile kernel), 0 = the tile kernel. */
+int lea_conv3d_bf16_set_stream1x1(int on);
+
+/* Output words per thread of the c8 resample, k in {1, 2, 4}; 0 restores the default
+ * (4 when up-sampling, else 1) (tools/resample_probe.py). */
+int lea_resample_bf16_set_batch(int k);
+
+/* Winograd entries: tile override (np in {1, 2} tile rows per wave, td in {1, 2}
+ * planes, f in {0 = planner, 2, 4, 8 = F(4,3) on 32-wide row pairs}; np = 0 resets;
+ * depth-paired shapes keep np = 1, td = 2 and F(4,3)). */
+int lea_conv3d_wino_set_tile_override(int np, int td, int f);
+
+/* Engine variant for the Winograd entries (same packed weights): 0 = the planner's
+ * choice, 1 = F(4,3) along W only, 2..4 = F(4,3) along W x F(2,3) along D
+ * (csrc/conv3d_wino2.hip: "conv3d_wino2_kernel<Q, WC, MTE, NW, OCC, PV, CV>") where the
+ * cout block allows it (16 or 32 couts per block): 2 = four waves of one 16-row
+ * cout tile, 3 = eight waves, 4 = two cout tiles per wave at one wave per SIMD. */
+int lea_conv3d_wino_set_variant(int variant);
+
+/* Depth pairs each W x D engine workgroup walks (its items = pairs x 4-channel chunks
+ * through one DMA pipeline); 0 restores the planner. */
+int lea_conv3d_wino2_set_walk(int spw);
+
+/* 1 (default) = the Winograd engines' buffer-addressed epilogue where the shape allows
+ * it (W % 4 == 0, 16-B aligned output / residual; residual loads issued together, the
+ * next chunk's DMA waited for without the stores), 0 = the per-group epilogue. */
+int lea_conv3d_wino_set_epi_buf(int on);
+
+/* couts <= 8 on the Winograd entries: 0 (default) = the depth-paired 1-D tile, 1 =
+ * packed and planned as 16-row cout blocks (the W x D engine).  Packing and launches
+ * must use the same mode. */
+int lea_conv3d_wino_set_small_cout(int mode);
+
+/* 48k-cout layers (not multiples of 32) on the Winograd entries: 1 (default) = 48-row
+ * blocks of the 1-D engine, 0 = 32-row blocks of the W x D engine (last block padded).
+ * Packing and launches must use the same setting. */
+int lea_conv3d_wino_set_block48(int on);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* LEASTEREO_HIP_TUNING_H */

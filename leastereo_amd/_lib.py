@@ -12,7 +12,7 @@ LIB_PATH = os.environ.get(
     "LEASTEREO_HIP_LIB",
     os.path.join(os.path.dirname(os.path.abspath(__file__)), "libleastereo_hip.so"))
 
-ABI_VERSION = 7
+ABI_VERSION = 8
 LEA_F32 = 0
 LEA_BF16 = 1
 LEA_RELU = 1
@@ -24,7 +24,8 @@ _i = ctypes.c_int
 _i64 = ctypes.c_int64
 _u = ctypes.c_uint
 
-# name -> (restype, argtypes); exactly the symbols include/leastereo_hip.h declares
+# name -> (restype, argtypes); exactly the symbols include/leastereo_hip.h and
+# include/leastereo_hip_tuning.h declare
 SIGNATURES = {
     "lea_abi_version": (_i, []),
     "lea_last_error": (ctypes.c_char_p, []),
@@ -132,8 +133,8 @@ def load():
     return _lib
 
 
-# A/B switches for the planners' tuning hooks (thread-local in the library: they apply
-# to the thread that loads it), e.g. LEASTEREO_WINO2_WALK=1 to disable the depth walk
+# A/B switches for the planners' tuning hooks (include/leastereo_hip_tuning.h; process-wide
+# in the library), e.g. LEASTEREO_WINO2_WALK=1 to disable the depth walk
 TUNING_ENV = {"LEASTEREO_WINO2_WALK": "lea_conv3d_wino2_set_walk",
               "LEASTEREO_EPI_BUF": "lea_conv3d_wino_set_epi_buf",
               "LEASTEREO_RS_GATHER": "lea_conv3d_set_rs_gather",

@@ -2,11 +2,13 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include <atomic>
 #include <cstdarg>
 #include <cstdint>
 #include <cstdio>
 
 #include "leastereo_hip.h"
+#include "leastereo_hip_tuning.h"
 
 namespace lea {
 

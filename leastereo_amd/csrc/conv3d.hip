@@ -117,7 +117,7 @@ __global__ __launch_bounds__(kConvThreads, 2) void conv3d_reg_kernel(const ConvA
 // staging: lane (g, n) of a wave forms its own B fragment of v_mfma_f32_16x16x4_f32 --
 // input channel 4 s + g of output voxel v0 + n -- from the 8 corners of aten's
 // trilinear expression (trilerp: same operands, same order as the register-staged
-// engine; the MFMA sums may associate differently), read by buffer loads (padding channels out of range read
+// engine; the MFMA sums may associate differently), read by buffer loads (padding channels' operands forced to
 // 0).  The A fragments (the k = 1 packing of this cout block) sit in LDS.  A wave walks
 // `tpw` consecutive 16-voxel tiles of the flat output run; every k-step's loads of a
 // 32-channel chunk are issued before its MFMAs.  HBM-bound: the input is read once.
@@ -176,7 +176,7 @@ __global__ __launch_bounds__(256) void conv1x1_rs_f32_kernel(const ConvArgs a, i
 #pragma unroll
       for (int s = 0; s < 8; ++s) {
         const int ci = ch * 32 + 4 * s + g;
-        const unsigned co = ci < a.cin ? (unsigned)ci * vin * 4u : 0xFFFFFF00u;  // padding channels read 0
+        const unsigned co = ci < a.cin ? (unsigned)ci * vin * 4u : 0u;  // padding channels: bv = 0 below
         const unsigned rr[4] = {r00, r01, r10, r11};
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
@@ -187,9 +187,12 @@ __global__ __launch_bounds__(256) void conv1x1_rs_f32_kernel(const ConvArgs a, i
 #pragma unroll
       for (int s = 0; s < 8; ++s) {
         const float* e = c[s];
-        const float bv = ad.l0 * (ah.l0 * (aw.l0 * e[0] + aw.l1 * e[1]) + ah.l1 * (aw.l0 * e[2] + aw.l1 * e[3])) +
-                         ad.l1 * (ah.l0 * (aw.l0 * e[4] + aw.l1 * e[5]) + ah.l1 * (aw.l0 * e[6] + aw.l1 * e[7]));
         const int ci = ch * 32 + 4 * s + g;
+        // padding channels (ci >= cin) read channel 0's voxels: their operand is forced to 0
+        // so a non-finite input there cannot reach other outputs through the zero weights
+        const float bv = ci >= a.cin ? 0.f :
+            ad.l0 * (ah.l0 * (aw.l0 * e[0] + aw.l1 * e[1]) + ah.l1 * (aw.l0 * e[2] + aw.l1 * e[3])) +
+            ad.l1 * (ah.l0 * (aw.l0 * e[4] + aw.l1 * e[5]) + ah.l1 * (aw.l0 * e[6] + aw.l1 * e[7]));
 #pragma unroll
         for (int m = 0; m < MT; ++m) {
           const int col = 16 * m + n;
@@ -519,7 +522,7 @@ inline int dma_lds_bytes(int mt, int nt, int tw, int td) {
   }
 }
 
-thread_local int g_tile_override[3] = {0, 0, 0};
+int g_tile_override[3] = {0, 0, 0};
 
 inline bool prefer_tw64(int W) {
   const int w64 = (W + 63) / 64 * 64, w32 = (W + 31) / 32 * 32;
@@ -528,7 +531,7 @@ inline bool prefer_tw64(int W) {
 
 // lea_conv3d_set_rs_gather: 1 (default) = the resampled 1x1 convs on the gather-GEMM
 // (conv1x1_rs_f32_kernel), 0 = the register-staged engine
-thread_local int g_rs_gather = 1;
+int g_rs_gather = 1;
 
 inline Plan make_plan(int B, int cout, int D, int H, int W, int k, bool resample) {
   Plan p;

@@ -802,9 +802,9 @@ struct Plan {
   bool s1x1;   // the streamed 1x1 (conv1x1_c8_kernel)
 };
 
-thread_local int g_override[3] = {0, 0, 0};  // th, td, mt (lea_conv3d_bf16_set_tile_override)
-thread_local int g_variant = 0;              // lea_conv3d_bf16_set_variant: 0 planner, 1 tile kernel only
-thread_local int g_stream1x1 = 1;            // lea_conv3d_bf16_set_stream1x1
+int g_override[3] = {0, 0, 0};  // th, td, mt (lea_conv3d_bf16_set_tile_override)
+int g_variant = 0;              // lea_conv3d_bf16_set_variant: 0 planner, 1 tile kernel only
+int g_stream1x1 = 1;            // lea_conv3d_bf16_set_stream1x1
 
 inline Plan plan(int B, int cout, int D, int H, int W, int ks, int cin) {
   // r01 sweep (tools/conv_sweep.py --bf16, profiles/r01_conv_sweep_bf16.txt): one
@@ -1124,7 +1124,7 @@ extern "C" int lea_from_c8_bf16(const void* x, int64_t x_bstride, float* y, int6
 }
 
 // resample words per thread (lea_resample_bf16_set_batch; 0 = up-sampling 4, else 1)
-static thread_local int g_resample_k = 0;
+static int g_resample_k = 0;
 
 extern "C" int lea_resample_bf16_set_batch(int k) {
   clear_error();

@@ -546,22 +546,22 @@ struct Plan {
   Plan2 p2;
 };
 
-thread_local int g_override[3] = {0, 0, 0};  // np, td, f (lea_conv3d_wino_set_tile_override)
+int g_override[3] = {0, 0, 0};  // np, td, f (lea_conv3d_wino_set_tile_override)
 // lea_conv3d_wino_set_variant: 0 = the planner's choice (5), 1 = F(4,3)-along-W engine only,
 // 2..4 = the W x D engine's tiles where it applies (2: four waves, one cout tile each;
 // 3: eight waves; 4: two cout tiles per wave at one wave per SIMD), 5..7 = the same
 // with the inputs transformed once per chunk into LDS (32-cout blocks; 16-cout blocks
 // keep 2)
-thread_local int g_variant = 0;
-thread_local int g_spw = 0;  // lea_conv3d_wino2_set_walk: depth pairs per workgroup (0 = planner)
+int g_variant = 0;
+int g_spw = 0;  // lea_conv3d_wino2_set_walk: depth pairs per workgroup (0 = planner)
 // lea_conv3d_wino_set_small_cout: couts <= 8 packed / planned as 16-row blocks for the
 // W x D engine (1) or depth-paired for the 1-D engine (0, the default: r02 sweep, L0 8->8
 // 175 us depth-paired vs 210 us on the W x D engine's half-empty 16-row block)
-thread_local int g_small16 = 0;
+int g_small16 = 0;
 // lea_conv3d_wino_set_block48: 48k-cout layers as 48-row blocks of the 1-D engine (1) or
 // as 32-row blocks of the W x D engine, the last one padded (0)
-thread_local int g_block48 = 1;
-thread_local int g_epibuf = 1;  // lea_conv3d_wino_set_epi_buf
+int g_block48 = 1;
+int g_epibuf = 1;  // lea_conv3d_wino_set_epi_buf
 inline int host_mt(int cout) {
   if (g_small16 && cout <= 8) return 1;
   const int mt = mt_of(cout);

@@ -115,7 +115,10 @@ class CellGraphExecutor:
             for i, (cell, nxt) in enumerate(zip(cells, cells[1:])):
                 if (self.SHARE_DOWNSAMPLE and cell.downup_sample != 0 and nxt.downup_sample == 0
                         and nxt.c_out == cell.c_out and 2 + cell.steps - cell.block_multiplier == 1
-                        and cell.preprocess.conv.weight.shape[1] == nxt.pre_preprocess.conv.weight.shape[1]):
+                        and cell.preprocess.conv.weight.shape[1] == nxt.pre_preprocess.conv.weight.shape[1]
+                        # the next cell applies pre_preprocess only when s0's channels differ
+                        # from its C_out (skip_model_3d.py:52); the memo path assumes it does
+                        and cell.preprocess.conv.weight.shape[1] != nxt.c_out):
                     mods = [nxt.pre_preprocess, cell.preprocess]
                     folded = [m.folded_bn() for m in mods]
                     self.p[f"cells.{i}.share"] = _conv_params(
@@ -360,6 +363,20 @@ class MatchingExecutor(CellGraphExecutor):
             if CV_STEM:
                 self.cv = self._cv_stem_pack(*kernels.cv_stem_split_weights(matching.stem0.conv.weight))
         self._use_winograd()
+
+
+class MatchingExecutorDirect(MatchingExecutor):
+    """newMatching.forward on the direct implicit-GEMM engine only: stem0 reads the
+    cost volume in place (no factored 2D maps) and no layer runs Winograd.  An
+    independent algorithm for the same f32 arithmetic, used by bench.py as the
+    per-pair cross-check of every rank's shard (precision "f32_direct")."""
+
+    def __init__(self, matching):
+        super().__init__(matching)
+        self.cv = None
+
+    def _use_winograd(self):
+        """Direct engine only."""
 
 
 class FeatureExecutor(CellGraphExecutor):
@@ -634,7 +651,8 @@ class FeatureExecutorBF16(_C8Layout, FeatureExecutor):
         elif lh == h // 4:
             y = self._resample(self.conv("last_6", self.conv("last_12", last), size=half), full)
         elif lh == h // 8:
-            y = self.conv("last_12", self.conv("last_24", last, size=quarter), size=half)
+            # new_model_2d.py:163: last_12(up_24(last_24(x))), then last_6(up_12(.)), up_6
+            y = self.conv("last_12", self.conv("last_24", last), size=quarter)
             y = self._resample(self.conv("last_6", y, size=half), full)
         else:
             raise ValueError(f"feature size {tuple(x.shape[2:])} is not legal for the feature net")

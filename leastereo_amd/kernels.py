@@ -131,6 +131,18 @@ def _probe_begin(b, cin, cout, d, h, w, k, accumulate, in_vox, resampled, name=N
     return probe, name, flops, nbytes, e0, flops * mfma_scale, (b, cin, cout, d, h, w, k)
 
 
+def _probe_launch(name, flops, nbytes, mfma=None):
+    """Start HIP-event timing of a launch that is not a 3D conv (2D convs, resamples,
+    the head, the disparity regression, layout conversions): ``flops`` / ``nbytes`` are
+    its algorithmic work, ``mfma`` the matrix-core products it issues (default: flops)."""
+    probe = _probe
+    if probe is None or (probe.names is not None and name not in probe.names):
+        return None
+    e0 = torch.cuda.Event(enable_timing=True)
+    e0.record()
+    return probe, name, float(flops), float(nbytes), e0, float(flops if mfma is None else mfma), None
+
+
 def _probe_end(rec):
     if rec is not None:
         probe, name, flops, nbytes, e0, mfma, shape = rec
@@ -290,12 +302,16 @@ def conv2d_bnrelu(x: torch.Tensor, packed: torch.Tensor, cout: int,
     out, ybs = _conv_out(x.shape, cout, (1, h, w), out, accumulate, x.device, x.dtype)
     rptr, rbs = _residual(out, accumulate, residual, ybs)
     flags = (LEA_RELU if relu else 0) | (LEA_RESIDUAL if rptr is not None else 0)
+    rec = None if _probe is None else _probe_launch(
+        conv2d_kernel_name(b, cout, h, w), 2.0 * b * h * w * cout * cin * 9,
+        4.0 * b * h * w * (cin + cout * (2 if rptr is not None else 1)) + 36.0 * cout * cin)
     check(_lib.load().lea_conv2d_bnrelu(
         x.data_ptr(), xbs, packed.data_ptr(),
         scale.data_ptr() if scale is not None else None,
         shift.data_ptr() if shift is not None else None,
         rptr, rbs, out.data_ptr(), ybs, b, cin, cout, h, w, flags, LEA_F32, _stream()),
         "lea_conv2d_bnrelu")
+    _probe_end(rec)
     return out
 
 
@@ -314,7 +330,8 @@ def feature_stem(x: torch.Tensor, w0: torch.Tensor, scale0, shift0, w1: torch.Te
     if x2 is not None:
         if tuple(x2.shape) != tuple(x.shape):
             raise ValueError(f"feature_stem: x2 {tuple(x2.shape)} differs from x {tuple(x.shape)}")
-        srcs.append(x2.contiguous())
+        x2 = x2.contiguous()  # both branches below read this tensor (pointer difference too)
+        srcs.append(x2)
     b, cin, hi, wi = x.shape
     c0, c1 = w0.shape[0], w1.shape[0]
     if tuple(w0.shape) != (c0, cin, 3, 3) or tuple(w1.shape) != (c1, c0, 3, 3):
@@ -331,11 +348,15 @@ def feature_stem(x: torch.Tensor, w0: torch.Tensor, scale0, shift0, w1: torch.Te
         srcs, b, xbs = [x], 2, (x2.data_ptr() - x.data_ptr()) // x.element_size()
     else:
         xbs = x.stride(0)
+    rec = None if _probe is None else _probe_launch(
+        "feature_stem_kernel", 2.0 * nb * ho * wo * (9 * 9 * cin * c0 + 9 * c0 * c1),
+        4.0 * nb * cin * hi * wi + out.numel() * out.element_size(), 0.0)
     for i, src in enumerate(srcs):
         check(_lib.load().lea_feature_stem_bnrelu(
             src.data_ptr(), xbs, w0.data_ptr(), ptr(scale0), ptr(shift0), w1.data_ptr(),
             ptr(scale1), ptr(shift1), out[i * b:].data_ptr(), out.stride(0), b, cin, c0, c1, hi, wi,
             _lib.LEA_BF16 if c8 else LEA_F32, _stream()), "lea_feature_stem_bnrelu")
+    _probe_end(rec)
     return out
 
 
@@ -353,10 +374,13 @@ def conv2d_s3_bnrelu(x: torch.Tensor, w: torch.Tensor, scale: torch.Tensor | Non
     xbs = _check_volume_view(x, "x")
     out = torch.empty((b, cout, 1, (hi - 1) // 3 + 1, (wi - 1) // 3 + 1), device=x.device,
                       dtype=x.dtype)
+    rec = None if _probe is None else _probe_launch(
+        "conv2d_s3_kernel", 2.0 * out.numel() * cin * 9, 4.0 * (x.numel() + out.numel()), 0.0)
     check(_lib.load().lea_conv2d_s3_bnrelu(
         x.data_ptr(), xbs, w.data_ptr(), scale.data_ptr() if scale is not None else None,
         shift.data_ptr() if shift is not None else None, out.data_ptr(), out.stride(0), b, cin,
         cout, hi, wi, LEA_RELU if relu else 0, LEA_F32, _stream()), "lea_conv2d_s3_bnrelu")
+    _probe_end(rec)
     return out
 
 
@@ -375,11 +399,14 @@ def resample_trilinear(x: torch.Tensor, size, align_corners: bool = True,
     if tuple(out.shape) != (b, c, do, ho, wo):
         raise ValueError(f"out shape {tuple(out.shape)} != {(b, c, do, ho, wo)}")
     ybs = _check_volume_view(out, "out")
+    rec = None if _probe is None else _probe_launch(
+        "resample3d_f32", 0.0, 4.0 * b * c * (di * hi * wi + do * ho * wo))
     check(_lib.load().lea_resample3d_trilinear(
         x.data_ptr(), xbs, out.data_ptr(), ybs, b, c, di, hi, wi, do, ho, wo,
         1 if align_corners else 0, scale.data_ptr() if scale is not None else None,
         shift.data_ptr() if shift is not None else None, LEA_RELU if relu else 0, LEA_F32,
         _stream()), "lea_resample3d_trilinear")
+    _probe_end(rec)
     return out
 
 
@@ -397,11 +424,14 @@ def tapsum_upsample(q: torch.Tensor, cout: int, size, scale: torch.Tensor | None
     lib = _lib.load()
     ws = torch.empty(lib.lea_tapsum_workspace_bytes(b, cout, hi, wi, do) // 4, device=q.device,
                      dtype=torch.float32)
+    rec = None if _probe is None else _probe_launch(
+        "tapsum_f32", 0.0, 4.0 * (q.shape[0] * q.shape[1] * di * hi * wi + out.numel()))
     check(lib.lea_tapsum_upsample(
         q.data_ptr(), qbs, out.data_ptr(), out.stride(0), b, cout, di, hi, wi, do, ho, wo,
         scale.data_ptr() if scale is not None else None,
         shift.data_ptr() if shift is not None else None, LEA_RELU if relu else 0,
         ws.data_ptr(), LEA_F32, _stream()), "lea_tapsum_upsample")
+    _probe_end(rec)
     return out
 
 
@@ -414,10 +444,13 @@ def disparity_regression(cost: torch.Tensor, maxdisp: int, fast_exp: bool = Fals
     cost = cost.contiguous()
     b, _, d3, h3, w3 = cost.shape
     disp = torch.empty((b, 3 * h3, 3 * w3), device=cost.device, dtype=torch.float32)
+    rec = None if _probe is None else _probe_launch(
+        "disparity_regression", 0.0, 4.0 * (cost.numel() + disp.numel()))
     check(_lib.load().lea_disparity_regression(cost.data_ptr(), disp.data_ptr(), b, d3, h3, w3,
                                                maxdisp, _lib.LEA_BF16 if fast_exp else LEA_F32,
                                                _stream()),
           "lea_disparity_regression")
+    _probe_end(rec)
     return disp
 
 
@@ -451,8 +484,10 @@ def to_c8(x: torch.Tensor) -> torch.Tensor:
     b, c, d, h, w = x5.shape
     xbs = _check_volume_view(x5, "x")
     out = torch.empty((b, c // 8, d, h, w, 8), device=x.device, dtype=torch.bfloat16)
+    rec = None if _probe is None else _probe_launch("to_c8_bf16", 0.0, 6.0 * out.numel())
     check(_lib.load().lea_to_c8_bf16(x5.data_ptr(), xbs, out.data_ptr(), out.stride(0), b, c,
                                      d * h * w, _stream()), "lea_to_c8_bf16")
+    _probe_end(rec)
     return out
 
 
@@ -594,11 +629,14 @@ def resample_trilinear_bf16(x: torch.Tensor, size, align_corners: bool = True,
     if tuple(out.shape) != (b, cb, do, ho, wo, 8):
         raise ValueError("out shape mismatch")
     ybs = _check_c8_view(out, "out")
+    rec = None if _probe is None else _probe_launch(
+        "resample3d_c8", 0.0, 2.0 * b * cb * 8 * (di * hi * wi + do * ho * wo))
     check(_lib.load().lea_resample3d_trilinear_bf16(
         x.data_ptr(), xbs, out.data_ptr(), ybs, b, cb * 8, di, hi, wi, do, ho, wo,
         1 if align_corners else 0, scale.data_ptr() if scale is not None else None,
         shift.data_ptr() if shift is not None else None, LEA_RELU if relu else 0, _stream()),
         "lea_resample3d_trilinear_bf16")
+    _probe_end(rec)
     return out
 
 
@@ -615,11 +653,14 @@ def tapsum_upsample_bf16(q: torch.Tensor, cout: int, size, scale=None, shift=Non
     lib = _lib.load()
     ws = torch.empty(lib.lea_tapsum_workspace_bytes(b, cout, hi, wi, do) // 4, device=q.device,
                      dtype=torch.float32)
+    rec = None if _probe is None else _probe_launch(
+        "tapsum_c8", 0.0, 2.0 * q.numel() + 4.0 * out.numel())
     check(lib.lea_tapsum_upsample(
         q.data_ptr(), qbs, out.data_ptr(), out.stride(0), b, cout, di, hi, wi, do, ho, wo,
         scale.data_ptr() if scale is not None else None,
         shift.data_ptr() if shift is not None else None, LEA_RELU if relu else 0, ws.data_ptr(),
         _lib.LEA_BF16, _stream()), "lea_tapsum_upsample(bf16)")
+    _probe_end(rec)
     return out
 
 
@@ -667,10 +708,14 @@ def conv2d_bnrelu_bf16(x: torch.Tensor, packed: torch.Tensor, cout: int, scale, 
     else:
         rptr, rbs = None, 0
     flags = (LEA_RELU if relu else 0) | (LEA_RESIDUAL if rptr is not None else 0)
+    rec = None if _probe is None else _probe_launch(
+        "conv2d_bf16", 2.0 * b * h * w * cout * cb * 8 * 9,
+        2.0 * b * h * w * (cb * 8 + cout * (2 if rptr is not None else 1)) + 18.0 * cout * cb * 8)
     check(_lib.load().lea_conv2d_bnrelu_bf16(
         x.data_ptr(), xbs, packed.data_ptr(), scale.data_ptr() if scale is not None else None,
         shift.data_ptr() if shift is not None else None, rptr, rbs, out.data_ptr(), ybs, b, cb * 8,
         cout, h, w, flags, _stream()), "lea_conv2d_bnrelu_bf16")
+    _probe_end(rec)
     return out
 
 

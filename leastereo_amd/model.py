@@ -160,9 +160,12 @@ class NewMatching(_ExecutorCache, nn.Module):
     _executor_cls = "MatchingExecutor"
 
     def set_precision(self, precision: str):
-        if precision not in ("f32", "bf16"):
-            raise ValueError(f"precision must be 'f32' or 'bf16', got {precision!r}")
-        cls = "MatchingExecutorBF16" if precision == "bf16" else "MatchingExecutor"
+        """"f32", "bf16", or "f32_direct" (f32 on the direct-conv engine over the
+        in-place cost volume: an independent algorithm, bench.py's per-pair check)."""
+        cls = {"f32": "MatchingExecutor", "bf16": "MatchingExecutorBF16",
+               "f32_direct": "MatchingExecutorDirect"}.get(precision)
+        if cls is None:
+            raise ValueError(f"precision must be 'f32', 'bf16' or 'f32_direct', got {precision!r}")
         if cls != self._executor_cls:
             self._executor_cls = cls
             self.invalidate()
@@ -238,6 +241,13 @@ class LEAStereo(nn.Module):
         # cost volume (:34-48) + matching (:50): stem0 reads the volume in place
         cost = self.matching.executor().run_features(fx, fy, self.maxdisp)
         return self.disp(cost, fast_exp=self.precision == "bf16")
+
+    def set_precision(self, precision: str):
+        """Switch the arithmetic ("f32" / "bf16" / "f32_direct"); weights are re-packed
+        on the next forward."""
+        self.matching.set_precision(precision)
+        self.feature.set_precision(precision)
+        self.precision = precision
 
     def graphed(self, batch: int, height: int, width: int):
         """``forward`` for one input shape captured into a HIP graph (SURVEY.md §7:

@@ -150,18 +150,58 @@ def test_bf16_e2e_vs_reference_fixture():
     assert ref.epe(d, torch.from_numpy(golden("e2e")["b1_h96_w192_md48/disp32"])) < 0.25
 
 
-def test_bf16_full_size_vs_f32_and_batch_invariance():
-    """576x960 D192, batch 2: bf16 vs the f32 HIP path (measured r01: 0.48 px EPE),
-    and the batch of 2 equals two single runs bit for bit."""
-    from tests.golden_util import normal
-    mb, mf = _model(192, "bf16"), _model(192, "f32")
-    left = normal(21, (2, 3, 576, 960)).to(DEV)
-    right = normal(22, (2, 3, 576, 960)).to(DEV)
+def _bf16_noise(cfg):
+    """The reference network's own bf16 noise figure at this config (EPE px per pair,
+    tests/golden/bf16_noise.json, made by tools/gen_bf16_noise.py)."""
+    import json
+    import os
+    from tests.golden_util import GOLD
+    with open(os.path.join(GOLD, "bf16_noise.json")) as f:
+        c = json.load(f)["cases"][cfg]
+    return c, sum(c["epe_px"]) / len(c["epe_px"])
+
+
+# HIP bf16 may be at most this factor noisier than the reference network run in bf16
+# (its f32 accumulation and f32 BN epilogue make it the less noisy of the two in practice)
+BF16_NOISE_FACTOR = 1.5
+
+
+def _record(name, values):
+    """Measured EPEs land in gpurun_out/ when the suite runs on the GPU box."""
+    import json
+    import os
+    d = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "gpurun_out")
+    if os.path.isdir(d):
+        with open(os.path.join(d, "bf16_epe.jsonl"), "a") as f:
+            f.write(json.dumps({"test": name, "epe_px": values}) + "\n")
+
+
+@pytest.mark.timeout(900)
+@pytest.mark.parametrize("cfg", ["c3", "c4"])
+def test_bf16_batch8_vs_oracle(cfg):
+    """Configs 3 (KITTI 384x1248 D192, bf16, batch 8) and 4 (576x960 D192, bf16, the
+    8 pairs of one GPU's shard): every pair of the batch vs the f32 CPU oracle
+    (oracle/torch_ref.leastereo_forward), EPE <= 1.5 x the reference network's own
+    bf16 noise figure; the f32 HIP path on the same batch vs the oracle at the f32 bar
+    (1e-3 px); and the batch equals eight single-pair runs bit for bit."""
+    from tests.golden_util import arch, normal, state_dict
+    case, noise = _bf16_noise(cfg)
+    h, w, md, seed = case["height"], case["width"], case["maxdisp"], case["seed"]
+    pairs = [(normal(seed + 2 * i, (1, 3, h, w)), normal(seed + 2 * i + 1, (1, 3, h, w)))
+             for i in range(8)]
+    left = torch.cat([p[0] for p in pairs]).to(DEV)
+    right = torch.cat([p[1] for p in pairs]).to(DEV)
+    mb, mf = _model(md, "bf16"), _model(md, "f32")
     with torch.no_grad():
-        db, df = mb(left, right), mf(left, right)
-        one = torch.cat([mb(left[i:i + 1], right[i:i + 1]) for i in range(2)])
+        db, df = mb(left, right).cpu(), mf(left, right).cpu()
+        one = torch.cat([mb(left[i:i + 1], right[i:i + 1]) for i in range(8)]).cpu()
+        want = torch.cat([ref.leastereo_forward(state_dict(), l, r, md, arch()) for l, r in pairs])
     assert torch.equal(db, one)
-    assert ref.epe(db.cpu(), df.cpu()) < 1.0
+    e_bf = [ref.epe(db[i], want[i]) for i in range(8)]
+    e_f32 = [ref.epe(df[i], want[i]) for i in range(8)]
+    _record(f"bf16_batch8_vs_oracle[{cfg}]", {"bf16": e_bf, "f32": e_f32, "noise": noise})
+    assert max(e_f32) < 1e-3, e_f32
+    assert max(e_bf) <= BF16_NOISE_FACTOR * noise, (e_bf, noise)
 
 
 def test_conv2d_bf16_vs_torch():

@@ -541,3 +541,9 @@ def test_fused_feature_stems_vs_torch(c8):
     one = kernels.feature_stem(x[:1].to(DEV), w0.to(DEV), s0.to(DEV), t0.to(DEV), w1.to(DEV), s1.to(DEV),
                                t1.to(DEV), c8, x2[1:].to(DEV))
     assert torch.equal(one, cat[[0, 3]])
+    # a non-contiguous right image (a transposed view of the same values) on that path
+    x2_nc = x2[1:].to(DEV).transpose(2, 3).contiguous().transpose(2, 3)
+    assert not x2_nc.is_contiguous()
+    one_nc = kernels.feature_stem(x[:1].to(DEV), w0.to(DEV), s0.to(DEV), t0.to(DEV), w1.to(DEV),
+                                  s1.to(DEV), t1.to(DEV), c8, x2_nc)
+    assert torch.equal(one_nc, cat[[0, 3]])

@@ -61,3 +61,57 @@ def test_single_process_defaults():
     x = torch.ones(3)
     assert parallel.gather_per_pair(x) is x
     assert not dist.is_initialized()
+
+
+# ---- bench.py's own launcher (the entry the driver and users start) ----
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _bench(*argv, env_extra=None, timeout=240):
+    import subprocess
+    import sys
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT")}
+    env.update(env_extra or {})
+    return subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), *argv], env=env,
+                          capture_output=True, text=True, timeout=timeout, cwd=REPO)
+
+
+@pytest.mark.parametrize("world,batch", [(2, 4), (3, 2)])
+def test_bench_launcher_spawns_ranks_and_gathers(world, batch):
+    """``python bench.py --gpus N`` (no torchrun env) starts N ranks itself; every rank
+    takes its contiguous shard of world*batch pairs and rank 0 prints the gathered
+    per-pair vector in rank order (stub step: no GPU, gloo)."""
+    import json
+    r = _bench("--gpus", str(world), "--batch", str(batch), "--steps", "3", "--stub", "1")
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout  # rank 0 only
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == world and d["stub"]
+    assert d["shards"] == [[k * batch, (k + 1) * batch] for k in range(world)]
+    assert d["pair_epe_px"]["per_pair"] == pytest.approx([i * 1e-3 for i in range(world * batch)])
+
+
+def test_bench_refuses_world_size_mismatch():
+    """A rank whose launcher started a different world than --gpus says exits non-zero."""
+    r = _bench("--gpus", "2", "--stub", "1", "--steps", "1",
+               env_extra={"WORLD_SIZE": "1", "RANK": "0", "LOCAL_RANK": "0"})
+    assert r.returncode == 2
+    assert "--gpus 2" in r.stderr
+
+
+def test_bench_parse_presets():
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("bench_mod", os.path.join(REPO, "bench.py"))
+    bench = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bench)
+    a = bench.parse(["--config", "c4"])
+    assert (a.height, a.width, a.maxdisp, a.batch, a.precision) == (576, 960, 192, 8, "bf16")
+    assert bench.config_name(a) == "c4"
+    a = bench.parse([])
+    assert bench.config_name(a) == "c2" and a.gpus == 1
+    # host core accounting is self-consistent
+    h = bench.host_cores()
+    assert 1 <= h["threads"] <= h["logical_cpus_in_affinity"]
+    assert h["physical_cores_in_affinity"] <= h["logical_cpus_in_affinity"]
