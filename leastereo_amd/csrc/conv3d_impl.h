@@ -75,6 +75,7 @@ struct ConvArgs {
   int ntiles, ndz, nblk;   // DMA engine's 1-D grid: tiles x depth groups x (B * ncob)
   unsigned flags;
   int spw;                 // W x D Winograd engine: depth pairs walked per workgroup (0 = 1)
+  unsigned* dbg;           // diagnostic builds only (LEA_EXP_STAMPS): per-wave phase cycles
 };
 
 // KD = kernel depth: KS for the 3D convs, 1 for the feature net's 2D 3x3 convs

@@ -105,6 +105,29 @@ __device__ __forceinline__ void aw4(const float a0, const float a1, const float 
   y[3] = fmaf(8.f, tm, sm) + a5;
 }
 
+// Diagnostic build (-DLEA_EXP_STAMPS, tools/build_variants.sh): s_memtime stamps around
+// the loop's phases, per-wave cycle sums stored to ConvArgs::dbg (never in the real kernel)
+#ifdef LEA_EXP_STAMPS
+constexpr int kStampPhases = 8;  // dma wait, barrier 1, dma issue, V pass, barrier 2, steps, epilogue, total
+__device__ __forceinline__ unsigned long long stamp() {
+  unsigned long long t;
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+  __builtin_amdgcn_sched_barrier(0);
+  return t;
+}
+#define LEA_STAMP(k)                  \
+  do {                                \
+    const unsigned long long t_ = stamp(); \
+    st_sum[k] += t_ - st_prev;        \
+    st_prev = t_;                     \
+  } while (0)
+#else
+#define LEA_STAMP(k) \
+  do {               \
+  } while (0)
+#endif
+
 template <int Q, int WC, int MTE, int NW, int OCC, bool PV, bool CV>
 __global__ __launch_bounds__(NW * 64, OCC) void conv3d_wino2_kernel(const ConvArgs a) {
   using C = Cfg2<Q, WC, MTE, NW, OCC, PV>;
@@ -377,12 +400,21 @@ __global__ __launch_bounds__(NW * 64, OCC) void conv3d_wino2_kernel(const ConvAr
       }
   };
 
+#ifdef LEA_EXP_STAMPS
+  unsigned long long st_sum[kStampPhases] = {};
+  unsigned long long st_prev = stamp();
+  const unsigned long long st_begin = st_prev;
+#endif
   issue(0, smem);
+  LEA_STAMP(2);
   for (int it = 0; it < nitems; ++it) {
     const int ch = it % nchunks;
     wait_item<NST>(ebuf && ch == 0 && it > 0);  // this wave's pieces of item it landed
+    LEA_STAMP(0);
     __syncthreads();  // ... and everyone's; item it-1's stage is free
+    LEA_STAMP(1);
     if (it + 1 < nitems) issue(it + 1, smem + ((it + 1) & 1) * C::STAGE);
+    LEA_STAMP(2);
     const float* xs = smem + (it & 1) * C::STAGE;
     const float* ws = xs + C::XS;
     if constexpr (PV) {
@@ -418,7 +450,9 @@ __global__ __launch_bounds__(NW * 64, OCC) void conv3d_wino2_kernel(const ConvAr
 #pragma unroll
         for (int k = 0; k < 6; ++k) tp[k] = make_float4(vf[4 * k], vf[4 * k + 1], vf[4 * k + 2], vf[4 * k + 3]);
       }
+      LEA_STAMP(3);
       __syncthreads();
+      LEA_STAMP(4);
     }
     // one kh step: the inputs (4 planes x 6 staged values as float2s, or the 24
     // pre-transformed V as float4s) and the 9 g values (kd, kw) per cout tile
@@ -512,6 +546,7 @@ __global__ __launch_bounds__(NW * 64, OCC) void conv3d_wino2_kernel(const ConvAr
     xform(raw[0], xf[0]);
     mfmas(xf[1]);
     mfmas(xf[0]);
+    LEA_STAMP(5);
     if (ch == nchunks - 1) {  // the pair's last chunk: its epilogue, fresh accumulators
       if (ebuf)
         epilogue_buf((pz0 + it / nchunks) * C::TD);
@@ -523,13 +558,43 @@ __global__ __launch_bounds__(NW * 64, OCC) void conv3d_wino2_kernel(const ConvAr
         for (int e = 0; e < NE; ++e)
 #pragma unroll
           for (int m = 0; m < MTE; ++m) acc[x][e][m] = f32x4{0.f, 0.f, 0.f, 0.f};
+      LEA_STAMP(6);
     }
   }
+#ifdef LEA_EXP_STAMPS
+  st_sum[7] = stamp() - st_begin;
+  if (a.dbg) {  // lane k < 8 stores phase k of this wave (a lane-indexed vector store)
+    unsigned v = 0;
+#pragma unroll
+    for (int k = 0; k < kStampPhases; ++k)
+      if (lane == k) v = (unsigned)st_sum[k];
+    if (lane < kStampPhases) a.dbg[((long long)blockIdx.x * NW + wave) * kStampPhases + lane] = v;
+  }
+#endif
 }
+
+#ifdef LEA_EXP_STAMPS
+unsigned* g_dbg = nullptr;
+}  // namespace wino
+}  // namespace lea
+// diagnostic export (not in the public headers): the per-wave phase buffer of the next
+// W x D launches, nblk * NW * 8 u32 (nullptr = off)
+extern "C" int lea_exp_wino2_stamps(void* buf) {
+  lea::wino::g_dbg = (unsigned*)buf;
+  return 0;
+}
+namespace lea {
+namespace wino {
+#endif
 
 thread_local char g_name2[96];
 
 
+#ifdef LEA_EXP_STAMPS
+#define LEA_WINO2_DBG a.dbg = g_dbg;
+#else
+#define LEA_WINO2_DBG
+#endif
 #define LEA_WINO2_CASE(Q, WC, MTE, NW, OCC, PV, CV)                                                \
   if (p.q == Q && p.wc == WC && p.mte == MTE && p.nw == NW && p.occ == OCC && p.pv == PV) {        \
     using C_ = Cfg2<Q, WC, MTE, NW, OCC, PV>;                                                      \
@@ -541,6 +606,7 @@ thread_local char g_name2[96];
     const long long n_ = (long long)a.ntiles * ((a.ndz + a.spw - 1) / a.spw) * B * a.ncob;         \
     LEA_CHECK_ARG(n_ < (1LL << 31), "lea_conv3d(wino2): grid too large");                          \
     a.nblk = (int)n_;                                                                              \
+    LEA_WINO2_DBG                                                                                  \
     conv3d_wino2_kernel<Q, WC, MTE, NW, OCC, PV, CV><<<dim3((unsigned)n_), NW * 64, 0, st>>>(a);   \
     return launch_status("lea_conv3d(wino2)");                                                    \
   }
