@@ -8,8 +8,14 @@ Restates the host-side steps around ``LEAStereo.forward`` (predict.py:144-243):
                        (``lea_standardize_crop_u8``; numpy checker: oracle/predict_ref.py)
   * ``crop_output``    predict.py:236-239  undo the padding on the disparity
   * ``read_pfm``       dataloaders/datasets/common.py:8-40
-  * ``main``           predict.py:249-286  the list-file loop (SceneFlow naming)
-Arithmetic runs on the HIP kernels; what stays on the host is file I/O (PIL, PFM).
+  * ``plot_disparity`` predict.py:246-247  turbo-coloured PNG, vmin 0, vmax 192
+  * ``save_float_png`` / ``crop_image``  predict.py:128-141,207-211  the satellite
+                       branch's skimage.io.imsave of float arrays (imageio's min-max
+                       8-bit conversion, restated: skimage / imageio are absent here)
+  * ``main``           predict.py:249-286  the list-file loop: --sceneflow writes
+                       {index}.png and {index}_gt.png (and {index}.npy, the raw
+                       disparity), --satellite writes {name}.png and {name}_in.png
+Arithmetic runs on the HIP kernels; what stays on the host is file I/O (PIL, PFM, PNG).
 
     python predict.py --sceneflow=1 --maxdisp=192 --crop_height=576 --crop_width=960 \
         --data_path=./dataset/SceneFlow/ --test_list=./lists/sceneflow_test.list \
@@ -85,6 +91,72 @@ def predict_pair(model, leftname, rightname, crop_height, crop_width, device="cu
     return crop_output(pred.cpu().numpy(), h, w, crop_height, crop_width)
 
 
+def plot_disparity(savename, data, max_disp=192):
+    """predict.py:246-247: ``plt.imsave(savename, data, vmin=0, vmax=max_disp, cmap='turbo')``."""
+    import matplotlib
+    matplotlib.use("Agg")
+    import matplotlib.pyplot as plt
+    plt.imsave(savename, data, vmin=0, vmax=max_disp, cmap="turbo")
+
+
+def float_to_u8(img: np.ndarray) -> np.ndarray:
+    """What skimage.io.imsave (predict.py:207,211) writes for a float array: its imageio
+    plugin's ``image_as_uint(im, bitdepth=8)`` -- values already in [0, 1] scale by 255,
+    anything else is min-max normalised first -- ``* 255 + 0.499999999`` then truncated
+    (imageio 2.x, a third-party dependency absent here; restated from its source)."""
+    im = np.asarray(img, dtype=np.float64)
+    mi, ma = float(np.nanmin(im)), float(np.nanmax(im))
+    if not (mi >= 0 and ma <= 1):
+        if not (np.isfinite(mi) and np.isfinite(ma)):
+            raise ValueError("image values are not finite")
+        if ma == mi:  # imageio returns the values cast as they are
+            return im.astype(np.uint8)
+        im = (im - mi) / (ma - mi)
+    return (im * 255.0 + 0.499999999).astype(np.uint8)
+
+
+def save_float_png(savename, img):
+    """skimage.io.imsave(savename, img) of predict.py:207,211 (PNG)."""
+    from PIL import Image
+    a = np.asarray(img)
+    if a.dtype != np.uint8:
+        a = float_to_u8(a)
+    Image.fromarray(a).save(savename)
+
+
+def crop_image(image, crop_height, crop_width):
+    """predict.py:128-141: zero-pad the HWC image into the bottom-right of the crop
+    (float32 result) when it fits, else centre-crop (its own dtype)."""
+    data = np.moveaxis(np.asarray(image), [2], [0])
+    n_layers, h, w = data.shape
+    if h <= crop_height and w <= crop_width:
+        result = np.zeros([n_layers, crop_height, crop_width], "float32")
+        result[:, crop_height - h: crop_height, crop_width - w: crop_width] = data
+    else:
+        start_x = (w - crop_width) // 2
+        start_y = (h - crop_height) // 2
+        result = data[:, start_y: start_y + crop_height, start_x: start_x + crop_width]
+    return np.moveaxis(result, [0], [2])
+
+
+def satellite_names(data_path, save_path, line):
+    """predict.py:258-263: the list line minus its last character names a directory
+    holding satiml.png / satimr.png; outputs <save_path><name>.png and <name>_in.png."""
+    cur = line[:-1]
+    return (data_path + cur + "/satiml.png", data_path + cur + "/satimr.png",
+            save_path + cur + ".png", save_path + cur + "_in.png")
+
+
+def test_satellite(model, leftname, rightname, savename, in_savename, crop_height, crop_width):
+    """predict.py:187-211: the disparity as a PNG (min-max 8-bit, as skimage writes a
+    float image) and the left input cropped / padded to the crop."""
+    from PIL import Image
+    disp = predict_pair(model, leftname, rightname, crop_height, crop_width)
+    save_float_png(savename, disp)
+    save_float_png(in_savename, crop_image(Image.open(leftname), crop_height, crop_width))
+    return disp
+
+
 def load_checkpoint(model, path):
     """predict.py:52-67: checkpoint['state_dict'] with an optional 'module.' prefix,
     loaded with a loader that executes nothing from the file."""
@@ -119,16 +191,27 @@ def main(argv=None):
     os.makedirs(opt.save_path, exist_ok=True)
     with open(opt.test_list) as f:
         lines = f.readlines()
+    if not (opt.sceneflow or opt.satellite):
+        raise NotImplementedError("predict.py has list layouts for --sceneflow and --satellite only "
+                                  "(the reference's other dataset flags write nothing)")
     for index, line in enumerate(lines):
+        if opt.satellite:  # predict.py:258-264
+            test_satellite(model, *satellite_names(opt.data_path, opt.save_path, line),
+                           opt.crop_height, opt.crop_width)
         if not opt.sceneflow:
-            raise NotImplementedError("only the --sceneflow list layout is restated")
+            continue
+        print(f"Running for sceneflow {index}")
         leftname, rightname, gtname = sceneflow_names(opt.data_path, line)
+        gt = None
+        if os.path.isfile(gtname):  # predict.py:275-277 (the reference requires it)
+            gt, _, _ = read_pfm(gtname)
+            plot_disparity(opt.save_path + f"{index:d}_gt.png", gt, 192)
         t0 = time.time()
         disp = predict_pair(model, leftname, rightname, opt.crop_height, opt.crop_width)
         print(f"Processing time: {time.time() - t0:.4f}")
+        plot_disparity(opt.save_path + f"{index:d}.png", disp, 192)  # predict.py:240
         np.save(os.path.join(opt.save_path, f"{index}.npy"), disp.astype(np.float32))
-        if os.path.isfile(gtname):
-            gt, _, _ = read_pfm(gtname)
+        if gt is not None:
             ch, cw = disp.shape
             h, w = gt.shape
             y0, x0 = max(int((h - ch) / 2), 0), max(int((w - cw) / 2), 0)

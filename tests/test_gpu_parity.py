@@ -433,6 +433,38 @@ def test_predict_cli_runs_on_a_list(tmp_path):
     assert rc == 0
     out = np.load(tmp_path / "out" / "0.npy")
     assert out.shape == (96, 192) and np.isfinite(out).all()
+    # the reference's turbo PNG of the prediction (predict.py:240,246-247)
+    png = np.asarray(Image.open(tmp_path / "out" / "0.png"))
+    assert png.shape[:2] == (96, 192)
+
+
+def test_predict_cli_satellite_branch(tmp_path):
+    """predict.py's --satellite loop (predict.py:187-211,258-264): <name>.png holds the
+    disparity as skimage writes a float image, <name>_in.png the cropped left input."""
+    from PIL import Image
+    from leastereo_amd import predict as P
+    g = golden("c1_sceneflow")
+    d = tmp_path / "sat" / "tile_01"
+    d.mkdir(parents=True)
+    Image.fromarray(g["left_u8"][:90, :180]).save(d / "satiml.png")
+    Image.fromarray(g["right_u8"][:90, :180]).save(d / "satimr.png")
+    (tmp_path / "list.txt").write_text("tile_01\n")
+    out = tmp_path / "out"
+    out.mkdir()
+    torch.save({"state_dict": state_dict()}, tmp_path / "ckpt.pth")
+    rc = P.main(["--satellite=1", "--maxdisp=48", "--crop_height=96", "--crop_width=192",
+                 f"--data_path={tmp_path}/sat/", f"--test_list={tmp_path}/list.txt",
+                 f"--save_path={out}/", f"--resume={tmp_path}/ckpt.pth"])
+    assert rc == 0
+    m = _model(48)
+    left, right, h, w = P.load_transform(*P.load_images(d / "satiml.png", d / "satimr.png"), 96, 192)
+    with torch.no_grad():
+        disp = P.crop_output(m(left, right).cpu().numpy(), h, w, 96, 192)
+    assert disp.shape == (90, 180)
+    np.testing.assert_array_equal(np.asarray(Image.open(out / "tile_01.png")), P.float_to_u8(disp))
+    inp = np.asarray(Image.open(out / "tile_01_in.png"))
+    assert inp.shape == (96, 192, 3)
+    np.testing.assert_array_equal(inp, P.float_to_u8(P.crop_image(g["left_u8"][:90, :180], 96, 192)))
 
 
 def test_batch_rows_are_independent():

@@ -78,3 +78,41 @@ def test_c1_oracle_matches_reference_disparity():
         d = ref.leastereo_forward(state_dict(), left, right, c["maxdisp"], arch())
     disp = P.crop_output(d.numpy(), *c["full_hw"], *c["crop_hw"])
     assert ref.epe(torch.from_numpy(disp), torch.from_numpy(golden("c1_sceneflow")["disp"])) < 1e-3
+
+
+def test_float_png_conversion_is_imageios():
+    """skimage.io.imsave of a float image (predict.py:207,211) through imageio's 8-bit
+    conversion (restated; parity unpinned -- neither library is importable here)."""
+    a = np.array([[0.0, 0.5], [1.0, 0.25]], np.float32)          # already in [0, 1]
+    np.testing.assert_array_equal(P.float_to_u8(a), [[0, 127], [255, 64]])
+    d = np.array([[10.0, 20.0], [30.0, 50.0]], np.float32)      # min-max normalised
+    np.testing.assert_array_equal(P.float_to_u8(d), [[0, 64], [127, 255]])
+    assert P.float_to_u8(np.full((2, 2), 7.0)).tolist() == [[7, 7], [7, 7]]
+
+
+def test_crop_image_pads_bottom_right_or_centre_crops():
+    img = (np.arange(5 * 7 * 3) % 251).astype(np.uint8).reshape(5, 7, 3)
+    pad = P.crop_image(img, 8, 12)
+    assert pad.shape == (8, 12, 3) and pad.dtype == np.float32
+    np.testing.assert_array_equal(pad[3:, 5:], img)
+    assert pad[:3].sum() == 0 and pad[:, :5].sum() == 0
+    crop = P.crop_image(img, 3, 4)
+    assert crop.dtype == np.uint8
+    np.testing.assert_array_equal(crop, img[1:4, 1:5])
+
+
+def test_satellite_and_plot_outputs(tmp_path):
+    l, r, s, i = P.satellite_names("/d/", "/o/", "tile_07\n")
+    assert (l, r, s, i) == ("/d/tile_07/satiml.png", "/d/tile_07/satimr.png", "/o/tile_07.png",
+                            "/o/tile_07_in.png")
+    from PIL import Image
+    disp = np.linspace(0, 200, 12 * 16, dtype=np.float32).reshape(12, 16)
+    P.plot_disparity(str(tmp_path / "d.png"), disp, 192)
+    png = np.asarray(Image.open(tmp_path / "d.png"))
+    assert png.shape[:2] == (12, 16)
+    import matplotlib
+    want = (matplotlib.colormaps["turbo"](np.clip(disp / 192, 0, 1)) * 255).round().astype(np.uint8)
+    assert np.abs(png[..., :3].astype(int) - want[..., :3]).max() <= 1
+    P.save_float_png(str(tmp_path / "f.png"), disp)
+    got = np.asarray(Image.open(tmp_path / "f.png"))
+    np.testing.assert_array_equal(got, P.float_to_u8(disp))
