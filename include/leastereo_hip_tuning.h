@@ -51,14 +51,19 @@ int lea_conv3d_wino_set_tile_override(int np, int td, int f);
 
 /* Engine variant for the Winograd entries (same packed weights): 0 = the planner's
  * choice, 1 = F(4,3) along W only, 2..4 = F(4,3) along W x F(2,3) along D
- * (csrc/conv3d_wino2.hip: "conv3d_wino2_kernel<Q, WC, MTE, NW, OCC, PV, CV>") where the
- * cout block allows it (16 or 32 couts per block): 2 = four waves of one 16-row
+ * (csrc/conv3d_wino2.hip: "conv3d_wino2_kernel<Q, WC, MTE, NW, OCC, PV, CV>", PV 0 = per-lane V, 1/2 =
+ * transform pass) where the cout block allows it (16 or 32 couts per block): 2 = four waves of one 16-row
  * cout tile, 3 = eight waves, 4 = two cout tiles per wave at one wave per SIMD. */
 int lea_conv3d_wino_set_variant(int variant);
 
 /* Depth pairs each W x D engine workgroup walks (its items = pairs x 4-channel chunks
  * through one DMA pipeline); 0 restores the planner. */
 int lea_conv3d_wino2_set_walk(int spw);
+
+/* 1 (default) = the W x D engine's transform-pass tiles stage their halo as 16-byte
+ * LDS-DMA pieces where rows are whole 16-byte blocks (W % 4 == 0, aligned sources;
+ * kernel name "..., 2, false>"), 0 = dword pieces ("..., 1, false>"). */
+int lea_conv3d_wino2_set_halo16(int on);
 
 /* 1 (default) = the Winograd engines' buffer-addressed epilogue where the shape allows
  * it (W % 4 == 0, 16-B aligned output / residual; residual loads issued together, the

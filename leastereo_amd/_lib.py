@@ -87,6 +87,7 @@ SIGNATURES = {
     "lea_conv3d_wino_set_tile_override": (_i, [_i, _i, _i]),
     "lea_conv3d_wino_set_variant": (_i, [_i]),
     "lea_conv3d_wino2_set_walk": (_i, [_i]),
+    "lea_conv3d_wino2_set_halo16": (_i, [_i]),
     "lea_conv3d_wino_set_epi_buf": (_i, [_i]),
     "lea_conv3d_set_rs_gather": (_i, [_i]),
     "lea_conv3d_bf16_set_stream1x1": (_i, [_i]),
@@ -136,6 +137,7 @@ def load():
 # A/B switches for the planners' tuning hooks (include/leastereo_hip_tuning.h; process-wide
 # in the library), e.g. LEASTEREO_WINO2_WALK=1 to disable the depth walk
 TUNING_ENV = {"LEASTEREO_WINO2_WALK": "lea_conv3d_wino2_set_walk",
+              "LEASTEREO_HALO16": "lea_conv3d_wino2_set_halo16",
               "LEASTEREO_EPI_BUF": "lea_conv3d_wino_set_epi_buf",
               "LEASTEREO_RS_GATHER": "lea_conv3d_set_rs_gather",
               "LEASTEREO_BF16_1X1": "lea_conv3d_bf16_set_stream1x1",

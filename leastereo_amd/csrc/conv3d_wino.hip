@@ -562,6 +562,7 @@ int g_small16 = 0;
 // as 32-row blocks of the W x D engine, the last one padded (0)
 int g_block48 = 1;
 int g_epibuf = 1;  // lea_conv3d_wino_set_epi_buf
+int g_halo16 = 1;  // lea_conv3d_wino2_set_halo16
 inline int host_mt(int cout) {
   if (g_small16 && cout <= 8) return 1;
   const int mt = mt_of(cout);
@@ -571,10 +572,10 @@ inline int host_mt(int cout) {
 // W x D engine tile for variant v (2..4), or nullptr-equivalent (q = 0) when the
 // layer's cout block has no such tile (couts <= 8 and the 48-row blocks stay 1-D)
 inline Plan2 plan2(int v, int mt, int q) {
-  Plan2 t{0, 0, 0, 0, 0, false, 0};
+  Plan2 t{0, 0, 0, 0, 0, 0, 0};
   if (mt != 1 && mt != 2) return t;
   if (v >= 5) {
-    t.pv = mt == 2;
+    t.pv = mt == 2 ? 1 : 0;
     v -= 3;
   }
   t.q = q;
@@ -644,6 +645,20 @@ inline Plan make_plan(int B, int cout, int D, int H, int W) {
   return p;
 }
 
+// The W x D transform-pass kernel stages its halo as 16-byte LDS-DMA pieces (PV = 2, 4
+// pieces per channel instead of 13 dword pieces) when rows are whole 16-byte blocks:
+// W % 4 == 0 and 16-byte aligned channel bases (r03 stamps: the DMA issue held 25-27 %
+// of the kernel's wave cycles with dword pieces).  Plain volumes only (not the cost volume).
+inline void plan_halo16(Plan& p, bool cv, int W, const ConvArgs* a) {
+  if (!p.d2 || p.p2.pv != 1 || p.p2.nw != 4 || p.p2.mte != 1 || cv || !g_halo16 || W % 4 != 0) return;
+  if (a) {
+    const bool al = ((uintptr_t)a->x & 15) == 0 && a->xbs % 4 == 0 &&
+                    (a->cin1 == a->cin || (((uintptr_t)a->x2 & 15) == 0 && a->x2bs % 4 == 0));
+    if (!al) return;
+  }
+  p.p2.pv = 2;
+}
+
 #define LEA_WINO_CASE(F, Q, MT, NP, TD, CV)                                                   \
   if (p.f == F && p.q == Q && p.mt == MT && p.np == NP && p.td == TD) {                       \
     using C_ = Cfg<F, Q, MT, NP, TD>;                                                         \
@@ -706,7 +721,8 @@ int common(ConvArgs& a, int B, bool cv, int dtype, void* stream) {
     set_error("lea_conv3d(wino): dtype %d unsupported", dtype);
     return LEA_E_UNSUPPORTED;
   }
-  const Plan p = make_plan(B, a.cout, a.D, a.H, a.W);
+  Plan p = make_plan(B, a.cout, a.D, a.H, a.W);
+  plan_halo16(p, cv, a.W, &a);
   if (g_epibuf && epi_buf_ok(a)) a.flags |= kEpiBuf;
   return run(p, a, B, as_stream(stream), cv);
 }
@@ -743,7 +759,9 @@ extern "C" int lea_conv3d_wino_pack_weights(const float* w, float* packed, int c
 
 extern "C" const char* lea_conv3d_wino_kernel_name(int B, int cout, int D, int H, int W, int costvolume) {
   if (B <= 0 || cout <= 0 || D <= 0 || H <= 0 || W <= 0) return nullptr;
-  return wino::name(wino::make_plan(B, cout, D, H, W), costvolume != 0);
+  wino::Plan p = wino::make_plan(B, cout, D, H, W);
+  wino::plan_halo16(p, costvolume != 0, W, nullptr);  // (assumes 16-byte aligned sources)
+  return wino::name(p, costvolume != 0);
 }
 
 extern "C" int lea_conv3d_wino_set_tile_override(int np, int td, int f) {
@@ -778,6 +796,13 @@ extern "C" int lea_conv3d_wino_set_small_cout(int mode) {
   clear_error();
   LEA_CHECK_ARG(mode == 0 || mode == 1, "lea_conv3d_wino_set_small_cout: mode=%d", mode);
   wino::g_small16 = mode;
+  return 0;
+}
+
+extern "C" int lea_conv3d_wino2_set_halo16(int on) {
+  clear_error();
+  LEA_CHECK_ARG(on == 0 || on == 1, "lea_conv3d_wino2_set_halo16: on=%d", on);
+  wino::g_halo16 = on;
   return 0;
 }
 

@@ -30,7 +30,7 @@
 namespace lea {
 namespace wino {
 
-template <int Q, int WC, int MTE, int NW, int OCC, bool PV>
+template <int Q, int WC, int MTE, int NW, int OCC, int PV>
 struct Cfg2 {
   static constexpr int F = 4, NX = 6, NE = 4, TD = 2;
   static constexpr int WR = NW / WC;             // row sets (waves along H)
@@ -46,11 +46,30 @@ struct Cfg2 {
   static constexpr int IMG = PLANES * PLANE;
   static constexpr int XSLOTS = (IMG + 63) / 64;
   // channel stride: for the per-lane V path, the 1-D engine's (the two channels of a
-  // 32-lane ds_read_b64 group on disjoint banks); for PV, = 32 mod 64 dwords, which
+  // 32-lane ds_read_b64 group on disjoint banks); for PV = 1, = 32 mod 64 dwords, which
   // with RW = 34 puts the transform pass's 32-lane reads (8 groups x 2 rows x 2
   // channels, see below) on 64 distinct banks
   static constexpr int CIS = PV ? (64 * XSLOTS + 32) : conflict_free_cis<F, Q>(64 * XSLOTS, RW);
-  static constexpr int XS = CIN_B * CIS;
+  // PV = 2: rows staged as 16-byte blocks from w0 - 4 (RWA = TW + 8 floats: 10 blocks
+  // cover the w0 - 1 .. w0 + TW halo columns), one channel's 4 planes x RH rows
+  // contiguous (BLK16 blocks = PIECES16 LDS-DMA pieces of 64 lanes, the last one
+  // partial); channel c starts at CB2(c) == {1, 3, 33, 35}[c] mod 64 dwords, so column
+  // w0 - 1 sits at an even dword (the pass's ds_read_b64s stay 8-byte aligned) and the
+  // pass's 32 lanes (8 groups x 4 channels of one row) read 64 distinct banks
+  static constexpr int RWA = TW + 8;
+  static constexpr int PLANEA = RH * RWA;
+  static constexpr int IMGA = PLANES * PLANEA;
+  static constexpr int BLK16 = IMGA / 4;
+  static constexpr int PIECES16 = (BLK16 + 63) / 64;
+  static constexpr int cb2(int c) {
+    int base = 1;
+    for (int k = 1; k <= c; ++k) {
+      const int want = (k & 1 ? 2 : 0) + (k & 2 ? 32 : 0) + 1, lo = base + IMGA;
+      base = lo + ((want - lo) % 64 + 64) % 64;
+    }
+    return base;
+  }
+  static constexpr int XS = PV == 2 ? (cb2(CIN_B - 1) + IMGA + 3) / 4 * 4 : CIN_B * CIS;
   static constexpr int WS = 27 * CIN_B * COP;    // g[kd*3+kh][kw][ci][co] of one chunk
   static constexpr int WSLOTS = (WS + 255) / 256;
   static constexpr int STAGE = XS + 256 * WSLOTS;
@@ -62,12 +81,16 @@ struct Cfg2 {
   // mod 8 floats the other 8, a channel stride of 0 mod 64 keeps the channel pairs
   // apart -- conflict-free
   static constexpr int TRS = Q * 24 + 4;         // floats per halo row
-  static constexpr int TCS = (RH * TRS + 63) / 64 * 64;  // floats per channel
+  // floats per channel: 0 mod 64 (PV = 1: the pass's 16-lane b128 writes pair rows,
+  // TRS = 4 mod 8 apart), 4 mod 8 (PV = 2: they pair channels)
+  static constexpr int TCS = PV == 2 ? (RH * TRS + 3) / 8 * 8 + 4 : (RH * TRS + 63) / 64 * 64;
   static constexpr int TS = PV ? CIN_B * TCS : 0;
   static constexpr int NUNIT = CIN_B * RH * Q;   // (channel, row, group) transforms per chunk
   static constexpr int WG_PER_CU = 4 * OCC / NW;
   static_assert(WG_PER_CU >= 1, "occupancy");
   static_assert(XS % 4 == 0 && WS % 4 == 0 && RW % 2 == 0 && PLANE % 2 == 0, "aligned LDS regions");
+  static_assert(PV != 2 || (TW == 32 && NW % PIECES16 == 0 && cb2(1) % 64 == 3 && cb2(2) % 64 == 33 &&
+                            cb2(3) % 64 == 35), "16-byte halo map");
   static_assert((2 * STAGE + TS) * 4 * WG_PER_CU <= 160 * 1024, "double-buffered stages fit the LDS");
 };
 
@@ -128,7 +151,7 @@ __device__ __forceinline__ unsigned long long stamp() {
   } while (0)
 #endif
 
-template <int Q, int WC, int MTE, int NW, int OCC, bool PV, bool CV>
+template <int Q, int WC, int MTE, int NW, int OCC, int PV, bool CV>
 __global__ __launch_bounds__(NW * 64, OCC) void conv3d_wino2_kernel(const ConvArgs a) {
   using C = Cfg2<Q, WC, MTE, NW, OCC, PV>;
   constexpr int F = C::F, NX = C::NX, NE = C::NE;
@@ -196,7 +219,28 @@ __global__ __launch_bounds__(NW * 64, OCC) void conv3d_wino2_kernel(const ConvAr
     if constexpr (CV) wco[t] = wc_;
   }
   unsigned voff[XSLOTS_W], voffr[CV ? XSLOTS_W : 1];
+  // PV = 2: this wave's 16-byte pieces are block slot j16 of every channel it stages
+  constexpr int PIECES16 = C::PIECES16;
+  const int j16 = wave % PIECES16, e16 = 64 * j16 + lane;
+  const bool ok16 = e16 < C::BLK16;  // the last piece is partial (exec-masked)
+  unsigned hwo16 = 0xFFFFFFF0u, voff16 = 0xFFFFFFF0u;
+  int pln16 = -1000;
+  if constexpr (PV == 2) {
+    const int p = e16 / (C::RH * (C::RWA / 4)), r = e16 - p * (C::RH * (C::RWA / 4));
+    const int rr = r / (C::RWA / 4), blk = r - rr * (C::RWA / 4);
+    const int h = h0 + rr - 1, w = w0 - 4 + 4 * blk;  // W % 4 == 0: a block is all in or all out
+    if (ok16 && (unsigned)h < (unsigned)a.H && (unsigned)w < (unsigned)a.W) {
+      hwo16 = (unsigned)(h * a.W + w) * 4u;
+      pln16 = p - 1;
+    }
+  }
   auto set_pair = [&](int d0) {  // DMA offsets of the pair at output planes d0, d0 + 1
+    if constexpr (PV == 2) {
+      const int d = d0 + pln16;
+      voff16 = (hwo16 != 0xFFFFFFF0u && (unsigned)d < (unsigned)a.D) ? hwo16 + (unsigned)d * (unsigned)HW * 4u
+                                                                      : 0xFFFFFFF0u;
+      return;
+    }
 #pragma unroll
     for (int t = 0; t < XSLOTS_W; ++t) {
       const int d = d0 + pln[t];
@@ -224,6 +268,20 @@ __global__ __launch_bounds__(NW * 64, OCC) void conv3d_wino2_kernel(const ConvAr
     }
     const long long cvol = CV ? (long long)HW : (long long)HW * a.D;  // channel stride
     const unsigned crec = CV ? (unsigned)HW * 4u : nrec;
+    if constexpr (PV == 2) {
+      static_assert(!CV || PV != 2, "16-byte halo: plain volumes only");
+#pragma unroll
+      for (int t = 0; t < CIN_B * PIECES16 / NW; ++t) {
+        const int ci = (wave + NW * t) / PIECES16;  // (this wave's slot j16 of channel ci)
+        const int c = ch * CIN_B + ci;
+        const float* base = c < a.cin1 ? a.x + (long long)b * a.xbs + (long long)c * cvol
+                                       : a.x2 + (long long)b * a.x2bs + (long long)(c - a.cin1) * cvol;
+        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)base, 0, crec, 0x00020000);
+        const int cb = ci == 0 ? C::cb2(0) : ci == 1 ? C::cb2(1) : ci == 2 ? C::cb2(2) : C::cb2(3);
+        if (ok16) dma_dwordx4_buf(rs, voff16, lds0 + 4 * (unsigned)(st - smem + cb + j16 * 256));
+      }
+      return;
+    }
 #pragma unroll
     for (int ci = 0; ci < CIN_B; ++ci) {
       const int c = ch * CIN_B + ci;
@@ -420,18 +478,32 @@ __global__ __launch_bounds__(NW * 64, OCC) void conv3d_wino2_kernel(const ConvAr
     if constexpr (PV) {
       // the workgroup transforms the chunk's halo once: unit (ci, row, group) reads
       // 4 planes x 6 inputs and writes its 24 V values
-      static_assert(!PV || (C::RW % 64 == 34 && C::CIS % 64 == 32 && C::RH % 2 == 0 && Q == 8),
+      static_assert(PV == 2 || (C::RW % 64 == 34 && C::CIS % 64 == 32 && C::RH % 2 == 0 && Q == 8),
                     "transform pass bank map");
+      static_assert(PV != 2 || (Q == 8 && CIN_B == 4), "transform pass bank map (16-byte halo)");
       for (int u = tid; u < C::NUNIT; u += NW * 64) {
-        // 32 consecutive units = 8 groups x 2 rows x 2 channels: the b64 reads' dword
-        // offsets 4 g + {0, RW, CIS, RW + CIS} cover the 64 banks once
-        const int g = u % Q, t = u / Q;
-        const int rl = t & 1, cl = (t >> 1) & 1, t2 = t >> 2;
-        const int r = 2 * (t2 % (C::RH / 2)) + rl, c = 2 * (t2 / (C::RH / 2)) + cl;
+        // PV = 1: 32 consecutive units = 8 groups x 2 rows x 2 channels: the b64 reads'
+        // dword offsets 4 g + {0, RW, CIS, RW + CIS} cover the 64 banks once.
+        // PV = 2: 8 groups x 4 channels of one row: 4 g + CB2(c) + 3 covers them (Cfg2)
+        int g, r, c, xo;
+        if constexpr (PV == 2) {
+          g = u % Q;
+          c = (u / Q) % CIN_B;
+          r = u / (Q * CIN_B);
+          const int cb = c == 0 ? C::cb2(0) : c == 1 ? C::cb2(1) : c == 2 ? C::cb2(2) : C::cb2(3);
+          xo = cb + r * C::RWA + 3 + F * g;
+        } else {
+          g = u % Q;
+          const int t = u / Q;
+          const int rl = t & 1, cl = (t >> 1) & 1, t2 = t >> 2;
+          r = 2 * (t2 % (C::RH / 2)) + rl;
+          c = 2 * (t2 / (C::RH / 2)) + cl;
+          xo = c * C::CIS + r * C::RW + F * g;
+        }
         float bw[C::PLANES][NX];
 #pragma unroll
         for (int pl = 0; pl < C::PLANES; ++pl) {
-          const float* sp = xs + c * C::CIS + pl * C::PLANE + r * C::RW + F * g;
+          const float* sp = xs + xo + pl * (PV == 2 ? C::PLANEA : C::PLANE);
           const float2 a0 = *reinterpret_cast<const float2*>(sp);
           const float2 a1 = *reinterpret_cast<const float2*>(sp + 2);
           const float2 a2 = *reinterpret_cast<const float2*>(sp + 4);
@@ -611,26 +683,27 @@ thread_local char g_name2[96];
     return launch_status("lea_conv3d(wino2)");                                                    \
   }
 #define LEA_WINO2_TILES(CV)                                                                        \
-  LEA_WINO2_CASE(8, 1, 1, 4, 2, false, CV) LEA_WINO2_CASE(8, 2, 1, 4, 2, false, CV)                \
-  LEA_WINO2_CASE(8, 2, 1, 8, 2, false, CV) LEA_WINO2_CASE(8, 1, 2, 4, 1, false, CV)                \
-  LEA_WINO2_CASE(16, 1, 1, 4, 2, false, CV) LEA_WINO2_CASE(16, 2, 1, 8, 2, false, CV)              \
-  LEA_WINO2_CASE(16, 1, 2, 4, 1, false, CV) LEA_WINO2_CASE(8, 2, 1, 4, 2, true, CV)                \
-  LEA_WINO2_CASE(8, 2, 1, 8, 2, true, CV) LEA_WINO2_CASE(8, 1, 2, 4, 1, true, CV)
+  LEA_WINO2_CASE(8, 1, 1, 4, 2, 0, CV) LEA_WINO2_CASE(8, 2, 1, 4, 2, 0, CV)                        \
+  LEA_WINO2_CASE(8, 2, 1, 8, 2, 0, CV) LEA_WINO2_CASE(8, 1, 2, 4, 1, 0, CV)                        \
+  LEA_WINO2_CASE(16, 1, 1, 4, 2, 0, CV) LEA_WINO2_CASE(16, 2, 1, 8, 2, 0, CV)                      \
+  LEA_WINO2_CASE(16, 1, 2, 4, 1, 0, CV) LEA_WINO2_CASE(8, 2, 1, 4, 2, 1, CV)                       \
+  LEA_WINO2_CASE(8, 2, 1, 8, 2, 1, CV) LEA_WINO2_CASE(8, 1, 2, 4, 1, 1, CV)
 
 int run2(const Plan2& p, ConvArgs a, int B, hipStream_t st, bool cv) {
   if (cv) {
     LEA_WINO2_TILES(true)
   } else {
     LEA_WINO2_TILES(false)
+    LEA_WINO2_CASE(8, 2, 1, 4, 2, 2, false)
   }
   set_error("lea_conv3d(wino2): no tile q=%d wc=%d mte=%d nw=%d occ=%d pv=%d", p.q, p.wc, p.mte, p.nw,
-            p.occ, (int)p.pv);
+            p.occ, p.pv);
   return LEA_E_UNSUPPORTED;
 }
 
 const char* name2(const Plan2& p, bool cv) {
-  snprintf(g_name2, sizeof(g_name2), "conv3d_wino2_kernel<%d, %d, %d, %d, %d, %s, %s>", p.q, p.wc, p.mte,
-           p.nw, p.occ, p.pv ? "true" : "false", cv ? "true" : "false");
+  snprintf(g_name2, sizeof(g_name2), "conv3d_wino2_kernel<%d, %d, %d, %d, %d, %d, %s>", p.q, p.wc, p.mte,
+           p.nw, p.occ, p.pv, cv ? "true" : "false");
   return g_name2;
 }
 

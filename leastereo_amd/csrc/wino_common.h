@@ -57,6 +57,11 @@ __device__ __forceinline__ void dma_dword(__amdgpu_buffer_rsrc_t rs, unsigned vo
   asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dword %1, %2, 0 offen lds\n\ts_mov_b32 m0, %0"
                : "=&s"(keep) : "v"(voff), "s"(rs), "s"(lds) : "memory");
 }
+__device__ __forceinline__ void dma_dwordx4_buf(__amdgpu_buffer_rsrc_t rs, unsigned voff, unsigned lds) {
+  unsigned keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, 0 offen lds\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep) : "v"(voff), "s"(rs), "s"(lds) : "memory");
+}
 __device__ __forceinline__ void dma_dwordx4(const float* src, unsigned lds) {
   unsigned keep;
   asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
@@ -113,7 +118,8 @@ inline bool epi_buf_ok(const ConvArgs& a) {
 // block of 16 WC MTE couts.
 struct Plan2 {
   int q, wc, mte, nw, occ;
-  bool pv;  // V transformed once per chunk into LDS by the workgroup
+  int pv;   // V transformed once per chunk into LDS by the workgroup: 1 = halo staged by
+            // dword LDS-DMA pieces, 2 = by 16-byte pieces (W % 4 == 0, aligned sources)
   int spw;  // depth pairs walked per workgroup
 };
 // Depth groups (pairs) per workgroup when the planner leaves it open (both engines) (r02 walk sweep,

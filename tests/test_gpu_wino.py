@@ -127,7 +127,7 @@ def test_wino_matches_the_direct_engine_at_full_size():
 
 @pytest.mark.parametrize("mode,name", [
     (0, "conv3d_wino_kernel<4, 16, 0, 1, 2, false>"),
-    (1, "conv3d_wino2_kernel<16, 1, 1, 4, 2, false, false>")])
+    (1, "conv3d_wino2_kernel<16, 1, 1, 4, 2, 0, false>")])
 def test_small_cout_tiles_match_the_direct_engine_at_full_size(mode, name):
     """The L0 8->8 cell op at config 2 (8 channels, 64x192x320) on both small-cout forms
     of the Winograd entries -- the depth-paired 1-D tile (couts of two planes per 16-row
@@ -386,3 +386,41 @@ def test_buffer_epilogue_is_bit_identical(b, cin, cout, shape, small, variant):
     want = torch.relu(want * scale.double().view(1, -1, 1, 1, 1) + shift.double().view(1, -1, 1, 1, 1))
     np.testing.assert_allclose(outs[3][:, 4:4 + cout].cpu().double().numpy(),
                                (want + r[:, 4:4 + cout].double()).cpu().numpy(), rtol=1e-4, atol=1e-4)
+
+
+@pytest.mark.parametrize("b,cin,c1,cout,shape,mode", [
+    (1, 32, 32, 32, (5, 9, 320), "acc"), (2, 128, 64, 64, (5, 9, 40), "res"),
+    (1, 64, 64, 32, (4, 7, 36), None), (1, 8, 8, 24, (3, 6, 68), "acc"),
+    (1, 32, 32, 96, (3, 6, 20), "res"), (2, 16, 8, 32, (7, 13, 4), None),
+    (1, 32, 32, 32, (1, 1, 4), None)])
+def test_wd_halo16_is_bit_identical_to_dword_pieces(b, cin, c1, cout, shape, mode):
+    """The W x D transform-pass kernel with its halo staged as 16-byte pieces (PV = 2,
+    rows of whole 16-byte blocks: W % 4 == 0) equals the dword-piece staging (PV = 1)
+    bit for bit -- same values in LDS, same transforms -- and float64 torch at the
+    engine bar; ragged H / D / W tiles (W = 36, 68, 4: partial 32-wide rows), two
+    sources (cin1 = c1), every epilogue."""
+    lib = _lib.load()
+    g = torch.Generator().manual_seed(cin + cout + shape[2])
+    x = torch.randn((b, cin) + shape, generator=g)
+    w = torch.randn(cout, cin, 3, 3, 3, generator=g) / np.sqrt(cin * 27)
+    scale = torch.rand(cout, generator=g) + 0.5
+    shift = torch.randn(cout, generator=g) * 0.1
+    r = torch.randn((b, cout) + shape, generator=g)
+    want = _ref(x, w, scale, shift, True, r if mode else None)
+    xs = x.to(DEV)
+    x1, x2 = (xs[:, :c1].contiguous(), xs[:, c1:].contiguous()) if c1 < cin else (xs, None)
+    pw = kernels.pack_conv_weight_wino(w.to(DEV))
+    outs = {}
+    for on in (1, 0):
+        assert lib.lea_conv3d_wino2_set_halo16(on) == 0
+        try:
+            name = kernels.wino_kernel_name(b, cout, *shape)
+            assert name.startswith("conv3d_wino2_kernel<8, 2, 1, 4, 2, %d," % (2 if on else 1)), name
+            out = r.to(DEV).clone() if mode == "acc" else None
+            outs[on] = kernels.conv3d_bnrelu_wino(x1, pw, cout, scale.to(DEV), shift.to(DEV), relu=True,
+                                                  out=out, accumulate=mode == "acc", x2=x2,
+                                                  residual=r.to(DEV) if mode == "res" else None)
+        finally:
+            lib.lea_conv3d_wino2_set_halo16(1)
+    assert torch.equal(outs[1], outs[0])
+    np.testing.assert_allclose(outs[1].cpu().double().numpy(), want.numpy(), rtol=1e-4, atol=1e-4)
