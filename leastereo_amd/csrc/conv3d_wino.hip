@@ -47,7 +47,7 @@
 namespace lea {
 namespace wino {
 
-template <int F, int Q, int MT, int NP, int TD>
+template <int F, int Q, int MT, int NP, int TD, bool H16 = false>
 struct Cfg {
   static constexpr bool DP = MT == 0;           // depth-paired (couts <= 8)
   static constexpr int MTE = DP ? 1 : MT;       // 16-row tiles per wave
@@ -68,7 +68,28 @@ struct Cfg {
   // channel stride >= whole pieces: the last piece's surplus lanes land in padding,
   // so no piece needs a per-lane exec mask
   static constexpr int CIS = conflict_free_cis<F, Q>(64 * XSLOTS, RW);
-  static constexpr int XS = CIN_B * CIS;
+  // H16: rows staged as 16-byte blocks from w0 - 4 (RWA = TW + 8 floats), one channel's
+  // planes x rows contiguous (PIECES16 pieces of 64 lanes, the last one partial), channel
+  // c at CB2(c) == {1, 3, 33, 35}[c] mod 64 dwords: column w0 - 1 at an even dword (the
+  // step's ds_read_b64s stay 8-byte aligned) and, for one tile row per lane group
+  // (Q = 16), the 32 lanes of a read (16 groups x 2 channels) on 64 distinct banks
+  static constexpr int RWA = TW + 8;
+  static constexpr int PLANEA = RH * RWA;
+  static constexpr int IMGA = PLANES * PLANEA;
+  static constexpr int BLK16 = IMGA / 4;
+  static constexpr int PIECES16 = (BLK16 + 63) / 64;
+  static constexpr int cb2(int c) {
+    int base = 1;
+    for (int k = 1; k <= c; ++k) {
+      const int want = (k & 1 ? 2 : 0) + (k & 2 ? 32 : 0) + 1, lo = base + IMGA;
+      base = lo + ((want - lo) % 64 + 64) % 64;
+    }
+    return base;
+  }
+  static_assert(!H16 || (Q == 16 && F == 4), "16-byte halo: one tile row per lane group");
+  static constexpr int XS = H16 ? (cb2(CIN_B - 1) + IMGA + 3) / 4 * 4 : CIN_B * CIS;
+  static constexpr int RWX = H16 ? RWA : RW;       // staged row / plane strides the steps read
+  static constexpr int PLX = H16 ? PLANEA : PLANE;
   static constexpr int WS = NSTEP * 3 * CIN_B * COP;  // the chunk's weights g[step][kw][ci][co]
   static constexpr int WSLOTS = (WS + 255) / 256;  // 256-float pieces (padded the same way)
   static constexpr int STAGE = XS + 256 * WSLOTS;
@@ -76,9 +97,10 @@ struct Cfg {
   static_assert(2 * STAGE * 4 * 2 <= 160 * 1024, "two double-buffered workgroups per CU");
 };
 
-template <int F, int Q, int MT, int NP, int TD, bool CV>
+template <int F, int Q, int MT, int NP, int TD, bool CV, bool H16 = false>
 __global__ __launch_bounds__(kConvThreads, 2) void conv3d_wino_kernel(const ConvArgs a) {
-  using C = Cfg<F, Q, MT, NP, TD>;
+  using C = Cfg<F, Q, MT, NP, TD, H16>;
+  static_assert(!(CV && H16), "16-byte halo: plain volumes only");
   constexpr int NX = C::NX;
   constexpr int XSLOTS = C::XSLOTS;
   constexpr int XSLOTS_W = (XSLOTS + kConvWaves - 1) / kConvWaves;
@@ -141,7 +163,35 @@ __global__ __launch_bounds__(kConvThreads, 2) void conv3d_wino_kernel(const Conv
     if constexpr (CV) wco[t] = wc_;
   }
   unsigned voff[XSLOTS_W], voffr[CV ? XSLOTS_W : 1];
+  // H16: piece t of this wave is k = wave + 4 t of the chunk's CIN_B x PIECES16 (channel
+  // k / PIECES16, block slot k % PIECES16)
+  constexpr int P16 = C::PIECES16, T16 = H16 ? (CIN_B * P16 + kConvWaves - 1) / kConvWaves : 1;
+  unsigned hwo16[T16], voff16[T16];
+  int pln16[T16];
+  bool ok16[T16];
+  if constexpr (H16) {
+#pragma unroll
+    for (int t = 0; t < T16; ++t) {
+      const int k = wave + kConvWaves * t, e = 64 * (k % P16) + lane;
+      ok16[t] = k < CIN_B * P16 && e < C::BLK16;
+      const int p = e / (C::RH * (C::RWA / 4)), r = e - p * (C::RH * (C::RWA / 4));
+      const int rr = r / (C::RWA / 4), blk = r - rr * (C::RWA / 4);
+      const int h = h0 + rr - 1, w = w0 - 4 + 4 * blk;  // W % 4 == 0: a block is all in or all out
+      const bool in = ok16[t] && (unsigned)h < (unsigned)a.H && (unsigned)w < (unsigned)a.W;
+      hwo16[t] = in ? (unsigned)(h * a.W + w) * 4u : 0xFFFFFFF0u;
+      pln16[t] = in ? p - 1 : -1000;
+    }
+  }
   auto set_group = [&](int d0) {  // DMA offsets of the depth group at output planes d0 ..
+    if constexpr (H16) {
+#pragma unroll
+      for (int t = 0; t < T16; ++t) {
+        const int d = d0 + pln16[t];
+        voff16[t] = (hwo16[t] != 0xFFFFFFF0u && (unsigned)d < (unsigned)a.D)
+                        ? hwo16[t] + (unsigned)d * (unsigned)HW * 4u : 0xFFFFFFF0u;
+      }
+      return;
+    }
 #pragma unroll
     for (int t = 0; t < XSLOTS_W; ++t) {
       const int d = d0 + pln[t];
@@ -169,6 +219,19 @@ __global__ __launch_bounds__(kConvThreads, 2) void conv3d_wino_kernel(const Conv
     }
     const long long cvol = CV ? (long long)HW : (long long)HW * a.D;  // channel stride
     const unsigned crec = CV ? (unsigned)HW * 4u : nrec;
+    if constexpr (H16) {
+#pragma unroll
+      for (int t = 0; t < T16; ++t) {
+        const int k = wave + kConvWaves * t, ci = k / P16;
+        const int c = ch * CIN_B + ci;
+        const float* base = c < a.cin1 ? a.x + (long long)b * a.xbs + (long long)c * cvol
+                                       : a.x2 + (long long)b * a.x2bs + (long long)(c - a.cin1) * cvol;
+        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)base, 0, crec, 0x00020000);
+        const int cb = ci == 0 ? C::cb2(0) : ci == 1 ? C::cb2(1) : ci == 2 ? C::cb2(2) : C::cb2(3);
+        if (ok16[t]) dma_dwordx4_buf(rs, voff16[t], lds0 + 4 * (unsigned)(st - smem + cb + (k % P16) * 256));
+      }
+      return;
+    }
 #pragma unroll
     for (int ci = 0; ci < CIN_B; ++ci) {
       const int c = ch * CIN_B + ci;
@@ -197,7 +260,10 @@ __global__ __launch_bounds__(kConvThreads, 2) void conv3d_wino_kernel(const Conv
   const int pq = p % Q, pr = p / Q;  // output group within the row, row within the lane group
   int xoff[NP];  // staged input column F pq (w0 + F pq - 1) of tile row (wave NP + j) RPG + pr
 #pragma unroll
-  for (int j = 0; j < NP; ++j) xoff[j] = ci * C::CIS + ((wave * NP + j) * C::RPG + pr) * C::RW + F * pq;
+  for (int j = 0; j < NP; ++j)
+    xoff[j] = H16 ? (ci == 0 ? C::cb2(0) : ci == 1 ? C::cb2(1) : ci == 2 ? C::cb2(2) : C::cb2(3)) +
+                        ((wave * NP + j) * C::RPG + pr) * C::RWA + 3 + F * pq
+                  : ci * C::CIS + ((wave * NP + j) * C::RPG + pr) * C::RW + F * pq;
   int woff[C::MTE];
 #pragma unroll
   for (int m = 0; m < C::MTE; ++m) woff[m] = ci * C::COP + a_col(m, ci, p, C::SWZ);
@@ -397,7 +463,7 @@ __global__ __launch_bounds__(kConvThreads, 2) void conv3d_wino_kernel(const Conv
       for (int t = 0; t < C::TDA; ++t)
 #pragma unroll
         for (int j = 0; j < NP; ++j) {
-          const float* sp = xs + xoff[j] + (t + kd) * C::PLANE + kh * C::RW;
+          const float* sp = xs + xoff[j] + (t + kd) * C::PLX + kh * C::RWX;
 #pragma unroll
           for (int q = 0; q <= F / 2; ++q) o.x2[t][j][q] = *reinterpret_cast<const float2*>(sp + 2 * q);
         }
@@ -544,6 +610,7 @@ struct Plan {
   int f, q, mt, np, td;
   bool d2;   // two-dimensional engine (conv3d_wino2.hip) with tile p2
   Plan2 p2;
+  bool h16;  // 1-D engine: halo staged as 16-byte pieces (plan_halo16)
 };
 
 int g_override[3] = {0, 0, 0};  // np, td, f (lea_conv3d_wino_set_tile_override)
@@ -600,6 +667,7 @@ inline Plan make_plan(int B, int cout, int D, int H, int W) {
   // 32-wide row pairs (L1, L2), F(2,3) for the 48-row blocks (their LDS budget);
   // two output planes per workgroup unless the volume is too shallow to fill the chip.
   Plan p;
+  p.h16 = false;
   p.mt = host_mt(cout);
   const long long ncob = (cout + cop_of(p.mt) - 1) / cop_of(p.mt);
   auto fits = [&](int tw) { return (W + tw - 1) / tw * tw * 10 <= W * 11; };  // <= 10 % padding
@@ -650,13 +718,18 @@ inline Plan make_plan(int B, int cout, int D, int H, int W) {
 // W % 4 == 0 and 16-byte aligned channel bases (r03 stamps: the DMA issue held 25-27 %
 // of the kernel's wave cycles with dword pieces).  Plain volumes only (not the cost volume).
 inline void plan_halo16(Plan& p, bool cv, int W, const ConvArgs* a) {
-  if (!p.d2 || p.p2.pv != 1 || p.p2.nw != 4 || p.p2.mte != 1 || cv || !g_halo16 || W % 4 != 0) return;
+  p.h16 = false;
+  if (cv || !g_halo16 || W % 4 != 0) return;
   if (a) {
     const bool al = ((uintptr_t)a->x & 15) == 0 && a->xbs % 4 == 0 &&
                     (a->cin1 == a->cin || (((uintptr_t)a->x2 & 15) == 0 && a->x2bs % 4 == 0));
     if (!al) return;
   }
-  p.p2.pv = 2;
+  if (p.d2) {
+    if (p.p2.pv == 1 && p.p2.nw == 4 && p.p2.mte == 1) p.p2.pv = 2;
+  } else if (p.mt == 0 && p.f == 4 && p.q == 16 && p.np == 1 && p.td == 2) {
+    p.h16 = true;  // the depth-paired 64-wide tile (the L0 8-channel cell ops)
+  }
 }
 
 #define LEA_WINO_CASE(F, Q, MT, NP, TD, CV)                                                   \
@@ -684,6 +757,18 @@ inline void plan_halo16(Plan& p, bool cv, int W, const ConvArgs* a) {
 int run(const Plan& p, ConvArgs a, int B, hipStream_t st, bool cv) {
   if (p.d2) return run2(p.p2, a, B, st, cv);
   a.ncob = (a.cout + cop_of(p.mt) - 1) / cop_of(p.mt);
+  if (p.h16) {
+    using C_ = Cfg<4, 16, 0, 1, 2, true>;
+    a.tiles_w = (a.W + C_::TW - 1) / C_::TW;
+    a.ntiles = a.tiles_w * ((a.H + C_::TH - 1) / C_::TH);
+    a.ndz = (a.D + 1) / 2;
+    a.spw = std::max(1, std::min(g_spw > 0 ? g_spw : auto_walk(a, B, 2), a.ndz));
+    const long long n_ = (long long)a.ntiles * ((a.ndz + a.spw - 1) / a.spw) * B * a.ncob;
+    LEA_CHECK_ARG(n_ < (1LL << 31), "lea_conv3d(wino): grid too large");
+    a.nblk = (int)n_;
+    conv3d_wino_kernel<4, 16, 0, 1, 2, false, true><<<dim3((unsigned)n_), kConvThreads, 0, st>>>(a);
+    return launch_status("lea_conv3d(wino)");
+  }
   if (cv) {
     LEA_WINO_TILES(true)
   } else {
@@ -697,8 +782,8 @@ thread_local char g_name[96];
 
 const char* name(const Plan& p, bool cv) {
   if (p.d2) return name2(p.p2, cv);
-  snprintf(g_name, sizeof(g_name), "conv3d_wino_kernel<%d, %d, %d, %d, %d, %s>", p.f, p.q, p.mt, p.np,
-           p.td, cv ? "true" : "false");
+  snprintf(g_name, sizeof(g_name), "conv3d_wino_kernel<%d, %d, %d, %d, %d, %s%s>", p.f, p.q, p.mt, p.np,
+           p.td, cv ? "true" : "false", p.h16 ? ", true" : "");
   return g_name;
 }
 

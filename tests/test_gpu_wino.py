@@ -126,7 +126,7 @@ def test_wino_matches_the_direct_engine_at_full_size():
 
 
 @pytest.mark.parametrize("mode,name", [
-    (0, "conv3d_wino_kernel<4, 16, 0, 1, 2, false>"),
+    (0, "conv3d_wino_kernel<4, 16, 0, 1, 2, false, true>"),
     (1, "conv3d_wino2_kernel<16, 1, 1, 4, 2, 0, false>")])
 def test_small_cout_tiles_match_the_direct_engine_at_full_size(mode, name):
     """The L0 8->8 cell op at config 2 (8 channels, 64x192x320) on both small-cout forms
@@ -392,13 +392,16 @@ def test_buffer_epilogue_is_bit_identical(b, cin, cout, shape, small, variant):
     (1, 32, 32, 32, (5, 9, 320), "acc"), (2, 128, 64, 64, (5, 9, 40), "res"),
     (1, 64, 64, 32, (4, 7, 36), None), (1, 8, 8, 24, (3, 6, 68), "acc"),
     (1, 32, 32, 96, (3, 6, 20), "res"), (2, 16, 8, 32, (7, 13, 4), None),
-    (1, 32, 32, 32, (1, 1, 4), None)])
+    (1, 32, 32, 32, (1, 1, 4), None),
+    # the depth-paired 1-D tile (couts <= 8, 64-wide rows): odd D, partial rows, 2 sources
+    (1, 8, 8, 8, (5, 9, 320), "acc"), (2, 16, 8, 8, (4, 7, 124), "res"), (1, 8, 8, 6, (3, 5, 60), None),
+    (1, 32, 32, 8, (6, 20, 188), None)])
 def test_wd_halo16_is_bit_identical_to_dword_pieces(b, cin, c1, cout, shape, mode):
-    """The W x D transform-pass kernel with its halo staged as 16-byte pieces (PV = 2,
-    rows of whole 16-byte blocks: W % 4 == 0) equals the dword-piece staging (PV = 1)
-    bit for bit -- same values in LDS, same transforms -- and float64 torch at the
-    engine bar; ragged H / D / W tiles (W = 36, 68, 4: partial 32-wide rows), two
-    sources (cin1 = c1), every epilogue."""
+    """The transform-pass W x D kernel (PV = 2) and the depth-paired 1-D kernel with their
+    halo staged as 16-byte pieces (rows of whole 16-byte blocks: W % 4 == 0) equal the
+    dword-piece staging bit for bit -- same values in LDS, same transforms -- and float64
+    torch at the engine bar; ragged H / D / W tiles (W = 36, 68, 4, 124, 60, 188: partial rows),
+    two sources (cin1 = c1), every epilogue."""
     lib = _lib.load()
     g = torch.Generator().manual_seed(cin + cout + shape[2])
     x = torch.randn((b, cin) + shape, generator=g)
@@ -415,7 +418,10 @@ def test_wd_halo16_is_bit_identical_to_dword_pieces(b, cin, c1, cout, shape, mod
         assert lib.lea_conv3d_wino2_set_halo16(on) == 0
         try:
             name = kernels.wino_kernel_name(b, cout, *shape)
-            assert name.startswith("conv3d_wino2_kernel<8, 2, 1, 4, 2, %d," % (2 if on else 1)), name
+            if cout <= 8:
+                assert name == "conv3d_wino_kernel<4, 16, 0, 1, 2, false%s>" % (", true" if on else ""), name
+            else:
+                assert name.startswith("conv3d_wino2_kernel<8, 2, 1, 4, 2, %d," % (2 if on else 1)), name
             out = r.to(DEV).clone() if mode == "acc" else None
             outs[on] = kernels.conv3d_bnrelu_wino(x1, pw, cout, scale.to(DEV), shift.to(DEV), relu=True,
                                                   out=out, accumulate=mode == "acc", x2=x2,
