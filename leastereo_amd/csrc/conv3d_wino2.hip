@@ -263,8 +263,10 @@ __global__ __launch_bounds__(NW * 64, OCC) void conv3d_wino2_kernel(const ConvAr
 #pragma unroll
     for (int t = 0; t < WSLOTS_W; ++t) {
       const int j = wave + NW * t;
+#ifndef LEA_EXP_NOWDMA
       if (j < WSLOTS)  // the last piece reads into the next chunk / the buffer's tail pad
         dma_dwordx4(wsrc + j * 256 + lane * 4, lds0 + 4 * (unsigned)(wdst - smem + j * 256));
+#endif
     }
     const long long cvol = CV ? (long long)HW : (long long)HW * a.D;  // channel stride
     const unsigned crec = CV ? (unsigned)HW * 4u : nrec;
@@ -278,7 +280,9 @@ __global__ __launch_bounds__(NW * 64, OCC) void conv3d_wino2_kernel(const ConvAr
                                        : a.x2 + (long long)b * a.x2bs + (long long)(c - a.cin1) * cvol;
         const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)base, 0, crec, 0x00020000);
         const int cb = ci == 0 ? C::cb2(0) : ci == 1 ? C::cb2(1) : ci == 2 ? C::cb2(2) : C::cb2(3);
+#ifndef LEA_EXP_NOHALO  // ablation builds (tools/wino2_ablate.sh): outputs wrong, timing only
         if (ok16) dma_dwordx4_buf(rs, voff16, lds0 + 4 * (unsigned)(st - smem + cb + j16 * 256));
+#endif
       }
       return;
     }
@@ -481,7 +485,11 @@ __global__ __launch_bounds__(NW * 64, OCC) void conv3d_wino2_kernel(const ConvAr
       static_assert(PV == 2 || (C::RW % 64 == 34 && C::CIS % 64 == 32 && C::RH % 2 == 0 && Q == 8),
                     "transform pass bank map");
       static_assert(PV != 2 || (Q == 8 && CIN_B == 4), "transform pass bank map (16-byte halo)");
+#ifdef LEA_EXP_NOVPASS
+      for (int u = tid; u < 0; u += NW * 64) {
+#else
       for (int u = tid; u < C::NUNIT; u += NW * 64) {
+#endif
         // PV = 1: 32 consecutive units = 8 groups x 2 rows x 2 channels: the b64 reads'
         // dword offsets 4 g + {0, RW, CIS, RW + CIS} cover the 64 banks once.
         // PV = 2: 8 groups x 4 channels of one row: 4 g + CB2(c) + 3 covers them (Cfg2)
@@ -523,7 +531,9 @@ __global__ __launch_bounds__(NW * 64, OCC) void conv3d_wino2_kernel(const ConvAr
         for (int k = 0; k < 6; ++k) tp[k] = make_float4(vf[4 * k], vf[4 * k + 1], vf[4 * k + 2], vf[4 * k + 3]);
       }
       LEA_STAMP(3);
+#ifndef LEA_EXP_NOBAR2
       __syncthreads();
+#endif
       LEA_STAMP(4);
     }
     // one kh step: the inputs (4 planes x 6 staged values as float2s, or the 24
@@ -601,7 +611,11 @@ __global__ __launch_bounds__(NW * 64, OCC) void conv3d_wino2_kernel(const ConvAr
         for (int e = 0; e < NE; ++e)
 #pragma unroll
           for (int m = 0; m < MTE; ++m)
+#ifdef LEA_EXP_NOMFMA  // keeps the operands live with one VALU op instead of the MFMA
+            acc[x][e][m][0] += T.u[x][e][m] * T.v[x][e];
+#else
             acc[x][e][m] = __builtin_amdgcn_mfma_f32_16x16x4f32(T.u[x][e][m], T.v[x][e], acc[x][e][m], 0, 0, 0);
+#endif
     };
     // 3 kh steps: LDS reads two steps ahead, transforms one step ahead
     Raw raw[2];
