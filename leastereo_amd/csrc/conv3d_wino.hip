@@ -122,14 +122,15 @@ __global__ __launch_bounds__(kConvThreads, 2) void conv3d_wino_kernel(const Conv
   // chunks through one DMA pipeline), as the W x D engine (conv3d_wino2.hip)
   const int spw = a.spw > 0 ? a.spw : 1;
   const int ngz = (a.ndz + spw - 1) / spw;
-  const int gz = lin % ngz;
-  const int tile = (lin / ngz) % a.ntiles;
-  const int bc = lin / (ngz * a.ntiles);
+  // cout block fastest: the blocks of one (tile, depth group) share its input in the L2
+  const int cob = lin % a.ncob;
+  const int rest = lin / a.ncob;
+  const int gz = rest % ngz;
+  const int tile = (rest / ngz) % a.ntiles;
+  const int b = rest / (ngz * a.ntiles);
   const int h0 = (tile / a.tiles_w) * C::TH;
   const int w0 = (tile % a.tiles_w) * C::TW;
   const int dz0 = gz * spw, ngroups = min(spw, a.ndz - dz0);
-  const int b = bc / a.ncob;
-  const int cob = bc - b * a.ncob;
   const int co0 = cob * C::COP;
   const int nchunks = a.cin / CIN_B;
   const int nitems = ngroups * nchunks;

@@ -178,14 +178,16 @@ __global__ __launch_bounds__(NW * 64, OCC) void conv3d_wino2_kernel(const ConvAr
   const int lin = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + idx;
   const int spw = a.spw > 0 ? a.spw : 1;
   const int ngz = (a.ndz + spw - 1) / spw;
-  const int gz = lin % ngz;
-  const int tile = (lin / ngz) % a.ntiles;
-  const int bc = lin / (ngz * a.ntiles);
+  // cout block fastest (r03): the blocks of one (tile, depth group) run side by side on
+  // one XCD and share its input through the L2 instead of each fetching it from HBM
+  const int cob = lin % a.ncob;
+  const int rest = lin / a.ncob;
+  const int gz = rest % ngz;
+  const int tile = (rest / ngz) % a.ntiles;
+  const int b = rest / (ngz * a.ntiles);
   const int h0 = (tile / a.tiles_w) * C::TH;
   const int w0 = (tile % a.tiles_w) * C::TW;
   const int pz0 = gz * spw, npairs = min(spw, a.ndz - pz0);
-  const int b = bc / a.ncob;
-  const int cob = bc - b * a.ncob;
   const int co0 = cob * C::COP;
   const int nchunks = a.cin / CIN_B;
   const int nitems = npairs * nchunks;
