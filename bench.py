@@ -281,7 +281,7 @@ def cpu_baseline(args, model, left0, right0, disp0, hip_step_s, device):
 # ------------------------------------------------------------------------ roofline
 def algorithm_name(kernel: str) -> str:
     """The convolution algorithm a conv kernel instantiation runs."""
-    if kernel.startswith("conv3d_wino2_kernel<"):
+    if kernel.startswith("conv3d_wino2"):
         return "winograd F(4,3) along W x F(2,3) along D"
     if kernel.startswith("conv3d_wino_kernel<"):
         return f"winograd F({kernel.split('<')[1].split(',')[0]},3) along W"

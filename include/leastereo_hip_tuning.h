@@ -65,6 +65,12 @@ int lea_conv3d_wino2_set_walk(int spw);
  * kernel name "..., 2, false>"), 0 = dword pieces ("..., 1, false>"). */
 int lea_conv3d_wino2_set_halo16(int on);
 
+/* 1 (default) = the 16-byte-halo W x D tile runs as the one-barrier pipeline
+ * ("conv3d_wino2p_kernel": item i's MFMAs interleaved with item i + 1's transform pass,
+ * weights loaded per lane from the packed buffer's lane-major copy), 0 = the two-barrier
+ * tile (PV = 2).  Same packed weights. */
+int lea_conv3d_wino2_set_pipeline(int on);
+
 /* 1 (default) = the Winograd engines' buffer-addressed epilogue where the shape allows
  * it (W % 4 == 0, 16-B aligned output / residual; residual loads issued together, the
  * next chunk's DMA waited for without the stores), 0 = the per-group epilogue. */

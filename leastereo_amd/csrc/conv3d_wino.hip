@@ -631,6 +631,7 @@ int g_small16 = 0;
 int g_block48 = 1;
 int g_epibuf = 1;  // lea_conv3d_wino_set_epi_buf
 int g_halo16 = 1;  // lea_conv3d_wino2_set_halo16
+int g_pipe = 1;    // lea_conv3d_wino2_set_pipeline
 inline int host_mt(int cout) {
   if (g_small16 && cout <= 8) return 1;
   const int mt = mt_of(cout);
@@ -727,7 +728,9 @@ inline void plan_halo16(Plan& p, bool cv, int W, const ConvArgs* a) {
     if (!al) return;
   }
   if (p.d2) {
-    if (p.p2.pv == 1 && p.p2.nw == 4 && p.p2.mte == 1) p.p2.pv = 2;
+    // the one-barrier pipeline uses the buffer-addressed epilogue only
+    const bool pipe = g_pipe && g_epibuf && (a == nullptr || epi_buf_ok(*a));
+    if (p.p2.pv == 1 && p.p2.nw == 4 && p.p2.mte == 1) p.p2.pv = pipe ? 3 : 2;
   } else if (p.mt == 0 && p.f == 4 && p.q == 16 && p.np == 1 && p.td == 2) {
     p.h16 = true;  // the depth-paired 64-wide tile (the L0 8-channel cell ops)
   }
@@ -821,8 +824,10 @@ using namespace lea;
 extern "C" size_t lea_conv3d_wino_packed_floats(int cout, int cin) {
   if (cout <= 0 || cin <= 0 || cin % wino::CIN_B != 0) return 0;
   const int mt = wino::host_mt(cout), cop = wino::cop_of(mt), nstep = mt == 0 ? 12 : 9;
-  // + one 256-float tail: the kernel stages whole 256-float pieces per chunk
-  return (size_t)((cout + cop - 1) / cop) * (cin / wino::CIN_B) * nstep * 3 * wino::CIN_B * cop + 256;
+  // + one 256-float tail: the kernel stages whole 256-float pieces per chunk; 32-cout
+  // blocks append the lane-major copy the one-barrier W x D tile loads (PV = 3)
+  return (size_t)((cout + cop - 1) / cop) * (cin / wino::CIN_B) * nstep * 3 * wino::CIN_B * cop + 256 +
+         (mt == 2 ? (size_t)wino::lane_weights_floats(cout, cin) : 0);
 }
 
 extern "C" int lea_conv3d_wino_pack_weights(const float* w, float* packed, int cout, int cin,
@@ -838,7 +843,12 @@ extern "C" int lea_conv3d_wino_pack_weights(const float* w, float* packed, int c
     case 0: wino::pack_wino_dp_kernel<<<grid, 256, 0, st>>>(w, packed, cout, cin, cin / wino::CIN_B, total); break;
     case 1: wino::pack_wino_kernel<1><<<grid, 256, 0, st>>>(w, packed, cout, cin, cin / wino::CIN_B, total); break;
     case 3: wino::pack_wino_kernel<3><<<grid, 256, 0, st>>>(w, packed, cout, cin, cin / wino::CIN_B, total); break;
-    default: wino::pack_wino_kernel<2><<<grid, 256, 0, st>>>(w, packed, cout, cin, cin / wino::CIN_B, total);
+    default: {
+      const long long lane = wino::lane_weights_floats(cout, cin), staged = total - lane;
+      wino::pack_wino_kernel<2><<<grid, 256, 0, st>>>(w, packed, cout, cin, cin / wino::CIN_B, staged);
+      const int g2 = (int)std::min<long long>((lane + 255) / 256, 4096);
+      wino::pack_wino_lane_kernel<<<g2, 256, 0, st>>>(w, packed + staged, cout, cin, cin / wino::CIN_B, lane);
+    }
   }
   return launch_status("lea_conv3d_wino_pack_weights");
 }
@@ -882,6 +892,13 @@ extern "C" int lea_conv3d_wino_set_small_cout(int mode) {
   clear_error();
   LEA_CHECK_ARG(mode == 0 || mode == 1, "lea_conv3d_wino_set_small_cout: mode=%d", mode);
   wino::g_small16 = mode;
+  return 0;
+}
+
+extern "C" int lea_conv3d_wino2_set_pipeline(int on) {
+  clear_error();
+  LEA_CHECK_ARG(on == 0 || on == 1, "lea_conv3d_wino2_set_pipeline: on=%d", on);
+  wino::g_pipe = on;
   return 0;
 }
 

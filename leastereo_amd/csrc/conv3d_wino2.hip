@@ -661,6 +661,310 @@ __global__ __launch_bounds__(NW * 64, OCC) void conv3d_wino2_kernel(const ConvAr
 #endif
 }
 
+
+// ------------------------------------------------------------------------------------
+// PV = 3 (r03): the transform-pass tile (Q = 8, two 16-row cout tiles x two row sets,
+// 16-byte halo) as a one-barrier pipeline.  Item i = (depth pair, 4-channel chunk):
+//   top      this wave's halo(i + 1) pieces and weight loads g(i) have landed (vmcnt),
+//            barrier: V(i) in tv[i & 1] is complete, halo(i + 1) has landed for all
+//   steps(i) V from tv[i & 1], U from g(i) in registers, 72 MFMAs per wave; interleaved
+//            with V-pass(i + 1): halo[(i + 1) & 1] -> tv[(i + 1) & 1] (last read by
+//            steps(i - 1), before the barrier)
+//   halo(i + 2) -> halo[i & 1] (read by V-pass(i), before the barrier), issued after
+//            step 0's transforms so the compiler's wait for g(i) never covers it
+//   g(i + 1) -> registers after the last U of item i (7 dwordx4 per lane)
+// The weights never touch LDS: each lane loads its (cout, channel)'s 27 taps of a chunk
+// from the lane-major copy lea_conv3d_wino_pack_weights appends for 32-cout blocks.
+// Ablations of the two-barrier tile (tools/wino2_ablate.sh, conv1/2: 858 us) put its
+// V-pass at 118 us and the weight DMA at 49 us, serialised with the MFMAs.
+constexpr int kGL = 28;  // floats per lane and chunk in the lane-major weights (27 taps + pad)
+
+__global__ __launch_bounds__(256, 2) void conv3d_wino2p_kernel(const ConvArgs a) {
+  using C = Cfg2<8, 2, 1, 4, 2, 2>;  // the PV = 2 tile's geometry and LDS maps
+  constexpr int Q = 8, WC = 2, NW = 4, F = 4, NX = 6, NE = 4, TD = 2;
+  constexpr int XS = C::XS, TS = C::TS;
+  static_assert((2 * XS + 2 * TS) * 4 * 2 <= 160 * 1024, "two workgroups per CU");
+  __shared__ __attribute__((aligned(16))) float smem[2 * XS + 2 * TS];
+  const unsigned lds0 = lds_addr(smem);
+  float* const halo = smem;            // halo[k] = smem + k * XS
+  float* const tvb = smem + 2 * XS;    // tv[k] = tvb + k * TS
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wc = wave % WC, wr = wave / WC;
+  const int nblk = a.nblk;
+  const int xcd = blockIdx.x % 8, idx = blockIdx.x / 8;
+  const int q8 = nblk / 8, r8 = nblk % 8;
+  const int lin = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + idx;
+  const int spw = a.spw > 0 ? a.spw : 1;
+  const int ngz = (a.ndz + spw - 1) / spw;
+  const int cob = lin % a.ncob;
+  const int rest = lin / a.ncob;
+  const int gz = rest % ngz;
+  const int tile = (rest / ngz) % a.ntiles;
+  const int b = rest / (ngz * a.ntiles);
+  const int h0 = (tile / a.tiles_w) * C::TH;
+  const int w0 = (tile % a.tiles_w) * C::TW;
+  const int pz0 = gz * spw, npairs = min(spw, a.ndz - pz0);
+  const int co0 = cob * C::COP;
+  const int nchunks = a.cin / CIN_B;
+  const int nitems = npairs * nchunks;
+  const int HW = a.H * a.W;
+  const unsigned nrec = (unsigned)(HW * a.D) * 4u;
+  const long long cvol = (long long)HW * a.D;
+  // lane-major weights: after the staged copy (ncob * nchunks * WS floats + 256 pad)
+  const float* wl = a.wp + (long long)a.ncob * nchunks * C::WS + 256 +
+                    ((long long)cob * nchunks * WC + wc) * 64 * kGL + lane * kGL;
+
+  // 16-byte halo pieces: block slot j16 = wave of every channel (4 per wave per item)
+  constexpr int PIECES16 = C::PIECES16;
+  static_assert(PIECES16 == NW, "one block slot per wave");
+  const int e16 = 64 * wave + lane;
+  const bool ok16 = e16 < C::BLK16;
+  unsigned hwo16 = 0xFFFFFFF0u, voff16 = 0xFFFFFFF0u;
+  int pln16 = -1000;
+  {
+    const int p = e16 / (C::RH * (C::RWA / 4)), r = e16 - p * (C::RH * (C::RWA / 4));
+    const int rr = r / (C::RWA / 4), blk = r - rr * (C::RWA / 4);
+    const int h = h0 + rr - 1, w = w0 - 4 + 4 * blk;
+    if (ok16 && (unsigned)h < (unsigned)a.H && (unsigned)w < (unsigned)a.W) {
+      hwo16 = (unsigned)(h * a.W + w) * 4u;
+      pln16 = p - 1;
+    }
+  }
+  auto issue_halo = [&](int item, int buf) {
+    const int ch = item % nchunks;
+    if (ch == 0) {
+      const int d = (pz0 + item / nchunks) * TD + pln16;
+      voff16 = (hwo16 != 0xFFFFFFF0u && (unsigned)d < (unsigned)a.D) ? hwo16 + (unsigned)d * (unsigned)HW * 4u
+                                                                      : 0xFFFFFFF0u;
+    }
+#pragma unroll
+    for (int ci = 0; ci < CIN_B; ++ci) {
+      const int c = ch * CIN_B + ci;
+      const float* base = c < a.cin1 ? a.x + (long long)b * a.xbs + (long long)c * cvol
+                                     : a.x2 + (long long)b * a.x2bs + (long long)(c - a.cin1) * cvol;
+      const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)base, 0, nrec, 0x00020000);
+      const int cb = ci == 0 ? C::cb2(0) : ci == 1 ? C::cb2(1) : ci == 2 ? C::cb2(2) : C::cb2(3);
+      if (ok16) dma_dwordx4_buf(rs, voff16, lds0 + 4 * (unsigned)(buf * XS + cb + wave * 256));
+    }
+  };
+  float4 gw[kGL / 4];  // this lane's taps of the current chunk: [kh][kd][kw]
+  auto load_g = [&](int item) {
+    const float4* src = reinterpret_cast<const float4*>(wl + (long long)(item % nchunks) * WC * 64 * kGL);
+#pragma unroll
+    for (int k = 0; k < kGL / 4; ++k) gw[k] = src[k];
+  };
+  // V-pass of one item: unit u = (group g, channel c, halo row r), as PV = 2
+  auto vpass = [&](int buf) {
+    const float* xs = halo + buf * XS;
+    float* tv = tvb + buf * TS;
+    for (int u = tid; u < C::NUNIT; u += NW * 64) {
+      const int g = u % Q, c = (u / Q) % CIN_B, r = u / (Q * CIN_B);
+      const int cb = c == 0 ? C::cb2(0) : c == 1 ? C::cb2(1) : c == 2 ? C::cb2(2) : C::cb2(3);
+      const float* sp0 = xs + cb + r * C::RWA + 3 + F * g;
+      float bw[C::PLANES][NX];
+#pragma unroll
+      for (int pl = 0; pl < C::PLANES; ++pl) {
+        const float* sp = sp0 + pl * C::PLANEA;
+        const float2 a0 = *reinterpret_cast<const float2*>(sp);
+        const float2 a1 = *reinterpret_cast<const float2*>(sp + 2);
+        const float2 a2 = *reinterpret_cast<const float2*>(sp + 4);
+        bw4(a0.x, a0.y, a1.x, a1.y, a2.x, a2.y, bw[pl]);
+      }
+      float v[NE][NX];
+#pragma unroll
+      for (int x = 0; x < NX; ++x) {
+        v[0][x] = bw[0][x] - bw[2][x];
+        v[1][x] = bw[1][x] + bw[2][x];
+        v[2][x] = bw[2][x] - bw[1][x];
+        v[3][x] = bw[1][x] - bw[3][x];
+      }
+      float4* tp = reinterpret_cast<float4*>(tv + c * C::TCS + r * C::TRS + 24 * g);
+      const float* vf = &v[0][0];
+#pragma unroll
+      for (int k = 0; k < 6; ++k) tp[k] = make_float4(vf[4 * k], vf[4 * k + 1], vf[4 * k + 2], vf[4 * k + 3]);
+    }
+  };
+
+  const int ci = lane >> 4, p = lane & 15;
+  const int pq = p % Q, pr = p / Q;
+  const int toff = ci * C::TCS + (wr * C::RPG + pr) * C::TRS + 24 * pq;
+  float sc[4], sh[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int co = co0 + 16 * wc + 4 * ci + r;
+    const bool cv = co < a.cout;
+    sc[r] = (cv && a.scale) ? a.scale[co] : 1.f;
+    sh[r] = (cv && a.shift) ? a.shift[co] : 0.f;
+  }
+  f32x4 acc[NX][NE];
+#pragma unroll
+  for (int x = 0; x < NX; ++x)
+#pragma unroll
+    for (int e = 0; e < NE; ++e) acc[x][e] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const bool relu = a.flags & LEA_RELU, resid = a.flags & LEA_RESIDUAL;
+  const long long DHW = (long long)HW * a.D;
+  const int w = w0 + F * pq;
+  const int h = h0 + wr * C::RPG + pr;
+  constexpr int NST = 4 * TD;
+  const int nco = min(C::COP, a.cout - co0);
+  const __amdgpu_buffer_rsrc_t yrs = block_rsrc(a.y + (long long)b * a.ybs + (long long)co0 * DHW, nco * DHW * 4);
+  const __amdgpu_buffer_rsrc_t rrs =
+      block_rsrc((resid ? a.res : a.y) + (long long)b * (resid ? a.rbs : a.ybs) + (long long)co0 * DHW, nco * DHW * 4);
+  auto epilogue = [&](int d0) {  // the buffer-addressed epilogue of conv3d_wino2_kernel
+    const bool lv = h < a.H && w < a.W;
+    unsigned off[4][TD];
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+      for (int t = 0; t < TD; ++t) {
+        const int cr = 16 * wc + 4 * ci + r, d = d0 + t;
+        off[r][t] = (lv && cr < nco && d < a.D) ? (unsigned)(cr * DHW + (long long)d * HW + h * a.W + w) * 4u
+                                                : kEpiOob;
+      }
+    f32x4 rv[4][TD];
+    if (resid) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int t = 0; t < TD; ++t) rv[r][t] = buf_load4(rrs, off[r][t]);
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      float n[NE][F];
+#pragma unroll
+      for (int e = 0; e < NE; ++e)
+        aw4(acc[0][e][r], acc[1][e][r], acc[2][e][r], acc[3][e][r], acc[4][e][r], acc[5][e][r], n[e]);
+#pragma unroll
+      for (int t = 0; t < TD; ++t) {
+        f32x4 y;
+#pragma unroll
+        for (int j = 0; j < F; ++j) {
+          const float s = t == 0 ? 0.5f * (n[1][j] + n[2][j]) : 0.5f * (n[1][j] - n[2][j]);
+          float v = t == 0 ? n[0][j] + s : s - n[3][j];
+          v = v * sc[r] + sh[r];
+          if (relu) v = fmaxf(v, 0.f);
+          y[j] = resid ? v + rv[r][t][j] : v;
+        }
+        buf_store4(yrs, off[r][t], y);
+      }
+    }
+  };
+
+  // prologue: halo(0), g(0), halo(1); V(0)
+  issue_halo(0, 0);
+  load_g(0);
+  if (nitems > 1) {
+    issue_halo(1, 1);
+    asm volatile("s_waitcnt vmcnt(4)" ::: "memory");  // all but halo(1)'s four pieces
+  } else {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __syncthreads();
+  vpass(0);
+  bool after_epi = false;
+  for (int it = 0; it < nitems; ++it) {
+    const int ch = it % nchunks;
+    // halo(it + 1) and g(it) landed (only an epilogue's stores may stay in flight)
+    if (after_epi)
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NST) : "memory");
+    else
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    const float* tv = tvb + (it & 1) * TS;
+    struct Raw {
+      float4 v4[6];
+    };
+    auto load_step = [&](int kh, Raw& o) {
+      const float4* tp = reinterpret_cast<const float4*>(tv + toff + kh * C::TRS);
+#pragma unroll
+      for (int k = 0; k < 6; ++k) o.v4[k] = tp[k];
+    };
+    struct Xf {
+      float v[NX][NE];
+      float u[NX][NE];
+    };
+    auto xform = [&](int kh, const Raw& o, Xf& T) {
+#pragma unroll
+      for (int k = 0; k < 6; ++k) {
+        const float e4[4] = {o.v4[k].x, o.v4[k].y, o.v4[k].z, o.v4[k].w};
+#pragma unroll
+        for (int i = 0; i < 4; ++i) T.v[(4 * k + i) % NX][(4 * k + i) / NX] = e4[i];
+      }
+      const float* g = reinterpret_cast<const float*>(gw) + kh * 9;
+      float uw[3][NX];
+#pragma unroll
+      for (int kd = 0; kd < 3; ++kd) gw4(g[kd * 3], g[kd * 3 + 1], g[kd * 3 + 2], uw[kd]);
+#pragma unroll
+      for (int x = 0; x < NX; ++x) {
+        const float s = uw[0][x] + uw[2][x];
+        T.u[x][0] = uw[0][x];
+        T.u[x][1] = s + uw[1][x];
+        T.u[x][2] = s - uw[1][x];
+        T.u[x][3] = uw[2][x];
+      }
+    };
+    auto mfmas = [&](const Xf& T) {
+#pragma unroll
+      for (int x = 0; x < NX; ++x)
+#pragma unroll
+        for (int e = 0; e < NE; ++e)
+          acc[x][e] = __builtin_amdgcn_mfma_f32_16x16x4f32(T.u[x][e], T.v[x][e], acc[x][e], 0, 0, 0);
+    };
+    Raw raw[2];
+    Xf xf[2];
+    __builtin_amdgcn_iglp_opt(0);
+    load_step(0, raw[0]);
+    load_step(1, raw[1]);
+    xform(0, raw[0], xf[0]);
+    // halo(it + 2) into the buffer V-pass(it) read (after g(it)'s first use: see above)
+    if (it + 2 < nitems) issue_halo(it + 2, it & 1);
+    load_step(2, raw[0]);
+    xform(1, raw[1], xf[1]);
+    mfmas(xf[0]);
+    if (it + 1 < nitems) vpass((it + 1) & 1);
+    xform(2, raw[0], xf[0]);
+    if (it + 1 < nitems) load_g(it + 1);
+    mfmas(xf[1]);
+    mfmas(xf[0]);
+    after_epi = false;
+    if (ch == nchunks - 1) {
+      epilogue((pz0 + it / nchunks) * TD);
+      after_epi = true;
+#pragma unroll
+      for (int x = 0; x < NX; ++x)
+#pragma unroll
+        for (int e = 0; e < NE; ++e) acc[x][e] = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+  }
+}
+
+// lane-major weights of the PV = 3 tile, appended after the staged copy: per (cout block
+// of 32, chunk, cout tile wc, lane = 16 ci + n): the 27 taps [kh][kd][kw] of cout
+// 32 cb + 16 wc + n and input channel 4 chunk + ci, then one zero
+__global__ void pack_wino_lane_kernel(const float* __restrict__ w, float* __restrict__ out, int cout, int cin,
+                                      int nchunks, long long total) {
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
+       i += (long long)gridDim.x * blockDim.x) {
+    long long q = i;
+    const int k = (int)(q % kGL); q /= kGL;
+    const int ln = (int)(q % 64); q /= 64;
+    const int wc = (int)(q % 2); q /= 2;
+    const int ch = (int)(q % nchunks);
+    const int cb = (int)(q / nchunks);
+    const int co = cb * 32 + 16 * wc + (ln & 15), c = ch * CIN_B + (ln >> 4);
+    const int kh = k / 9, kd = (k % 9) / 3, kw = k % 3;
+    out[i] = (k < 27 && co < cout && c < cin) ? w[(((long long)co * cin + c) * 9 + kd * 3 + kh) * 3 + kw] : 0.f;
+  }
+}
+
+long long lane_weights_floats(int cout, int cin) {
+  return (long long)((cout + 31) / 32) * (cin / CIN_B) * 2 * 64 * kGL;
+}
+
 #ifdef LEA_EXP_STAMPS
 unsigned* g_dbg = nullptr;
 }  // namespace wino
@@ -711,6 +1015,19 @@ int run2(const Plan2& p, ConvArgs a, int B, hipStream_t st, bool cv) {
   } else {
     LEA_WINO2_TILES(false)
     LEA_WINO2_CASE(8, 2, 1, 4, 2, 2, false)
+    if (p.q == 8 && p.wc == 2 && p.mte == 1 && p.nw == 4 && p.occ == 2 && p.pv == 3) {
+      using C_ = Cfg2<8, 2, 1, 4, 2, 2>;
+      a.ncob = (a.cout + C_::COP - 1) / C_::COP;
+      a.tiles_w = (a.W + C_::TW - 1) / C_::TW;
+      a.ntiles = a.tiles_w * ((a.H + C_::TH - 1) / C_::TH);
+      a.ndz = (a.D + C_::TD - 1) / C_::TD;
+      a.spw = std::max(1, std::min(p.spw > 0 ? p.spw : auto_walk(a, B, C_::WG_PER_CU), a.ndz));
+      const long long n_ = (long long)a.ntiles * ((a.ndz + a.spw - 1) / a.spw) * B * a.ncob;
+      LEA_CHECK_ARG(n_ < (1LL << 31), "lea_conv3d(wino2): grid too large");
+      a.nblk = (int)n_;
+      conv3d_wino2p_kernel<<<dim3((unsigned)n_), 256, 0, st>>>(a);
+      return launch_status("lea_conv3d(wino2p)");
+    }
   }
   set_error("lea_conv3d(wino2): no tile q=%d wc=%d mte=%d nw=%d occ=%d pv=%d", p.q, p.wc, p.mte, p.nw,
             p.occ, p.pv);
@@ -718,6 +1035,7 @@ int run2(const Plan2& p, ConvArgs a, int B, hipStream_t st, bool cv) {
 }
 
 const char* name2(const Plan2& p, bool cv) {
+  if (p.pv == 3 && !cv) return "conv3d_wino2p_kernel";
   snprintf(g_name2, sizeof(g_name2), "conv3d_wino2_kernel<%d, %d, %d, %d, %d, %d, %s>", p.q, p.wc, p.mte,
            p.nw, p.occ, p.pv, cv ? "true" : "false");
   return g_name2;

@@ -876,6 +876,8 @@ def wino_mfma_scale(cout: int, name: str) -> float:
     kernel's F (first template argument of ``name``), times the padding of cout to
     the engine's 16/32/48-row block.  The W x D engine (conv3d_wino2_kernel<Q, WC, MTE,
     ...>) issues 24 products per 72: 1/3, with couts padded to 16 WC MTE."""
+    if name.startswith("conv3d_wino2p_kernel"):  # the one-barrier W x D tile: 32-cout blocks
+        return (-(-cout // 32) * 32) / cout / 3.0
     if name.startswith("conv3d_wino2_kernel<"):
         _, wc, mte = (int(t) for t in name.split("<", 1)[1].split(",")[:3])
         cop = 16 * wc * mte

@@ -392,16 +392,18 @@ def test_buffer_epilogue_is_bit_identical(b, cin, cout, shape, small, variant):
     (1, 32, 32, 32, (5, 9, 320), "acc"), (2, 128, 64, 64, (5, 9, 40), "res"),
     (1, 64, 64, 32, (4, 7, 36), None), (1, 8, 8, 24, (3, 6, 68), "acc"),
     (1, 32, 32, 96, (3, 6, 20), "res"), (2, 16, 8, 32, (7, 13, 4), None),
-    (1, 32, 32, 32, (1, 1, 4), None),
+    (1, 32, 32, 32, (1, 1, 4), None), (1, 4, 4, 32, (2, 3, 8), "res"), (2, 8, 8, 64, (9, 5, 72), "acc"),
     # the depth-paired 1-D tile (couts <= 8, 64-wide rows): odd D, partial rows, 2 sources
     (1, 8, 8, 8, (5, 9, 320), "acc"), (2, 16, 8, 8, (4, 7, 124), "res"), (1, 8, 8, 6, (3, 5, 60), None),
     (1, 32, 32, 8, (6, 20, 188), None)])
 def test_wd_halo16_is_bit_identical_to_dword_pieces(b, cin, c1, cout, shape, mode):
-    """The transform-pass W x D kernel (PV = 2) and the depth-paired 1-D kernel with their
-    halo staged as 16-byte pieces (rows of whole 16-byte blocks: W % 4 == 0) equal the
-    dword-piece staging bit for bit -- same values in LDS, same transforms -- and float64
-    torch at the engine bar; ragged H / D / W tiles (W = 36, 68, 4, 124, 60, 188: partial rows),
-    two sources (cin1 = c1), every epilogue."""
+    """The transform-pass W x D tile with its halo staged as 16-byte pieces (rows of whole
+    16-byte blocks: W % 4 == 0) -- as the one-barrier pipeline (conv3d_wino2p_kernel, weights
+    from the lane-major copy, the default) and as the two-barrier tile (PV = 2) -- and the
+    depth-paired 1-D kernel with 16-byte pieces equal the dword-piece staging bit for bit
+    (same values in LDS, same transforms, same accumulation order) and float64 torch at the
+    engine bar; ragged H / D / W tiles (W = 36, 68, 4, 124, 60, 188: partial rows), a single
+    item (cin 4, one pair), two sources (cin1 = c1), every epilogue."""
     lib = _lib.load()
     g = torch.Generator().manual_seed(cin + cout + shape[2])
     x = torch.randn((b, cin) + shape, generator=g)
@@ -414,19 +416,22 @@ def test_wd_halo16_is_bit_identical_to_dword_pieces(b, cin, c1, cout, shape, mod
     x1, x2 = (xs[:, :c1].contiguous(), xs[:, c1:].contiguous()) if c1 < cin else (xs, None)
     pw = kernels.pack_conv_weight_wino(w.to(DEV))
     outs = {}
-    for on in (1, 0):
-        assert lib.lea_conv3d_wino2_set_halo16(on) == 0
+    for on, pipe in ((1, 1), (1, 0), (0, 1)):
+        assert lib.lea_conv3d_wino2_set_halo16(on) == 0 and lib.lea_conv3d_wino2_set_pipeline(pipe) == 0
         try:
             name = kernels.wino_kernel_name(b, cout, *shape)
             if cout <= 8:
                 assert name == "conv3d_wino_kernel<4, 16, 0, 1, 2, false%s>" % (", true" if on else ""), name
+            elif on and pipe:
+                assert name == "conv3d_wino2p_kernel", name
             else:
                 assert name.startswith("conv3d_wino2_kernel<8, 2, 1, 4, 2, %d," % (2 if on else 1)), name
             out = r.to(DEV).clone() if mode == "acc" else None
-            outs[on] = kernels.conv3d_bnrelu_wino(x1, pw, cout, scale.to(DEV), shift.to(DEV), relu=True,
-                                                  out=out, accumulate=mode == "acc", x2=x2,
-                                                  residual=r.to(DEV) if mode == "res" else None)
+            outs[(on, pipe)] = kernels.conv3d_bnrelu_wino(x1, pw, cout, scale.to(DEV), shift.to(DEV), relu=True,
+                                                          out=out, accumulate=mode == "acc", x2=x2,
+                                                          residual=r.to(DEV) if mode == "res" else None)
         finally:
             lib.lea_conv3d_wino2_set_halo16(1)
-    assert torch.equal(outs[1], outs[0])
-    np.testing.assert_allclose(outs[1].cpu().double().numpy(), want.numpy(), rtol=1e-4, atol=1e-4)
+            lib.lea_conv3d_wino2_set_pipeline(1)
+    assert torch.equal(outs[(1, 1)], outs[(0, 1)]) and torch.equal(outs[(1, 0)], outs[(0, 1)])
+    np.testing.assert_allclose(outs[(1, 1)].cpu().double().numpy(), want.numpy(), rtol=1e-4, atol=1e-4)
