@@ -680,9 +680,15 @@ __global__ __launch_bounds__(NW * 64, OCC) void conv3d_wino2_kernel(const ConvAr
 constexpr int kGL = 28;  // floats per lane and chunk in the lane-major weights (27 taps + pad)
 
 __global__ __launch_bounds__(256, 2) void conv3d_wino2p_kernel(const ConvArgs a) {
-  using C = Cfg2<8, 2, 1, 4, 2, 2>;  // the PV = 2 tile's geometry and LDS maps
-  constexpr int Q = 8, WC = 2, NW = 4, F = 4, NX = 6, NE = 4, TD = 2;
-  constexpr int XS = C::XS, TS = C::TS;
+  using C = Cfg2<8, 2, 1, 4, 2, 2>;  // the PV = 2 tile's geometry and maps (tv, V-pass banks)
+  constexpr int Q = 8, WC = 2, F = 4, NX = 6, NE = 4, TD = 2;
+  // halo channels 1024 floats apart (the PV = 2 map's bases mod 64): every lane of the 4
+  // pieces per channel, the partial last one too, writes inside its channel's region, so
+  // the pieces need no exec mask and the loop body stays one basic block
+  constexpr int CB0 = 1, CB1 = CB0 + 1024 + 2, CB2 = CB1 + 1024 + 30, CB3 = CB2 + 1024 + 2;
+  static_assert(CB1 % 64 == 3 && CB2 % 64 == 33 && CB3 % 64 == 35, "V-pass bank map");
+  constexpr int XS = (CB3 + 1024 + 3) / 4 * 4, TS = C::TS;
+  static_assert(C::NUNIT == 3 * 64 && C::BLK16 <= 4 * 64, "tile geometry");
   static_assert((2 * XS + 2 * TS) * 4 * 2 <= 160 * 1024, "two workgroups per CU");
   __shared__ __attribute__((aligned(16))) float smem[2 * XS + 2 * TS];
   const unsigned lds0 = lds_addr(smem);
@@ -717,12 +723,11 @@ __global__ __launch_bounds__(256, 2) void conv3d_wino2p_kernel(const ConvArgs a)
   const float* wl = a.wp + (long long)a.ncob * nchunks * C::WS + 256 +
                     ((long long)cob * nchunks * WC + wc) * 64 * kGL + lane * kGL;
 
-  // 16-byte halo pieces: block slot j16 = wave of every channel (4 per wave per item)
-  constexpr int PIECES16 = C::PIECES16;
-  static_assert(PIECES16 == NW, "one block slot per wave");
+  // 16-byte halo pieces: block slot j16 = wave of every channel (4 per wave per item);
+  // lanes past the halo (e16 >= BLK16) read out of range: zeros into the channel's pad
   const int e16 = 64 * wave + lane;
   const bool ok16 = e16 < C::BLK16;
-  unsigned hwo16 = 0xFFFFFFF0u, voff16 = 0xFFFFFFF0u;
+  unsigned hwo16 = 0xFFFFFFF0u;
   int pln16 = -1000;
   {
     const int p = e16 / (C::RH * (C::RWA / 4)), r = e16 - p * (C::RH * (C::RWA / 4));
@@ -733,21 +738,19 @@ __global__ __launch_bounds__(256, 2) void conv3d_wino2p_kernel(const ConvArgs a)
       pln16 = p - 1;
     }
   }
-  auto issue_halo = [&](int item, int buf) {
+  auto issue_halo = [&](int item, int buf) {  // branch-free: every lane, every channel
     const int ch = item % nchunks;
-    if (ch == 0) {
-      const int d = (pz0 + item / nchunks) * TD + pln16;
-      voff16 = (hwo16 != 0xFFFFFFF0u && (unsigned)d < (unsigned)a.D) ? hwo16 + (unsigned)d * (unsigned)HW * 4u
-                                                                      : 0xFFFFFFF0u;
-    }
+    const int d = (pz0 + item / nchunks) * TD + pln16;
+    const unsigned vo = (hwo16 != 0xFFFFFFF0u && (unsigned)d < (unsigned)a.D)
+                            ? hwo16 + (unsigned)d * (unsigned)HW * 4u : 0xFFFFFFF0u;
 #pragma unroll
     for (int ci = 0; ci < CIN_B; ++ci) {
       const int c = ch * CIN_B + ci;
       const float* base = c < a.cin1 ? a.x + (long long)b * a.xbs + (long long)c * cvol
                                      : a.x2 + (long long)b * a.x2bs + (long long)(c - a.cin1) * cvol;
       const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)base, 0, nrec, 0x00020000);
-      const int cb = ci == 0 ? C::cb2(0) : ci == 1 ? C::cb2(1) : ci == 2 ? C::cb2(2) : C::cb2(3);
-      if (ok16) dma_dwordx4_buf(rs, voff16, lds0 + 4 * (unsigned)(buf * XS + cb + wave * 256));
+      constexpr int cbs[4] = {CB0, CB1, CB2, CB3};
+      dma_dwordx4_buf(rs, vo, lds0 + 4 * (unsigned)(buf * XS + cbs[ci] + wave * 256));
     }
   };
   float4 gw[kGL / 4];  // this lane's taps of the current chunk: [kh][kd][kw]
@@ -756,14 +759,19 @@ __global__ __launch_bounds__(256, 2) void conv3d_wino2p_kernel(const ConvArgs a)
 #pragma unroll
     for (int k = 0; k < kGL / 4; ++k) gw[k] = src[k];
   };
-  // V-pass of one item: unit u = (group g, channel c, halo row r), as PV = 2
+  // V-pass of one item: unit u = (group g, channel c, halo row r), as PV = 2; branch-free:
+  // the fourth wave repeats the first wave's units and stores the same values
+  const int vu = tid % C::NUNIT;
+  const int vg = vu % Q, vc = (vu / Q) % CIN_B, vr = vu / (Q * CIN_B);
+  const int vxo = (vc == 0 ? CB0 : vc == 1 ? CB1 : vc == 2 ? CB2 : CB3) + vr * C::RWA + 3 + F * vg;
+  const int vto = vc * C::TCS + vr * C::TRS + 24 * vg;
   auto vpass = [&](int buf) {
     const float* xs = halo + buf * XS;
     float* tv = tvb + buf * TS;
-    for (int u = tid; u < C::NUNIT; u += NW * 64) {
-      const int g = u % Q, c = (u / Q) % CIN_B, r = u / (Q * CIN_B);
-      const int cb = c == 0 ? C::cb2(0) : c == 1 ? C::cb2(1) : c == 2 ? C::cb2(2) : C::cb2(3);
-      const float* sp0 = xs + cb + r * C::RWA + 3 + F * g;
+    {
+      const int g = vg;
+      (void)g;
+      const float* sp0 = xs + vxo;
       float bw[C::PLANES][NX];
 #pragma unroll
       for (int pl = 0; pl < C::PLANES; ++pl) {
@@ -781,7 +789,7 @@ __global__ __launch_bounds__(256, 2) void conv3d_wino2p_kernel(const ConvArgs a)
         v[2][x] = bw[2][x] - bw[1][x];
         v[3][x] = bw[1][x] - bw[3][x];
       }
-      float4* tp = reinterpret_cast<float4*>(tv + c * C::TCS + r * C::TRS + 24 * g);
+      float4* tp = reinterpret_cast<float4*>(tv + vto);
       const float* vf = &v[0][0];
 #pragma unroll
       for (int k = 0; k < 6; ++k) tp[k] = make_float4(vf[4 * k], vf[4 * k + 1], vf[4 * k + 2], vf[4 * k + 3]);
@@ -920,14 +928,16 @@ __global__ __launch_bounds__(256, 2) void conv3d_wino2p_kernel(const ConvArgs a)
     load_step(0, raw[0]);
     load_step(1, raw[1]);
     xform(0, raw[0], xf[0]);
-    // halo(it + 2) into the buffer V-pass(it) read (after g(it)'s first use: see above)
-    if (it + 2 < nitems) issue_halo(it + 2, it & 1);
+    // halo(it + 2) into the buffer V-pass(it) read (after g(it)'s first use: see above);
+    // past the last item the DMA / V-pass / loads repeat the last one (nothing reads
+    // them), so the body is one basic block the scheduler can interleave with the MFMAs
+    issue_halo(min(it + 2, nitems - 1), it & 1);
     load_step(2, raw[0]);
     xform(1, raw[1], xf[1]);
     mfmas(xf[0]);
-    if (it + 1 < nitems) vpass((it + 1) & 1);
+    vpass((it + 1) & 1);
     xform(2, raw[0], xf[0]);
-    if (it + 1 < nitems) load_g(it + 1);
+    load_g(min(it + 1, nitems - 1));
     mfmas(xf[1]);
     mfmas(xf[0]);
     after_epi = false;
@@ -940,6 +950,8 @@ __global__ __launch_bounds__(256, 2) void conv3d_wino2p_kernel(const ConvArgs a)
         for (int e = 0; e < NE; ++e) acc[x][e] = f32x4{0.f, 0.f, 0.f, 0.f};
     }
   }
+  // the last iterations' repeated DMA still writes this workgroup's LDS: let it land
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
 // lane-major weights of the PV = 3 tile, appended after the staged copy: per (cout block
