@@ -750,14 +750,20 @@ __global__ __launch_bounds__(256, 2) void conv3d_wino2p_kernel(const ConvArgs a)
                                      : a.x2 + (long long)b * a.x2bs + (long long)(c - a.cin1) * cvol;
       const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)base, 0, nrec, 0x00020000);
       constexpr int cbs[4] = {CB0, CB1, CB2, CB3};
+#ifndef LEA_EXP_NOHALO
       dma_dwordx4_buf(rs, vo, lds0 + 4 * (unsigned)(buf * XS + cbs[ci] + wave * 256));
+#endif
     }
   };
   float4 gw[kGL / 4];  // this lane's taps of the current chunk: [kh][kd][kw]
   auto load_g = [&](int item) {
     const float4* src = reinterpret_cast<const float4*>(wl + (long long)(item % nchunks) * WC * 64 * kGL);
+#ifdef LEA_EXP_NOWDMA
+    for (int k = 0; k < kGL / 4; ++k) gw[k] = make_float4(1.f, 0.5f, 0.25f, (float)item);
+#else
 #pragma unroll
     for (int k = 0; k < kGL / 4; ++k) gw[k] = src[k];
+#endif
   };
   // V-pass of one item: unit u = (group g, channel c, halo row r), as PV = 2; branch-free:
   // the fourth wave repeats the first wave's units and stores the same values
@@ -920,7 +926,11 @@ __global__ __launch_bounds__(256, 2) void conv3d_wino2p_kernel(const ConvArgs a)
       for (int x = 0; x < NX; ++x)
 #pragma unroll
         for (int e = 0; e < NE; ++e)
+#ifdef LEA_EXP_NOMFMA
+          acc[x][e][0] += T.u[x][e] * T.v[x][e];
+#else
           acc[x][e] = __builtin_amdgcn_mfma_f32_16x16x4f32(T.u[x][e], T.v[x][e], acc[x][e], 0, 0, 0);
+#endif
     };
     Raw raw[2];
     Xf xf[2];
@@ -935,7 +945,9 @@ __global__ __launch_bounds__(256, 2) void conv3d_wino2p_kernel(const ConvArgs a)
     load_step(2, raw[0]);
     xform(1, raw[1], xf[1]);
     mfmas(xf[0]);
+#ifndef LEA_EXP_NOVPASS
     vpass((it + 1) & 1);
+#endif
     xform(2, raw[0], xf[0]);
     load_g(min(it + 1, nitems - 1));
     mfmas(xf[1]);

@@ -1,12 +1,13 @@
 #!/bin/bash
 # Ablation of the W x D transform-pass kernel (timing only, outputs wrong): builds
 # leastereo_amd/var_<name>.so with one phase knocked out each, then times the 32-cout
-# layers on each build (tools/wino2_sweep.py, planner's variant, HIP events).
+# layers on each build (tools/wino2_sweep.py, planner's variant, HIP events).  NOWDMA
+# drops the weight DMA (two-barrier tile) or the per-lane weight loads (pipelined tile).
 #   build here:  bash tools/wino2_ablate.sh build
 #   run on GPU:  bash tools/wino2_ablate.sh run
 set -u
 cd "$(dirname "$0")/.."
-VARS="base: nohalo:-DLEA_EXP_NOHALO nowdma:-DLEA_EXP_NOWDMA novpass:-DLEA_EXP_NOVPASS nobar2:-DLEA_EXP_NOBAR2 nomfma:-DLEA_EXP_NOMFMA nodma:-DLEA_EXP_NOHALO_-DLEA_EXP_NOWDMA"
+VARS=${VARS:-"base: nohalo:-DLEA_EXP_NOHALO nowdma:-DLEA_EXP_NOWDMA novpass:-DLEA_EXP_NOVPASS nobar2:-DLEA_EXP_NOBAR2 nomfma:-DLEA_EXP_NOMFMA nodma:-DLEA_EXP_NOHALO_-DLEA_EXP_NOWDMA"}
 if [ "${1:-run}" = build ]; then
   specs=""
   for v in $VARS; do n=${v%%:*}; f=${v#*:}; specs="$specs $n:-fno-slp-vectorize ${f//_-D/ -D}"; done
