@@ -678,7 +678,6 @@ __global__ __launch_bounds__(NW * 64, OCC) void conv3d_wino2_kernel(const ConvAr
 // Ablations of the two-barrier tile (tools/wino2_ablate.sh, conv1/2: 858 us) put its
 // V-pass at 118 us and the weight DMA at 49 us, serialised with the MFMAs.
 constexpr int kGL = 28;  // floats per lane and chunk in the lane-major weights (27 taps + pad)
-constexpr int kGLoads = 7;  // global loads of one chunk's taps (6 dwordx4 + 1 dwordx3, as hipcc emits them)
 
 __global__ __launch_bounds__(256, 2) void conv3d_wino2p_kernel(const ConvArgs a) {
   using C = Cfg2<8, 2, 1, 4, 2, 2>;  // the PV = 2 tile's geometry and maps (tv, V-pass banks)
@@ -756,17 +755,14 @@ __global__ __launch_bounds__(256, 2) void conv3d_wino2p_kernel(const ConvArgs a)
 #endif
     }
   };
-  // this lane's taps of a chunk ([kh][kd][kw] + pad) as 16-byte buffer loads (fixed width:
-  // hipcc would shrink a plain load of the pad-ended tail to 12 bytes)
-  typedef float4 Taps[kGL / 4];
-  const __amdgpu_buffer_rsrc_t wrs = block_rsrc(wl - lane * kGL, (long long)nchunks * WC * 64 * kGL * 4);
-  auto load_g = [&](int item, Taps& dst) {
-    const unsigned base = (unsigned)((item % nchunks) * WC * 64 * kGL + lane * kGL) * 4u;
+  float4 gw[kGL / 4];  // this lane's taps of the current chunk: [kh][kd][kw]
+  auto load_g = [&](int item) {
+    const float4* src = reinterpret_cast<const float4*>(wl + (long long)(item % nchunks) * WC * 64 * kGL);
 #ifdef LEA_EXP_NOWDMA
-    for (int k = 0; k < kGL / 4; ++k) dst[k] = make_float4(1.f, 0.5f, 0.25f, (float)item);
+    for (int k = 0; k < kGL / 4; ++k) gw[k] = make_float4(1.f, 0.5f, 0.25f, (float)item);
 #else
 #pragma unroll
-    for (int k = 0; k < kGL / 4; ++k) dst[k] = __builtin_bit_cast(float4, buf_load4(wrs, base + 16u * k));
+    for (int k = 0; k < kGL / 4; ++k) gw[k] = src[k];
 #endif
   };
   // V-pass of one item: unit u = (group g, channel c, halo row r), as PV = 2; branch-free:
@@ -873,10 +869,8 @@ __global__ __launch_bounds__(256, 2) void conv3d_wino2p_kernel(const ConvArgs a)
   };
 
   // prologue: halo(0), g(0), halo(1); V(0)
-  Taps ga, gb;  // the taps of items it (even) / it + 1 (odd): two bodies per loop turn,
-                // so the prefetch lands in the registers that use it (no copies, no wait)
   issue_halo(0, 0);
-  load_g(0, ga);
+  load_g(0);
   if (nitems > 1) {
     issue_halo(1, 1);
     asm volatile("s_waitcnt vmcnt(4)" ::: "memory");  // all but halo(1)'s four pieces
@@ -886,15 +880,13 @@ __global__ __launch_bounds__(256, 2) void conv3d_wino2p_kernel(const ConvArgs a)
   __syncthreads();
   vpass(0);
   bool after_epi = false;
-  auto body = [&](const int it, const Taps& gw, Taps& gnext) {
+  for (int it = 0; it < nitems; ++it) {
     const int ch = it % nchunks;
-    // halo(it + 1) landed; younger than its pieces are only item it-1's seven weight loads
-    // (the compiler waits for them before their first use, in xform(0)) and, after an
-    // epilogue, its NST stores (its residual loads were waited for before they were used)
+    // halo(it + 1) and g(it) landed (only an epilogue's stores may stay in flight)
     if (after_epi)
-      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NST + kGLoads) : "memory");
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NST) : "memory");
     else
-      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(kGLoads) : "memory");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     const float* tv = tvb + (it & 1) * TS;
     struct Raw {
@@ -957,7 +949,7 @@ __global__ __launch_bounds__(256, 2) void conv3d_wino2p_kernel(const ConvArgs a)
     vpass((it + 1) & 1);
 #endif
     xform(2, raw[0], xf[0]);
-    load_g(min(it + 1, nitems - 1), gnext);
+    load_g(min(it + 1, nitems - 1));
     mfmas(xf[1]);
     mfmas(xf[0]);
     after_epi = false;
@@ -969,10 +961,6 @@ __global__ __launch_bounds__(256, 2) void conv3d_wino2p_kernel(const ConvArgs a)
 #pragma unroll
         for (int e = 0; e < NE; ++e) acc[x][e] = f32x4{0.f, 0.f, 0.f, 0.f};
     }
-  };
-  for (int it = 0; it < nitems; it += 2) {
-    body(it, ga, gb);
-    if (it + 1 < nitems) body(it + 1, gb, ga);
   }
   // the last iterations' repeated DMA still writes this workgroup's LDS: let it land
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
