@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define LEA_ABI_VERSION 8
+#define LEA_ABI_VERSION 9
 
 #define LEA_F32 0
 #define LEA_BF16 1
@@ -273,9 +273,10 @@ int lea_conv3d_bnrelu_costvolume_wino(const void* left, const void* right, int64
                                       void* stream);
 /* Kernel instantiation the Winograd entries launch for this shape
  * ("conv3d_wino_kernel<F, Q, MT, NP, TD, CV>", or on the W x D engine
- * "conv3d_wino2_kernel<Q, WC, MTE, NW, OCC, PV, CV>").  The engines' tuning hooks are
- * in leastereo_hip_tuning.h. */
-const char* lea_conv3d_wino_kernel_name(int B, int cout, int D, int H, int W, int costvolume);
+ * "conv3d_wino2_kernel<Q, WC, MTE, NW, OCC, PV, CV>" / "conv3d_wino2p_kernel"; cin = 0:
+ * unknown, planned as a deep layer).  The engines' tuning hooks are in
+ * leastereo_hip_tuning.h. */
+const char* lea_conv3d_wino_kernel_name(int B, int cin, int cout, int D, int H, int W, int costvolume);
 
 /* ---- Matching-net stem0 over the cost volume, factored (csrc/cv_stem.hip) ----
  * Replaces retrain/LEAStereo.py:34-48 + skip_model_3d.py:141 like

@@ -12,7 +12,7 @@ LIB_PATH = os.environ.get(
     "LEASTEREO_HIP_LIB",
     os.path.join(os.path.dirname(os.path.abspath(__file__)), "libleastereo_hip.so"))
 
-ABI_VERSION = 8
+ABI_VERSION = 9
 LEA_F32 = 0
 LEA_BF16 = 1
 LEA_RELU = 1
@@ -83,7 +83,7 @@ SIGNATURES = {
                                     _i, _i, _i, _i, _i, _i, _u, _i, _p]),
     "lea_conv3d_bnrelu_costvolume_wino": (_i, [_p, _p, _i64, _p, _p, _p, _p, _i64, _i, _i, _i,
                                                _i, _i, _i, _u, _i, _p]),
-    "lea_conv3d_wino_kernel_name": (ctypes.c_char_p, [_i, _i, _i, _i, _i, _i]),
+    "lea_conv3d_wino_kernel_name": (ctypes.c_char_p, [_i, _i, _i, _i, _i, _i, _i]),
     "lea_conv3d_wino_set_tile_override": (_i, [_i, _i, _i]),
     "lea_conv3d_wino_set_variant": (_i, [_i]),
     "lea_conv3d_wino2_set_walk": (_i, [_i]),

@@ -719,7 +719,8 @@ inline Plan make_plan(int B, int cout, int D, int H, int W) {
 // pieces per channel instead of 13 dword pieces) when rows are whole 16-byte blocks:
 // W % 4 == 0 and 16-byte aligned channel bases (r03 stamps: the DMA issue held 25-27 %
 // of the kernel's wave cycles with dword pieces).  Plain volumes only (not the cost volume).
-inline void plan_halo16(Plan& p, bool cv, int W, const ConvArgs* a) {
+inline void plan_halo16(Plan& p, bool cv, int W, const ConvArgs* a, int cin = 0) {
+  if (a) cin = a->cin;
   p.h16 = false;
   if (cv || !g_halo16 || W % 4 != 0) return;
   if (a) {
@@ -729,7 +730,9 @@ inline void plan_halo16(Plan& p, bool cv, int W, const ConvArgs* a) {
   }
   if (p.d2) {
     // the one-barrier pipeline uses the buffer-addressed epilogue only
-    const bool pipe = g_pipe && g_epibuf && (a == nullptr || epi_buf_ok(*a));
+    // (layers of one or two chunks per depth pair stay on the two-barrier tile: L0 8->24
+    // ran 286 us there, 296-301 us pipelined -- r03 sweeps)
+    const bool pipe = g_pipe && g_epibuf && (a == nullptr || epi_buf_ok(*a)) && (cin == 0 || cin > 2 * CIN_B);
     if (p.p2.pv == 1 && p.p2.nw == 4 && p.p2.mte == 1) p.p2.pv = pipe ? 3 : 2;
   } else if (p.mt == 0 && p.f == 4 && p.q == 16 && p.np == 1 && p.td == 2) {
     p.h16 = true;  // the depth-paired 64-wide tile (the L0 8-channel cell ops)
@@ -853,10 +856,11 @@ extern "C" int lea_conv3d_wino_pack_weights(const float* w, float* packed, int c
   return launch_status("lea_conv3d_wino_pack_weights");
 }
 
-extern "C" const char* lea_conv3d_wino_kernel_name(int B, int cout, int D, int H, int W, int costvolume) {
+extern "C" const char* lea_conv3d_wino_kernel_name(int B, int cin, int cout, int D, int H, int W,
+                                                   int costvolume) {
   if (B <= 0 || cout <= 0 || D <= 0 || H <= 0 || W <= 0) return nullptr;
   wino::Plan p = wino::make_plan(B, cout, D, H, W);
-  wino::plan_halo16(p, costvolume != 0, W, nullptr);  // (assumes 16-byte aligned sources)
+  wino::plan_halo16(p, costvolume != 0, W, nullptr, cin);  // (assumes 16-byte aligned sources)
   return wino::name(p, costvolume != 0);
 }
 

@@ -889,8 +889,8 @@ def wino_mfma_scale(cout: int, name: str) -> float:
     return (f + 2) / (3.0 * f) * (-(-cout // cop) * cop) / cout
 
 
-def wino_kernel_name(b, cout, d, h, w, costvolume=False):
-    name = _lib.load().lea_conv3d_wino_kernel_name(b, cout, d, h, w, 1 if costvolume else 0)
+def wino_kernel_name(b, cout, d, h, w, costvolume=False, cin=0):
+    name = _lib.load().lea_conv3d_wino_kernel_name(b, cin, cout, d, h, w, 1 if costvolume else 0)
     return name.decode() if name else None
 
 
@@ -930,7 +930,7 @@ def conv3d_bnrelu_wino(x: torch.Tensor, packed: torch.Tensor, cout: int,
     out, ybs = _conv_out(x.shape, cout, (d, h, w), out, accumulate, x.device, x.dtype)
     rptr, rbs = _residual(out, accumulate, residual, ybs)
     flags = (LEA_RELU if relu else 0) | (LEA_RESIDUAL if rptr is not None else 0)
-    name = wino_kernel_name(b, cout, d, h, w)
+    name = wino_kernel_name(b, cout, d, h, w, cin=cin + cin2)
     rec = _probe_begin(b, cin + cin2, cout, d, h, w, 3, rptr is not None, b * d * h * w, False,
                        name=name, mfma_scale=wino_mfma_scale(cout, name))
     check(_lib.load().lea_conv3d_bnrelu_wino(
@@ -957,7 +957,7 @@ def conv3d_bnrelu_costvolume_wino(fl: torch.Tensor, fr: torch.Tensor, maxdisp: i
     b, c, h, w = fl.shape
     d3 = int(maxdisp / 3)
     out = torch.empty((b, cout, d3, h, w), device=fl.device, dtype=fl.dtype)
-    name = wino_kernel_name(b, cout, d3, h, w, True)
+    name = wino_kernel_name(b, cout, d3, h, w, True, cin=2 * c)
     rec = _probe_begin(b, 2 * c, cout, d3, h, w, 3, False, 0, False,
                        name=name, mfma_scale=wino_mfma_scale(cout, name))
     check(_lib.load().lea_conv3d_bnrelu_costvolume_wino(

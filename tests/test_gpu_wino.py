@@ -236,7 +236,7 @@ def test_wino2_vs_torch(wino_variant, variant, b, cin, cout, shape, mode):
     """The W x D engine's tiles: odd D (the last pair's second plane masked), D = 1,
     W not a multiple of 4, ragged H tiles, every epilogue, couts padding a block."""
     wino_variant(variant)
-    name = kernels.wino_kernel_name(b, cout, *shape)
+    name = kernels.wino_kernel_name(b, cout, *shape, cin=cin)
     assert name.startswith("conv3d_wino2"), name
     g = torch.Generator().manual_seed(cin * 7 + cout + variant)
     x = torch.randn((b, cin) + shape, generator=g)
@@ -419,10 +419,10 @@ def test_wd_halo16_is_bit_identical_to_dword_pieces(b, cin, c1, cout, shape, mod
     for on, pipe in ((1, 1), (1, 0), (0, 1)):
         assert lib.lea_conv3d_wino2_set_halo16(on) == 0 and lib.lea_conv3d_wino2_set_pipeline(pipe) == 0
         try:
-            name = kernels.wino_kernel_name(b, cout, *shape)
+            name = kernels.wino_kernel_name(b, cout, *shape, cin=cin)
             if cout <= 8:
                 assert name == "conv3d_wino_kernel<4, 16, 0, 1, 2, false%s>" % (", true" if on else ""), name
-            elif on and pipe:
+            elif on and pipe and cin > 8:  # (one or two chunks per pair: the two-barrier tile)
                 assert name == "conv3d_wino2p_kernel", name
             else:
                 assert name.startswith("conv3d_wino2_kernel<8, 2, 1, 4, 2, %d," % (2 if on else 1)), name

@@ -31,7 +31,7 @@ def main():
     for name, (cin, cout, k, (d, h, w), count, *acc) in LAYERS.items():
         if k != 3 or not kernels.wino_eligible(cout, cin, k) or (only and name not in only):
             continue
-        kname = kernels.wino_kernel_name(1, cout, d, h, w)
+        kname = kernels.wino_kernel_name(1, cout, d, h, w, cin=cin)
         if not kname.startswith("conv3d_wino2"):
             continue
         acc = bool(acc and acc[0])

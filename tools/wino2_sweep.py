@@ -52,7 +52,7 @@ def main():
             pw = kernels.pack_conv_weight_wino(wt)
             assert lib.lea_conv3d_wino_set_variant(v) == 0
             assert lib.lea_conv3d_wino2_set_walk(walk) == 0
-            kname = kernels.wino_kernel_name(a.batch, cout, d, h, w) + (f" spw{walk}" if walk else "") + \
+            kname = kernels.wino_kernel_name(a.batch, cout, d, h, w, cin=cin) + (f" spw{walk}" if walk else "") + \
                 ("" if cout > 8 else f" small{sm}") + ("" if cout % 48 or cout % 32 == 0 else f" b48={b48}")
             y = r.clone()
             kernels.conv3d_bnrelu_wino(x, pw, cout, scale, shift, True, y, acc)

@@ -62,7 +62,7 @@ def main():
         lib.lea_conv3d_wino_set_tile_override(0, 0, 0)
         res["wino default"] = timed(lambda: kernels.conv3d_bnrelu_wino(x, pw, cout, scale, shift, True, y, acc),
                                     a.iters)
-        default = kernels.wino_kernel_name(a.batch, cout, d, h, w)
+        default = kernels.wino_kernel_name(a.batch, cout, d, h, w, cin=cin)
         for kk, ms in res.items():
             print(f"{name:26s} {kk:18s} {ms * 1e3:8.1f} us  {flops / ms / 1e9:6.1f} TF/s  x{count}", flush=True)
         print(f"  -> default {default}", flush=True)
