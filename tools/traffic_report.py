@@ -29,8 +29,12 @@ def load(d, counter):
 
 
 def short(n):
+    """Our kernel name (lea_*_kernel_name) of a rocprof name: 'fn<args>' or plain 'fn'."""
     m = re.search(r"lea::(?:\w+::)*(\w+)<([^>]*)>", n)
-    return f"{m.group(1)}<{m.group(2)}>" if m else None
+    if m:
+        return f"{m.group(1)}<{m.group(2)}>"
+    m = re.search(r"lea::(?:\w+::)*(\w+)\(", n)
+    return m.group(1) if m else None
 
 
 fetch, names = load(sys.argv[1], "FETCH_SIZE")
