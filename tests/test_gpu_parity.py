@@ -463,7 +463,7 @@ def test_predict_cli_satellite_branch(tmp_path):
     assert disp.shape == (90, 180)
     np.testing.assert_array_equal(np.asarray(Image.open(out / "tile_01.png")), P.float_to_u8(disp))
     inp = np.asarray(Image.open(out / "tile_01_in.png"))
-    assert inp.shape == (96, 192, 3)
+    assert inp.shape == (96, 192, g["left_u8"].shape[2])  # every layer of the image (predict.py:128-141)
     np.testing.assert_array_equal(inp, P.float_to_u8(P.crop_image(g["left_u8"][:90, :180], 96, 192)))
 
 
