@@ -432,14 +432,17 @@ def run(args, info):
     bf16 = args.precision == "bf16"
     peak = BF16_MFMA_PEAK_TFLOPS if bf16 else FP32_PEAK_TFLOPS
     achieved = issued / (ms_per_launch * 1e-3) / 1e12
+    alg_bytes = dom["bytes"] / launches  # inputs + output (+ residual) + weights, once
     traffic = None
     cfg = config_name(args)
     tf_file = os.path.join(REPO, "profiles", "hbm_traffic.json")
     if os.path.exists(tf_file):
         with open(tf_file) as f:
             tf = json.load(f)
-        # per-config entries (tools/traffic_merge.py) first: bytes per launch depend on shapes
-        traffic = (tf.get(f"{dominant}@{cfg}") or tf.get(dominant, {})).get("bytes_per_launch")
+        # per-config entries (tools/traffic_merge.py); the plain entries are the c2 workload's
+        # (bytes per launch depend on the shapes)
+        entry = tf.get(f"{dominant}@{cfg}") or (tf.get(dominant) if cfg == "c2" else None) or {}
+        traffic = entry.get("bytes_per_launch")
     ms_step = elapsed / args.steps * 1e3
     workload = WORKLOADS.get(cfg, f"{args.height}x{args.width} D={args.maxdisp} {args.precision}, "
                                   f"batch {args.batch} per GPU")
@@ -466,7 +469,8 @@ def run(args, info):
                    "launch": "hip graph replay" if args.graph else "eager"},
         "roofline": {"bound": "mfma", "kernel": dominant, "algorithm": algorithm_name(dominant),
                      "achieved": achieved, "peak": peak, "unit": "TFLOP/s", "frac": achieved / peak,
-                     "traffic": traffic,
+                     "traffic": traffic, "algorithmic_bytes_per_launch": alg_bytes,
+                     "traffic_over_algorithmic": None if traffic is None else traffic / alg_bytes,
                      "work": "MFMA FLOPs the kernel issues per launch (Winograd products, cout "
                              "padded to its blocks); DESIGN.md §4 gives the per-launch formula",
                      "flops_per_launch": issued, "ms_per_launch": ms_per_launch,
