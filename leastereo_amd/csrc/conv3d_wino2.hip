@@ -185,11 +185,8 @@ __global__ __launch_bounds__(NW * 64, OCC) void conv3d_wino2_kernel(const ConvAr
   const int gz = rest % ngz;
   const int tile = (rest / ngz) % a.ntiles;
   const int b = rest / (ngz * a.ntiles);
-  // tiles H-fastest: the workgroups running together on an XCD are H neighbours, which
-  // share 2 of their 6 staged rows (the 8 extra columns of a W neighbour cost less)
-  const int tiles_h = a.ntiles / a.tiles_w;
-  const int h0 = (tile % tiles_h) * C::TH;
-  const int w0 = (tile / tiles_h) * C::TW;
+  const int h0 = (tile / a.tiles_w) * C::TH;
+  const int w0 = (tile % a.tiles_w) * C::TW;
   const int pz0 = gz * spw, npairs = min(spw, a.ndz - pz0);
   const int co0 = cob * C::COP;
   const int nchunks = a.cin / CIN_B;
@@ -713,11 +710,8 @@ __global__ __launch_bounds__(256, 2) void conv3d_wino2p_kernel(const ConvArgs a)
   const int gz = rest % ngz;
   const int tile = (rest / ngz) % a.ntiles;
   const int b = rest / (ngz * a.ntiles);
-  // tiles H-fastest: the workgroups running together on an XCD are H neighbours, which
-  // share 2 of their 6 staged rows (the 8 extra columns of a W neighbour cost less)
-  const int tiles_h = a.ntiles / a.tiles_w;
-  const int h0 = (tile % tiles_h) * C::TH;
-  const int w0 = (tile / tiles_h) * C::TW;
+  const int h0 = (tile / a.tiles_w) * C::TH;
+  const int w0 = (tile % a.tiles_w) * C::TW;
   const int pz0 = gz * spw, npairs = min(spw, a.ndz - pz0);
   const int co0 = cob * C::COP;
   const int nchunks = a.cin / CIN_B;
