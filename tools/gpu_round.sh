@@ -1,5 +1,5 @@
 #!/bin/bash
-# Round-3 closing profile set (TAG): smoke, the GPU suite, HBM traffic passes (c2 fp32,
+# The round's closing profile set (TAG): smoke, the GPU suite, HBM traffic passes (c2 fp32,
 # c3/c4 bf16) merged into profiles/hbm_traffic.json, rocprofv3 kernel stats of the c2
 # bench, then the c2 (with the CPU baseline legs), c3, c4 and c5 bench lines.
 set -u
