@@ -215,8 +215,10 @@ __global__ __launch_bounds__(kConvThreads, 2) void conv3d_wino_kernel(const Conv
 #pragma unroll
     for (int t = 0; t < WSLOTS_W; ++t) {
       const int j = wave + kConvWaves * t;
+#ifndef LEA_EXP_NOWDMA
       if (j < WSLOTS)  // the last piece reads into the next chunk / the buffer's tail pad
         dma_dwordx4(wsrc + j * 256 + lane * 4, lds0 + 4 * (unsigned)(wdst - smem + j * 256));
+#endif
     }
     const long long cvol = CV ? (long long)HW : (long long)HW * a.D;  // channel stride
     const unsigned crec = CV ? (unsigned)HW * 4u : nrec;
@@ -229,7 +231,9 @@ __global__ __launch_bounds__(kConvThreads, 2) void conv3d_wino_kernel(const Conv
                                        : a.x2 + (long long)b * a.x2bs + (long long)(c - a.cin1) * cvol;
         const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)base, 0, crec, 0x00020000);
         const int cb = ci == 0 ? C::cb2(0) : ci == 1 ? C::cb2(1) : ci == 2 ? C::cb2(2) : C::cb2(3);
+#ifndef LEA_EXP_NOHALO  // ablation builds: outputs wrong, timing only
         if (ok16[t]) dma_dwordx4_buf(rs, voff16[t], lds0 + 4 * (unsigned)(st - smem + cb + (k % P16) * 256));
+#endif
       }
       return;
     }
@@ -252,7 +256,9 @@ __global__ __launch_bounds__(kConvThreads, 2) void conv3d_wino_kernel(const Conv
         const int j = wave + kConvWaves * t;
         unsigned vo = voff[t];
         if constexpr (CV) vo = voff[t] ^ ((voff[t] ^ voffr[t]) & rmask);
+#ifndef LEA_EXP_NOHALO
         if (j < XSLOTS) dma_dword(rs, vo, lds0 + 4 * (unsigned)(st - smem + ci * C::CIS + j * 64));
+#endif
       }
     }
   };
@@ -444,6 +450,9 @@ __global__ __launch_bounds__(kConvThreads, 2) void conv3d_wino_kernel(const Conv
   }
   };
 
+#ifdef LEA_EXP_STAGGER  // timing experiment: the second workgroup of a CU starts late
+  if (blockIdx.x >= 256 && blockIdx.x < 512) __builtin_amdgcn_s_sleep(LEA_EXP_STAGGER);
+#endif
   issue(0, smem);
   for (int it = 0; it < nitems; ++it) {
     const int ch = it % nchunks;

@@ -307,7 +307,9 @@ __global__ __launch_bounds__(NW * 64, OCC) void conv3d_wino2_kernel(const ConvAr
         const int j = wave + NW * t;
         unsigned vo = voff[t];
         if constexpr (CV) vo = voff[t] ^ ((voff[t] ^ voffr[t]) & rmask);
+#ifndef LEA_EXP_NOHALO
         if (j < XSLOTS) dma_dword(rs, vo, lds0 + 4 * (unsigned)(st - smem + ci * C::CIS + j * 64));
+#endif
       }
     }
   };
@@ -475,7 +477,9 @@ __global__ __launch_bounds__(NW * 64, OCC) void conv3d_wino2_kernel(const ConvAr
     const int ch = it % nchunks;
     wait_item<NST>(ebuf && ch == 0 && it > 0);  // this wave's pieces of item it landed
     LEA_STAMP(0);
+#ifndef LEA_EXP_NOBAR1  // ablation builds (tools/wino2_ablate.sh): outputs wrong, timing only
     __syncthreads();  // ... and everyone's; item it-1's stage is free
+#endif
     LEA_STAMP(1);
     if (it + 1 < nitems) issue(it + 1, smem + ((it + 1) & 1) * C::STAGE);
     LEA_STAMP(2);
@@ -555,7 +559,12 @@ __global__ __launch_bounds__(NW * 64, OCC) void conv3d_wino2_kernel(const ConvAr
         for (int pl = 0; pl < C::PLANES; ++pl) {
           const float* sp = xs + xoff + pl * C::PLANE + kh * C::RW;
 #pragma unroll
-          for (int q = 0; q < 3; ++q) o.x2[pl][q] = *reinterpret_cast<const float2*>(sp + 2 * q);
+          for (int q = 0; q < 3; ++q)
+#ifdef LEA_EXP_NOLDSRD
+            o.x2[pl][q] = make_float2((float)(kh + it), (float)(pl * q) + sp[0] * 0.f);
+#else
+            o.x2[pl][q] = *reinterpret_cast<const float2*>(sp + 2 * q);
+#endif
         }
       }
 #pragma unroll
@@ -564,7 +573,11 @@ __global__ __launch_bounds__(NW * 64, OCC) void conv3d_wino2_kernel(const ConvAr
         for (int kw = 0; kw < 3; ++kw)
 #pragma unroll
           for (int m = 0; m < MTE; ++m)
+#ifdef LEA_EXP_NOLDSRD
+            o.g[kd * 3 + kw][m] = (float)(kd + kw * kh + it);
+#else
             o.g[kd * 3 + kw][m] = ws[((kd * 3 + kh) * 3 + kw) * CIN_B * C::COP + woff[m]];
+#endif
     };
     struct Xf {
       float v[NX][NE];
@@ -582,18 +595,36 @@ __global__ __launch_bounds__(NW * 64, OCC) void conv3d_wino2_kernel(const ConvAr
         float bw[C::PLANES][NX];
 #pragma unroll
         for (int pl = 0; pl < C::PLANES; ++pl)
+#ifdef LEA_EXP_NOXF  // no transforms: V and U straight from the staged values
+        {
+          const float e6[6] = {o.x2[pl][0].x, o.x2[pl][0].y, o.x2[pl][1].x, o.x2[pl][1].y, o.x2[pl][2].x, o.x2[pl][2].y};
+          for (int x = 0; x < NX; ++x) bw[pl][x] = e6[x];
+        }
+#else
           bw4(o.x2[pl][0].x, o.x2[pl][0].y, o.x2[pl][1].x, o.x2[pl][1].y, o.x2[pl][2].x, o.x2[pl][2].y, bw[pl]);
+#endif
 #pragma unroll
         for (int x = 0; x < NX; ++x) {
+#ifdef LEA_EXP_NOXF
+          for (int e = 0; e < NE; ++e) T.v[x][e] = bw[e][x];
+#else
           T.v[x][0] = bw[0][x] - bw[2][x];
           T.v[x][1] = bw[1][x] + bw[2][x];
           T.v[x][2] = bw[2][x] - bw[1][x];
           T.v[x][3] = bw[1][x] - bw[3][x];
+#endif
         }
       }
 #pragma unroll
       for (int m = 0; m < MTE; ++m) {
         float uw[3][NX];
+#ifdef LEA_EXP_NOXF
+        for (int kd = 0; kd < 3; ++kd)
+          for (int x = 0; x < NX; ++x) uw[kd][x] = o.g[kd * 3 + x % 3][m];
+        for (int x = 0; x < NX; ++x)
+          for (int e = 0; e < NE; ++e) T.u[x][e][m] = uw[e % 3][x];
+        continue;
+#endif
 #pragma unroll
         for (int kd = 0; kd < 3; ++kd) gw4(o.g[kd * 3][m], o.g[kd * 3 + 1][m], o.g[kd * 3 + 2][m], uw[kd]);
 #pragma unroll

@@ -1,0 +1,19 @@
+#!/bin/bash
+# scratch lease script for the current experiment (overwritten per experiment; results
+# worth keeping are copied into profiles/)
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+export TMPDIR=/tmp
+mkdir -p gpurun_out/abl
+for n in base nohalo nodma w1base w1nohalo w1nodma; do
+  LEASTEREO_HIP_LIB=leastereo_amd/var_$n.so timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv \
+    -d gpurun_out/abl/$n -o run -- python3 tools/wino2_sweep.py --variants 0 --iters 20 --only cell_16to16_k3_L1,cell_8to8_k3_L0,cell_16to48_k3_L1_s1grp \
+    > gpurun_out/abl/$n.log 2>&1
+  rc=$?; [ $rc -eq 0 ] || { echo "$n rc=$rc"; tail -3 gpurun_out/abl/$n.log; exit $rc; }
+  f=$(ls gpurun_out/abl/$n/*kernel_stats.csv | head -1)
+  python3 -c "
+import csv,sys
+for r in csv.DictReader(open('$f')):
+    if 'wino' in r['Name']: print('$n', r['Name'][:70], 'calls', r['Calls'], 'avg_us', round(float(r['AverageNs'])/1e3,1))
+"
+done
