@@ -49,7 +49,11 @@ struct Cfg2 {
   // 32-lane ds_read_b64 group on disjoint banks); for PV = 1, = 32 mod 64 dwords, which
   // with RW = 34 puts the transform pass's 32-lane reads (8 groups x 2 rows x 2
   // channels, see below) on 64 distinct banks
-  static constexpr int CIS = PV ? (64 * XSLOTS + 32) : conflict_free_cis<F, Q>(64 * XSLOTS, RW);
+  // (per-lane V: room for whole pieces of every wave -- NW * ceil(XSLOTS / NW) -- so the
+  // staging issues the same count from each wave without a branch; the surplus pieces
+  // read out of range: zeros into the padding)
+  static constexpr int CIS = PV ? (64 * XSLOTS + 32)
+                                : conflict_free_cis<F, Q>(64 * NW * ((XSLOTS + NW - 1) / NW), RW);
   // PV = 2: rows staged as 16-byte blocks from w0 - 4 (RWA = TW + 8 floats: 10 blocks
   // cover the w0 - 1 .. w0 + TW halo columns), one channel's 4 planes x RH rows
   // contiguous (BLK16 blocks = PIECES16 LDS-DMA pieces of 64 lanes, the last one
@@ -298,15 +302,10 @@ __global__ __launch_bounds__(NW * 64, OCC) void conv3d_wino2_kernel(const ConvAr
 #pragma unroll
     for (int ci = 0; ci < CIN_B; ++ci) {
       const int c = ch * CIN_B + ci;
-      const float* base = a.x;
-      unsigned n = 0;
-      if (c < a.cin1) {
-        base = a.x + (long long)b * a.xbs + (long long)c * cvol;
-        n = crec;
-      } else if (c < a.cin) {
-        base = a.x2 + (long long)b * a.x2bs + (long long)(c - a.cin1) * cvol;
-        n = crec;
-      }
+      // selects, not branches: the chunk's staging stays one basic block
+      const float* base = c < a.cin1 ? a.x + (long long)b * a.xbs + (long long)c * cvol
+                                     : a.x2 + (long long)b * a.x2bs + (long long)(c - a.cin1) * cvol;
+      const unsigned n = c < a.cin ? crec : 0u;
       const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)base, 0, n, 0x00020000);
       const unsigned rmask = (CV && c >= a.cin1) ? 0xFFFFFFFFu : 0u;  // chunks never straddle cin1
 #pragma unroll
@@ -315,7 +314,7 @@ __global__ __launch_bounds__(NW * 64, OCC) void conv3d_wino2_kernel(const ConvAr
         unsigned vo = voff[t];
         if constexpr (CV) vo = voff[t] ^ ((voff[t] ^ voffr[t]) & rmask);
 #ifndef LEA_EXP_NOHALO
-        if (j < XSLOTS) dma_dword(rs, vo, lds0 + 4 * (unsigned)(st - smem + ci * C::CIS + j * 64));
+        if (PV == 0 || j < XSLOTS) dma_dword(rs, vo, lds0 + 4 * (unsigned)(st - smem + ci * C::CIS + j * 64));
 #endif
       }
     }

@@ -4,12 +4,19 @@
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
-mkdir -p gpurun_out
+mkdir -p gpurun_out/abl
 timeout -k 10 300 python3 -u -m pytest tests/test_gpu_wino.py -x -q -m gpu --timeout 120 --timeout-method thread > gpurun_out/t_wino.log 2>&1
-rc=$?; tail -3 gpurun_out/t_wino.log; [ $rc -eq 0 ] || exit $rc
-VARS="base: gs28: base: gs28:" ONLY=stem1_32to32_k3_L0,conv12_128to64_k3_L1,cell_32to96_k3_L2_s1grp,cell_8to24_k3_L0_s1grp \
-  bash tools/wino2_ablate.sh run > gpurun_out/exp.txt 2>&1
-rc=$?; cat gpurun_out/exp.txt; [ $rc -eq 0 ] || exit $rc
-SWEEP_ARGS="--only stem1_32to32_k3_L0,conv12_128to64_k3_L1 --variants 0 --iters 10" FILTERS="conv3d_wino2p" \
-  bash tools/gpu_pmc_layer.sh > gpurun_out/pmc_dom.txt 2>&1
-rc=$?; tail -2 gpurun_out/pmc_dom.txt; exit $rc
+rc=$?; tail -2 gpurun_out/t_wino.log; [ $rc -eq 0 ] || exit $rc
+for n in base bf base bf; do
+  LEASTEREO_HIP_LIB=leastereo_amd/var_$n.so timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv \
+    -d gpurun_out/abl/$n -o run -- python3 tools/wino2_sweep.py --variants 0 --iters 20 --only cell_16to16_k3_L1 \
+    > gpurun_out/abl/$n.log 2>&1
+  rc=$?; [ $rc -eq 0 ] || { echo "$n rc=$rc"; tail -3 gpurun_out/abl/$n.log; exit $rc; }
+  f=$(ls gpurun_out/abl/$n/*kernel_stats.csv | head -1)
+  python3 -c "
+import csv
+for r in csv.DictReader(open('$f')):
+    if 'wino2_kernel' in r['Name']: print('$n', r['Name'][:70], 'calls', r['Calls'], 'avg_us', round(float(r['AverageNs'])/1e3,1))
+"
+  rm -rf gpurun_out/abl/$n
+done
