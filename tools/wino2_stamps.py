@@ -32,7 +32,7 @@ def main():
         if k != 3 or not kernels.wino_eligible(cout, cin, k) or (only and name not in only):
             continue
         kname = kernels.wino_kernel_name(1, cout, d, h, w, cin=cin)
-        if not kname.startswith("conv3d_wino2"):
+        if not kname.startswith("conv3d_wino2_kernel<"):  # (the pipelined tile has no stamps)
             continue
         acc = bool(acc and acc[0])
         g = torch.Generator(device=dev).manual_seed(0)
