@@ -14,7 +14,7 @@ all: $(LIB)
 # cycles than the scalar pairs it replaces (MI355X_MICROARCH.md, filler prices)
 build/obj/conv3d_wino.o build/obj/conv3d_wino2.o: HIPFLAGS += -fno-slp-vectorize
 
-build/obj/%.o: leastereo_amd/csrc/%.hip $(wildcard leastereo_amd/csrc/*.h) include/leastereo_hip.h
+build/obj/%.o: leastereo_amd/csrc/%.hip $(wildcard leastereo_amd/csrc/*.h) include/leastereo_hip.h include/leastereo_hip_tuning.h
 	@mkdir -p build/obj
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
@@ -25,7 +25,29 @@ resource-usage: $(SRC)
 	@mkdir -p build/ru
 	for f in $(SRC); do $(HIPCC) $(HIPFLAGS) -c $$f -o build/ru/$$(basename $$f).o -Rpass-analysis=kernel-resource-usage 2>&1 | grep -E "Function Name|VGPRs:|AGPRs|ScratchSize|Occupancy|LDS Size" ; done
 
+# Host-side AddressSanitizer build of the C-ABI boundary: every unit with
+# ASan on its host side only (the device code is built as usual and never launched:
+# the driver, tests/asan/capi_asan.cpp, drives each entry point through its argument
+# checks and the host queries).  Runs on a machine without a GPU.
+ASANFLAGS := -O1 -g -std=c++17 -fPIC --offload-arch=$(ARCH) -Iinclude -Ileastereo_amd/csrc -Xarch_host -fsanitize=address \
+             -Xarch_host -fno-omit-frame-pointer
+ASANOBJ   := $(patsubst leastereo_amd/csrc/%.hip,build/asan/%.o,$(SRC))
+
+build/asan/%.o: leastereo_amd/csrc/%.hip $(wildcard leastereo_amd/csrc/*.h) include/leastereo_hip.h include/leastereo_hip_tuning.h
+	@mkdir -p build/asan
+	$(HIPCC) $(ASANFLAGS) -c $< -o $@
+
+build/asan/capi_asan_main.o: tests/asan/capi_asan.cpp include/leastereo_hip.h include/leastereo_hip_tuning.h
+	@mkdir -p build/asan
+	$(HIPCC) $(ASANFLAGS) -c $< -o $@
+
+build/asan/capi_asan: build/asan/capi_asan_main.o $(ASANOBJ)
+	$(HIPCC) --offload-arch=$(ARCH) -fno-gpu-sanitize -fsanitize=address -o $@ $^
+
+asan: build/asan/capi_asan
+	ASAN_OPTIONS=detect_leaks=0:abort_on_error=1 ./build/asan/capi_asan
+
 clean:
 	rm -rf build $(LIB)
 
-.PHONY: all clean resource-usage
+.PHONY: all clean resource-usage asan
