@@ -73,6 +73,10 @@ class CellGraphExecutor:
     # size) feeds one stacked 1x1 conv for both cells (the bf16 executors memoise every
     # resample instead); LEASTEREO_SHARE_DOWNSAMPLE=0 keeps two passes
     SHARE_DOWNSAMPLE = os.environ.get("LEASTEREO_SHARE_DOWNSAMPLE", "1") != "0"
+    # a three-op sibling group of 16-channel 3D ops (the L1 cells: 16 -> 48) as a 32-cout
+    # launch on the pipelined W x D kernel plus a 16-cout one (r03: 66 + 43 us vs 124 us on
+    # the 1-D 48-row engine); the f32 Winograd matching executor only
+    SPLIT_S1_GROUP48 = False
 
     def __init__(self, net):
         from .model import ConvBR
@@ -100,11 +104,15 @@ class CellGraphExecutor:
                         or 2 + steps[0] < first_cat_state):
                     continue
                 mods = [cell._ops[op] for _, op in group]
-                w = torch.cat([m.conv.weight for m in mods], 0)
-                folded = [m.folded_bn() for m in mods]
-                scale = torch.cat([f[0] for f in folded]).contiguous()
-                shift = torch.cat([f[1] for f in folded]).contiguous()
-                self.p[f"cells.{i}.s1_group"] = _conv_params(mods[0], w, (scale, shift))
+                split = (self.SPLIT_S1_GROUP48 and WINOGRAD and len(mods) == 3 and cell.c_out == 16
+                         and mods[0].conv.weight.dim() == 5 and mods[0].conv.weight.shape[2] == 3)
+                for key, part in ((("s1_group", mods[:2]), ("s1_group_tail", mods[2:])) if split
+                                  else (("s1_group", mods),)):
+                    w = torch.cat([m.conv.weight for m in part], 0)
+                    folded = [m.folded_bn() for m in part]
+                    scale = torch.cat([f[0] for f in folded]).contiguous()
+                    shift = torch.cat([f[1] for f in folded]).contiguous()
+                    self.p[f"cells.{i}.{key}"] = _conv_params(part[0], w, (scale, shift))
                 self.s1_group[i] = group
             # a cell that resamples s1, followed by a same-level cell: the next cell's s0
             # is this s1 (Cell.forward returns prev_input, skip_model_3d.py:75) at the same
@@ -166,9 +174,11 @@ class CellGraphExecutor:
             for name, p in self.p.items():
                 if p.kind != "3d" or not kernels.wino_eligible(p.cout, p.cin, p.k):
                     continue
-                if name.endswith("s1_group"):
+                if name.endswith("s1_group") or name.endswith("s1_group_tail"):
                     i = int(name.split(".")[1])
                     mods = [self.m.cells[i]._ops[op] for _, op in self.s1_group[i]]
+                    if f"cells.{i}.s1_group_tail" in self.p:
+                        mods = mods[2:] if name.endswith("_tail") else mods[:2]
                     w = torch.cat([m.conv.weight for m in mods], 0)
                 else:
                     w = self.m.get_submodule(name).conv.weight
@@ -244,7 +254,11 @@ class CellGraphExecutor:
         written = set()
         if group:  # ops on s1 of every step, one launch, straight into their slots
             k0 = 2 + group[0][0] - (n_states - bm)
-            self.conv(f"cells.{i}.s1_group", s1, out=self._channels(out, k0 * c, (k0 + len(group)) * c))
+            if f"cells.{i}.s1_group_tail" in self.p:
+                self.conv(f"cells.{i}.s1_group", s1, out=self._channels(out, k0 * c, (k0 + 2) * c))
+                self.conv(f"cells.{i}.s1_group_tail", s1, out=self._channels(out, (k0 + 2) * c, (k0 + 3) * c))
+            else:
+                self.conv(f"cells.{i}.s1_group", s1, out=self._channels(out, k0 * c, (k0 + len(group)) * c))
             written = {k for k, _ in group}
         done = set(group)
         for step, terms in enumerate(cell.plan):
@@ -272,6 +286,8 @@ class CellGraphExecutor:
 
 
 class MatchingExecutor(CellGraphExecutor):
+    SPLIT_S1_GROUP48 = os.environ.get("LEASTEREO_SPLIT_GROUP48", "1") != "0"
+
     def run(self, x):
         """newMatching.forward (skip_model_3d.py:140-174): [B,64,D3,H3,W3] -> [B,1,D3,H3,W3]."""
         return self._from_stem0(self.conv("stem0", x))
@@ -370,6 +386,8 @@ class MatchingExecutorDirect(MatchingExecutor):
     cost volume in place (no factored 2D maps) and no layer runs Winograd.  An
     independent algorithm for the same f32 arithmetic, used by bench.py as the
     per-pair cross-check of every rank's shard (precision "f32_direct")."""
+
+    SPLIT_S1_GROUP48 = False
 
     def __init__(self, matching):
         super().__init__(matching)
@@ -507,6 +525,8 @@ class MatchingExecutorBF16(_C8Layout, MatchingExecutor):
     ([B, C/8, D, H, W, 8] bfloat16), convs on the bf16 matrix cores with f32
     accumulation and the f32 BN epilogue; the head's output (the matching cost)
     is f32 for the disparity regression.  Same graph as MatchingExecutor."""
+
+    SPLIT_S1_GROUP48 = False
 
     def __init__(self, matching):
         from .model import ConvBR

@@ -23,6 +23,7 @@ LAYERS = {
     "stem1_32to32_k3_L0": (32, 32, 3, L0, 1),
     "conv12_128to64_k3_L1": (128, 64, 3, L1, 2),
     "cell_16to48_k3_L1_s1grp": (16, 48, 3, L1, 6),
+    "cell_16to32_k3_L1_s1grp2": (16, 32, 3, L1, 0),  # (a candidate split of the 16->48 group)
     "cell_16to16_k3_L1": (16, 16, 3, L1, 18, True),
     "cell_32to96_k3_L2_s1grp": (32, 96, 3, L2, 5),
     "cell_32to32_k3_L2": (32, 32, 3, L2, 15, True),
