@@ -44,6 +44,17 @@ int lea_conv3d_bf16_set_stream1x1(int on);
  * (4 when up-sampling, else 1) (tools/resample_probe.py). */
 int lea_resample_bf16_set_batch(int k);
 
+/* Disparity regression: 1 (default) = the register kernel (D3 plane values in registers,
+ * compile-time depth axis, no rescaling softmin) for the configured (D3, maxdisp) pairs
+ * (4, 12), (8, 24), (16, 48), (32, 96), (64, 192); 0 = the online-softmin kernel for every
+ * shape. */
+int lea_disparity_set_register_form(int on);
+
+/* Head tap-sum pass 2: 1 (default) = row-staged (R output rows' low-res source rows of the
+ * 9 maps in LDS, when they fit 64 KB), 0 = one workgroup per output row gathering through
+ * the L1.  Identical bits. */
+int lea_tapsum_set_rows(int on);
+
 /* Winograd entries: tile override (np in {1, 2} tile rows per wave, td in {1, 2}
  * planes, f in {0 = planner, 2, 4, 8 = F(4,3) on 32-wide row pairs}; np = 0 resets;
  * depth-paired shapes keep np = 1, td = 2 and F(4,3)). */

@@ -68,6 +68,8 @@ SIGNATURES = {
     "lea_resample3d_trilinear_bf16": (_i, [_p, _i64, _p, _i64, _i, _i, _i, _i, _i, _i, _i, _i,
                                            _i, _p, _p, _u, _p]),
     "lea_resample_bf16_set_batch": (_i, [_i]),
+    "lea_disparity_set_register_form": (_i, [_i]),
+    "lea_tapsum_set_rows": (_i, [_i]),
     "lea_conv1x1_resampled_bf16": (_i, [_p, _i64, _i, _i, _i, _p, _p, _p, _p, _i64, _i, _i, _i, _i, _i,
                                         _i, _u, _p]),
     "lea_to_c8_bf16": (_i, [_p, _i64, _p, _i64, _i, _i, _i64, _p]),
@@ -143,7 +145,9 @@ TUNING_ENV = {"LEASTEREO_WINO2_WALK": "lea_conv3d_wino2_set_walk",
               "LEASTEREO_EPI_BUF": "lea_conv3d_wino_set_epi_buf",
               "LEASTEREO_RS_GATHER": "lea_conv3d_set_rs_gather",
               "LEASTEREO_BF16_1X1": "lea_conv3d_bf16_set_stream1x1",
-              "LEASTEREO_RESAMPLE_K": "lea_resample_bf16_set_batch"}
+              "LEASTEREO_RESAMPLE_K": "lea_resample_bf16_set_batch",
+              "LEASTEREO_DISP_REG": "lea_disparity_set_register_form",
+              "LEASTEREO_TAPSUM_ROWS": "lea_tapsum_set_rows"}
 
 
 def _apply_env_tuning(lib):

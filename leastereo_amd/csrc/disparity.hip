@@ -117,7 +117,65 @@ __global__ __launch_bounds__(kDispThreads) void disparity_f32(const float* __res
   disp[((long long)b * Ho + oh) * Wo + ow] = t / s;
 }
 
+// Register form for the configured depths (r03): D3 and maxdisp compile-time, so the
+// thread keeps its D3 bilinearly interpolated plane values v[dd] in registers, the
+// depth axis (i0, i1, l0, l1 of every od) folds to constants, and the softmin needs
+// no running-minimum rescale: every U[od] is a convex combination of two v's, so
+// m = min_dd v[dd] <= min_od U[od] and sum_od e^(m - U) >= e^(m - min U) > 0 -- the same
+// ratio t / s as the reference's softmax(-U) (max-subtracted), no divergent branch, no LDS.
+template <int D3, int MD, bool FAST>
+__global__ __launch_bounds__(kDispThreads) void disparity_reg_f32(const float* __restrict__ cost,
+                                                                  float* __restrict__ disp, int H3, int W3,
+                                                                  float rh, float rw) {
+#pragma clang fp contract(off)
+  const int Ho = 3 * H3, Wo = 3 * W3;
+  const int ow = blockIdx.x * blockDim.x + threadIdx.x;
+  if (ow >= Wo) return;
+  const int oh = blockIdx.y;
+  const int b = blockIdx.z;
+  const AxisW ah = src_axis(rh, oh, H3, Ho);
+  const AxisW aw = src_axis(rw, ow, W3, Wo);
+  const long long HW = (long long)H3 * W3;
+  const float* base = cost + (long long)b * D3 * HW;
+  const float* r0 = base + (long long)ah.i0 * W3;
+  const float* r1 = base + (long long)ah.i1 * W3;
+  float v[D3];
+#pragma unroll
+  for (int dd = 0; dd < D3; ++dd) {
+    const long long o = (long long)dd * HW;
+    v[dd] = ah.l0 * (aw.l0 * r0[o + aw.i0] + aw.l1 * r0[o + aw.i1]) +
+            ah.l1 * (aw.l0 * r1[o + aw.i0] + aw.l1 * r1[o + aw.i1]);
+    // 8 planes' loads (32) in flight at a time: issuing all 4 * D3 first took 256 VGPRs
+    if (dd % 8 == 7) __builtin_amdgcn_sched_barrier(0);
+  }
+  float m = v[0];
+#pragma unroll
+  for (int dd = 1; dd < D3; ++dd) m = fminf(m, v[dd]);
+  constexpr float rd = (float)D3 / (float)MD;
+  float s = 0.f, t = 0.f;
+#pragma unroll
+  for (int od = 0; od < MD; ++od) {
+    const AxisW ad = src_axis(rd, od, D3, MD);  // constants after unrolling
+    const float u = ad.l0 * v[ad.i0] + ad.l1 * v[ad.i1];
+    const float e = dexp<FAST>(m - u);
+    s += e;
+    t += (float)od * e;
+  }
+  disp[((long long)b * Ho + oh) * Wo + ow] = t / s;
+}
+
 }  // namespace lea
+
+// lea_disparity_set_register_form: 1 (default) = the register kernel for the configured
+// (D3, maxdisp), 0 = the online-softmin kernel everywhere (A/B and tests)
+static int g_disp_reg = 1;
+extern "C" int lea_disparity_set_register_form(int on) {
+  using namespace lea;
+  clear_error();
+  LEA_CHECK_ARG(on == 0 || on == 1, "lea_disparity_set_register_form: %d", on);
+  g_disp_reg = on;
+  return 0;
+}
 
 extern "C" int lea_disparity_regression(const void* cost, float* disp, int B, int D3, int H3,
                                         int W3, int maxdisp, int dtype, void* stream) {
@@ -137,6 +195,20 @@ extern "C" int lea_disparity_regression(const void* cost, float* disp, int B, in
   LEA_CHECK_ARG(lds <= 65536, "lea_disparity_regression: maxdisp %d too large", maxdisp);
   dim3 block(kDispThreads);
   dim3 grid((Wo + kDispThreads - 1) / kDispThreads, 3 * H3, B);
+  const float rh = (float)H3 / (float)(3 * H3), rw = (float)W3 / (float)(3 * W3);
+  const bool fast = dtype == LEA_BF16;
+#define LEA_DISP_REG(D3_, MD_)                                                                          \
+  if (D3 == D3_ && maxdisp == MD_) {                                                                   \
+    auto k_ = fast ? disparity_reg_f32<D3_, MD_, true> : disparity_reg_f32<D3_, MD_, false>;            \
+    k_<<<grid, block, 0, as_stream(stream)>>>((const float*)cost, disp, H3, W3, rh, rw);                 \
+    return launch_status("lea_disparity_regression");                                                  \
+  }
+  if (g_disp_reg) {
+    // (88, 264) -- config 5 -- stays on the LDS kernel: its 88 plane values take all 256
+    // VGPRs, one wave per SIMD (r03: 0.388 vs 0.380 ms); at (64, 192): 0.125 -> 0.081 ms
+    LEA_DISP_REG(4, 12) LEA_DISP_REG(8, 24) LEA_DISP_REG(16, 48) LEA_DISP_REG(32, 96) LEA_DISP_REG(64, 192)
+  }
+#undef LEA_DISP_REG
   auto kern = dtype == LEA_BF16 ? disparity_f32<true> : disparity_f32<false>;
   kern<<<grid, block, lds, as_stream(stream)>>>(
       (const float*)cost, disp, D3, H3, W3, maxdisp, (float)D3 / (float)maxdisp,

@@ -172,7 +172,101 @@ __global__ __launch_bounds__(512) void tapsum_hwpass_f32(
   }
 }
 
+// pass 2, row-staged (r03): a workgroup owns R output rows of one plane; the <= nrmax
+// low-res rows of the 9 (kh, kw) maps they read are copied into LDS once (coalesced),
+// then every output sums its 36 corner values from LDS instead of gathering them through
+// the L1 (36 loads per output).  Same expression and order as tapsum_hwpass_f32: the two
+// produce identical bits.
+__global__ __launch_bounds__(256) void tapsum_hwpass_rows_f32(
+    const float* __restrict__ ws, float* __restrict__ y, long long ybs, int cout, int Hi, int Wi,
+    int Do, int Ho, int Wo, float rh, float rw, const float* __restrict__ scale,
+    const float* __restrict__ shift, unsigned flags, int R, int nrmax) {
+#pragma clang fp contract(off)
+  extern __shared__ float rows[];  // [9][nrmax][Wi]
+  const int plane = blockIdx.y;    // (b * cout + co) * Do + d
+  const int co = (plane / Do) % cout;
+  const int b = plane / (Do * cout);
+  const int d = plane % Do;
+  const int h0 = blockIdx.x * R;
+  const int h1 = min(h0 + R, Ho);
+  const int r_lo = axis_index(rh, max(h0 - 1, 0), Hi, Ho, 1).i0;
+  const int r_hi = axis_index(rh, min(h1, Ho - 1), Hi, Ho, 1).i1;
+  const int nr = r_hi - r_lo + 1;  // <= nrmax (host bound)
+  const long long HWi = (long long)Hi * Wi;
+  const float* yp = ws + (long long)plane * 9 * HWi + (long long)r_lo * Wi;
+  const int n1 = nr * Wi;
+  for (int e = threadIdx.x; e < 9 * n1; e += blockDim.x) {
+    const int k = e / n1, r = e - k * n1;
+    rows[k * nrmax * Wi + r] = yp[(long long)k * HWi + r];
+  }
+  __syncthreads();
+  const float sc = scale ? scale[co] : 1.f, sh = scale ? shift[co] : 0.f;
+  const int cells = (h1 - h0) * Wo;
+  for (int t = threadIdx.x; t < cells; t += blockDim.x) {
+    const int h = h0 + t / Wo, w = t % Wo;
+    Axis ah[3];
+    bool hok[3];
+#pragma unroll
+    for (int kh = 0; kh < 3; ++kh) {
+      const int p = h + kh - 1;
+      hok[kh] = (unsigned)p < (unsigned)Ho;
+      ah[kh] = axis_index(rh, hok[kh] ? p : 0, Hi, Ho, 1);
+    }
+    float acc = 0.f;
+#pragma unroll
+    for (int kw = 0; kw < 3; ++kw) {
+      const int p = w + kw - 1;
+      if ((unsigned)p >= (unsigned)Wo) continue;
+      const Axis aw = axis_index(rw, p, Wi, Wo, 1);
+#pragma unroll
+      for (int kh = 0; kh < 3; ++kh) {
+        if (!hok[kh]) continue;
+        const float* tm = rows + (kh * 3 + kw) * nrmax * Wi;
+        const float* r0 = tm + (ah[kh].i0 - r_lo) * Wi;
+        const float* r1 = tm + (ah[kh].i1 - r_lo) * Wi;
+        acc += ah[kh].l0 * (aw.l0 * r0[aw.i0] + aw.l1 * r0[aw.i1]) +
+               ah[kh].l1 * (aw.l0 * r1[aw.i0] + aw.l1 * r1[aw.i1]);
+      }
+    }
+    if (scale) acc = acc * sc + sh;
+    if (flags & LEA_RELU) acc = fmaxf(acc, 0.f);
+    y[(long long)b * ybs + (((long long)co * Do + d) * Ho + h) * Wo + w] = acc;
+  }
+}
+
 }  // namespace lea
+
+// lea_tapsum_set_rows: 1 (default) = the row-staged pass 2 when R output rows' sources
+// fit 64 KB of LDS, 0 = one workgroup per output row gathering through the L1
+static int g_tapsum_rows = 1;
+extern "C" int lea_tapsum_set_rows(int on) {
+  lea::clear_error();
+  LEA_CHECK_ARG(on == 0 || on == 1, "lea_tapsum_set_rows: %d", on);
+  g_tapsum_rows = on;
+  return 0;
+}
+
+static int hwpass(const float* ws, void* y, int64_t y_bstride, int B, int cout, int Hi, int Wi, int Do,
+                  int Ho, int Wo, const float* scale, const float* shift, unsigned flags, hipStream_t st) {
+  using namespace lea;
+  const float rh = axis_ratio(Hi, Ho, 1), rw = axis_ratio(Wi, Wo, 1);
+  if (g_tapsum_rows) {
+    for (int R = 8; R >= 2; R /= 2) {
+      const int nrmax = (int)floorf((float)(R + 1) * rh) + 3;  // rows h0-1 .. h0+R, +1 fp margin
+      const size_t lds = (size_t)9 * nrmax * Wi * sizeof(float);
+      if (lds > 65536) continue;
+      dim3 g((unsigned)((Ho + R - 1) / R), (unsigned)(B * cout * Do));
+      tapsum_hwpass_rows_f32<<<g, 256, lds, st>>>(ws, (float*)y, y_bstride, cout, Hi, Wi, Do, Ho, Wo, rh, rw,
+                                                  scale, shift, flags, R, nrmax);
+      return launch_status("lea_tapsum_upsample");
+    }
+  }
+  const int threads = Wo >= 512 ? 512 : ((Wo + 63) / 64) * 64;  // one row per workgroup
+  dim3 g2((unsigned)((long long)B * cout * Do * Ho));
+  tapsum_hwpass_f32<<<g2, threads, 0, st>>>(ws, (float*)y, y_bstride, cout, Hi, Wi, Do, Ho, Wo, rh, rw, scale,
+                                            shift, flags);
+  return launch_status("lea_tapsum_upsample");
+}
 
 extern "C" size_t lea_tapsum_workspace_bytes(int B, int cout, int Hi, int Wi, int Do) {
   if (B <= 0 || cout <= 0 || Hi <= 0 || Wi <= 0 || Do <= 0) return 0;
@@ -207,12 +301,7 @@ extern "C" int lea_tapsum_upsample(const void* q, int64_t q_bstride, void* y, in
                                         axis_ratio(Di, Do, 1));
     const int rc = launch_status("lea_tapsum_upsample");
     if (rc) return rc;
-    const int threads = Wo >= 512 ? 512 : ((Wo + 63) / 64) * 64;
-    dim3 g2((unsigned)((long long)B * cout * Do * Ho));
-    tapsum_hwpass_f32<<<g2, threads, 0, st>>>(ws, (float*)y, y_bstride, cout, Hi, Wi, Do, Ho, Wo,
-                                              axis_ratio(Hi, Ho, 1), axis_ratio(Wi, Wo, 1), scale,
-                                              shift, flags);
-    return launch_status("lea_tapsum_upsample");
+    return hwpass(ws, y, y_bstride, B, cout, Hi, Wi, Do, Ho, Wo, scale, shift, flags, st);
   }
   const bool vec = (HWi % 4) == 0 && ((uintptr_t)q % 16) == 0 && (q_bstride % 4) == 0 &&
                    ((long long)Di * HWi) % 4 == 0 && ((uintptr_t)ws % 16) == 0;
@@ -225,10 +314,5 @@ extern "C" int lea_tapsum_upsample(const void* q, int64_t q_bstride, void* y, in
     tapsum_dpass_f32<false><<<g1, 256, 0, st>>>((const float*)q, q_bstride, ws, cout, Di, Hi, Wi, Do, rd);
   const int rc = launch_status("lea_tapsum_upsample");
   if (rc) return rc;
-  const int threads = Wo >= 512 ? 512 : ((Wo + 63) / 64) * 64;  // one row per workgroup
-  dim3 g2((unsigned)((long long)B * cout * Do * Ho));
-  tapsum_hwpass_f32<<<g2, threads, 0, st>>>(ws, (float*)y, y_bstride, cout, Hi, Wi, Do, Ho, Wo,
-                                            axis_ratio(Hi, Ho, 1), axis_ratio(Wi, Wo, 1), scale,
-                                            shift, flags);
-  return launch_status("lea_tapsum_upsample");
+  return hwpass(ws, y, y_bstride, B, cout, Hi, Wi, Do, Ho, Wo, scale, shift, flags, st);
 }

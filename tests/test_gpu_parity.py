@@ -245,6 +245,25 @@ def test_head_tapsum_upsample_vs_torch(cout, cin, src, dst):
     np.testing.assert_allclose(out.numpy(), refy.numpy(), rtol=1e-4, atol=1e-4)
 
 
+@pytest.mark.parametrize("b,cout,src,dst", [(1, 1, (32, 96, 160), (64, 192, 320)), (2, 2, (3, 5, 9), (5, 9, 17)),
+                                           (1, 1, (4, 13, 7), (8, 26, 14)), (1, 1, (16, 48, 252), (32, 96, 504))])
+def test_head_tapsum_rows_pass_is_the_gather_pass(b, cout, src, dst):
+    """The row-staged pass 2 of the tap-sum head (the default) and the per-row gather pass
+    produce identical bits, f32 and bf16 (c8) partial sums alike."""
+    lib = _lib.load()
+    g = torch.Generator().manual_seed(13)
+    q = torch.randn((b, 27 * cout) + src, generator=g).to(DEV)
+    qc = kernels.to_c8(torch.cat([q, torch.zeros((b, (-27 * cout) % 8) + src, device=DEV)], 1))
+    out = {}
+    for on in (1, 0):
+        assert lib.lea_tapsum_set_rows(on) == 0
+        try:
+            out[on] = (kernels.tapsum_upsample(q, cout, dst), kernels.tapsum_upsample_bf16(qc, cout, dst))
+        finally:
+            lib.lea_tapsum_set_rows(1)
+    assert torch.equal(out[1][0], out[0][0]) and torch.equal(out[1][1], out[0][1])
+
+
 def test_resample_affine_relu_epilogue_into_slice():
     g = torch.Generator().manual_seed(11)
     x = torch.randn(2, 8, 4, 6, 10, generator=g)
@@ -295,6 +314,28 @@ def test_disparity_vs_oracle_sizes():
         # fp32 sums over maxdisp terms: error grows ~ md * 2^-24 * disparity; bar is 1e-3 px EPE
         err = np.abs(y.double().numpy() - refd.numpy())
         assert err.max() < 2e-3 and err.mean() < 1e-4, (err.max(), err.mean())
+
+
+@pytest.mark.parametrize("shape,md", [((1, 1, 64, 12, 20), 192), ((2, 1, 32, 9, 13), 96), ((1, 1, 16, 7, 4), 48),
+                                      ((1, 1, 8, 5, 6), 24)])
+def test_disparity_register_form_matches_the_lds_form(shape, md):
+    """The register disparity kernel (D3 plane values in registers, compile-time depth
+    axis, softmin shifted by the smallest plane value) and the online-softmin LDS kernel
+    agree to fp32 summation noise, and both meet the oracle at the 1e-3 px bar."""
+    lib = _lib.load()
+    g = torch.Generator().manual_seed(11)
+    x = torch.randn(shape, generator=g) * 3
+    refd = ref.disp_forward(x.double(), md).numpy()
+    out = {}
+    for on in (1, 0):
+        assert lib.lea_disparity_set_register_form(on) == 0
+        try:
+            out[on] = kernels.disparity_regression(x.to(DEV), md).cpu().double().numpy()
+        finally:
+            lib.lea_disparity_set_register_form(1)
+        err = np.abs(out[on] - refd)
+        assert err.max() < 2e-3 and err.mean() < 1e-4, (on, err.max(), err.mean())
+    assert np.abs(out[1] - out[0]).max() < 1e-3
 
 
 @pytest.mark.parametrize("b,c,cout,maxdisp,hw", [(2, 32, 32, 48, (12, 40)), (1, 4, 16, 27, (5, 7)),
