@@ -403,6 +403,7 @@ def run(args, info):
             with kernels.KernelProbe([dominant]) as probe:
                 model(left, right)
         dom = probe.summary()[dominant]
+        dom_shapes = probe.by_shape(dominant)
         step_ms = sorted(ev[i].elapsed_time(ev[i + 1]) for i in range(args.steps))
     elapsed = parallel.max_over_ranks(elapsed, device)
 
@@ -475,6 +476,12 @@ def run(args, info):
                              "padded to its blocks); DESIGN.md §4 gives the per-launch formula",
                      "flops_per_launch": issued, "ms_per_launch": ms_per_launch,
                      "launches_per_step": launches / args.steps,
+                     "by_shape": [{"shape": "B%d %d->%d @ %dx%dx%d k%d" % sh if sh else None,
+                                   "launches_per_step": d["launches"] / args.steps,
+                                   "ms_per_launch": d["ms"] / d["launches"],
+                                   "issued_tflops": d["mfma_flops"] / d["ms"] / 1e9,
+                                   "frac": d["mfma_flops"] / d["ms"] / 1e9 / peak}
+                                  for sh, d in sorted(dom_shapes.items(), key=lambda kv: -kv[1]["ms"])],
                      "direct_equivalent": {"flops_per_launch": direct,
                                            "achieved": direct / (ms_per_launch * 1e-3) / 1e12,
                                            "note": "the reference algorithm's (direct convolution's) "

@@ -53,6 +53,21 @@ class KernelProbe:
             d["mfma_flops"] += mfma
         return out
 
+    def by_shape(self, name):
+        """Launches of kernel ``name`` grouped by layer shape (B, cin, cout, D, H, W, k)."""
+        torch.cuda.synchronize()
+        out = {}
+        for n, flops, nbytes, e0, e1, mfma, shape in self.records:
+            if n != name:
+                continue
+            d = out.setdefault(shape, {"launches": 0, "flops": 0.0, "bytes": 0.0, "ms": 0.0, "mfma_flops": 0.0})
+            d["launches"] += 1
+            d["flops"] += flops
+            d["bytes"] += nbytes
+            d["ms"] += e0.elapsed_time(e1)
+            d["mfma_flops"] += mfma
+        return out
+
 
 _probe = None
 
