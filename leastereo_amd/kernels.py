@@ -245,8 +245,8 @@ def conv3d_bnrelu_costvolume(fl: torch.Tensor, fr: torch.Tensor, maxdisp: int, p
     b, c, h, w = fl.shape
     d3 = int(maxdisp / 3)
     out = torch.empty((b, cout, d3, h, w), device=fl.device, dtype=fl.dtype)
-    rec = _probe_begin(b, 2 * c, cout, d3, h, w, 3, False, 0, False,
-                       name=costvolume_kernel_name(b, cout, d3, h, w))
+    rec = None if _probe is None else _probe_begin(b, 2 * c, cout, d3, h, w, 3, False, 0, False,
+                                                   name=costvolume_kernel_name(b, cout, d3, h, w))
     check(_lib.load().lea_conv3d_bnrelu_costvolume(
         fl.data_ptr(), fr.data_ptr(), fl.stride(0), packed.data_ptr(),
         scale.data_ptr() if scale is not None else None,
@@ -570,8 +570,9 @@ def conv3d_bnrelu_bf16(x: torch.Tensor, packed: torch.Tensor, cout: int, k: int,
     else:
         rptr, rbs = None, 0
     flags = (LEA_RELU if relu else 0) | (LEA_RESIDUAL if rptr is not None else 0)
-    rec = _probe_begin(b, cb * 8 + cin2, cout, d, h, w, k, rptr is not None, b * d * h * w, False,
-                       name=conv_kernel_name_bf16(b, cout, cb * 8 + cin2, d, h, w, k), esz=2)
+    rec = None if _probe is None else _probe_begin(
+        b, cb * 8 + cin2, cout, d, h, w, k, rptr is not None, b * d * h * w, False,
+        name=conv_kernel_name_bf16(b, cout, cb * 8 + cin2, d, h, w, k), esz=2)
     check(_lib.load().lea_conv3d_bnrelu_bf16(
         x.data_ptr(), xbs, x2.data_ptr() if x2 is not None else None, x2bs, cin2, packed.data_ptr(),
         scale.data_ptr() if scale is not None else None,
@@ -620,8 +621,9 @@ def conv3d_bnrelu_costvolume_bf16(fl: torch.Tensor, fr: torch.Tensor, maxdisp: i
     b, cb, _, h, w, _ = fl.shape
     d3 = int(maxdisp / 3)
     out = torch.empty((b, cout // 8, d3, h, w, 8), device=fl.device, dtype=torch.bfloat16)
-    rec = _probe_begin(b, 2 * cb * 8, cout, d3, h, w, 3, False, 0, False,
-                       name=conv_kernel_name_bf16(b, cout, 2 * cb * 8, d3, h, w, 3, True), esz=2)
+    rec = None if _probe is None else _probe_begin(
+        b, 2 * cb * 8, cout, d3, h, w, 3, False, 0, False,
+        name=conv_kernel_name_bf16(b, cout, 2 * cb * 8, d3, h, w, 3, True), esz=2)
     check(_lib.load().lea_conv3d_bnrelu_costvolume_bf16(
         fl.data_ptr(), fr.data_ptr(), fbs, packed.data_ptr(),
         scale.data_ptr() if scale is not None else None,
@@ -945,9 +947,11 @@ def conv3d_bnrelu_wino(x: torch.Tensor, packed: torch.Tensor, cout: int,
     out, ybs = _conv_out(x.shape, cout, (d, h, w), out, accumulate, x.device, x.dtype)
     rptr, rbs = _residual(out, accumulate, residual, ybs)
     flags = (LEA_RELU if relu else 0) | (LEA_RESIDUAL if rptr is not None else 0)
-    name = wino_kernel_name(b, cout, d, h, w, cin=cin + cin2)
-    rec = _probe_begin(b, cin + cin2, cout, d, h, w, 3, rptr is not None, b * d * h * w, False,
-                       name=name, mfma_scale=wino_mfma_scale(cout, name))
+    rec = None
+    if _probe is not None:  # (the kernel-name query only when a probe listens)
+        name = wino_kernel_name(b, cout, d, h, w, cin=cin + cin2)
+        rec = _probe_begin(b, cin + cin2, cout, d, h, w, 3, rptr is not None, b * d * h * w, False,
+                           name=name, mfma_scale=wino_mfma_scale(cout, name))
     check(_lib.load().lea_conv3d_bnrelu_wino(
         x.data_ptr(), xbs, x2.data_ptr() if x2 is not None else None, x2bs, cin2,
         packed.data_ptr(),
@@ -972,9 +976,11 @@ def conv3d_bnrelu_costvolume_wino(fl: torch.Tensor, fr: torch.Tensor, maxdisp: i
     b, c, h, w = fl.shape
     d3 = int(maxdisp / 3)
     out = torch.empty((b, cout, d3, h, w), device=fl.device, dtype=fl.dtype)
-    name = wino_kernel_name(b, cout, d3, h, w, True, cin=2 * c)
-    rec = _probe_begin(b, 2 * c, cout, d3, h, w, 3, False, 0, False,
-                       name=name, mfma_scale=wino_mfma_scale(cout, name))
+    rec = None
+    if _probe is not None:
+        name = wino_kernel_name(b, cout, d3, h, w, True, cin=2 * c)
+        rec = _probe_begin(b, 2 * c, cout, d3, h, w, 3, False, 0, False,
+                           name=name, mfma_scale=wino_mfma_scale(cout, name))
     check(_lib.load().lea_conv3d_bnrelu_costvolume_wino(
         fl.data_ptr(), fr.data_ptr(), fl.stride(0), packed.data_ptr(),
         scale.data_ptr() if scale is not None else None,
