@@ -28,6 +28,7 @@ LAYERS = {
     "cell_32to96_k3_L2_s1grp": (32, 96, 3, L2, 5),
     "cell_32to32_k3_L2": (32, 32, 3, L2, 15, True),
     "cell_8to24_k3_L0_s1grp": (8, 24, 3, L0, 1),
+    "cell_8to16_k3_L0_s1grp2": (8, 16, 3, L0, 0),  # (a candidate split of the 8->24 group)
     "cell_8to8_k3_L0": (8, 8, 3, L0, 3, True),
     "last3_32to1_k3_L0": (32, 1, 3, L0, 1),
     "pre_64to8_k1_L1": (64, 8, 1, L1, 2),

@@ -4,11 +4,17 @@
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
-mkdir -p gpurun_out
-timeout -k 10 600 python3 -u -m pytest tests/test_gpu_parity.py tests/test_gpu_bench.py -x -q -m gpu --timeout 200 --timeout-method thread -k "e2e or full or bench or c1" > gpurun_out/t_q.log 2>&1
-rc=$?; tail -2 gpurun_out/t_q.log; [ $rc -eq 0 ] || exit $rc
-for r in 1 2 3; do
-  timeout -k 10 300 python3 bench.py --steps 20 --warmup 5 --cpu-baseline 0 --epe 0 --pair-check 0 > gpurun_out/q.json 2> gpurun_out/q.err
-  rc=$?; [ $rc -eq 0 ] || { tail -5 gpurun_out/q.err; exit $rc; }
-  python3 -c "import json; d=json.load(open('gpurun_out/q.json')); print('c2', round(d['value'],1), round(d['step_ms']['median'],3), round(d['roofline']['frac'],3))"
+mkdir -p gpurun_out/abl
+for n in w1base q16 w1base q16; do
+  LEASTEREO_HIP_LIB=leastereo_amd/var_$n.so timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv \
+    -d gpurun_out/abl/$n -o run -- python3 tools/wino2_sweep.py --variants 0 --iters 20 --only cell_16to16_k3_L1,cell_16to32_k3_L1_s1grp2 \
+    > gpurun_out/abl/$n.log 2>&1
+  rc=$?; [ $rc -eq 0 ] || { echo "$n rc=$rc"; tail -3 gpurun_out/abl/$n.log; exit $rc; }
+  f=$(ls gpurun_out/abl/$n/*kernel_stats.csv | head -1)
+  python3 -c "
+import csv
+for r in csv.DictReader(open('$f')):
+    if 'wino2' in r['Name'] and 'pack' not in r['Name']: print('$n', r['Name'][:70], 'calls', r['Calls'], 'avg_us', round(float(r['AverageNs'])/1e3,1))
+"
+  rm -rf gpurun_out/abl/$n
 done
