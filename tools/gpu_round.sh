@@ -22,8 +22,8 @@ for ctr in FETCH_SIZE WRITE_SIZE; do
 done
 python3 tools/traffic_report.py gpurun_out/traffic/c2_FETCH_SIZE gpurun_out/traffic/c2_WRITE_SIZE gpurun_out/traffic/c2.json | head -6
 python3 -c "import json; o=json.load(open('profiles/hbm_traffic.json')); n=json.load(open('gpurun_out/traffic/c2.json')); o={k: v for k, v in o.items() if '@' in k}; o.update(n); json.dump(o, open('profiles/hbm_traffic.json', 'w'), indent=1, sort_keys=True)"
-bash tools/gpu_traffic_bf16.sh || exit $?
-for c in c3 c4; do python3 tools/traffic_merge.py $c gpurun_out/traffic_$c.json; done
+CONFIGS="c3 c4 c5" bash tools/gpu_traffic_bf16.sh || exit $?
+for c in c3 c4 c5; do python3 tools/traffic_merge.py $c gpurun_out/traffic_$c.json; done
 cp profiles/hbm_traffic.json gpurun_out/traffic/hbm_traffic_merged.json
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_$TAG -o run -- \
   python3 bench.py --steps 5 --warmup 2 --cpu-baseline 0 --epe 0 --pair-check 0 > gpurun_out/prof_$TAG.json 2> gpurun_out/prof_$TAG.err

@@ -1,11 +1,12 @@
 #!/bin/bash
 # HBM traffic passes (FETCH_SIZE, WRITE_SIZE: one rocprofv3 --pmc run each) over the
-# c3 and c4 bf16 benches -> gpurun_out/traffic_<cfg>.json (merge: tools/traffic_merge.py)
+# benches of CONFIGS (default: the c3 and c4 bf16 ones) -> gpurun_out/traffic_<cfg>.json
+# (merge: tools/traffic_merge.py)
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 mkdir -p gpurun_out/traffic_bf16
-for c in c3 c4; do
+for c in ${CONFIGS:-c3 c4}; do
   B="python3 bench.py --config $c --steps 2 --warmup 1 --cpu-baseline 0 --epe 0 --pair-check 0"
   for ctr in FETCH_SIZE WRITE_SIZE; do
     timeout -k 10 300 rocprofv3 --pmc $ctr --kernel-trace --output-format csv -d gpurun_out/traffic_bf16/${c}_$ctr -o run -- $B \
