@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define LEA_ABI_VERSION 9
+#define LEA_ABI_VERSION 10
 
 #define LEA_F32 0
 #define LEA_BF16 1
@@ -337,6 +337,50 @@ int lea_disparity_metrics(const float* pred, int64_t pred_bstride, const float* 
                           int64_t gt_bstride, int B, int H, int W, float maxdisp, int round_pred,
                           int z_shift, int thr1, int thr2, int thr3, unsigned char* correct,
                           double* out, void* workspace, void* stream);
+
+/* ---- training backward of ConvBR3d (operations_3d.py:31-47
+ * as train.py:130-178 runs it: BatchNorm3d in train mode) ----
+ * All tensors NCDHW contiguous fp32, V = D*H*W.  Composition (csrc/conv3d_grad.hip):
+ *   forward  z = lea_conv3d_bnrelu(x, w; no scale/shift, flags 0)
+ *            y = lea_bn_forward_f32(z)
+ *   backward dz = lea_bn_backward_f32(dy, y, z)
+ *            dx = lea_conv3d_bnrelu(dz, pack(lea_conv3d_flip_weights(w)); flags 0)
+ *            dw = lea_conv3d_wgrad(x, dz)                                        */
+
+/* dw[co][ci][kd][kh][kw] = sum_{b,d,h,w} dz[b][co][d][h][w] * x[b][ci][d+kd-k/2][h+kh-k/2][w+kw-k/2]
+ * (zero padding; the weight gradient of a stride-1, pad k/2 Conv3d without bias,
+ * which torch computes in aten's convolution_backward).  dw is overwritten;
+ * workspace: lea_conv3d_wgrad_workspace_bytes(...) bytes (per-wave partials, summed
+ * in a fixed order: the result is deterministic).  k in {1, 3}.                  */
+size_t lea_conv3d_wgrad_workspace_bytes(int B, int cin, int cout, int D, int H, int W, int k);
+int lea_conv3d_wgrad(const float* x, const float* dz, float* dw, void* workspace, size_t ws_bytes,
+                     int B, int cin, int cout, int D, int H, int W, int k, void* stream);
+
+/* wt[ci][co][kd][kh][kw] = w[co][ci][k-1-kd][k-1-kh][k-1-kw]: the input gradient of a
+ * stride-1, pad k/2 conv is the forward conv of dz with this weight.             */
+int lea_conv3d_flip_weights(const float* w, float* wt, int cout, int cin, int k, void* stream);
+
+/* BatchNorm3d + optional ReLU (flags LEA_RELU), operations_3d.py:44-46 in
+ * torch.nn.BatchNorm3d's semantics: training = 1 normalises by the batch mean and
+ * biased variance over (B, D, H, W) and updates running_mean / running_var with
+ * momentum (unbiased variance; both may be NULL to skip the update); training = 0
+ * uses the running stats.  gamma/beta NULL = 1/0.  y = relu((z - mean) * invstd *
+ * gamma + beta); mean/invstd ([C], device) are written for the backward.
+ * workspace: lea_bn_workspace_bytes(C) bytes (train mode).                      */
+size_t lea_bn_workspace_bytes(int C);
+int lea_bn_forward_f32(const float* z, float* y, int B, int C, int64_t V, const float* gamma,
+                       const float* beta, float* running_mean, float* running_var, float momentum,
+                       float eps, int training, unsigned flags, float* mean, float* invstd,
+                       void* workspace, void* stream);
+
+/* Backward of lea_bn_forward_f32: g = dy * [y > 0] (LEA_RELU) or dy;
+ * dbeta = sum g, dgamma = sum g * xhat (xhat = (z - mean) * invstd, either may be NULL);
+ * dz = gamma * invstd * (g - dbeta/N - xhat * dgamma/N) in train mode,
+ * gamma * invstd * g in eval mode (N = B * V).  workspace: lea_bn_workspace_bytes(C). */
+int lea_bn_backward_f32(const float* dy, const float* y, const float* z, float* dz, int B, int C,
+                        int64_t V, const float* gamma, const float* mean, const float* invstd,
+                        int training, unsigned flags, float* dgamma, float* dbeta, void* workspace,
+                        void* stream);
 
 #ifdef __cplusplus
 }

@@ -1,0 +1,421 @@
+// Training backward of the matching net's hot op: ConvBR3d
+// (models/operations_3d.py:31-47) with BatchNorm3d in train mode (batch statistics,
+// running-stat update, as train.py:130-178 runs it) or eval mode, and its gradients.
+//
+//   forward   z = conv3d(x, w)                     (lea_conv3d_bnrelu, no BN, no ReLU)
+//             y = relu(gamma * (z - mean) * invstd + beta)          lea_bn_forward_f32
+//   backward  g  = dy * [y > 0]                     (ReLU mask, when the op has one)
+//             dgamma = sum g * xhat, dbeta = sum g, xhat = (z - mean) * invstd
+//             dz = gamma * invstd * (g - dbeta / N - xhat * dgamma / N)   (train mode)
+//             dz = gamma * invstd * g                                     (eval mode)
+//                                                                   lea_bn_backward_f32
+//             dx = conv3d(dz, flip(w)^T)            (lea_conv3d_flip_weights + the
+//                                                    forward engine: stride 1, pad k/2)
+//             dw = sum_{b, v} dz[co][v] x[ci][v + tap]                lea_conv3d_wgrad
+//
+// Weight gradient: a GEMM with M = cout, N = cin * k^3 and K = B * D * H * W (millions
+// of voxels), on v_mfma_f32_16x16x4f32.  A workgroup owns one (input-channel chunk,
+// 16 * MT couts) block and walks a strided set of 64-voxel row segments (K split over
+// nsplit workgroups): per segment it stages dz[co][64] and the chunk's halo rows
+// x[ci][kd][kh][64 + k - 1] in LDS, and its four waves take a quarter of the segment's
+// 16 K-steps each.  A (lane l) = dz[co = 16 m + (l & 15)][voxel 4 s + (l >> 4)],
+// B (lane l) = x[(tap, ci) = column l & 15][same voxel]; N tile = 4 taps x 4 channels
+// (k = 3: 7 tiles, the 28th tap slot zero) or 16 channels (k = 1).  Each wave stores
+// its partial block once; a second kernel sums the 4 * nsplit partials in a fixed
+// order, so dw is deterministic.  The reductions of the BN statistics are two-level
+// in double (per-slice partials, then a fixed-order sum), also deterministic.
+#include <algorithm>
+
+#include "common.h"
+
+namespace lea {
+namespace grad {
+
+using f32x4 = __attribute__((__vector_size__(4 * sizeof(float)))) float;
+
+constexpr int SEG = 64;   // voxels (along W) per K segment
+constexpr int NWAVE = 4;  // waves per workgroup
+
+template <int KS>
+struct WCfg {
+  static constexpr int TAPS = KS * KS * KS;
+  static constexpr int CI = KS == 3 ? 4 : 16;    // input channels per chunk
+  static constexpr int TPT = 16 / CI;            // taps per 16-column N tile
+  static constexpr int NT = (TAPS + TPT - 1) / TPT;
+  static constexpr int XC = SEG + KS - 1;        // staged columns per halo row
+  static constexpr int XR = KS * KS;             // staged (kd, kh) rows per channel
+  static constexpr int XS = CI * XR * XC;
+};
+
+struct WArgs {
+  const float* x;
+  const float* dz;
+  float* part;
+  int B, cin, cout, D, H, W;
+  int nwseg, nseg, nsplit;
+};
+
+template <int KS, int MT>
+__global__ __launch_bounds__(256) void wgrad_kernel(const WArgs a) {
+  using C = WCfg<KS>;
+  constexpr int NT = C::NT;
+  __shared__ float xs[C::XS];
+  __shared__ float gs[16 * MT * SEG];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int ci0 = blockIdx.y * C::CI, co0 = blockIdx.z * 16 * MT;
+  const long long HW = (long long)a.H * a.W, V = HW * a.D;
+  const int j = lane & 15, kr = lane >> 4;
+
+  // this lane's B column per N tile: (tap, channel) -> LDS offset without the voxel
+  int boff[NT];
+  bool bval[NT];
+#pragma unroll
+  for (int nt = 0; nt < NT; ++nt) {
+    const int tap = nt * C::TPT + j / C::CI, ci = j % C::CI;
+    const int kd = tap / (KS * KS), kh = (tap / KS) % KS, kw = tap % KS;
+    bval[nt] = tap < C::TAPS;
+    boff[nt] = bval[nt] ? (ci * C::XR + kd * KS + kh) * C::XC + kw : 0;
+  }
+  f32x4 acc[MT][NT];
+#pragma unroll
+  for (int m = 0; m < MT; ++m)
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) acc[m][nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  for (int seg = blockIdx.x; seg < a.nseg; seg += a.nsplit) {
+    const int wsg = seg % a.nwseg;
+    int r = seg / a.nwseg;
+    const int h = r % a.H;
+    r /= a.H;
+    const int d = r % a.D, b = r / a.D;
+    const int w0 = wsg * SEG;
+    __syncthreads();  // the previous segment's LDS reads are done
+    for (int e = tid; e < C::XS; e += 256) {
+      const int col = e % C::XC, t = e / C::XC;
+      const int row = t % C::XR, ci = t / C::XR;
+      const int dd = d + row / KS - KS / 2, hh = h + row % KS - KS / 2, ww = w0 + col - KS / 2;
+      const int c = ci0 + ci;
+      float v = 0.f;
+      if (c < a.cin && (unsigned)dd < (unsigned)a.D && (unsigned)hh < (unsigned)a.H && (unsigned)ww < (unsigned)a.W)
+        v = a.x[((long long)b * a.cin + c) * V + dd * HW + (long long)hh * a.W + ww];
+      xs[e] = v;
+    }
+    for (int e = tid; e < 16 * MT * SEG; e += 256) {
+      const int col = e % SEG, co = e / SEG;
+      const int c = co0 + co, ww = w0 + col;
+      gs[e] = (c < a.cout && ww < a.W) ? a.dz[((long long)b * a.cout + c) * V + d * HW + (long long)h * a.W + ww]
+                                       : 0.f;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < SEG / (4 * NWAVE); ++q) {
+      const int v = 4 * (wave + NWAVE * q) + kr;
+      float av[MT];
+#pragma unroll
+      for (int m = 0; m < MT; ++m) av[m] = gs[(16 * m + j) * SEG + v];
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt) {
+        const float bv = bval[nt] ? xs[boff[nt] + v] : 0.f;
+#pragma unroll
+        for (int m = 0; m < MT; ++m) acc[m][nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[m], bv, acc[m][nt], 0, 0, 0);
+      }
+    }
+  }
+  // partial (blockIdx.x, wave): [cout][cin][taps]; this block writes its (chunk, couts) part
+  const long long nw = (long long)a.cout * a.cin * C::TAPS;
+  float* const part = a.part + (long long)(blockIdx.x * NWAVE + wave) * nw;
+#pragma unroll
+  for (int m = 0; m < MT; ++m)
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) {
+      const int tap = nt * C::TPT + j / C::CI, ci = ci0 + j % C::CI;
+#pragma unroll
+      for (int r4 = 0; r4 < 4; ++r4) {
+        const int co = co0 + 16 * m + 4 * kr + r4;
+        if (tap < C::TAPS && ci < a.cin && co < a.cout)
+          part[((long long)co * a.cin + ci) * C::TAPS + tap] = acc[m][nt][r4];
+      }
+    }
+}
+
+__global__ void sum_partials_kernel(const float* __restrict__ part, float* __restrict__ out, long long n, int np) {
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
+    float s = 0.f;
+    for (int p = 0; p < np; ++p) s += part[(long long)p * n + i];
+    out[i] = s;
+  }
+}
+
+__global__ void flip_weights_kernel(const float* __restrict__ w, float* __restrict__ wt, int cout, int cin, int ks) {
+  const int taps = ks * ks * ks;
+  const long long n = (long long)cout * cin * taps;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
+    const int tap = (int)(i % taps);
+    const long long q = i / taps;
+    const int co = (int)(q % cout), ci = (int)(q / cout);  // wt[ci][co][tap]
+    wt[i] = w[((long long)co * cin + ci) * taps + (taps - 1 - tap)];
+  }
+}
+
+// ---- BatchNorm3d statistics: per channel, two double sums over (b, v) ----
+constexpr int kSlices = 64;  // per-channel slices of the first reduction level
+
+enum { kMomentsZ = 0, kMomentsGrad = 1 };
+
+struct BnArgs {
+  const float* z;
+  const float* dy;
+  const float* y;
+  const float* mean;
+  const float* invstd;
+  int B, C;
+  long long V;
+  int relu;
+};
+
+__device__ __forceinline__ double block_sum(double v, double* red) {
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_down(v, o, 64);
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  __syncthreads();
+  if (lane == 0) red[wave] = v;
+  __syncthreads();
+  double s = 0.0;
+  if (threadIdx.x == 0)
+    for (int w = 0; w < (int)(blockDim.x >> 6); ++w) s += red[w];
+  return s;
+}
+
+// MODE kMomentsZ: (sum z, sum z^2); kMomentsGrad: (sum g, sum g * xhat), g = dy [* (y > 0)]
+template <int MODE>
+__global__ __launch_bounds__(256) void bn_moments_kernel(const BnArgs a, double* __restrict__ part) {
+  __shared__ double red[8];
+  const int c = blockIdx.y, s = blockIdx.x;
+  const long long n = (long long)a.B * a.V;
+  const long long e0 = n * s / kSlices, e1 = n * (s + 1) / kSlices;
+  const float mu = MODE == kMomentsGrad ? a.mean[c] : 0.f, is = MODE == kMomentsGrad ? a.invstd[c] : 0.f;
+  double s0 = 0.0, s1 = 0.0;
+  for (long long e = e0 + threadIdx.x; e < e1; e += blockDim.x) {
+    const long long b = e / a.V, v = e - b * a.V;
+    const long long i = (b * a.C + c) * a.V + v;
+    const float zv = a.z[i];
+    if (MODE == kMomentsZ) {
+      s0 += zv;
+      s1 += (double)zv * zv;
+    } else {
+      float g = a.dy[i];
+      if (a.relu && !(a.y[i] > 0.f)) g = 0.f;
+      s0 += g;
+      s1 += (double)g * ((zv - mu) * is);
+    }
+  }
+  const double t0 = block_sum(s0, red);
+  const double t1 = block_sum(s1, red);
+  if (threadIdx.x == 0) {
+    part[((long long)c * kSlices + s) * 2] = t0;
+    part[((long long)c * kSlices + s) * 2 + 1] = t1;
+  }
+}
+
+// forward finalize: batch mean / biased variance -> mean, invstd; running stats
+// (torch: running_var takes the unbiased variance, momentum-weighted)
+__global__ void bn_train_finalize_kernel(const double* __restrict__ part, int C, long long n, float eps, float momentum,
+                                         float* __restrict__ mean, float* __restrict__ invstd, float* running_mean,
+                                         float* running_var) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  double s0 = 0.0, s1 = 0.0;
+  for (int s = 0; s < kSlices; ++s) {
+    s0 += part[((long long)c * kSlices + s) * 2];
+    s1 += part[((long long)c * kSlices + s) * 2 + 1];
+  }
+  const double mu = s0 / (double)n;
+  double var = s1 / (double)n - mu * mu;
+  if (var < 0.0) var = 0.0;
+  mean[c] = (float)mu;
+  invstd[c] = (float)(1.0 / sqrt(var + (double)eps));
+  if (running_mean) {
+    const double unb = n > 1 ? var * (double)n / (double)(n - 1) : var;
+    running_mean[c] = (float)((1.0 - momentum) * running_mean[c] + momentum * mu);
+    running_var[c] = (float)((1.0 - momentum) * running_var[c] + momentum * unb);
+  }
+}
+
+__global__ void bn_eval_stats_kernel(int C, float eps, const float* __restrict__ running_mean,
+                                     const float* __restrict__ running_var, float* __restrict__ mean,
+                                     float* __restrict__ invstd) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  mean[c] = running_mean[c];
+  invstd[c] = 1.f / sqrtf(running_var[c] + eps);
+}
+
+// y = relu((z - mean) * invstd * gamma + beta)  (aten's batch_norm element order)
+__global__ void bn_apply_kernel(const float* __restrict__ z, float* __restrict__ y, int C, long long V, long long n,
+                                const float* __restrict__ mean, const float* __restrict__ invstd,
+                                const float* __restrict__ gamma, const float* __restrict__ beta, int relu) {
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
+    const int c = (int)((i / V) % C);
+    float v = (z[i] - mean[c]) * invstd[c];
+    v = v * (gamma ? gamma[c] : 1.f) + (beta ? beta[c] : 0.f);
+    y[i] = relu ? fmaxf(v, 0.f) : v;
+  }
+}
+
+// backward finalize: dgamma, dbeta and the per-channel coefficients of
+// dz = k * (g - mg - xhat * mgx): k = gamma * invstd, mg = dbeta / n, mgx = dgamma / n
+// (train); eval: mg = mgx = 0
+__global__ void bn_bwd_finalize_kernel(const double* __restrict__ part, int C, long long n, int train,
+                                       const float* __restrict__ gamma, const float* __restrict__ invstd,
+                                       float* dgamma, float* dbeta, float* __restrict__ coef) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  double s0 = 0.0, s1 = 0.0;
+  for (int s = 0; s < kSlices; ++s) {
+    s0 += part[((long long)c * kSlices + s) * 2];
+    s1 += part[((long long)c * kSlices + s) * 2 + 1];
+  }
+  if (dbeta) dbeta[c] = (float)s0;
+  if (dgamma) dgamma[c] = (float)s1;
+  coef[3 * c] = (gamma ? gamma[c] : 1.f) * invstd[c];
+  coef[3 * c + 1] = train ? (float)(s0 / (double)n) : 0.f;
+  coef[3 * c + 2] = train ? (float)(s1 / (double)n) : 0.f;
+}
+
+__global__ void bn_bwd_apply_kernel(const BnArgs a, const float* __restrict__ coef, float* __restrict__ dz,
+                                    long long n) {
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
+    const int c = (int)((i / a.V) % a.C);
+    float g = a.dy[i];
+    if (a.relu && !(a.y[i] > 0.f)) g = 0.f;
+    const float xh = (a.z[i] - a.mean[c]) * a.invstd[c];
+    dz[i] = coef[3 * c] * (g - coef[3 * c + 1] - xh * coef[3 * c + 2]);
+  }
+}
+
+inline int mt_for(int cout) { return cout <= 16 ? 1 : cout <= 32 ? 2 : 4; }
+
+// K split: about 2048 workgroups, at most 64 MB of partials
+inline int nsplit_for(int B, int cin, int cout, int D, int H, int W, int k) {
+  const int taps = k * k * k, ci = k == 3 ? WCfg<3>::CI : WCfg<1>::CI;
+  const long long nblk = (long long)((cin + ci - 1) / ci) * ((cout + 16 * mt_for(cout) - 1) / (16 * mt_for(cout)));
+  const long long nseg = (long long)B * D * H * ((W + SEG - 1) / SEG);
+  long long s = 2048 / nblk;
+  const long long per = (long long)NWAVE * cout * cin * taps * 4;
+  s = std::min(s, (64LL << 20) / per);
+  s = std::min(s, nseg);
+  return (int)std::max(1LL, s);
+}
+
+inline int grid_for(long long n) { return (int)std::min<long long>((n + 255) / 256, 4096); }
+
+}  // namespace grad
+}  // namespace lea
+
+using namespace lea;
+using namespace lea::grad;
+
+extern "C" size_t lea_conv3d_wgrad_workspace_bytes(int B, int cin, int cout, int D, int H, int W, int k) {
+  if (B <= 0 || cin <= 0 || cout <= 0 || D <= 0 || H <= 0 || W <= 0 || (k != 1 && k != 3)) return 0;
+  const int ns = nsplit_for(B, cin, cout, D, H, W, k);
+  return (size_t)ns * NWAVE * cout * cin * k * k * k * sizeof(float);
+}
+
+extern "C" int lea_conv3d_wgrad(const float* x, const float* dz, float* dw, void* workspace, size_t ws_bytes, int B,
+                                int cin, int cout, int D, int H, int W, int k, void* stream) {
+  LEA_CHECK_ARG(x && dz && dw && workspace, "lea_conv3d_wgrad: null pointer");
+  LEA_CHECK_ARG(B > 0 && cin > 0 && cout > 0 && D > 0 && H > 0 && W > 0, "lea_conv3d_wgrad: bad shape");
+  LEA_CHECK_ARG(k == 1 || k == 3, "lea_conv3d_wgrad: k=%d unsupported", k);
+  LEA_CHECK_ARG((long long)D * H <= (1LL << 30) / B, "lea_conv3d_wgrad: volume too large");
+  const size_t need = lea_conv3d_wgrad_workspace_bytes(B, cin, cout, D, H, W, k);
+  LEA_CHECK_ARG(ws_bytes >= need, "lea_conv3d_wgrad: workspace %zu < %zu bytes", ws_bytes, need);
+  hipStream_t st = as_stream(stream);
+  WArgs a;
+  a.x = x;
+  a.dz = dz;
+  a.part = (float*)workspace;
+  a.B = B;
+  a.cin = cin;
+  a.cout = cout;
+  a.D = D;
+  a.H = H;
+  a.W = W;
+  a.nwseg = (W + SEG - 1) / SEG;
+  a.nseg = B * D * H * a.nwseg;
+  a.nsplit = nsplit_for(B, cin, cout, D, H, W, k);
+  const int mt = mt_for(cout);
+  const int ci = k == 3 ? WCfg<3>::CI : WCfg<1>::CI;
+  const dim3 grid((unsigned)a.nsplit, (unsigned)((cin + ci - 1) / ci), (unsigned)((cout + 16 * mt - 1) / (16 * mt)));
+  LEA_CHECK_ARG(grid.y <= 65535 && grid.z <= 65535, "lea_conv3d_wgrad: grid too large");
+#define LEA_WGRAD(KS, MT) \
+  if (k == KS && mt == MT) wgrad_kernel<KS, MT><<<grid, 256, 0, st>>>(a);
+  LEA_WGRAD(3, 1) LEA_WGRAD(3, 2) LEA_WGRAD(3, 4) LEA_WGRAD(1, 1) LEA_WGRAD(1, 2) LEA_WGRAD(1, 4)
+#undef LEA_WGRAD
+  int rc = launch_status("lea_conv3d_wgrad");
+  if (rc) return rc;
+  const long long n = (long long)cout * cin * k * k * k;
+  sum_partials_kernel<<<grid_for(n), 256, 0, st>>>(a.part, dw, n, a.nsplit * NWAVE);
+  return launch_status("lea_conv3d_wgrad(sum)");
+}
+
+extern "C" int lea_conv3d_flip_weights(const float* w, float* wt, int cout, int cin, int k, void* stream) {
+  LEA_CHECK_ARG(w && wt && w != wt, "lea_conv3d_flip_weights: null or aliased pointer");
+  LEA_CHECK_ARG(cout > 0 && cin > 0 && (k == 1 || k == 3), "lea_conv3d_flip_weights: bad shape");
+  const long long n = (long long)cout * cin * k * k * k;
+  flip_weights_kernel<<<grid_for(n), 256, 0, as_stream(stream)>>>(w, wt, cout, cin, k);
+  return launch_status("lea_conv3d_flip_weights");
+}
+
+extern "C" size_t lea_bn_workspace_bytes(int C) {
+  return C > 0 ? (size_t)C * kSlices * 2 * sizeof(double) + (size_t)C * 3 * sizeof(float) : 0;
+}
+
+extern "C" int lea_bn_forward_f32(const float* z, float* y, int B, int C, int64_t V, const float* gamma,
+                                  const float* beta, float* running_mean, float* running_var, float momentum,
+                                  float eps, int training, unsigned flags, float* mean, float* invstd,
+                                  void* workspace, void* stream) {
+  LEA_CHECK_ARG(z && y && mean && invstd, "lea_bn_forward_f32: null pointer");
+  LEA_CHECK_ARG(B > 0 && C > 0 && V > 0, "lea_bn_forward_f32: bad shape");
+  LEA_CHECK_ARG((running_mean == nullptr) == (running_var == nullptr), "lea_bn_forward_f32: running stats pair");
+  LEA_CHECK_ARG(training || running_mean, "lea_bn_forward_f32: eval mode needs the running stats");
+  LEA_CHECK_ARG(!training || workspace, "lea_bn_forward_f32: train mode needs the workspace");
+  LEA_CHECK_ARG(eps > 0.f && momentum >= 0.f && momentum <= 1.f, "lea_bn_forward_f32: eps/momentum");
+  hipStream_t st = as_stream(stream);
+  const long long n = (long long)B * C * V;
+  if (training) {
+    BnArgs a{z, nullptr, nullptr, nullptr, nullptr, B, C, V, 0};
+    bn_moments_kernel<kMomentsZ><<<dim3(kSlices, C), 256, 0, st>>>(a, (double*)workspace);
+    int rc = launch_status("lea_bn_forward_f32(moments)");
+    if (rc) return rc;
+    bn_train_finalize_kernel<<<(C + 63) / 64, 64, 0, st>>>((const double*)workspace, C, (long long)B * V, eps,
+                                                           momentum, mean, invstd, running_mean, running_var);
+  } else {
+    bn_eval_stats_kernel<<<(C + 63) / 64, 64, 0, st>>>(C, eps, running_mean, running_var, mean, invstd);
+  }
+  int rc = launch_status("lea_bn_forward_f32(stats)");
+  if (rc) return rc;
+  bn_apply_kernel<<<grid_for(n), 256, 0, st>>>(z, y, C, V, n, mean, invstd, gamma, beta, (flags & LEA_RELU) ? 1 : 0);
+  return launch_status("lea_bn_forward_f32(apply)");
+}
+
+extern "C" int lea_bn_backward_f32(const float* dy, const float* y, const float* z, float* dz, int B, int C,
+                                   int64_t V, const float* gamma, const float* mean, const float* invstd,
+                                   int training, unsigned flags, float* dgamma, float* dbeta, void* workspace,
+                                   void* stream) {
+  LEA_CHECK_ARG(dy && z && dz && mean && invstd && workspace, "lea_bn_backward_f32: null pointer");
+  LEA_CHECK_ARG(!(flags & LEA_RELU) || y, "lea_bn_backward_f32: LEA_RELU needs y");
+  LEA_CHECK_ARG(B > 0 && C > 0 && V > 0, "lea_bn_backward_f32: bad shape");
+  hipStream_t st = as_stream(stream);
+  const long long n = (long long)B * C * V;
+  BnArgs a{z, dy, y, mean, invstd, B, C, V, (flags & LEA_RELU) ? 1 : 0};
+  double* part = (double*)workspace;
+  float* coef = (float*)(part + (long long)C * kSlices * 2);
+  bn_moments_kernel<kMomentsGrad><<<dim3(kSlices, C), 256, 0, st>>>(a, part);
+  int rc = launch_status("lea_bn_backward_f32(moments)");
+  if (rc) return rc;
+  bn_bwd_finalize_kernel<<<(C + 63) / 64, 64, 0, st>>>(part, C, (long long)B * V, training ? 1 : 0, gamma, invstd,
+                                                       dgamma, dbeta, coef);
+  rc = launch_status("lea_bn_backward_f32(finalize)");
+  if (rc) return rc;
+  bn_bwd_apply_kernel<<<grid_for(n), 256, 0, st>>>(a, coef, dz, n);
+  return launch_status("lea_bn_backward_f32(apply)");
+}

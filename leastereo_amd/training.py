@@ -1,0 +1,169 @@
+"""Training backward of the matching net's hot op on the HIP library (SURVEY.md
+§8f rank 4): ``ConvBR3d`` is a drop-in for ``models/operations_3d.py:31-47``'s
+``ConvBR`` (same constructor, same state_dict keys ``conv.weight``,
+``bn.{weight,bias,running_mean,running_var,num_batches_tracked}``) whose forward and
+backward run on ``csrc/conv3d_grad.hip`` plus the forward conv engine, so
+``train.py:130-178``'s step (``model.train()``, ``loss.backward()``,
+``optimizer.step()``) differentiates through it with torch autograd.
+
+Forward (train mode: batch statistics, running-stat update with ``bn.momentum``;
+eval mode: running statistics):
+    z = conv3d(x, w)                  lea_conv3d_bnrelu (stride 1, pad k // 2, no BN)
+    y = relu(bn(z))                   lea_bn_forward_f32
+Backward:
+    dz, dgamma, dbeta                 lea_bn_backward_f32 (ReLU mask from y)
+    dx = conv3d(dz, flip(w)^T)        lea_conv3d_flip_weights + lea_conv3d_bnrelu
+    dw = sum dz (x) x                 lea_conv3d_wgrad (deterministic MFMA reduction)
+
+Only the hot path's ConvBR shapes are supported (stride 1, padding k // 2, k in
+{1, 3}, bias-free as the reference's); anything else raises.  There is no CPU
+fallback: CPU tensors raise like every other wrapper in ``kernels``.
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn as nn
+
+from . import _lib, kernels
+from ._lib import LEA_RELU, check
+
+
+def _stream():
+    return torch.cuda.current_stream().cuda_stream
+
+
+def flip_weights(w: torch.Tensor) -> torch.Tensor:
+    """[cout, cin, k, k, k] -> [cin, cout, k, k, k] spatially flipped (the input
+    gradient's conv weight)."""
+    kernels._require_cuda(w)
+    w = w.detach().contiguous()
+    cout, cin, k = w.shape[0], w.shape[1], w.shape[-1]
+    wt = torch.empty((cin, cout, k, k, k), device=w.device, dtype=torch.float32)
+    check(_lib.load().lea_conv3d_flip_weights(w.data_ptr(), wt.data_ptr(), cout, cin, k, _stream()),
+          "lea_conv3d_flip_weights")
+    return wt
+
+
+def conv3d_wgrad(x: torch.Tensor, dz: torch.Tensor, k: int) -> torch.Tensor:
+    """Weight gradient of a stride-1, pad k // 2 Conv3d: x [B, cin, D, H, W],
+    dz [B, cout, D, H, W] -> dw [cout, cin, k, k, k]."""
+    kernels._require_cuda(x, dz)
+    x, dz = x.contiguous(), dz.contiguous()
+    b, cin, d, h, w = x.shape
+    cout = dz.shape[1]
+    if dz.shape[0] != b or tuple(dz.shape[2:]) != (d, h, w):
+        raise ValueError(f"conv3d_wgrad: dz {tuple(dz.shape)} does not match x {tuple(x.shape)}")
+    lib = _lib.load()
+    nws = lib.lea_conv3d_wgrad_workspace_bytes(b, cin, cout, d, h, w, k)
+    if nws == 0:
+        raise ValueError(f"conv3d_wgrad: unsupported shape {tuple(x.shape)} -> {cout}, k={k}")
+    ws = torch.empty(nws // 4, device=x.device, dtype=torch.float32)
+    dw = torch.empty((cout, cin, k, k, k), device=x.device, dtype=torch.float32)
+    check(lib.lea_conv3d_wgrad(x.data_ptr(), dz.data_ptr(), dw.data_ptr(), ws.data_ptr(), nws, b, cin, cout,
+                               d, h, w, k, _stream()), "lea_conv3d_wgrad")
+    return dw
+
+
+def _bn_workspace(c, device):
+    n = _lib.load().lea_bn_workspace_bytes(c)
+    return torch.empty((n + 7) // 8, device=device, dtype=torch.float64)
+
+
+def _ptr(t):
+    return t.data_ptr() if t is not None else None
+
+
+class _ConvBR3dFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, weight, gamma, beta, running_mean, running_var, training, momentum, eps, use_bn,
+                relu):
+        kernels._require_cuda(x, weight)
+        x = x.contiguous()
+        b, cin, d, h, w = x.shape
+        cout, k = weight.shape[0], weight.shape[-1]
+        if weight.shape[1] != cin:
+            raise ValueError(f"ConvBR3d: weight {tuple(weight.shape)} does not take {cin} channels")
+        z = kernels.conv3d_bnrelu(x, kernels.pack_conv_weight(weight), cout, k, None, None,
+                                  relu=not use_bn and relu)
+        v = d * h * w
+        lib = _lib.load()
+        if use_bn:
+            y = torch.empty_like(z)
+            mean = torch.empty(cout, device=x.device, dtype=torch.float32)
+            invstd = torch.empty_like(mean)
+            ws = _bn_workspace(cout, x.device)
+            check(lib.lea_bn_forward_f32(z.data_ptr(), y.data_ptr(), b, cout, v, _ptr(gamma), _ptr(beta),
+                                         _ptr(running_mean), _ptr(running_var), float(momentum), float(eps),
+                                         1 if training else 0, LEA_RELU if relu else 0, mean.data_ptr(),
+                                         invstd.data_ptr(), ws.data_ptr(), _stream()), "lea_bn_forward_f32")
+        else:
+            y = z
+            mean = torch.zeros(cout, device=x.device, dtype=torch.float32)
+            invstd = torch.ones_like(mean)
+        ctx.save_for_backward(x, weight, gamma, z, y, mean, invstd)
+        ctx.cfg = (bool(training) and use_bn, use_bn, relu, k)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, weight, gamma, z, y, mean, invstd = ctx.saved_tensors
+        train, use_bn, relu, k = ctx.cfg
+        dy = dy.contiguous()
+        b, cout = dy.shape[:2]
+        v = dy.shape[2] * dy.shape[3] * dy.shape[4]
+        need_g = use_bn and gamma is not None and (ctx.needs_input_grad[2] or ctx.needs_input_grad[3])
+        dgamma = torch.empty(cout, device=dy.device, dtype=torch.float32) if need_g else None
+        dbeta = torch.empty_like(dgamma) if need_g else None
+        dz = torch.empty_like(dy)
+        ws = _bn_workspace(cout, dy.device)
+        check(_lib.load().lea_bn_backward_f32(
+            dy.data_ptr(), y.data_ptr(), z.data_ptr(), dz.data_ptr(), b, cout, v,
+            _ptr(gamma) if use_bn else None, mean.data_ptr(), invstd.data_ptr(), 1 if train else 0,
+            LEA_RELU if relu else 0, _ptr(dgamma), _ptr(dbeta), ws.data_ptr(), _stream()),
+            "lea_bn_backward_f32")
+        dx = dw = None
+        if ctx.needs_input_grad[0]:
+            wt = flip_weights(weight)
+            dx = kernels.conv3d_bnrelu(dz, kernels.pack_conv_weight(wt), x.shape[1], k, None, None, relu=False)
+        if ctx.needs_input_grad[1]:
+            dw = conv3d_wgrad(x, dz, k)
+        return (dx, dw, dgamma if ctx.needs_input_grad[2] else None,
+                dbeta if ctx.needs_input_grad[3] else None) + (None,) * 7
+
+
+def convbr3d(x, weight, bn: nn.BatchNorm3d | None, relu: bool = True, training: bool = False):
+    """Functional form: ConvBR3d of x with ``weight`` and (optionally) ``bn``."""
+    if bn is None:
+        return _ConvBR3dFn.apply(x, weight, None, None, None, None, False, 0.0, 1e-5, False, relu)
+    track = bn.track_running_stats and bn.running_mean is not None
+    use_batch = training or not track
+    momentum = bn.momentum if bn.momentum is not None else 0.0
+    if training and track:
+        bn.num_batches_tracked.add_(1)
+        if bn.momentum is None:  # cumulative moving average (torch's momentum=None)
+            momentum = 1.0 / float(bn.num_batches_tracked.item())
+    return _ConvBR3dFn.apply(x, weight, bn.weight, bn.bias, bn.running_mean if (track and training) or not use_batch
+                             else None, bn.running_var if (track and training) or not use_batch else None,
+                             use_batch, momentum, bn.eps, True, relu)
+
+
+class ConvBR3d(nn.Module):
+    """``models/operations_3d.py:31-47`` ConvBR on the HIP library, with gradients."""
+
+    def __init__(self, C_in, C_out, kernel_size, stride=1, padding=None, bn=True, relu=True):
+        super().__init__()
+        padding = kernel_size // 2 if padding is None else padding
+        if kernel_size not in (1, 3) or stride != 1 or padding != kernel_size // 2:
+            raise NotImplementedError(f"ConvBR3d: k={kernel_size} stride={stride} padding={padding} "
+                                      "(the hot path's convs are k in {1, 3}, stride 1, pad k // 2)")
+        self.relu = relu
+        self.use_bn = bn
+        self.conv = nn.Conv3d(C_in, C_out, kernel_size, stride=stride, padding=padding, bias=False)
+        self.bn = nn.BatchNorm3d(C_out)
+        # operations_3d.py:49-56's init
+        nn.init.kaiming_normal_(self.conv.weight, mode="fan_out", nonlinearity="relu")
+        nn.init.constant_(self.bn.weight, 1)
+        nn.init.constant_(self.bn.bias, 0)
+
+    def forward(self, x):
+        return convbr3d(x, self.conv.weight, self.bn if self.use_bn else None, self.relu, self.training)

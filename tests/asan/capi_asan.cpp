@@ -128,6 +128,22 @@ int main() {
   expect_err("standardize null", lea_standardize_crop_u8(nullptr, p, 1, 8, 8, 3, f, f, 8, 8, p, nullptr));
   expect_err("metrics null", lea_disparity_metrics(nullptr, 0, f, 0, 1, 4, 4, 192.f, 0, 0, 1, 2, 3, nullptr,
                                                    nullptr, p, nullptr));
+  // training backward (csrc/conv3d_grad.hip)
+  if (lea_conv3d_wgrad_workspace_bytes(1, 16, 16, 4, 8, 70, 3) == 0 || lea_bn_workspace_bytes(16) == 0 ||
+      lea_conv3d_wgrad_workspace_bytes(1, 16, 16, 4, 8, 70, 5) != 0) {
+    std::printf("FAIL training workspace queries\n");
+    ++g_fail;
+  }
+  expect_err("wgrad null", lea_conv3d_wgrad(nullptr, f, f, p, 1 << 20, 1, 16, 16, 4, 8, 70, 3, nullptr));
+  expect_err("wgrad k", lea_conv3d_wgrad(f, f, f, p, 1 << 20, 1, 16, 16, 4, 8, 70, 5, nullptr));
+  expect_err("wgrad workspace", lea_conv3d_wgrad(f, f, f, p, 4, 1, 16, 16, 4, 8, 70, 3, nullptr));
+  expect_err("flip alias", lea_conv3d_flip_weights(f, f, 16, 16, 3, nullptr));
+  expect_err("bn fwd null", lea_bn_forward_f32(nullptr, f, 1, 16, 64, nullptr, nullptr, nullptr, nullptr, 0.1f,
+                                               1e-5f, 1, 0, f, f, p, nullptr));
+  expect_err("bn fwd eval stats", lea_bn_forward_f32(f, f, 1, 16, 64, nullptr, nullptr, nullptr, nullptr, 0.1f,
+                                                     1e-5f, 0, 0, f, f, p, nullptr));
+  expect_err("bn bwd relu y", lea_bn_backward_f32(f, nullptr, f, f, 1, 16, 64, nullptr, f, f, 1, LEA_RELU,
+                                                  nullptr, nullptr, p, nullptr));
   // tuning hooks: out-of-range values are rejected
   expect_err("walk range", lea_conv3d_wino2_set_walk(-1));
   expect_err("resample batch range", lea_resample_bf16_set_batch(3));

@@ -1,0 +1,139 @@
+"""Training backward of ConvBR3d (leastereo_amd/training.py,
+csrc/conv3d_grad.hip) against torch autograd of the reference's ConvBR
+(models/operations_3d.py:31-47: Conv3d bias-free -> BatchNorm3d -> ReLU) in float64 on
+the CPU, on the same seeded inputs.  The reference's train.py:130-178 runs the layer in
+train mode (batch statistics, running-stat update); eval mode is covered too.
+
+Tolerance (fp32 kernels vs the float64 reference): every output / gradient within
+2e-4 * max|reference| + 1e-6 elementwise; running statistics within 1e-5 relative."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+
+
+def _ref(x, w, g, bt, rm, rv, training, momentum, eps, use_bn, relu, dy):
+    x = x.detach().cpu().double().requires_grad_(True)
+    w = w.detach().cpu().double().requires_grad_(True)
+    g = g.detach().cpu().double().requires_grad_(True)
+    bt = bt.detach().cpu().double().requires_grad_(True)
+    rm, rv = rm.detach().cpu().double().clone(), rv.detach().cpu().double().clone()
+    z = F.conv3d(x, w, padding=w.shape[-1] // 2)
+    if use_bn:
+        z = F.batch_norm(z, rm, rv, g, bt, training, momentum, eps)
+    if relu:
+        z = F.relu(z)
+    z.backward(dy.detach().cpu().double())
+    return z.detach(), x.grad, w.grad, g.grad, bt.grad, rm, rv
+
+
+def _close(a, r, what):
+    a = a.detach().double().cpu()
+    tol = 2e-4 * float(r.abs().max()) + 1e-6
+    err = float((a - r).abs().max())
+    assert err <= tol, f"{what}: max|d| {err:.3e} > {tol:.3e}"
+
+
+CASES = [
+    # B, cin, cout, D, H, W, k, training, bn, relu
+    (2, 8, 8, 6, 10, 70, 3, True, True, True),     # L0 cell shape, ragged W segments
+    (1, 16, 16, 4, 8, 16, 3, True, True, True),    # L1 cell
+    (2, 64, 32, 3, 5, 9, 3, False, True, True),    # eval mode (frozen statistics)
+    (1, 32, 1, 4, 6, 20, 3, False, False, False),  # last_3: no BN, no ReLU
+    (2, 24, 48, 3, 4, 33, 1, True, True, True),    # 1x1 preprocess
+    (1, 128, 64, 2, 4, 12, 3, True, True, True),   # conv1 / conv2
+    (1, 4, 80, 2, 3, 7, 3, True, True, False),     # two cout blocks, BN without ReLU
+    (1, 3, 5, 1, 1, 1, 3, True, True, True),       # one voxel per sample (padding only)
+]
+
+
+@pytest.mark.parametrize("case", CASES, ids=lambda c: "x".join(map(str, c[:7])) + f"-t{int(c[7])}b{int(c[8])}r{int(c[9])}")
+def test_convbr3d_forward_backward_vs_fp64(case):
+    from leastereo_amd.training import _ConvBR3dFn
+    b, cin, cout, d, h, w, k, training, use_bn, relu = case
+    gen = torch.Generator().manual_seed(7 + cin * 31 + cout)
+    x = torch.randn(b, cin, d, h, w, generator=gen)
+    wt = torch.randn(cout, cin, k, k, k, generator=gen) * (2.0 / (cin * k ** 3)) ** 0.5
+    g = 1 + 0.2 * torch.randn(cout, generator=gen)
+    bt = 0.1 * torch.randn(cout, generator=gen)
+    rm = 0.1 * torch.randn(cout, generator=gen)
+    rv = 1 + torch.rand(cout, generator=gen)
+    dy = torch.randn(b, cout, d, h, w, generator=gen)
+    momentum, eps = 0.1, 1e-5
+    ref = _ref(x, wt, g, bt, rm, rv, training, momentum, eps, use_bn, relu, dy)
+
+    xd = x.to(DEV).requires_grad_(True)
+    wd = wt.to(DEV).requires_grad_(True)
+    gd = g.to(DEV).requires_grad_(True)
+    bd = bt.to(DEV).requires_grad_(True)
+    rmd, rvd = rm.to(DEV), rv.to(DEV)
+    y = _ConvBR3dFn.apply(xd, wd, gd if use_bn else None, bd if use_bn else None, rmd if use_bn else None,
+                          rvd if use_bn else None, training, momentum, eps, use_bn, relu)
+    y.backward(dy.to(DEV))
+    torch.cuda.synchronize()
+    _close(y, ref[0], "y")
+    _close(xd.grad, ref[1], "dx")
+    _close(wd.grad, ref[2], "dw")
+    if use_bn:
+        _close(gd.grad, ref[3], "dgamma")
+        _close(bd.grad, ref[4], "dbeta")
+        assert torch.allclose(rmd.cpu().double(), ref[5], rtol=1e-5, atol=1e-6)
+        assert torch.allclose(rvd.cpu().double(), ref[6], rtol=1e-5, atol=1e-6)
+
+
+def test_wgrad_deterministic_and_vs_torch_at_l1_size():
+    """The weight gradient at a full-size L1 cell (C2: 16 -> 16 on 32 x 96 x 160) against
+    torch's own GPU fp32 convolution backward (size-independent bar: 1e-4 of the
+    gradient's scale), and bit-identical across two calls (fixed-order partial sums)."""
+    from leastereo_amd.training import conv3d_wgrad
+    gen = torch.Generator(device=DEV).manual_seed(3)
+    x = torch.randn(1, 16, 32, 96, 160, device=DEV, generator=gen)
+    dz = torch.randn(1, 16, 32, 96, 160, device=DEV, generator=gen)
+    a = conv3d_wgrad(x, dz, 3)
+    b = conv3d_wgrad(x, dz, 3)
+    assert torch.equal(a, b)
+    with torch.backends.cudnn.flags(enabled=True, deterministic=True, allow_tf32=False):
+        r = torch.nn.grad.conv3d_weight(x.double().cpu(), (16, 16, 3, 3, 3), dz.double().cpu(), padding=1)
+    err = float((a.double().cpu() - r).abs().max())
+    assert err <= 1e-4 * float(r.abs().max()), err
+
+
+def test_train_steps_match_torch():
+    """train.py:150-158's step (train mode, smooth_l1, SGD) through two stacked ConvBR3d
+    layers: parameters and running statistics after three steps match the same steps
+    taken by torch's own modules in float64."""
+    from leastereo_amd.training import ConvBR3d
+    torch.manual_seed(0)
+    ours = torch.nn.Sequential(ConvBR3d(8, 16, 3, 1, 1), ConvBR3d(16, 1, 3, 1, 1, bn=False, relu=False)).to(DEV)
+    ref = torch.nn.Sequential(
+        torch.nn.Conv3d(8, 16, 3, padding=1, bias=False), torch.nn.BatchNorm3d(16), torch.nn.ReLU(),
+        torch.nn.Conv3d(16, 1, 3, padding=1, bias=False)).double()
+    with torch.no_grad():
+        ref[0].weight.copy_(ours[0].conv.weight.double().cpu())
+        ref[3].weight.copy_(ours[1].conv.weight.double().cpu())
+    opt = torch.optim.SGD(ours.parameters(), lr=0.05, momentum=0.9)
+    ropt = torch.optim.SGD(ref.parameters(), lr=0.05, momentum=0.9)
+    ours.train()
+    ref.train()
+    gen = torch.Generator().manual_seed(11)
+    for _ in range(3):
+        x = torch.randn(2, 8, 4, 6, 40, generator=gen)
+        t = torch.randn(2, 1, 4, 6, 40, generator=gen)
+        opt.zero_grad()
+        loss = F.smooth_l1_loss(ours(x.to(DEV)), t.to(DEV))
+        loss.backward()
+        opt.step()
+        ropt.zero_grad()
+        rloss = F.smooth_l1_loss(ref(x.double()), t.double())
+        rloss.backward()
+        ropt.step()
+        assert abs(loss.item() - rloss.item()) <= 1e-5 * abs(rloss.item()) + 1e-7
+    pairs = [(ours[0].conv.weight, ref[0].weight), (ours[0].bn.weight, ref[1].weight),
+             (ours[0].bn.bias, ref[1].bias), (ours[0].bn.running_mean, ref[1].running_mean),
+             (ours[0].bn.running_var, ref[1].running_var), (ours[1].conv.weight, ref[3].weight)]
+    for a, r in pairs:
+        assert torch.allclose(a.detach().double().cpu(), r.detach(), rtol=1e-4, atol=1e-5)
+    assert int(ours[0].bn.num_batches_tracked) == int(ref[1].num_batches_tracked) == 3
