@@ -382,6 +382,17 @@ int lea_bn_backward_f32(const float* dy, const float* y, const float* z, float* 
                         int training, unsigned flags, float* dgamma, float* dbeta, void* workspace,
                         void* stream);
 
+/* Backward of lea_resample3d_trilinear without epilogue (F.interpolate trilinear,
+ * skip_model_3d.py:48,50,162, align_corners 1; build_model_2d.py:53, 0):
+ * dx[b][c] = interp^T(dy[b][c]), as three deterministic 1-D transposed passes with
+ * the forward's source-index rule.  dy: [B, C, Do, Ho, Wo], dx: [B, C, Di, Hi, Wi],
+ * contiguous; workspace: lea_resample3d_backward_workspace_bytes(...) bytes.     */
+size_t lea_resample3d_backward_workspace_bytes(int B, int C, int Di, int Hi, int Wi, int Do, int Ho,
+                                               int Wo);
+int lea_resample3d_trilinear_backward(const float* dy, float* dx, void* workspace, size_t ws_bytes,
+                                      int B, int C, int Di, int Hi, int Wi, int Do, int Ho, int Wo,
+                                      int align_corners, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -292,6 +292,39 @@ __global__ void bn_bwd_apply_kernel(const BnArgs a, const float* __restrict__ co
   }
 }
 
+
+// ---- trilinear resample backward (F.interpolate's, skip_model_3d.py:48,50,162) ----
+// The forward is separable (a product of per-axis linear interpolations), so its
+// transpose is three 1-D transposed passes (W, then H, then D).  Each pass gathers:
+// input index i of the axis collects l0(p) g[p] over the outputs p with i0(p) = i and
+// l1(p) g[p] over those with i1(p) = i (axis_index: the forward's own index rule), p
+// scanned over a window that covers every such output -- deterministic, no atomics.
+__global__ void interp_t_kernel(const float* __restrict__ g, float* __restrict__ out, long long outer, int n_out,
+                                int n_in, long long inner, float ratio, int ac) {
+  const long long n = outer * n_in * inner;
+  for (long long e = blockIdx.x * (long long)blockDim.x + threadIdx.x; e < n; e += (long long)gridDim.x * blockDim.x) {
+    const long long r = e % inner;
+    const long long t = e / inner;
+    const int i = (int)(t % n_in);
+    const long long o = t / n_in;
+    int p0 = 0, p1 = n_out - 1;
+    if (ratio > 0.f) {  // outputs whose source lies in [i - 1, i + 1]
+      p0 = max(0, (int)floorf(fminf(((float)i - 0.5f) / ratio - 0.5f, ((float)i - 1.f) / ratio)) - 2);
+      p1 = min(n_out - 1, (int)ceilf(((float)i + 1.f + 0.5f) / ratio) + 2);
+    }
+    const float* gp = g + o * n_out * inner + r;
+    float s = 0.f;
+    for (int p = p0; p <= p1; ++p) {
+      const Axis ax = axis_index(ratio, p, n_in, n_out, ac);
+      float wgt = 0.f;
+      if (ax.i0 == i) wgt += ax.l0;
+      if (ax.i1 == i) wgt += ax.l1;
+      if (wgt != 0.f) s += wgt * gp[(long long)p * inner];
+    }
+    out[e] = s;
+  }
+}
+
 inline int mt_for(int cout) { return cout <= 16 ? 1 : cout <= 32 ? 2 : 4; }
 
 // K split: about 2048 workgroups, at most 64 MB of partials
@@ -418,4 +451,33 @@ extern "C" int lea_bn_backward_f32(const float* dy, const float* y, const float*
   if (rc) return rc;
   bn_bwd_apply_kernel<<<grid_for(n), 256, 0, st>>>(a, coef, dz, n);
   return launch_status("lea_bn_backward_f32(apply)");
+}
+
+extern "C" size_t lea_resample3d_backward_workspace_bytes(int B, int C, int Di, int Hi, int Wi, int Do, int Ho,
+                                                        int Wo) {
+  if (B <= 0 || C <= 0 || Di <= 0 || Hi <= 0 || Wi <= 0 || Do <= 0 || Ho <= 0 || Wo <= 0) return 0;
+  return (size_t)B * C * ((size_t)Do * Ho * Wi + (size_t)Do * Hi * Wi) * sizeof(float);
+}
+
+extern "C" int lea_resample3d_trilinear_backward(const float* dy, float* dx, void* workspace, size_t ws_bytes, int B,
+                                                 int C, int Di, int Hi, int Wi, int Do, int Ho, int Wo,
+                                                 int align_corners, void* stream) {
+  LEA_CHECK_ARG(dy && dx && workspace && dy != dx, "lea_resample3d_trilinear_backward: null or aliased pointer");
+  const size_t need = lea_resample3d_backward_workspace_bytes(B, C, Di, Hi, Wi, Do, Ho, Wo);
+  LEA_CHECK_ARG(need > 0, "lea_resample3d_trilinear_backward: bad shape");
+  LEA_CHECK_ARG(ws_bytes >= need, "lea_resample3d_trilinear_backward: workspace %zu < %zu bytes", ws_bytes, need);
+  hipStream_t st = as_stream(stream);
+  const int ac = align_corners ? 1 : 0;
+  float* gw = (float*)workspace;                      // [B C Do Ho Wi]
+  float* gh = gw + (size_t)B * C * Do * Ho * Wi;      // [B C Do Hi Wi]
+  const long long bc = (long long)B * C;
+  interp_t_kernel<<<grid_for(bc * Do * Ho * Wi), 256, 0, st>>>(dy, gw, bc * Do * Ho, Wo, Wi, 1, axis_ratio(Wi, Wo, ac), ac);
+  int rc = launch_status("lea_resample3d_trilinear_backward(w)");
+  if (rc) return rc;
+  interp_t_kernel<<<grid_for(bc * Do * Hi * Wi), 256, 0, st>>>(gw, gh, bc * Do, Ho, Hi, Wi, axis_ratio(Hi, Ho, ac), ac);
+  rc = launch_status("lea_resample3d_trilinear_backward(h)");
+  if (rc) return rc;
+  interp_t_kernel<<<grid_for(bc * Di * Hi * Wi), 256, 0, st>>>(gh, dx, bc, Do, Di, (long long)Hi * Wi,
+                                                               axis_ratio(Di, Do, ac), ac);
+  return launch_status("lea_resample3d_trilinear_backward(d)");
 }

@@ -131,6 +131,43 @@ class _ConvBR3dFn(torch.autograd.Function):
                 dbeta if ctx.needs_input_grad[3] else None) + (None,) * 7
 
 
+def resample3d_backward(dy: torch.Tensor, in_size, align_corners: bool = True) -> torch.Tensor:
+    """Transpose of ``kernels.resample_trilinear``: dy [B, C, Do, Ho, Wo] -> dx
+    [B, C, *in_size]."""
+    kernels._require_cuda(dy)
+    dy = dy.contiguous()
+    b, c, do, ho, wo = dy.shape
+    di, hi, wi = (int(s) for s in in_size)
+    lib = _lib.load()
+    nws = lib.lea_resample3d_backward_workspace_bytes(b, c, di, hi, wi, do, ho, wo)
+    if nws == 0:
+        raise ValueError(f"resample3d_backward: bad shape {tuple(dy.shape)} <- {tuple(in_size)}")
+    ws = torch.empty(nws // 4, device=dy.device, dtype=torch.float32)
+    dx = torch.empty((b, c, di, hi, wi), device=dy.device, dtype=torch.float32)
+    check(lib.lea_resample3d_trilinear_backward(dy.data_ptr(), dx.data_ptr(), ws.data_ptr(), nws, b, c, di, hi,
+                                                wi, do, ho, wo, 1 if align_corners else 0, _stream()),
+          "lea_resample3d_trilinear_backward")
+    return dx
+
+
+class _Resample3dFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, size, align_corners):
+        ctx.cfg = (tuple(x.shape[2:]), bool(align_corners))
+        return kernels.resample_trilinear(x.contiguous(), size, align_corners=align_corners)
+
+    @staticmethod
+    def backward(ctx, dy):
+        in_size, ac = ctx.cfg
+        return resample3d_backward(dy, in_size, ac), None, None
+
+
+def interpolate3d(x: torch.Tensor, size, align_corners: bool = True) -> torch.Tensor:
+    """``F.interpolate(x, size, mode='trilinear', align_corners=...)`` on the HIP
+    library, differentiable (skip_model_3d.py:48,50,162; build_model_2d.py:53)."""
+    return _Resample3dFn.apply(x, tuple(int(s) for s in size), align_corners)
+
+
 def convbr3d(x, weight, bn: nn.BatchNorm3d | None, relu: bool = True, training: bool = False):
     """Functional form: ConvBR3d of x with ``weight`` and (optionally) ``bn``."""
     if bn is None:

@@ -144,6 +144,10 @@ int main() {
                                                      1e-5f, 0, 0, f, f, p, nullptr));
   expect_err("bn bwd relu y", lea_bn_backward_f32(f, nullptr, f, f, 1, 16, 64, nullptr, f, f, 1, LEA_RELU,
                                                   nullptr, nullptr, p, nullptr));
+  expect_err("resample bwd null", lea_resample3d_trilinear_backward(nullptr, f, p, 1 << 20, 1, 2, 4, 4, 4, 8, 8,
+                                                                    8, 1, nullptr));
+  expect_err("resample bwd ws", lea_resample3d_trilinear_backward(f, f + 64, p, 4, 1, 2, 4, 4, 4, 8, 8, 8, 1,
+                                                                  nullptr));
   // tuning hooks: out-of-range values are rejected
   expect_err("walk range", lea_conv3d_wino2_set_walk(-1));
   expect_err("resample batch range", lea_resample_bf16_set_batch(3));

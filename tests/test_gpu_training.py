@@ -137,3 +137,28 @@ def test_train_steps_match_torch():
     for a, r in pairs:
         assert torch.allclose(a.detach().double().cpu(), r.detach(), rtol=1e-4, atol=1e-5)
     assert int(ours[0].bn.num_batches_tracked) == int(ref[1].num_batches_tracked) == 3
+
+
+@pytest.mark.parametrize("src,dst,ac", [
+    ((16, 48, 80), (32, 96, 160), True),   # L2 -> L1 up-sampling (skip_model_3d.py:48)
+    ((32, 96, 160), (16, 48, 80), True),   # L1 -> L2 down-sampling
+    ((9, 7, 13), (5, 4, 7), True),         # odd sizes (scale_dimension's (n + 1) / 2)
+    ((5, 4, 7), (9, 7, 13), True),
+    ((4, 6, 10), (12, 18, 30), False),     # Disp's x3 (build_model_2d.py:53, align_corners=False)
+    ((3, 1, 5), (3, 1, 5), True),          # identity axis, a single-plane axis
+    ((1, 2, 3), (4, 1, 6), True),          # an axis of output size 1
+])
+def test_interpolate3d_backward_vs_fp64(src, dst, ac):
+    from leastereo_amd.training import interpolate3d
+    gen = torch.Generator().manual_seed(sum(src) + sum(dst))
+    x = torch.randn((2, 3) + src, generator=gen)
+    dy = torch.randn((2, 3) + dst, generator=gen)
+    xr = x.double().requires_grad_(True)
+    yr = F.interpolate(xr, size=dst, mode="trilinear", align_corners=ac)
+    yr.backward(dy.double())
+    xd = x.to(DEV).requires_grad_(True)
+    y = interpolate3d(xd, dst, ac)
+    y.backward(dy.to(DEV))
+    torch.cuda.synchronize()
+    _close(y, yr.detach(), "y")
+    _close(xd.grad, xr.grad, "dx")
