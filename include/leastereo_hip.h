@@ -393,6 +393,22 @@ int lea_resample3d_trilinear_backward(const float* dy, float* dx, void* workspac
                                       int B, int C, int Di, int Hi, int Wi, int Do, int Ho, int Wo,
                                       int align_corners, void* stream);
 
+/* Backward of lea_disparity_regression (build_model_2d.py:33-42,52-57): with
+ * U = trilinear(cost, [maxdisp, 3H3, 3W3], align_corners=False), p = softmax(-U, d),
+ * disp = sum_d d p_d (disp: the forward's output), writes
+ *   dU[b, d, h, w] = -dout[b, h, w] * p_d * (d - disp[b, h, w])   ([B, maxdisp, 3H3, 3W3]);
+ * dcost = lea_resample3d_trilinear_backward(dU, align_corners = 0).              */
+int lea_disparity_regression_backward(const float* cost, const float* disp, const float* dout,
+                                      float* dU, int B, int D3, int H3, int W3, int maxdisp,
+                                      void* stream);
+
+/* Backward of lea_build_cost_volume (retrain/LEAStereo.py:34-48):
+ *   dleft[b,c,h,w]  = sum_{i <= w} dcost[b, c, i, h, w]
+ *   dright[b,c,h,w] = sum_{i < W - w} dcost[b, C + c, i, h, w + i]
+ * dcost: [B, 2C, D3, H, W]; dleft/dright: [B, C, H, W]; fp32.                    */
+int lea_build_cost_volume_backward(const float* dcost, float* dleft, float* dright, int B, int C,
+                                   int H, int W, int D3, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -114,6 +114,8 @@ SIGNATURES = {
     "lea_bn_forward_f32": (_i, [_p, _p, _i, _i, _i64, _p, _p, _p, _p, ctypes.c_float, ctypes.c_float,
                                 _i, _u, _p, _p, _p, _p]),
     "lea_bn_backward_f32": (_i, [_p, _p, _p, _p, _i, _i, _i64, _p, _p, _p, _i, _u, _p, _p, _p, _p]),
+    "lea_disparity_regression_backward": (_i, [_p, _p, _p, _p, _i, _i, _i, _i, _i, _p]),
+    "lea_build_cost_volume_backward": (_i, [_p, _p, _p, _i, _i, _i, _i, _i, _p]),
     "lea_resample3d_backward_workspace_bytes": (ctypes.c_size_t, [_i, _i, _i, _i, _i, _i, _i, _i]),
     "lea_resample3d_trilinear_backward": (_i, [_p, _p, _p, ctypes.c_size_t, _i, _i, _i, _i, _i, _i, _i, _i,
                                                _i, _p]),

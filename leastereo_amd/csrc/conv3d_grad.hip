@@ -325,6 +325,65 @@ __global__ void interp_t_kernel(const float* __restrict__ g, float* __restrict__
   }
 }
 
+// ---- Disp + DisparityRegression backward (build_model_2d.py:33-42,52-57) ----
+// disp = sum_d d p_d, p = softmax(-U), U = trilinear(cost, ac=False): per output pixel
+// dU_d = -dout * p_d * (d - disp); one thread per pixel walks D twice (min / sum, then
+// the writes), U re-interpolated with the forward's source-index rule.
+__global__ __launch_bounds__(256) void disp_bwd_kernel(const float* __restrict__ cost, const float* __restrict__ disp,
+                                                       const float* __restrict__ dout, float* __restrict__ dU,
+                                                       int D3, int H3, int W3, int maxdisp, float rd, float rh,
+                                                       float rw) {
+  const int Ho = 3 * H3, Wo = 3 * W3;
+  const int ow = blockIdx.x * blockDim.x + threadIdx.x;
+  if (ow >= Wo) return;
+  const int oh = blockIdx.y, b = blockIdx.z;
+  const Axis ah = axis_index(rh, oh, H3, Ho, 0), aw = axis_index(rw, ow, W3, Wo, 0);
+  const long long HW = (long long)H3 * W3;
+  const float* c = cost + (long long)b * D3 * HW;
+  auto plane = [&](int d) {
+    const float* q = c + d * HW;
+    return ah.l0 * (aw.l0 * q[ah.i0 * W3 + aw.i0] + aw.l1 * q[ah.i0 * W3 + aw.i1]) +
+           ah.l1 * (aw.l0 * q[ah.i1 * W3 + aw.i0] + aw.l1 * q[ah.i1 * W3 + aw.i1]);
+  };
+  auto U = [&](int od) {
+    const Axis ad = axis_index(rd, od, D3, maxdisp, 0);
+    return ad.l0 * plane(ad.i0) + ad.l1 * plane(ad.i1);
+  };
+  float m = 3.4e38f;
+  for (int od = 0; od < maxdisp; ++od) m = fminf(m, U(od));
+  float s = 0.f;
+  for (int od = 0; od < maxdisp; ++od) s += expf(m - U(od));
+  const long long pix = ((long long)b * Ho + oh) * Wo + ow;
+  const float g = dout[pix] / s, dsp = disp[pix];
+  const long long plane_o = (long long)Ho * Wo;
+  float* out = dU + (long long)b * maxdisp * plane_o + (long long)oh * Wo + ow;
+  for (int od = 0; od < maxdisp; ++od) out[od * plane_o] = -g * expf(m - U(od)) * ((float)od - dsp);
+}
+
+// ---- cost-volume backward (retrain/LEAStereo.py:34-48) ----
+// cost[b, c, i, h, w] = L[b, c, h, w], cost[b, C + c, i, h, w] = R[b, c, h, w - i] (w >= i):
+// dL[b, c, h, w] = sum_{i <= w} dcost[b, c, i, h, w],
+// dR[b, c, h, w] = sum_{i < W - w} dcost[b, C + c, i, h, w + i]
+__global__ void cost_volume_bwd_kernel(const float* __restrict__ dcost, float* __restrict__ dl,
+                                       float* __restrict__ dr, int B, int C, int H, int W, int D3) {
+  const long long n = (long long)B * C * H * W;
+  for (long long e = blockIdx.x * (long long)blockDim.x + threadIdx.x; e < n; e += (long long)gridDim.x * blockDim.x) {
+    const int w = (int)(e % W);
+    long long t = e / W;
+    const int h = (int)(t % H);
+    t /= H;
+    const int c = (int)(t % C), b = (int)(t / C);
+    const long long HW = (long long)H * W, vol = (long long)D3 * HW;
+    const float* gl = dcost + ((long long)b * 2 * C + c) * vol + (long long)h * W + w;
+    const float* gr = dcost + ((long long)b * 2 * C + C + c) * vol + (long long)h * W + w;
+    float sl = 0.f, sr = 0.f;
+    for (int i = 0; i < D3 && i <= w; ++i) sl += gl[i * HW];
+    for (int i = 0; i < D3 && w + i < W; ++i) sr += gr[i * HW + i];
+    dl[e] = sl;
+    dr[e] = sr;
+  }
+}
+
 inline int mt_for(int cout) { return cout <= 16 ? 1 : cout <= 32 ? 2 : 4; }
 
 // K split: about 2048 workgroups, at most 64 MB of partials
@@ -480,4 +539,25 @@ extern "C" int lea_resample3d_trilinear_backward(const float* dy, float* dx, voi
   interp_t_kernel<<<grid_for(bc * Di * Hi * Wi), 256, 0, st>>>(gh, dx, bc, Do, Di, (long long)Hi * Wi,
                                                                axis_ratio(Di, Do, ac), ac);
   return launch_status("lea_resample3d_trilinear_backward(d)");
+}
+
+extern "C" int lea_disparity_regression_backward(const float* cost, const float* disp, const float* dout, float* dU,
+                                                 int B, int D3, int H3, int W3, int maxdisp, void* stream) {
+  LEA_CHECK_ARG(cost && disp && dout && dU, "lea_disparity_regression_backward: null pointer");
+  LEA_CHECK_ARG(B > 0 && D3 > 0 && H3 > 0 && W3 > 0 && maxdisp > 0 && B <= 65535 && 3 * H3 <= 65535,
+                "lea_disparity_regression_backward: bad shape");
+  const dim3 grid((unsigned)((3 * W3 + 255) / 256), (unsigned)(3 * H3), (unsigned)B);
+  disp_bwd_kernel<<<grid, 256, 0, as_stream(stream)>>>(cost, disp, dout, dU, D3, H3, W3, maxdisp,
+                                                      axis_ratio(D3, maxdisp, 0), axis_ratio(H3, 3 * H3, 0),
+                                                      axis_ratio(W3, 3 * W3, 0));
+  return launch_status("lea_disparity_regression_backward");
+}
+
+extern "C" int lea_build_cost_volume_backward(const float* dcost, float* dleft, float* dright, int B, int C, int H,
+                                              int W, int D3, void* stream) {
+  LEA_CHECK_ARG(dcost && dleft && dright && dleft != dright, "lea_build_cost_volume_backward: null pointer");
+  LEA_CHECK_ARG(B > 0 && C > 0 && H > 0 && W > 0 && D3 > 0, "lea_build_cost_volume_backward: bad shape");
+  const long long n = (long long)B * C * H * W;
+  cost_volume_bwd_kernel<<<grid_for(n), 256, 0, as_stream(stream)>>>(dcost, dleft, dright, B, C, H, W, D3);
+  return launch_status("lea_build_cost_volume_backward");
 }

@@ -168,6 +168,54 @@ def interpolate3d(x: torch.Tensor, size, align_corners: bool = True) -> torch.Te
     return _Resample3dFn.apply(x, tuple(int(s) for s in size), align_corners)
 
 
+class _DisparityFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, cost, maxdisp):
+        disp = kernels.disparity_regression(cost, maxdisp)
+        ctx.save_for_backward(cost.contiguous(), disp)
+        ctx.maxdisp = maxdisp
+        return disp
+
+    @staticmethod
+    def backward(ctx, dout):
+        cost, disp = ctx.saved_tensors
+        b, _, d3, h3, w3 = cost.shape
+        du = torch.empty((b, 1, ctx.maxdisp, 3 * h3, 3 * w3), device=cost.device, dtype=torch.float32)
+        check(_lib.load().lea_disparity_regression_backward(
+            cost.data_ptr(), disp.data_ptr(), dout.contiguous().data_ptr(), du.data_ptr(), b, d3, h3, w3,
+            ctx.maxdisp, _stream()), "lea_disparity_regression_backward")
+        return resample3d_backward(du, (d3, h3, w3), align_corners=False), None
+
+
+def disparity_regression(cost: torch.Tensor, maxdisp: int) -> torch.Tensor:
+    """Disp + DisparityRegression (build_model_2d.py:33-42,52-57), differentiable:
+    [B, 1, D3, H3, W3] -> [B, 3 H3, 3 W3]."""
+    return _DisparityFn.apply(cost, int(maxdisp))
+
+
+class _CostVolumeFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, fl, fr, maxdisp):
+        ctx.shape = tuple(fl.shape)
+        return kernels.build_cost_volume(fl.contiguous(), fr.contiguous(), maxdisp)
+
+    @staticmethod
+    def backward(ctx, dcost):
+        b, c, h, w = ctx.shape
+        dcost = dcost.contiguous()
+        dl = torch.empty(ctx.shape, device=dcost.device, dtype=torch.float32)
+        dr = torch.empty_like(dl)
+        check(_lib.load().lea_build_cost_volume_backward(dcost.data_ptr(), dl.data_ptr(), dr.data_ptr(), b, c, h,
+                                                         w, dcost.shape[2], _stream()),
+              "lea_build_cost_volume_backward")
+        return dl, dr, None
+
+
+def build_cost_volume(fl: torch.Tensor, fr: torch.Tensor, maxdisp: int) -> torch.Tensor:
+    """retrain/LEAStereo.py:34-48's cost volume, differentiable."""
+    return _CostVolumeFn.apply(fl, fr, int(maxdisp))
+
+
 def convbr3d(x, weight, bn: nn.BatchNorm3d | None, relu: bool = True, training: bool = False):
     """Functional form: ConvBR3d of x with ``weight`` and (optionally) ``bn``."""
     if bn is None:

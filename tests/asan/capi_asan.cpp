@@ -148,6 +148,8 @@ int main() {
                                                                     8, 1, nullptr));
   expect_err("resample bwd ws", lea_resample3d_trilinear_backward(f, f + 64, p, 4, 1, 2, 4, 4, 4, 8, 8, 8, 1,
                                                                   nullptr));
+  expect_err("disp bwd null", lea_disparity_regression_backward(nullptr, f, f, f, 1, 8, 4, 4, 24, nullptr));
+  expect_err("cv bwd alias", lea_build_cost_volume_backward(f, f, f, 1, 4, 4, 4, 4, nullptr));
   // tuning hooks: out-of-range values are rejected
   expect_err("walk range", lea_conv3d_wino2_set_walk(-1));
   expect_err("resample batch range", lea_resample_bf16_set_batch(3));

@@ -162,3 +162,50 @@ def test_interpolate3d_backward_vs_fp64(src, dst, ac):
     torch.cuda.synchronize()
     _close(y, yr.detach(), "y")
     _close(xd.grad, xr.grad, "dx")
+
+
+@pytest.mark.parametrize("b,d3,h3,w3,maxdisp", [(2, 8, 5, 7, 24), (1, 16, 4, 6, 48), (1, 6, 3, 4, 17)])
+def test_disparity_regression_backward_vs_fp64(b, d3, h3, w3, maxdisp):
+    """build_model_2d.py:52-57 then :33-42 (upsample, softmax(-x), sum d * p)."""
+    from leastereo_amd.training import disparity_regression
+    gen = torch.Generator().manual_seed(d3 * 7 + maxdisp)
+    cost = 2 * torch.randn(b, 1, d3, h3, w3, generator=gen)
+    dout = torch.randn(b, 3 * h3, 3 * w3, generator=gen)
+    cr = cost.double().requires_grad_(True)
+    u = F.interpolate(cr, [maxdisp, 3 * h3, 3 * w3], mode="trilinear", align_corners=False)
+    p = F.softmax(-torch.squeeze(u, 1), dim=1)
+    ref = torch.sum(p * torch.arange(maxdisp, dtype=torch.float64).view(1, maxdisp, 1, 1), 1)
+    ref.backward(dout.double())
+    cd = cost.to(DEV).requires_grad_(True)
+    disp = disparity_regression(cd, maxdisp)
+    disp.backward(dout.to(DEV))
+    torch.cuda.synchronize()
+    _close(disp, ref.detach(), "disp")
+    _close(cd.grad, cr.grad, "dcost")
+
+
+@pytest.mark.parametrize("b,c,h,w,maxdisp", [(2, 4, 3, 16, 24), (1, 32, 2, 12, 48), (1, 3, 2, 5, 30)])
+def test_cost_volume_backward_vs_fp64(b, c, h, w, maxdisp):
+    """retrain/LEAStereo.py:34-48 (D3 may exceed W: the last case)."""
+    from leastereo_amd.training import build_cost_volume
+    gen = torch.Generator().manual_seed(c * 5 + w)
+    fl, fr = torch.randn(b, c, h, w, generator=gen), torch.randn(b, c, h, w, generator=gen)
+    d3 = int(maxdisp / 3)
+    dcost = torch.randn(b, 2 * c, d3, h, w, generator=gen)
+    lr, rr = fl.double().requires_grad_(True), fr.double().requires_grad_(True)
+    cost = lr.new_zeros(b, 2 * c, d3, h, w)
+    for i in range(d3):
+        if i > 0:
+            cost[:, :c, i, :, i:] = lr[:, :, :, i:]
+            cost[:, c:, i, :, i:] = rr[:, :, :, :-i]
+        else:
+            cost[:, :c, i, :, :] = lr
+            cost[:, c:, i, :, :] = rr
+    cost.backward(dcost.double())
+    ld, rd = fl.to(DEV).requires_grad_(True), fr.to(DEV).requires_grad_(True)
+    out = build_cost_volume(ld, rd, maxdisp)
+    out.backward(dcost.to(DEV))
+    torch.cuda.synchronize()
+    assert torch.equal(out.cpu().double(), cost.detach())
+    _close(ld.grad, lr.grad, "dleft")
+    _close(rd.grad, rr.grad, "dright")
