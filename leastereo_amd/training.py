@@ -252,3 +252,78 @@ class ConvBR3d(nn.Module):
 
     def forward(self, x):
         return convbr3d(x, self.conv.weight, self.bn if self.use_bn else None, self.relu, self.training)
+
+
+# ------------------------------------------------- the matching net's training forward
+def _convbr(m, x, training):
+    """A ``model.ConvBR`` parameter container (operations_3d.py:31-47) through the
+    differentiable HIP op."""
+    return convbr3d(x, m.conv.weight, m.bn if m.use_bn else None, m.relu, training)
+
+
+def _cell(cell, s0, s1, training):
+    """Cell.forward, retrain/skip_model_3d.py:41-75 (pairwise sums and the cat stay
+    torch autograd glue; every conv, BN, ReLU and resample runs on the HIP library)."""
+    from .arch import scale_dimension
+    prev_input = s1
+    if cell.downup_sample != 0:
+        sc = 0.5 if cell.downup_sample < 0 else 2
+        s1 = interpolate3d(s1, [scale_dimension(n, sc) for n in s1.shape[2:]])
+    if tuple(s0.shape[2:]) != tuple(s1.shape[2:]):
+        s0 = interpolate3d(s0, s1.shape[2:])
+    if s0.shape[1] != cell.c_out:
+        s0 = _convbr(cell.pre_preprocess, s0, training)
+    s1 = _convbr(cell.preprocess, s1, training)
+    states = [s0, s1]
+    for terms in cell.plan:
+        new = [(_convbr(cell._ops[k], states[j], training) if cell.op_kinds[k] == "conv" else states[j])
+               for k, j in terms]
+        s = new[0]
+        for t in new[1:]:
+            s = s + t
+        states.append(s)
+    return prev_input, torch.cat(states[-cell.block_multiplier:], dim=1)
+
+
+def matching_forward(net, cost: torch.Tensor, training: bool = True) -> torch.Tensor:
+    """newMatching.forward (retrain/skip_model_3d.py:140-174) on ``net``
+    (``model.NewMatching``'s parameters) with gradients: the op order of the
+    reference (no fused or commuted forms), BN in train mode when ``training``."""
+    if cost.dim() != 5:
+        raise ValueError("cost must be [B, C, D3, H3, W3]")
+    d, h, w = cost.shape[2:]
+    stem0 = _convbr(net.stem0, cost, training)
+    stem1 = _convbr(net.stem1, stem0, training)
+    outs, prev = [], (stem0, stem1)
+    n = len(net.cells)
+    for i in range(n):
+        if i == 5 and n == 12:
+            prev = (outs[4][0], _convbr(net.conv1, torch.cat((outs[1][1], outs[4][1]), 1), training))
+        elif i == 9 and n == 12:
+            prev = (outs[8][0], _convbr(net.conv2, torch.cat((outs[4][1], outs[8][1]), 1), training))
+        outs.append(_cell(net.cells[i], prev[0], prev[1], training))
+        prev = outs[-1]
+    last = outs[-1][1]
+    lh = last.shape[3]
+    full, half, quarter = (d, h, w), (d // 2, h // 2, w // 2), (d // 4, h // 4, w // 4)
+    if lh == h:
+        y = last
+    elif lh == h // 2:
+        y = interpolate3d(_convbr(net.last_6, last, training), full)
+    elif lh == h // 4:
+        y = interpolate3d(_convbr(net.last_6, interpolate3d(_convbr(net.last_12, last, training), half),
+                                  training), full)
+    elif lh == h // 8:
+        y = interpolate3d(_convbr(net.last_24, last, training), quarter)
+        y = interpolate3d(_convbr(net.last_12, y, training), half)
+        y = interpolate3d(_convbr(net.last_6, y, training), full)
+    else:
+        raise ValueError(f"matching-net output size {tuple(last.shape[2:])} has no head")
+    return _convbr(net.last_3, y, training)
+
+
+def cost_to_disparity_train(model, fl: torch.Tensor, fr: torch.Tensor) -> torch.Tensor:
+    """retrain/LEAStereo.py:34-51 from the two feature maps, differentiable: cost
+    volume -> matching net (BN in the model's train/eval mode) -> Disp."""
+    cost = build_cost_volume(fl, fr, model.maxdisp)
+    return disparity_regression(matching_forward(model.matching, cost, model.training), model.maxdisp)

@@ -209,3 +209,56 @@ def test_cost_volume_backward_vs_fp64(b, c, h, w, maxdisp):
     assert torch.equal(out.cpu().double(), cost.detach())
     _close(ld.grad, lr.grad, "dleft")
     _close(rd.grad, rr.grad, "dright")
+
+
+def test_matching_train_step_vs_reference_golden():
+    """One train.py:150-156 step of the matching path -- cost volume (LEAStereo.py:34-48),
+    newMatching in train mode (skip_model_3d.py:140-174), Disp (build_model_2d.py:52-57),
+    smooth_l1 over the validity mask -- against the reference itself run in float64
+    (tests/golden/train_step.npz, tools/gen_golden_train.py) at 96 x 192 D48.
+    Bars (fp32 HIP vs float64 reference): disparity 1e-3 px, loss 1e-5 relative, every
+    stored gradient within 2e-3 of its largest magnitude, batch statistics 1e-4 relative."""
+    import numpy as np
+    from leastereo_amd.config import LEAStereoArgs, default_arch_args
+    from leastereo_amd.model import LEAStereo
+    from leastereo_amd.training import cost_to_disparity_train
+    from leastereo_amd.weights import seeded_normal
+    from tests.golden_util import golden, state_dict
+    g = golden("train_step")
+    m = LEAStereo(default_arch_args(LEAStereoArgs(maxdisp=48)), DEV)
+    m.load_state_dict(state_dict(), strict=True)
+    m = m.to(DEV)
+    for mod in m.modules():
+        if isinstance(mod, torch.nn.BatchNorm3d):
+            mod.momentum = 1.0
+    m.train()
+    fl = torch.from_numpy(seeded_normal(301, (1, 32, 32, 64))).to(DEV).requires_grad_(True)
+    fr = torch.from_numpy(seeded_normal(302, (1, 32, 32, 64))).to(DEV).requires_grad_(True)
+    target = torch.from_numpy(seeded_normal(303, (1, 96, 192))).to(DEV) * 4 + 20
+    disp = cost_to_disparity_train(m, fl, fr)
+    mask = (target < 48) & (target > 0.001)
+    loss = F.smooth_l1_loss(disp[mask], target[mask], reduction="mean")
+    loss.backward()
+    torch.cuda.synchronize()
+    assert float((disp.detach().cpu() - torch.from_numpy(g["disp"])).abs().max()) <= 1e-3
+    assert abs(loss.item() - float(g["loss"])) <= 1e-5 * abs(float(g["loss"]))
+    got = {"d_fea_l": fl.grad, "d_fea_r": fr.grad}
+    params = dict(m.named_parameters())
+    bufs = dict(m.named_buffers())
+    for k in g:
+        if k.startswith("grad/"):
+            name = k[5:]
+            t = params[name].grad
+            got[k] = t[:8] if name in ("matching.conv1.conv.weight", "matching.conv2.conv.weight") else t
+        elif k.startswith("mean/") or k.startswith("var/"):
+            got[k] = bufs[k.split("/", 1)[1] + (".running_mean" if k.startswith("mean/") else ".running_var")]
+    worst = {}
+    for k, t in got.items():
+        r = torch.from_numpy(np.asarray(g[k], dtype=np.float64))
+        a = t.detach().double().cpu()
+        assert a.shape == r.shape, k
+        rel = float((a - r).abs().max()) / max(float(r.abs().max()), 1e-12)
+        worst[k] = rel
+        bar = 1e-4 if k.startswith(("mean/", "var/")) else 2e-3
+        assert rel <= bar, f"{k}: {rel:.3e} > {bar}"
+    print("worst relative error per tensor:", {k: f"{v:.1e}" for k, v in sorted(worst.items())})
