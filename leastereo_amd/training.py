@@ -222,6 +222,8 @@ def convbr3d(x, weight, bn: nn.BatchNorm3d | None, relu: bool = True, training: 
         return _ConvBR3dFn.apply(x, weight, None, None, None, None, False, 0.0, 1e-5, False, relu)
     track = bn.track_running_stats and bn.running_mean is not None
     use_batch = training or not track
+    if use_batch and x.shape[0] * x.shape[2] * x.shape[3] * x.shape[4] == 1:
+        raise ValueError(f"Expected more than 1 value per channel when training, got input size {tuple(x.shape)}")
     momentum = bn.momentum if bn.momentum is not None else 0.0
     if training and track:
         bn.num_batches_tracked.add_(1)

@@ -46,7 +46,7 @@ CASES = [
     (2, 24, 48, 3, 4, 33, 1, True, True, True),    # 1x1 preprocess
     (1, 128, 64, 2, 4, 12, 3, True, True, True),   # conv1 / conv2
     (1, 4, 80, 2, 3, 7, 3, True, True, False),     # two cout blocks, BN without ReLU
-    (1, 3, 5, 1, 1, 1, 3, True, True, True),       # one voxel per sample (padding only)
+    (2, 3, 5, 1, 1, 1, 3, True, True, True),       # one voxel per sample (padding only)
 ]
 
 
@@ -82,6 +82,14 @@ def test_convbr3d_forward_backward_vs_fp64(case):
         _close(bd.grad, ref[4], "dbeta")
         assert torch.allclose(rmd.cpu().double(), ref[5], rtol=1e-5, atol=1e-6)
         assert torch.allclose(rvd.cpu().double(), ref[6], rtol=1e-5, atol=1e-6)
+
+
+def test_single_value_per_channel_in_train_mode_raises():
+    """torch's batch_norm refuses one value per channel in train mode; so does ConvBR3d."""
+    from leastereo_amd.training import ConvBR3d
+    m = ConvBR3d(3, 5, 3, 1, 1).to(DEV).train()
+    with pytest.raises(ValueError):
+        m(torch.randn(1, 3, 1, 1, 1, device=DEV))
 
 
 def test_wgrad_deterministic_and_vs_torch_at_l1_size():
