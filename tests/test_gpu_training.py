@@ -224,8 +224,10 @@ def test_matching_train_step_vs_reference_golden():
     newMatching in train mode (skip_model_3d.py:140-174), Disp (build_model_2d.py:52-57),
     smooth_l1 over the validity mask -- against the reference itself run in float64
     (tests/golden/train_step.npz, tools/gen_golden_train.py) at 96 x 192 D48.
-    Bars (fp32 HIP vs float64 reference): disparity 1e-3 px, loss 1e-5 relative, every
-    stored gradient within 2e-3 of its largest magnitude, batch statistics 1e-4 relative."""
+    Bars: the reference's OWN fp32 step differs from its float64 step (train-mode BN over
+    a batch of one, a sharp softmin: disparity 1.1e-2 px, gradients 0.3-9 % of their
+    scale; ``noise/*`` in the fixture, measured by the generator); every quantity here
+    must be within 3x that figure (plus 1e-4 of its scale, 1e-6 for the statistics)."""
     import numpy as np
     from leastereo_amd.config import LEAStereoArgs, default_arch_args
     from leastereo_amd.model import LEAStereo
@@ -248,8 +250,11 @@ def test_matching_train_step_vs_reference_golden():
     loss = F.smooth_l1_loss(disp[mask], target[mask], reduction="mean")
     loss.backward()
     torch.cuda.synchronize()
-    assert float((disp.detach().cpu() - torch.from_numpy(g["disp"])).abs().max()) <= 1e-3
-    assert abs(loss.item() - float(g["loss"])) <= 1e-5 * abs(float(g["loss"]))
+    noise = {k[6:]: float(v) for k, v in g.items() if k.startswith("noise/")}
+    derr = float((disp.detach().cpu().double() - torch.from_numpy(g["disp"]).double()).abs().max())
+    assert derr <= 3 * noise["disp"] + 1e-4, (derr, noise["disp"])
+    lrel = abs(loss.item() - float(g["loss"])) / abs(float(g["loss"]))
+    assert lrel <= 3 * noise["loss"] + 1e-6, (lrel, noise["loss"])
     got = {"d_fea_l": fl.grad, "d_fea_r": fr.grad}
     params = dict(m.named_parameters())
     bufs = dict(m.named_buffers())
@@ -266,7 +271,8 @@ def test_matching_train_step_vs_reference_golden():
         a = t.detach().double().cpu()
         assert a.shape == r.shape, k
         rel = float((a - r).abs().max()) / max(float(r.abs().max()), 1e-12)
-        worst[k] = rel
-        bar = 1e-4 if k.startswith(("mean/", "var/")) else 2e-3
-        assert rel <= bar, f"{k}: {rel:.3e} > {bar}"
-    print("worst relative error per tensor:", {k: f"{v:.1e}" for k, v in sorted(worst.items())})
+        bar = 3 * noise[k] + (1e-6 if k.startswith(("mean/", "var/")) else 1e-4)
+        worst[k] = (rel, noise[k])
+        assert rel <= bar, f"{k}: {rel:.3e} > {bar:.3e} (reference fp32 noise {noise[k]:.3e})"
+    print(f"disp max |d| {derr:.2e} px (reference fp32: {noise['disp']:.2e}); relative error / reference "
+          "fp32 noise per tensor:", {k: f"{v[0]:.1e}/{v[1]:.1e}" for k, v in sorted(worst.items())})
