@@ -27,3 +27,25 @@ def test_cpu_tensor_raises_no_fallback():
     m = ConvBR3d(4, 4, 3, 1, 1)
     with pytest.raises(_lib.HipKernelError):
         m(torch.randn(1, 4, 2, 3, 4))
+
+
+def test_train_step_golden_matches_model_shapes():
+    """tests/golden/train_step.npz (the reference's own float64 train step) names
+    parameters of this model with its shapes, and carries a noise figure per quantity."""
+    from leastereo_amd.config import LEAStereoArgs, default_arch_args
+    from leastereo_amd.model import LEAStereo
+    from tests.golden_util import golden
+    g = golden("train_step")
+    m = LEAStereo(default_arch_args(LEAStereoArgs(maxdisp=48)), "cpu")
+    params = dict(m.named_parameters())
+    n = 0
+    for k, v in g.items():
+        if k.startswith("grad/"):
+            name = k[5:]
+            shape = tuple(params[name].shape)
+            if name.endswith(("conv1.conv.weight", "conv2.conv.weight")):
+                shape = (8,) + shape[1:]
+            assert tuple(v.shape) == shape, k
+            assert "noise/" + k in g
+            n += 1
+    assert n == 15 and g["disp"].shape == (1, 96, 192) and 0 < float(g["noise/disp"]) < 0.05
