@@ -21,8 +21,8 @@
 // 16 K-steps each.  A (lane l) = dz[co = 16 m + (l & 15)][voxel 4 s + (l >> 4)],
 // B (lane l) = x[(tap, ci) = column l & 15][same voxel]; N tile = 4 taps x 4 channels
 // (k = 3: 7 tiles, the 28th tap slot zero) or 16 channels (k = 1).  Each wave stores
-// its partial block once; a second kernel sums the 4 * nsplit partials in a fixed
-// order, so dw is deterministic.  The reductions of the BN statistics are two-level
+// its partial block once; two more kernels sum the 4 * nsplit partials in a fixed
+// order (32 groups in parallel, then the groups), so dw is deterministic.  The reductions of the BN statistics are two-level
 // in double (per-slice partials, then a fixed-order sum), also deterministic.
 #include <algorithm>
 
@@ -44,7 +44,15 @@ struct WCfg {
   static constexpr int NT = (TAPS + TPT - 1) / TPT;
   static constexpr int XC = SEG + KS - 1;        // staged columns per halo row
   static constexpr int XR = KS * KS;             // staged (kd, kh) rows per channel
-  static constexpr int XS = CI * XR * XC;
+  static constexpr int XS = CI * XR * XC;        // staged halo values per segment
+  // LDS strides (floats): a row of 70 and a channel of 630 (k = 3), a channel of 68
+  // (k = 1) put the 64 lanes of every B read on 64 distinct banks (exhaustive check
+  // over the 7 N tiles and 16 K steps); the dz tile's rows are 68 apart (4 j + kr)
+  static constexpr int XRS = KS == 3 ? 70 : SEG;
+  static constexpr int CIS = KS == 3 ? 630 : 68;
+  static constexpr int XLDS = CI * CIS;
+  static constexpr int GRS = 68;
+  static constexpr int PX = (XS + 255) / 256;    // prefetched halo values per thread
 };
 
 struct WArgs {
@@ -55,12 +63,15 @@ struct WArgs {
   int nwseg, nseg, nsplit;
 };
 
+// Per segment: 4 K-steps x NT x MT MFMAs per wave from LDS; the next segment's halo
+// and dz values are loaded into registers before this segment's MFMAs (they land
+// under them) and written to LDS after the next barrier.
 template <int KS, int MT>
 __global__ __launch_bounds__(256) void wgrad_kernel(const WArgs a) {
   using C = WCfg<KS>;
-  constexpr int NT = C::NT;
-  __shared__ float xs[C::XS];
-  __shared__ float gs[16 * MT * SEG];
+  constexpr int NT = C::NT, PX = C::PX, PG = MT * 4;  // 16 MT rows x 64 / 256 threads
+  __shared__ float xs[C::XLDS];
+  __shared__ float gs[16 * MT * C::GRS];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int ci0 = blockIdx.y * C::CI, co0 = blockIdx.z * 16 * MT;
   const long long HW = (long long)a.H * a.W, V = HW * a.D;
@@ -74,45 +85,63 @@ __global__ __launch_bounds__(256) void wgrad_kernel(const WArgs a) {
     const int tap = nt * C::TPT + j / C::CI, ci = j % C::CI;
     const int kd = tap / (KS * KS), kh = (tap / KS) % KS, kw = tap % KS;
     bval[nt] = tap < C::TAPS;
-    boff[nt] = bval[nt] ? (ci * C::XR + kd * KS + kh) * C::XC + kw : 0;
+    boff[nt] = bval[nt] ? ci * C::CIS + (kd * KS + kh) * C::XRS + kw : 0;
   }
-  f32x4 acc[MT][NT];
-#pragma unroll
-  for (int m = 0; m < MT; ++m)
-#pragma unroll
-    for (int nt = 0; nt < NT; ++nt) acc[m][nt] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  for (int seg = blockIdx.x; seg < a.nseg; seg += a.nsplit) {
+  // the staging slots of this thread: halo value t = e / (ci, row, col), dz value t = (co, col)
+  float px[PX], pg[PG];
+  auto load_seg = [&](int seg) {
     const int wsg = seg % a.nwseg;
     int r = seg / a.nwseg;
     const int h = r % a.H;
     r /= a.H;
     const int d = r % a.D, b = r / a.D;
     const int w0 = wsg * SEG;
-    __syncthreads();  // the previous segment's LDS reads are done
-    for (int e = tid; e < C::XS; e += 256) {
-      const int col = e % C::XC, t = e / C::XC;
-      const int row = t % C::XR, ci = t / C::XR;
+#pragma unroll
+    for (int t = 0; t < PX; ++t) {
+      const int e = tid + 256 * t;
+      const int col = e % C::XC, r2 = e / C::XC;
+      const int row = r2 % C::XR, c = ci0 + r2 / C::XR;
       const int dd = d + row / KS - KS / 2, hh = h + row % KS - KS / 2, ww = w0 + col - KS / 2;
-      const int c = ci0 + ci;
-      float v = 0.f;
-      if (c < a.cin && (unsigned)dd < (unsigned)a.D && (unsigned)hh < (unsigned)a.H && (unsigned)ww < (unsigned)a.W)
-        v = a.x[((long long)b * a.cin + c) * V + dd * HW + (long long)hh * a.W + ww];
-      xs[e] = v;
+      const bool ok = e < C::XS && c < a.cin && (unsigned)dd < (unsigned)a.D && (unsigned)hh < (unsigned)a.H &&
+                      (unsigned)ww < (unsigned)a.W;
+      px[t] = ok ? a.x[((long long)b * a.cin + c) * V + dd * HW + (long long)hh * a.W + ww] : 0.f;
     }
-    for (int e = tid; e < 16 * MT * SEG; e += 256) {
-      const int col = e % SEG, co = e / SEG;
-      const int c = co0 + co, ww = w0 + col;
-      gs[e] = (c < a.cout && ww < a.W) ? a.dz[((long long)b * a.cout + c) * V + d * HW + (long long)h * a.W + ww]
+#pragma unroll
+    for (int t = 0; t < PG; ++t) {
+      const int e = tid + 256 * t, col = e % SEG, c = co0 + e / SEG, ww = w0 + col;
+      pg[t] = (c < a.cout && ww < a.W) ? a.dz[((long long)b * a.cout + c) * V + d * HW + (long long)h * a.W + ww]
                                        : 0.f;
     }
+  };
+
+  f32x4 acc[MT][NT];
+#pragma unroll
+  for (int m = 0; m < MT; ++m)
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) acc[m][nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  if ((int)blockIdx.x < a.nseg) load_seg(blockIdx.x);
+  for (int seg = blockIdx.x; seg < a.nseg; seg += a.nsplit) {
+    __syncthreads();  // the previous segment's LDS reads are done
+#pragma unroll
+    for (int t = 0; t < PX; ++t) {
+      const int e = tid + 256 * t;
+      const int col = e % C::XC, r2 = e / C::XC;
+      if (e < C::XS) xs[(r2 / C::XR) * C::CIS + (r2 % C::XR) * C::XRS + col] = px[t];
+    }
+#pragma unroll
+    for (int t = 0; t < PG; ++t) {
+      const int e = tid + 256 * t;
+      gs[(e / SEG) * C::GRS + e % SEG] = pg[t];
+    }
     __syncthreads();
+    if (seg + a.nsplit < a.nseg) load_seg(seg + a.nsplit);
 #pragma unroll
     for (int q = 0; q < SEG / (4 * NWAVE); ++q) {
       const int v = 4 * (wave + NWAVE * q) + kr;
       float av[MT];
 #pragma unroll
-      for (int m = 0; m < MT; ++m) av[m] = gs[(16 * m + j) * SEG + v];
+      for (int m = 0; m < MT; ++m) av[m] = gs[(16 * m + j) * C::GRS + v];
 #pragma unroll
       for (int nt = 0; nt < NT; ++nt) {
         const float bv = bval[nt] ? xs[boff[nt] + v] : 0.f;
@@ -138,10 +167,29 @@ __global__ __launch_bounds__(256) void wgrad_kernel(const WArgs a) {
     }
 }
 
-__global__ void sum_partials_kernel(const float* __restrict__ part, float* __restrict__ out, long long n, int np) {
+// fixed-order two-level sum of the np partials: stage 1, workgroup (element block x,
+// group y) sums partials y, y + G, ... of 64 elements (wave w takes every 4th of them,
+// coalesced over the lanes), then its 4 waves in order; stage 2 sums the G groups
+constexpr int kSumGroups = 32;
+
+__global__ __launch_bounds__(256) void sum_partials_stage1(const float* __restrict__ part, float* __restrict__ part2,
+                                                           long long n, int np) {
+  __shared__ float red[NWAVE][64];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const long long e = blockIdx.x * 64LL + lane;
+  const int G = gridDim.y, y = blockIdx.y;
+  float s = 0.f;
+  if (e < n)
+    for (int p = y + G * wave; p < np; p += G * NWAVE) s += part[(long long)p * n + e];
+  red[wave][lane] = s;
+  __syncthreads();
+  if (wave == 0 && e < n) part2[(long long)y * n + e] = ((red[0][lane] + red[1][lane]) + red[2][lane]) + red[3][lane];
+}
+
+__global__ void sum_partials_stage2(const float* __restrict__ part2, float* __restrict__ out, long long n, int G) {
   for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
     float s = 0.f;
-    for (int p = 0; p < np; ++p) s += part[(long long)p * n + i];
+    for (int y = 0; y < G; ++y) s += part2[(long long)y * n + i];
     out[i] = s;
   }
 }
@@ -384,16 +432,17 @@ __global__ void cost_volume_bwd_kernel(const float* __restrict__ dcost, float* _
   }
 }
 
-inline int mt_for(int cout) { return cout <= 16 ? 1 : cout <= 32 ? 2 : 4; }
+// couts per block: 16 or 32 (MT = 4 held 392 registers: one wave per SIMD)
+inline int mt_for(int cout) { return cout <= 16 ? 1 : 2; }
 
-// K split: about 2048 workgroups, at most 64 MB of partials
+// K split: about 2048 workgroups, at most 256 MB of partials
 inline int nsplit_for(int B, int cin, int cout, int D, int H, int W, int k) {
   const int taps = k * k * k, ci = k == 3 ? WCfg<3>::CI : WCfg<1>::CI;
   const long long nblk = (long long)((cin + ci - 1) / ci) * ((cout + 16 * mt_for(cout) - 1) / (16 * mt_for(cout)));
   const long long nseg = (long long)B * D * H * ((W + SEG - 1) / SEG);
   long long s = 2048 / nblk;
   const long long per = (long long)NWAVE * cout * cin * taps * 4;
-  s = std::min(s, (64LL << 20) / per);
+  s = std::min(s, (256LL << 20) / per);
   s = std::min(s, nseg);
   return (int)std::max(1LL, s);
 }
@@ -409,7 +458,7 @@ using namespace lea::grad;
 extern "C" size_t lea_conv3d_wgrad_workspace_bytes(int B, int cin, int cout, int D, int H, int W, int k) {
   if (B <= 0 || cin <= 0 || cout <= 0 || D <= 0 || H <= 0 || W <= 0 || (k != 1 && k != 3)) return 0;
   const int ns = nsplit_for(B, cin, cout, D, H, W, k);
-  return (size_t)ns * NWAVE * cout * cin * k * k * k * sizeof(float);
+  return ((size_t)ns * NWAVE + kSumGroups) * cout * cin * k * k * k * sizeof(float);
 }
 
 extern "C" int lea_conv3d_wgrad(const float* x, const float* dz, float* dw, void* workspace, size_t ws_bytes, int B,
@@ -440,13 +489,18 @@ extern "C" int lea_conv3d_wgrad(const float* x, const float* dz, float* dw, void
   LEA_CHECK_ARG(grid.y <= 65535 && grid.z <= 65535, "lea_conv3d_wgrad: grid too large");
 #define LEA_WGRAD(KS, MT) \
   if (k == KS && mt == MT) wgrad_kernel<KS, MT><<<grid, 256, 0, st>>>(a);
-  LEA_WGRAD(3, 1) LEA_WGRAD(3, 2) LEA_WGRAD(3, 4) LEA_WGRAD(1, 1) LEA_WGRAD(1, 2) LEA_WGRAD(1, 4)
+  LEA_WGRAD(3, 1) LEA_WGRAD(3, 2) LEA_WGRAD(1, 1) LEA_WGRAD(1, 2)
 #undef LEA_WGRAD
   int rc = launch_status("lea_conv3d_wgrad");
   if (rc) return rc;
   const long long n = (long long)cout * cin * k * k * k;
-  sum_partials_kernel<<<grid_for(n), 256, 0, st>>>(a.part, dw, n, a.nsplit * NWAVE);
-  return launch_status("lea_conv3d_wgrad(sum)");
+  const int np = a.nsplit * NWAVE, G = std::min(kSumGroups, np);
+  float* const part2 = a.part + (long long)np * n;
+  sum_partials_stage1<<<dim3((unsigned)((n + 63) / 64), (unsigned)G), 256, 0, st>>>(a.part, part2, n, np);
+  rc = launch_status("lea_conv3d_wgrad(sum 1)");
+  if (rc) return rc;
+  sum_partials_stage2<<<grid_for(n), 256, 0, st>>>(part2, dw, n, G);
+  return launch_status("lea_conv3d_wgrad(sum 2)");
 }
 
 extern "C" int lea_conv3d_flip_weights(const float* w, float* wt, int cout, int cin, int k, void* stream) {

@@ -8,11 +8,12 @@ backward run on ``csrc/conv3d_grad.hip`` plus the forward conv engine, so
 
 Forward (train mode: batch statistics, running-stat update with ``bn.momentum``;
 eval mode: running statistics):
-    z = conv3d(x, w)                  lea_conv3d_bnrelu (stride 1, pad k // 2, no BN)
+    z = conv3d(x, w)                  lea_conv3d_bnrelu[_wino] (stride 1, pad k // 2, no BN;
+                                      the inference planner's engine choice)
     y = relu(bn(z))                   lea_bn_forward_f32
 Backward:
     dz, dgamma, dbeta                 lea_bn_backward_f32 (ReLU mask from y)
-    dx = conv3d(dz, flip(w)^T)        lea_conv3d_flip_weights + lea_conv3d_bnrelu
+    dx = conv3d(dz, flip(w)^T)        lea_conv3d_flip_weights + lea_conv3d_bnrelu[_wino]
     dw = sum dz (x) x                 lea_conv3d_wgrad (deterministic MFMA reduction)
 
 Only the hot path's ConvBR shapes are supported (stride 1, padding k // 2, k in
@@ -73,6 +74,16 @@ def _ptr(t):
     return t.data_ptr() if t is not None else None
 
 
+def _conv(x: torch.Tensor, w: torch.Tensor, relu: bool = False) -> torch.Tensor:
+    """Bias-free stride-1, pad k // 2 conv (optionally ReLU) on the engine the inference
+    planner would pick for this shape (Winograd where eligible and measured faster)."""
+    cout, cin, k = w.shape[0], w.shape[1], w.shape[-1]
+    b, _, d, h, wd = x.shape
+    if kernels.wino_eligible(cout, cin, k) and kernels.wino_preferred(b, cout, cin, d, h, wd):
+        return kernels.conv3d_bnrelu_wino(x, kernels.pack_conv_weight_wino(w), cout, None, None, relu=relu)
+    return kernels.conv3d_bnrelu(x, kernels.pack_conv_weight(w), cout, k, None, None, relu=relu)
+
+
 class _ConvBR3dFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, gamma, beta, running_mean, running_var, training, momentum, eps, use_bn,
@@ -83,8 +94,7 @@ class _ConvBR3dFn(torch.autograd.Function):
         cout, k = weight.shape[0], weight.shape[-1]
         if weight.shape[1] != cin:
             raise ValueError(f"ConvBR3d: weight {tuple(weight.shape)} does not take {cin} channels")
-        z = kernels.conv3d_bnrelu(x, kernels.pack_conv_weight(weight), cout, k, None, None,
-                                  relu=not use_bn and relu)
+        z = _conv(x, weight, relu=not use_bn and relu)
         v = d * h * w
         lib = _lib.load()
         if use_bn:
@@ -123,8 +133,7 @@ class _ConvBR3dFn(torch.autograd.Function):
             "lea_bn_backward_f32")
         dx = dw = None
         if ctx.needs_input_grad[0]:
-            wt = flip_weights(weight)
-            dx = kernels.conv3d_bnrelu(dz, kernels.pack_conv_weight(wt), x.shape[1], k, None, None, relu=False)
+            dx = _conv(dz, flip_weights(weight))
         if ctx.needs_input_grad[1]:
             dw = conv3d_wgrad(x, dz, k)
         return (dx, dw, dgamma if ctx.needs_input_grad[2] else None,
