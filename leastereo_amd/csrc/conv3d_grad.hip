@@ -242,8 +242,8 @@ __global__ __launch_bounds__(256) void bn_moments_kernel(const BnArgs a, double*
   const long long e0 = n * s / kSlices, e1 = n * (s + 1) / kSlices;
   const float mu = MODE == kMomentsGrad ? a.mean[c] : 0.f, is = MODE == kMomentsGrad ? a.invstd[c] : 0.f;
   double s0 = 0.0, s1 = 0.0;
-  for (long long e = e0 + threadIdx.x; e < e1; e += blockDim.x) {
-    const long long b = e / a.V, v = e - b * a.V;
+  long long e = e0 + threadIdx.x, b = e / a.V, v = e - b * a.V;  // (b, v) stepped, not divided
+  for (; e < e1; e += blockDim.x) {
     const long long i = (b * a.C + c) * a.V + v;
     const float zv = a.z[i];
     if (MODE == kMomentsZ) {
@@ -254,6 +254,11 @@ __global__ __launch_bounds__(256) void bn_moments_kernel(const BnArgs a, double*
       if (a.relu && !(a.y[i] > 0.f)) g = 0.f;
       s0 += g;
       s1 += (double)g * ((zv - mu) * is);
+    }
+    v += blockDim.x;
+    while (v >= a.V) {
+      v -= a.V;
+      ++b;
     }
   }
   const double t0 = block_sum(s0, red);
@@ -298,14 +303,17 @@ __global__ void bn_eval_stats_kernel(int C, float eps, const float* __restrict__
 }
 
 // y = relu((z - mean) * invstd * gamma + beta)  (aten's batch_norm element order)
-__global__ void bn_apply_kernel(const float* __restrict__ z, float* __restrict__ y, int C, long long V, long long n,
+// grid: (voxel blocks, B * C rows); row r = b * C + c
+__global__ void bn_apply_kernel(const float* __restrict__ z, float* __restrict__ y, int C, long long V,
                                 const float* __restrict__ mean, const float* __restrict__ invstd,
                                 const float* __restrict__ gamma, const float* __restrict__ beta, int relu) {
-  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
-    const int c = (int)((i / V) % C);
-    float v = (z[i] - mean[c]) * invstd[c];
-    v = v * (gamma ? gamma[c] : 1.f) + (beta ? beta[c] : 0.f);
-    y[i] = relu ? fmaxf(v, 0.f) : v;
+  const int c = (int)(blockIdx.y % C);
+  const float mu = mean[c], is = invstd[c], g = gamma ? gamma[c] : 1.f, bt = beta ? beta[c] : 0.f;
+  const float* zr = z + (long long)blockIdx.y * V;
+  float* yr = y + (long long)blockIdx.y * V;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < V; i += (long long)gridDim.x * blockDim.x) {
+    const float v = (zr[i] - mu) * is * g + bt;
+    yr[i] = relu ? fmaxf(v, 0.f) : v;
   }
 }
 
@@ -329,14 +337,16 @@ __global__ void bn_bwd_finalize_kernel(const double* __restrict__ part, int C, l
   coef[3 * c + 2] = train ? (float)(s1 / (double)n) : 0.f;
 }
 
-__global__ void bn_bwd_apply_kernel(const BnArgs a, const float* __restrict__ coef, float* __restrict__ dz,
-                                    long long n) {
-  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
-    const int c = (int)((i / a.V) % a.C);
+__global__ void bn_bwd_apply_kernel(const BnArgs a, const float* __restrict__ coef, float* __restrict__ dz) {
+  const int c = (int)(blockIdx.y % a.C);
+  const float mu = a.mean[c], is = a.invstd[c], k = coef[3 * c], mg = coef[3 * c + 1], mgx = coef[3 * c + 2];
+  const long long r0 = (long long)blockIdx.y * a.V;
+  for (long long v = blockIdx.x * (long long)blockDim.x + threadIdx.x; v < a.V; v += (long long)gridDim.x * blockDim.x) {
+    const long long i = r0 + v;
     float g = a.dy[i];
     if (a.relu && !(a.y[i] > 0.f)) g = 0.f;
-    const float xh = (a.z[i] - a.mean[c]) * a.invstd[c];
-    dz[i] = coef[3 * c] * (g - coef[3 * c + 1] - xh * coef[3 * c + 2]);
+    const float xh = (a.z[i] - mu) * is;
+    dz[i] = k * (g - mg - xh * mgx);
   }
 }
 
@@ -448,6 +458,12 @@ inline int nsplit_for(int B, int cin, int cout, int D, int H, int W, int k) {
 }
 
 inline int grid_for(long long n) { return (int)std::min<long long>((n + 255) / 256, 4096); }
+// (voxel blocks, B * C rows) for the per-channel elementwise kernels
+inline dim3 row_grid(int B, int C, long long V) {
+  const long long rows = (long long)B * C;
+  return dim3((unsigned)std::max<long long>(1, std::min<long long>((V + 255) / 256, 4096 / std::min(rows, 4096LL) + 1)),
+              (unsigned)rows);
+}
 
 }  // namespace grad
 }  // namespace lea
@@ -520,13 +536,12 @@ extern "C" int lea_bn_forward_f32(const float* z, float* y, int B, int C, int64_
                                   float eps, int training, unsigned flags, float* mean, float* invstd,
                                   void* workspace, void* stream) {
   LEA_CHECK_ARG(z && y && mean && invstd, "lea_bn_forward_f32: null pointer");
-  LEA_CHECK_ARG(B > 0 && C > 0 && V > 0, "lea_bn_forward_f32: bad shape");
+  LEA_CHECK_ARG(B > 0 && C > 0 && V > 0 && (long long)B * C <= 65535, "lea_bn_forward_f32: bad shape");
   LEA_CHECK_ARG((running_mean == nullptr) == (running_var == nullptr), "lea_bn_forward_f32: running stats pair");
   LEA_CHECK_ARG(training || running_mean, "lea_bn_forward_f32: eval mode needs the running stats");
   LEA_CHECK_ARG(!training || workspace, "lea_bn_forward_f32: train mode needs the workspace");
   LEA_CHECK_ARG(eps > 0.f && momentum >= 0.f && momentum <= 1.f, "lea_bn_forward_f32: eps/momentum");
   hipStream_t st = as_stream(stream);
-  const long long n = (long long)B * C * V;
   if (training) {
     BnArgs a{z, nullptr, nullptr, nullptr, nullptr, B, C, V, 0};
     bn_moments_kernel<kMomentsZ><<<dim3(kSlices, C), 256, 0, st>>>(a, (double*)workspace);
@@ -539,7 +554,7 @@ extern "C" int lea_bn_forward_f32(const float* z, float* y, int B, int C, int64_
   }
   int rc = launch_status("lea_bn_forward_f32(stats)");
   if (rc) return rc;
-  bn_apply_kernel<<<grid_for(n), 256, 0, st>>>(z, y, C, V, n, mean, invstd, gamma, beta, (flags & LEA_RELU) ? 1 : 0);
+  bn_apply_kernel<<<row_grid(B, C, V), 256, 0, st>>>(z, y, C, V, mean, invstd, gamma, beta, (flags & LEA_RELU) ? 1 : 0);
   return launch_status("lea_bn_forward_f32(apply)");
 }
 
@@ -549,9 +564,8 @@ extern "C" int lea_bn_backward_f32(const float* dy, const float* y, const float*
                                    void* stream) {
   LEA_CHECK_ARG(dy && z && dz && mean && invstd && workspace, "lea_bn_backward_f32: null pointer");
   LEA_CHECK_ARG(!(flags & LEA_RELU) || y, "lea_bn_backward_f32: LEA_RELU needs y");
-  LEA_CHECK_ARG(B > 0 && C > 0 && V > 0, "lea_bn_backward_f32: bad shape");
+  LEA_CHECK_ARG(B > 0 && C > 0 && V > 0 && (long long)B * C <= 65535, "lea_bn_backward_f32: bad shape");
   hipStream_t st = as_stream(stream);
-  const long long n = (long long)B * C * V;
   BnArgs a{z, dy, y, mean, invstd, B, C, V, (flags & LEA_RELU) ? 1 : 0};
   double* part = (double*)workspace;
   float* coef = (float*)(part + (long long)C * kSlices * 2);
@@ -562,7 +576,7 @@ extern "C" int lea_bn_backward_f32(const float* dy, const float* y, const float*
                                                        dgamma, dbeta, coef);
   rc = launch_status("lea_bn_backward_f32(finalize)");
   if (rc) return rc;
-  bn_bwd_apply_kernel<<<grid_for(n), 256, 0, st>>>(a, coef, dz, n);
+  bn_bwd_apply_kernel<<<row_grid(B, C, V), 256, 0, st>>>(a, coef, dz);
   return launch_status("lea_bn_backward_f32(apply)");
 }
 
