@@ -395,11 +395,13 @@ int lea_resample3d_trilinear_backward(const float* dy, float* dx, void* workspac
 
 /* Backward of lea_disparity_regression (build_model_2d.py:33-42,52-57): with
  * U = trilinear(cost, [maxdisp, 3H3, 3W3], align_corners=False), p = softmax(-U, d),
- * disp = sum_d d p_d (disp: the forward's output), writes
- *   dU[b, d, h, w] = -dout[b, h, w] * p_d * (d - disp[b, h, w])   ([B, maxdisp, 3H3, 3W3]);
- * dcost = lea_resample3d_trilinear_backward(dU, align_corners = 0).              */
+ * disp = sum_d d p_d (disp: the forward's output),
+ *   dU[b, d, h, w] = -dout[b, h, w] * p_d * (d - disp[b, h, w]),
+ * and writes dV = its transpose along D only (the depth lerp's two taps per d summed
+ * onto the D3 cost planes): [B, D3, 3H3, 3W3].  dcost = the H/W part,
+ * lea_resample3d_trilinear_backward(dV, [D3, H3, W3] <- [D3, 3H3, 3W3], align_corners = 0). */
 int lea_disparity_regression_backward(const float* cost, const float* disp, const float* dout,
-                                      float* dU, int B, int D3, int H3, int W3, int maxdisp,
+                                      float* dV, int B, int D3, int H3, int W3, int maxdisp,
                                       void* stream);
 
 /* Backward of lea_build_cost_volume (retrain/LEAStereo.py:34-48):

@@ -371,6 +371,10 @@ __global__ void interp_t_kernel(const float* __restrict__ g, float* __restrict__
       p1 = min(n_out - 1, (int)ceilf(((float)i + 1.f + 0.5f) / ratio) + 2);
     }
     const float* gp = g + o * n_out * inner + r;
+    if (n_in == n_out) {  // the forward's identity axis (axis_index: i0 = i1 = o, l0 = 1)
+      out[e] = gp[(long long)i * inner];
+      continue;
+    }
     float s = 0.f;
     for (int p = p0; p <= p1; ++p) {
       const Axis ax = axis_index(ratio, p, n_in, n_out, ac);
@@ -385,10 +389,14 @@ __global__ void interp_t_kernel(const float* __restrict__ g, float* __restrict__
 
 // ---- Disp + DisparityRegression backward (build_model_2d.py:33-42,52-57) ----
 // disp = sum_d d p_d, p = softmax(-U), U = trilinear(cost, ac=False): per output pixel
-// dU_d = -dout * p_d * (d - disp); one thread per pixel walks D twice (min / sum, then
-// the writes), U re-interpolated with the forward's source-index rule.
+// dU_d = -dout * p_d * (d - disp).  One thread per pixel walks D three times (min, sum,
+// then dU), U re-interpolated with the forward's source-index rule; the D part of the
+// interpolation's transpose is applied on the fly -- dU_d goes to the two cost planes
+// its depth lerp read (i0 with l0, i1 with l1; i0 is non-decreasing in d, so a
+// two-value window flushes each plane once, in order) -- and the kernel writes
+// dV[b][dd][oh][ow] over the D3 planes instead of dU over maxdisp.
 __global__ __launch_bounds__(256) void disp_bwd_kernel(const float* __restrict__ cost, const float* __restrict__ disp,
-                                                       const float* __restrict__ dout, float* __restrict__ dU,
+                                                       const float* __restrict__ dout, float* __restrict__ dV,
                                                        int D3, int H3, int W3, int maxdisp, float rd, float rh,
                                                        float rw) {
   const int Ho = 3 * H3, Wo = 3 * W3;
@@ -403,19 +411,37 @@ __global__ __launch_bounds__(256) void disp_bwd_kernel(const float* __restrict__
     return ah.l0 * (aw.l0 * q[ah.i0 * W3 + aw.i0] + aw.l1 * q[ah.i0 * W3 + aw.i1]) +
            ah.l1 * (aw.l0 * q[ah.i1 * W3 + aw.i0] + aw.l1 * q[ah.i1 * W3 + aw.i1]);
   };
-  auto U = [&](int od) {
-    const Axis ad = axis_index(rd, od, D3, maxdisp, 0);
-    return ad.l0 * plane(ad.i0) + ad.l1 * plane(ad.i1);
-  };
+  auto U = [&](const Axis& ad) { return ad.l0 * plane(ad.i0) + ad.l1 * plane(ad.i1); };
   float m = 3.4e38f;
-  for (int od = 0; od < maxdisp; ++od) m = fminf(m, U(od));
+  for (int od = 0; od < maxdisp; ++od) m = fminf(m, U(axis_index(rd, od, D3, maxdisp, 0)));
   float s = 0.f;
-  for (int od = 0; od < maxdisp; ++od) s += expf(m - U(od));
+  for (int od = 0; od < maxdisp; ++od) s += expf(m - U(axis_index(rd, od, D3, maxdisp, 0)));
   const long long pix = ((long long)b * Ho + oh) * Wo + ow;
   const float g = dout[pix] / s, dsp = disp[pix];
   const long long plane_o = (long long)Ho * Wo;
-  float* out = dU + (long long)b * maxdisp * plane_o + (long long)oh * Wo + ow;
-  for (int od = 0; od < maxdisp; ++od) out[od * plane_o] = -g * expf(m - U(od)) * ((float)od - dsp);
+  float* out = dV + (long long)b * D3 * plane_o + (long long)oh * Wo + ow;
+  int lo = 0;
+  float a0 = 0.f, a1 = 0.f;  // plane lo, lo + 1
+  for (int od = 0; od < maxdisp; ++od) {
+    const Axis ad = axis_index(rd, od, D3, maxdisp, 0);
+    const float du = -g * expf(m - U(ad)) * ((float)od - dsp);
+    while (ad.i0 > lo) {
+      out[lo * plane_o] = a0;
+      a0 = a1;
+      a1 = 0.f;
+      ++lo;
+    }
+    a0 += ad.l0 * du;
+    if (ad.i1 != ad.i0)
+      a1 += ad.l1 * du;
+    else
+      a0 += ad.l1 * du;
+  }
+  for (; lo < D3; ++lo) {
+    out[lo * plane_o] = a0;
+    a0 = a1;
+    a1 = 0.f;
+  }
 }
 
 // ---- cost-volume backward (retrain/LEAStereo.py:34-48) ----

@@ -189,11 +189,12 @@ class _DisparityFn(torch.autograd.Function):
     def backward(ctx, dout):
         cost, disp = ctx.saved_tensors
         b, _, d3, h3, w3 = cost.shape
-        du = torch.empty((b, 1, ctx.maxdisp, 3 * h3, 3 * w3), device=cost.device, dtype=torch.float32)
+        # dU transposed along D in the kernel (never materialised over maxdisp planes)
+        dv = torch.empty((b, 1, d3, 3 * h3, 3 * w3), device=cost.device, dtype=torch.float32)
         check(_lib.load().lea_disparity_regression_backward(
-            cost.data_ptr(), disp.data_ptr(), dout.contiguous().data_ptr(), du.data_ptr(), b, d3, h3, w3,
+            cost.data_ptr(), disp.data_ptr(), dout.contiguous().data_ptr(), dv.data_ptr(), b, d3, h3, w3,
             ctx.maxdisp, _stream()), "lea_disparity_regression_backward")
-        return resample3d_backward(du, (d3, h3, w3), align_corners=False), None
+        return resample3d_backward(dv, (d3, h3, w3), align_corners=False), None
 
 
 def disparity_regression(cost: torch.Tensor, maxdisp: int) -> torch.Tensor:
