@@ -94,8 +94,10 @@ def parse(argv=None):
     p.add_argument("--pair-check", type=int, default=1,
                    help="per-pair EPE of every rank's shard vs an independent HIP path, all-gathered")
     p.add_argument("--breakdown", type=int, default=0, help="print per-kernel times to stderr")
-    p.add_argument("--graph", type=int, default=0,
-                   help="time a HIP-graph replay of the forward (LEAStereo.graphed) instead of eager launches")
+    p.add_argument("--graph", type=int, default=1,
+                   help="1: time a HIP-graph replay of the forward (LEAStereo.graphed: one host call per "
+                        "step, same kernels; same-box A/B at C2 +1.2 %%, profiles/r03_graph_ab.txt); "
+                        "0: eager launches")
     p.add_argument("--precision", choices=("f32", "bf16"), default="f32",
                    help="matching-net arithmetic (bf16 = BASELINE configs 3/4)")
     p.add_argument("--config", choices=sorted(CONFIGS), default=None,
