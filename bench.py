@@ -447,6 +447,7 @@ def run(args, info):
         entry = tf.get(f"{dominant}@{cfg}") or (tf.get(dominant) if cfg == "c2" else None) or {}
         traffic = entry.get("bytes_per_launch")
     ms_step = elapsed / args.steps * 1e3
+    probed_steps = 1 if args.graph else args.steps  # forwards the dominant kernel's probe saw
     workload = WORKLOADS.get(cfg, f"{args.height}x{args.width} D={args.maxdisp} {args.precision}, "
                                   f"batch {args.batch} per GPU")
     result = {
@@ -477,9 +478,11 @@ def run(args, info):
                      "work": "MFMA FLOPs the kernel issues per launch (Winograd products, cout "
                              "padded to its blocks); DESIGN.md §4 gives the per-launch formula",
                      "flops_per_launch": issued, "ms_per_launch": ms_per_launch,
-                     "launches_per_step": launches / args.steps,
+                     "launches_per_step": launches / probed_steps,
+                     "timed_over": "one eager forward after the timed graph replays (replays bypass "
+                                   "the launch probe)" if args.graph else "every step of the timed region",
                      "by_shape": [{"shape": "B%d %d->%d @ %dx%dx%d k%d" % sh if sh else None,
-                                   "launches_per_step": d["launches"] / args.steps,
+                                   "launches_per_step": d["launches"] / probed_steps,
                                    "ms_per_launch": d["ms"] / d["launches"],
                                    "issued_tflops": d["mfma_flops"] / d["ms"] / 1e9,
                                    "frac": d["mfma_flops"] / d["ms"] / 1e9 / peak}
