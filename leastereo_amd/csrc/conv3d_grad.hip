@@ -366,9 +366,11 @@ __global__ void interp_t_kernel(const float* __restrict__ g, float* __restrict__
     const int i = (int)(t % n_in);
     const long long o = t / n_in;
     int p0 = 0, p1 = n_out - 1;
-    if (ratio > 0.f) {  // outputs whose source lies in [i - 1, i + 1]
-      p0 = max(0, (int)floorf(fminf(((float)i - 0.5f) / ratio - 0.5f, ((float)i - 1.f) / ratio)) - 2);
-      p1 = min(n_out - 1, (int)ceilf(((float)i + 1.f + 0.5f) / ratio) + 2);
+    if (ratio > 0.f) {  // outputs whose source index i0 is i - 1 or i (one output of slack per side)
+      const float lo = ac ? ((float)i - 1.f) / ratio : ((float)i - 0.5f) / ratio - 0.5f;
+      const float hi = ac ? ((float)i + 1.f) / ratio : ((float)i + 1.5f) / ratio - 0.5f;
+      p0 = max(0, (int)floorf(lo) - 1);
+      p1 = min(n_out - 1, (int)ceilf(hi) + 1);
     }
     const float* gp = g + o * n_out * inner + r;
     if (n_in == n_out) {  // the forward's identity axis (axis_index: i0 = i1 = o, l0 = 1)
