@@ -25,9 +25,11 @@ Extras in the JSON line:
   path_roofline  sum over every launch of one forward of max(issued MFMA FLOP / peak,
                  VALU FLOP / peak, algorithmic bytes / 8 TB/s), for the algorithms
                  actually run, over the measured step time; plus the HBM-only fraction
-  pair_epe_px    per pair of every rank's shard: |HIP - an independent HIP path|
-                 (f32: the direct-conv engine over the in-place cost volume; bf16: the
-                 f32 path), all-gathered over ranks (the data path's one collective)
+  pair_epe_px    per pair of every rank's shard: |HIP - a second HIP path| (f32: the
+                 matching net on the direct-conv engine over the in-place cost volume and
+                 the LDS disparity kernel -- the feature net is the same code in both;
+                 bf16: the f32 path), all-gathered over ranks (the data path's one
+                 collective)
   epe_px         per rank: HIP vs the reference's own fp32 output (golden e2e case)
   cpu_baseline   the CPU oracle (oracle/torch_ref.py, the reference's aten op sequence
                  restated) on the host's physical cores, rank 0, N = 1: C2 (this
@@ -90,6 +92,10 @@ def parse(argv=None):
     p.add_argument("--cpu-timed", type=int, default=3, help="timed CPU forwards per config (+1 warm-up)")
     p.add_argument("--cpu-configs", default="c2,c1", help="CPU baseline configs (c2 = this workload)")
     p.add_argument("--cpu-fp64", type=int, default=1, help="HIP vs a float64 CPU forward at C2")
+    p.add_argument("--gpu-eager", default="default",
+                   help="torch-ROCm GPU-eager leg of the reference op sequence at C1 (BASELINE.md §4), "
+                        "comma list of MIOpen modes: default (immediate mode) and/or benchmark "
+                        "(torch.backends.cudnn.benchmark: MIOpen find per shape); empty to skip")
     p.add_argument("--epe", type=int, default=1, help="check EPE vs the reference golden disparity")
     p.add_argument("--pair-check", type=int, default=1,
                    help="per-pair EPE of every rank's shard vs an independent HIP path, all-gathered")
@@ -210,6 +216,23 @@ def host_cores():
             "cgroup_cpu_quota": quota, "model": model}
 
 
+def rank_threads(world: int) -> int:
+    """Host threads per rank: the physical cores the process may use split over the
+    node's ranks (8 ranks on a 16-core share would otherwise each start 16 threads
+    for the model build and the pair check)."""
+    return max(1, host_cores()["threads"] // max(1, world))
+
+
+def gather_step_stats(step_ms, device):
+    """All-gather every rank's (median, p10, p90) step time [ms] so a straggler shows
+    up in rank 0's line; [] per rank in rank order."""
+    mine = torch.tensor([_quantile(step_ms, 0.5), _quantile(step_ms, 0.1), _quantile(step_ms, 0.9)],
+                        dtype=torch.float64, device=device)
+    allv = parallel.gather_per_pair(mine).view(-1, 3).cpu()
+    return [{"rank": r, "median": float(v[0]), "p10": float(v[1]), "p90": float(v[2])}
+            for r, v in enumerate(allv)]
+
+
 def _time_cpu(fn, timed):
     fn()  # warm-up
     t0 = time.perf_counter()
@@ -272,12 +295,58 @@ def cpu_baseline(args, model, left0, right0, disp0, hip_step_s, device):
                 entry["epe_px_hip_vs_fp64"] = ref.epe(hip_out, want64)
                 entry["epe_px_cpu_f32_vs_fp64"] = ref.epe(want, want64)
             res["configs"][cfg] = entry
+        modes = [m for m in args.gpu_eager.split(",") if m]
+        if modes:
+            res["torch_gpu_eager"] = gpu_eager_baseline(sd, a, device, modes, args.cpu_timed)
     head = res["configs"].get("c2") or next(iter(res["configs"].values()))
     res["value"] = head["cpu_pairs_s"]
     res["sample"] = (f"oracle/torch_ref.py on torch CPU ({cores['model']}, {cores['threads']} threads = "
                      f"physical cores available to the process), {head['timing']}: "
                      + "; ".join(f"{k}: {v['workload']}" for k, v in res["configs"].items()))
     return res
+
+
+def gpu_eager_baseline(sd, arch, device, modes, timed):
+    """BASELINE.md §4's torch-ROCm GPU-eager column: the reference's aten op sequence
+    (oracle/torch_ref.py, as predict.py:227-229 runs the model) on this GPU through
+    MIOpen, fp32 (no TF32), at C1 -- the SceneFlow sample pair, 288x576 D96 -- beside
+    the HIP path on the same pair.  C2 eager is skipped: MIOpen's 3D convolutions at
+    576x960 D192 take minutes per forward in the default mode."""
+    from oracle import torch_ref as ref
+    from tests.golden_util import c1_inputs
+    l, r = (t.to(device) for t in c1_inputs())
+    md = 96
+    sd_dev = {k: v.to(device) for k, v in sd.items()}
+    hip_s, hip_out = _time_hip(build_model(md, device, "f32"), l, r)
+    out = {"workload": "SceneFlow sample pair 0001 (predict.py preprocessing), 288x576 D=96, B=1 fp32",
+           "hip_pairs_s": 1.0 / hip_s, "modes": {}}
+    prev = torch.backends.cudnn.benchmark
+    try:
+        for mode in modes:
+            torch.backends.cudnn.benchmark = mode == "benchmark"
+            warm = 1 if mode == "default" else 3  # benchmark: MIOpen's find on the first call(s)
+            t0 = time.perf_counter()
+            with torch.no_grad():
+                for _ in range(warm):
+                    ref.leastereo_forward(sd_dev, l, r, md, arch)
+                torch.cuda.synchronize()
+                t_warm = time.perf_counter() - t0
+                t0 = time.perf_counter()
+                for _ in range(timed):
+                    want = ref.leastereo_forward(sd_dev, l, r, md, arch)
+                torch.cuda.synchronize()
+            s = (time.perf_counter() - t0) / timed
+            out["modes"][mode] = {
+                "pairs_s": 1.0 / s, "s_per_pair": s, "warmup_s": t_warm,
+                "hip_vs_eager_speedup": s / hip_s, "epe_px_hip_vs_eager": ref.epe(hip_out, want),
+                "timing": f"{warm} warm-up + {timed} timed forwards, torch.backends.cudnn.benchmark="
+                          f"{mode == 'benchmark'}, allow_tf32=False"}
+            del want
+    finally:
+        torch.backends.cudnn.benchmark = prev
+    del sd_dev
+    torch.cuda.empty_cache()
+    return out
 
 
 # ------------------------------------------------------------------------ roofline
@@ -322,19 +391,28 @@ def run_stub(args, info):
     'processes' its shard of world*batch pairs and reports pair index * 1e-3 as its
     per-pair value, so the gathered vector shows the order the ranks' shards land in."""
     parallel.init("gloo", info, None)
+    threads = rank_threads(info.world)
+    torch.set_num_threads(threads)
     shard = parallel.shard(info.world * args.batch, info)
     parallel.barrier()
     t0 = time.perf_counter()
+    step_ms = []
     for _ in range(args.steps):
+        ts = time.perf_counter()
         torch.zeros(args.batch, 8, 8).add_(1.0)
+        step_ms.append((time.perf_counter() - ts) * 1e3 + info.rank)  # rank-tagged: order check
     parallel.barrier()
     elapsed = parallel.max_over_ranks(time.perf_counter() - t0, torch.device("cpu"))
+    per_rank = gather_step_stats(sorted(step_ms), torch.device("cpu"))
+    all_threads = parallel.gather_per_pair(torch.tensor([torch.get_num_threads()], dtype=torch.int64))
     per_pair = parallel.gather_per_pair(torch.tensor([i * 1e-3 for i in shard], dtype=torch.float32))
     shards = parallel.gather_per_pair(torch.tensor([shard.start, shard.stop], dtype=torch.int64))
     if info.is_main:
         print(json.dumps({"metric": METRIC, "value": info.world * args.batch * args.steps / max(elapsed, 1e-9),
                           "unit": "pairs/s", "n_gpus": info.world, "steps": args.steps, "stub": True,
                           "shards": shards.view(-1, 2).tolist(),
+                          "per_rank_step_ms": per_rank, "threads_per_rank": all_threads.tolist(),
+                          "host_threads": host_cores()["threads"],
                           "pair_epe_px": {"per_pair": [float(v) for v in per_pair]}}), flush=True)
     parallel.finalize()
 
@@ -345,6 +423,7 @@ def run(args, info):
     if world > 1:
         torch.cuda.set_device(device)
     parallel.init("nccl", info, device)  # nccl = RCCL over xGMI on ROCm
+    torch.set_num_threads(rank_threads(world))  # the cpu_baseline leg (N = 1) resets it
     torch.backends.cudnn.allow_tf32 = False
     torch.backends.cuda.matmul.allow_tf32 = False
 
@@ -408,19 +487,32 @@ def run(args, info):
         dom_shapes = probe.by_shape(dominant)
         step_ms = sorted(ev[i].elapsed_time(ev[i + 1]) for i in range(args.steps))
     elapsed = parallel.max_over_ranks(elapsed, device)
+    per_rank_steps = gather_step_stats(step_ms, device)
 
     # after the timed region: the per-pair check of this rank's shard against an
     # independent HIP path, then the data path's one collective (all-gather over ranks)
     pair = None
     if args.pair_check:
         ref_prec = "f32_direct" if args.precision == "f32" else "f32"
-        with torch.no_grad():
-            check = build_model(args.maxdisp, device, ref_prec)(left, right)
-            e = (out.double() - check.double()).abs().mean(dim=(1, 2)).float()
+        from leastereo_amd import _lib
+        lib = _lib.load()
+        # the check's disparity regression runs on the online-softmin LDS kernel (the
+        # timed forward uses the register form for the configured depths)
+        _lib.check(lib.lea_disparity_set_register_form(0), "lea_disparity_set_register_form")
+        try:
+            with torch.no_grad():
+                check = build_model(args.maxdisp, device, ref_prec)(left, right)
+                torch.cuda.synchronize()
+        finally:
+            _lib.check(lib.lea_disparity_set_register_form(1), "lea_disparity_set_register_form")
+        e = (out.double() - check.double()).abs().mean(dim=(1, 2)).float()
         del check
         per_pair = [float(v) for v in parallel.gather_per_pair(e).cpu()]
-        pair = {"vs": ("HIP f32 on the direct-conv engine over the in-place cost volume (no Winograd, "
-                       "no factored stem0)" if args.precision == "f32" else "HIP f32 path, same weights"),
+        pair = {"vs": ("HIP f32 with the matching net on the direct-conv engine over the in-place cost "
+                       "volume (no Winograd, no factored stem0) and the online-softmin LDS disparity "
+                       "kernel; the feature net's engine is shared with the timed path"
+                       if args.precision == "f32" else
+                       "HIP f32 path, same weights, online-softmin LDS disparity kernel"),
                 "pairs": world * args.batch, "max": max(per_pair), "mean": sum(per_pair) / len(per_pair),
                 "per_pair": per_pair}
     epe = None
@@ -460,6 +552,8 @@ def run(args, info):
         "ms_per_step": ms_step,
         "step_ms": {"median": _quantile(step_ms, 0.5), "p10": _quantile(step_ms, 0.1),
                     "p90": _quantile(step_ms, 0.9), "source": "HIP events between steps, this rank"},
+        "per_rank_step_ms": per_rank_steps,
+        "host_threads_per_rank": torch.get_num_threads(),
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,

@@ -10,6 +10,18 @@
 #include "leastereo_hip.h"
 #include "leastereo_hip_tuning.h"
 
+// Ablation switches (tools/wino2_ablate.sh, tools/wino2_stamps.py) knock phases out of
+// the product kernels for timing; most of them make the outputs WRONG.  They only build
+// together with LEA_ABLATION_BUILD, which the variant scripts set (never the Makefile).
+#if !defined(LEA_ABLATION_BUILD) &&                                                      \
+    (defined(LEA_EXP_STAMPS) || defined(LEA_EXP_NOWDMA) || defined(LEA_EXP_NOHALO) ||    \
+     defined(LEA_EXP_NORES) || defined(LEA_EXP_NOSTORE) || defined(LEA_EXP_NOBAR1) ||    \
+     defined(LEA_EXP_NOBAR2) || defined(LEA_EXP_NOVPASS) || defined(LEA_EXP_NOLDSRD) ||  \
+     defined(LEA_EXP_NOXF) || defined(LEA_EXP_NOMFMA) || defined(LEA_EXP_NOWAIT) ||      \
+     defined(LEA_EXP_STAGGER))
+#error "LEA_EXP_* ablation switches give wrong outputs: build them only with -DLEA_ABLATION_BUILD"
+#endif
+
 namespace lea {
 
 // Last error text of the calling host thread (lea_last_error()).
@@ -51,7 +63,7 @@ __host__ inline float axis_ratio(int in, int out, int ac) {
   return (float)in / (float)out;
 }
 
-__device__ __forceinline__ Axis axis_index(float ratio, int o, int in, int out, int ac) {
+__host__ __device__ __forceinline__ Axis axis_index(float ratio, int o, int in, int out, int ac) {
 #pragma clang fp contract(off)
   Axis a;
   if (in == out) {

@@ -191,7 +191,7 @@ __global__ __launch_bounds__(256) void tapsum_hwpass_rows_f32(
   const int h1 = min(h0 + R, Ho);
   const int r_lo = axis_index(rh, max(h0 - 1, 0), Hi, Ho, 1).i0;
   const int r_hi = axis_index(rh, min(h1, Ho - 1), Hi, Ho, 1).i1;
-  const int nr = r_hi - r_lo + 1;  // <= nrmax (host bound)
+  const int nr = min(r_hi - r_lo + 1, nrmax);  // == the host's count; the min keeps LDS in bounds
   const long long HWi = (long long)Hi * Wi;
   const float* yp = ws + (long long)plane * 9 * HWi + (long long)r_lo * Wi;
   const int n1 = nr * Wi;
@@ -252,7 +252,15 @@ static int hwpass(const float* ws, void* y, int64_t y_bstride, int B, int cout, 
   const float rh = axis_ratio(Hi, Ho, 1), rw = axis_ratio(Wi, Wo, 1);
   if (g_tapsum_rows) {
     for (int R = 8; R >= 2; R /= 2) {
-      const int nrmax = (int)floorf((float)(R + 1) * rh) + 3;  // rows h0-1 .. h0+R, +1 fp margin
+      // rows h0-1 .. h0+R of every block, from the kernel's own index expression on the
+      // host (the same IEEE float ops, contraction off): the exact largest row count
+      int nrmax = 0;
+      for (int h0 = 0; h0 < Ho; h0 += R) {
+        const int h1 = h0 + R < Ho ? h0 + R : Ho;
+        const int lo = axis_index(rh, h0 > 0 ? h0 - 1 : 0, Hi, Ho, 1).i0;
+        const int hi = axis_index(rh, h1 < Ho - 1 ? h1 : Ho - 1, Hi, Ho, 1).i1;
+        nrmax = hi - lo + 1 > nrmax ? hi - lo + 1 : nrmax;
+      }
       const size_t lds = (size_t)9 * nrmax * Wi * sizeof(float);
       if (lds > 65536) continue;
       dim3 g((unsigned)((Ho + R - 1) / R), (unsigned)(B * cout * Do));

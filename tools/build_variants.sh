@@ -9,7 +9,7 @@ for spec in "$@"; do
   name=${spec%%:*}; flags=${spec#*:}
   mkdir -p build/var/$name
   /opt/rocm/bin/hipcc -O3 -std=c++17 --offload-arch=gfx950 -fPIC -Wall -Wno-unused-function -Iinclude \
-    -Ileastereo_amd/csrc -munsafe-fp-atomics $flags -c leastereo_amd/csrc/$UNIT.hip -o build/var/$name/$UNIT.o &
+    -Ileastereo_amd/csrc -munsafe-fp-atomics -DLEA_ABLATION_BUILD $flags -c leastereo_amd/csrc/$UNIT.hip -o build/var/$name/$UNIT.o &
 done
 wait
 for spec in "$@"; do

@@ -87,6 +87,9 @@ def main():
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--impl", default="hip,torch")
+    ap.add_argument("--torch-modes", default="default,benchmark",
+                    help="MIOpen modes for the torch leg: default (immediate mode) and/or benchmark "
+                         "(torch.backends.cudnn.benchmark=True: MIOpen's find per shape, more warm-up)")
     args = ap.parse_args()
     torch.backends.cudnn.allow_tf32 = False
     dev = "cuda"
@@ -98,7 +101,8 @@ def main():
         x = torch.randn(1, cin, d, h, w, device=dev, generator=gen).requires_grad_(True)
         dy = torch.randn(1, cout, d, h, w, device=dev, generator=gen)
         ms = timed(lambda: m(x).backward(dy), args.steps, args.warmup)
-        fl = 2.0 * 2 * cin * cout * 27 * d * h * w
+        fl = 2.0 * cin * cout * 27 * d * h * w  # one direct conv: 2 FLOPs per MAC
+        # forward + data gradient + weight gradient = three convs' work
         print(json.dumps({"what": "convbr3d_fwd_bwd", "layer": name, "ms": round(ms, 3),
                           "direct_tflops": round(3 * fl / ms / 1e9, 1)}), flush=True)
     model = LEAStereo(default_arch_args(LEAStereoArgs(maxdisp=args.maxdisp)), dev).to(dev).train()
@@ -107,10 +111,16 @@ def main():
     fr = torch.randn(1, 32, h3, w3, device=dev, generator=gen).requires_grad_(True)
     target = torch.rand(1, 3 * h3, 3 * w3, device=dev, generator=gen) * args.maxdisp
     for impl in args.impl.split(","):
-        ms = timed(lambda: step_fn(model, fl, fr, target, impl), args.steps, args.warmup)
-        print(json.dumps({"what": "matching_train_step", "impl": impl, "height": args.height, "width": args.width,
-                          "maxdisp": args.maxdisp, "ms": round(ms, 2),
-                          "peak_gb": round(torch.cuda.max_memory_allocated() / 2 ** 30, 1)}), flush=True)
+        for mode in (args.torch_modes.split(",") if impl == "torch" else ["-"]):
+            torch.backends.cudnn.benchmark = mode == "benchmark"
+            warm = args.warmup + (3 if mode == "benchmark" else 0)
+            t0 = time.perf_counter()
+            ms = timed(lambda: step_fn(model, fl, fr, target, impl), args.steps, warm)
+            print(json.dumps({"what": "matching_train_step", "impl": impl, "miopen_mode": mode,
+                              "height": args.height, "width": args.width, "maxdisp": args.maxdisp,
+                              "ms": round(ms, 2), "warmup_steps": warm,
+                              "wall_s": round(time.perf_counter() - t0, 1),
+                              "peak_gb": round(torch.cuda.max_memory_allocated() / 2 ** 30, 1)}), flush=True)
 
 
 if __name__ == "__main__":
