@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define LEA_ABI_VERSION 10
+#define LEA_ABI_VERSION 11
 
 #define LEA_F32 0
 #define LEA_BF16 1
@@ -355,6 +355,28 @@ int lea_disparity_metrics(const float* pred, int64_t pred_bstride, const float* 
 size_t lea_conv3d_wgrad_workspace_bytes(int B, int cin, int cout, int D, int H, int W, int k);
 int lea_conv3d_wgrad(const float* x, const float* dz, float* dw, void* workspace, size_t ws_bytes,
                      int B, int cin, int cout, int D, int H, int W, int k, void* stream);
+
+/* The feature net's Conv2d 3x3 / stride 1 / pad 1 (operations_2d.py:31-47, the cells and
+ * stem0/stem2 of new_model_2d.py:93-95): dw[co][ci][kh][kw] = sum_{b,h,w} dz[b][co][h][w] *
+ * x[b][ci][h+kh-1][w+kw-1], the same deterministic MFMA reduction as lea_conv3d_wgrad.
+ * x: [B, cin, H, W], dz: [B, cout, H, W], dw: [cout, cin, 3, 3].  The input gradient is
+ * lea_conv2d_bnrelu of dz with w flipped along (kh, kw) and transposed to [cin, cout, 3, 3]. */
+size_t lea_conv2d_wgrad_workspace_bytes(int B, int cin, int cout, int H, int W);
+int lea_conv2d_wgrad(const float* x, const float* dz, float* dw, void* workspace, size_t ws_bytes,
+                     int B, int cin, int cout, int H, int W, void* stream);
+
+/* Backward of lea_conv2d_s3_bnrelu's convolution (stem1, new_model_2d.py:94; stride 3,
+ * pad 1, 3x3: every input pixel is read by exactly one output tap), w: [cout, cin, 3, 3]:
+ *   dx[b][ci][y][x] = sum_co w[co][ci][(y+1)%3][(x+1)%3] * dz[b][co][(y+1)/3][(x+1)/3]
+ *   dw[co][ci][kh][kw] = sum_{b,oy,ox} dz[b][co][oy][ox] * x[b][ci][3oy+kh-1][3ox+kw-1]
+ * x/dx: [B, cin, Hi, Wi]; dz: [B, cout, (Hi-1)/3+1, (Wi-1)/3+1]; contiguous fp32.
+ * workspace: lea_conv2d_s3_wgrad_workspace_bytes(...) bytes (per-slice partials, summed
+ * in a fixed order). */
+int lea_conv2d_s3_backward_data(const float* dz, const float* w, float* dx, int B, int cin, int cout,
+                                int Hi, int Wi, void* stream);
+size_t lea_conv2d_s3_wgrad_workspace_bytes(int B, int cin, int cout, int Hi, int Wi);
+int lea_conv2d_s3_wgrad(const float* x, const float* dz, float* dw, void* workspace, size_t ws_bytes,
+                        int B, int cin, int cout, int Hi, int Wi, void* stream);
 
 /* wt[ci][co][kd][kh][kw] = w[co][ci][k-1-kd][k-1-kh][k-1-kw]: the input gradient of a
  * stride-1, pad k/2 conv is the forward conv of dz with this weight.             */

@@ -12,7 +12,7 @@ LIB_PATH = os.environ.get(
     "LEASTEREO_HIP_LIB",
     os.path.join(os.path.dirname(os.path.abspath(__file__)), "libleastereo_hip.so"))
 
-ABI_VERSION = 10
+ABI_VERSION = 11
 LEA_F32 = 0
 LEA_BF16 = 1
 LEA_RELU = 1
@@ -109,6 +109,11 @@ SIGNATURES = {
     # training backward of ConvBR3d (csrc/conv3d_grad.hip)
     "lea_conv3d_wgrad_workspace_bytes": (ctypes.c_size_t, [_i, _i, _i, _i, _i, _i, _i]),
     "lea_conv3d_wgrad": (_i, [_p, _p, _p, _p, ctypes.c_size_t, _i, _i, _i, _i, _i, _i, _i, _p]),
+    "lea_conv2d_wgrad_workspace_bytes": (ctypes.c_size_t, [_i, _i, _i, _i, _i]),
+    "lea_conv2d_wgrad": (_i, [_p, _p, _p, _p, ctypes.c_size_t, _i, _i, _i, _i, _i, _p]),
+    "lea_conv2d_s3_backward_data": (_i, [_p, _p, _p, _i, _i, _i, _i, _i, _p]),
+    "lea_conv2d_s3_wgrad_workspace_bytes": (ctypes.c_size_t, [_i, _i, _i, _i, _i]),
+    "lea_conv2d_s3_wgrad": (_i, [_p, _p, _p, _p, ctypes.c_size_t, _i, _i, _i, _i, _i, _p]),
     "lea_conv3d_flip_weights": (_i, [_p, _p, _i, _i, _i, _p]),
     "lea_bn_workspace_bytes": (ctypes.c_size_t, [_i]),
     "lea_bn_forward_f32": (_i, [_p, _p, _i, _i, _i64, _p, _p, _p, _p, ctypes.c_float, ctypes.c_float,

@@ -36,20 +36,21 @@ using f32x4 = __attribute__((__vector_size__(4 * sizeof(float)))) float;
 constexpr int SEG = 64;   // voxels (along W) per K segment
 constexpr int NWAVE = 4;  // waves per workgroup
 
-template <int KS>
+// KD = KS: the 3D conv's taps; KD = 1, KS = 3: a Conv2d 3x3 (the feature net, D = 1)
+template <int KS, int KD = KS>
 struct WCfg {
-  static constexpr int TAPS = KS * KS * KS;
+  static constexpr int TAPS = KD * KS * KS;
   static constexpr int CI = KS == 3 ? 4 : 16;    // input channels per chunk
   static constexpr int TPT = 16 / CI;            // taps per 16-column N tile
   static constexpr int NT = (TAPS + TPT - 1) / TPT;
   static constexpr int XC = SEG + KS - 1;        // staged columns per halo row
-  static constexpr int XR = KS * KS;             // staged (kd, kh) rows per channel
+  static constexpr int XR = KD * KS;             // staged (kd, kh) rows per channel
   static constexpr int XS = CI * XR * XC;        // staged halo values per segment
-  // LDS strides (floats): a row of 70 and a channel of 630 (k = 3), a channel of 68
-  // (k = 1) put the 64 lanes of every B read on 64 distinct banks (exhaustive check
-  // over the 7 N tiles and 16 K steps); the dz tile's rows are 68 apart (4 j + kr)
+  // LDS strides (floats): a row of 70 and a channel of 630 (k = 3), 210 (2D 3x3), a
+  // channel of 68 (k = 1) put the 64 lanes of every B read on 64 distinct banks
+  // (exhaustive check over the N tiles and 16 K steps); the dz tile's rows are 68 apart
   static constexpr int XRS = KS == 3 ? 70 : SEG;
-  static constexpr int CIS = KS == 3 ? 630 : 68;
+  static constexpr int CIS = KS == 3 ? XR * 70 : 68;
   static constexpr int XLDS = CI * CIS;
   static constexpr int GRS = 68;
   static constexpr int PX = (XS + 255) / 256;    // prefetched halo values per thread
@@ -66,9 +67,9 @@ struct WArgs {
 // Per segment: 4 K-steps x NT x MT MFMAs per wave from LDS; the next segment's halo
 // and dz values are loaded into registers before this segment's MFMAs (they land
 // under them) and written to LDS after the next barrier.
-template <int KS, int MT>
+template <int KS, int KD, int MT>
 __global__ __launch_bounds__(256) void wgrad_kernel(const WArgs a) {
-  using C = WCfg<KS>;
+  using C = WCfg<KS, KD>;
   constexpr int NT = C::NT, PX = C::PX, PG = MT * 4;  // 16 MT rows x 64 / 256 threads
   __shared__ float xs[C::XLDS];
   __shared__ float gs[16 * MT * C::GRS];
@@ -83,7 +84,7 @@ __global__ __launch_bounds__(256) void wgrad_kernel(const WArgs a) {
 #pragma unroll
   for (int nt = 0; nt < NT; ++nt) {
     const int tap = nt * C::TPT + j / C::CI, ci = j % C::CI;
-    const int kd = tap / (KS * KS), kh = (tap / KS) % KS, kw = tap % KS;
+    const int kd = tap / (KS * KS), kh = (tap / KS) % KS, kw = tap % KS;  // kd = 0 when KD = 1
     bval[nt] = tap < C::TAPS;
     boff[nt] = bval[nt] ? ci * C::CIS + (kd * KS + kh) * C::XRS + kw : 0;
   }
@@ -101,7 +102,7 @@ __global__ __launch_bounds__(256) void wgrad_kernel(const WArgs a) {
       const int e = tid + 256 * t;
       const int col = e % C::XC, r2 = e / C::XC;
       const int row = r2 % C::XR, c = ci0 + r2 / C::XR;
-      const int dd = d + row / KS - KS / 2, hh = h + row % KS - KS / 2, ww = w0 + col - KS / 2;
+      const int dd = d + row / KS - KD / 2, hh = h + row % KS - KS / 2, ww = w0 + col - KS / 2;
       const bool ok = e < C::XS && c < a.cin && (unsigned)dd < (unsigned)a.D && (unsigned)hh < (unsigned)a.H &&
                       (unsigned)ww < (unsigned)a.W;
       px[t] = ok ? a.x[((long long)b * a.cin + c) * V + dd * HW + (long long)hh * a.W + ww] : 0.f;
@@ -474,8 +475,8 @@ __global__ void cost_volume_bwd_kernel(const float* __restrict__ dcost, float* _
 inline int mt_for(int cout) { return cout <= 16 ? 1 : 2; }
 
 // K split: about 2048 workgroups, at most 256 MB of partials
-inline int nsplit_for(int B, int cin, int cout, int D, int H, int W, int k) {
-  const int taps = k * k * k, ci = k == 3 ? WCfg<3>::CI : WCfg<1>::CI;
+inline int nsplit_for(int B, int cin, int cout, int D, int H, int W, int k, int kd) {
+  const int taps = kd * k * k, ci = k == 3 ? WCfg<3>::CI : WCfg<1>::CI;
   const long long nblk = (long long)((cin + ci - 1) / ci) * ((cout + 16 * mt_for(cout) - 1) / (16 * mt_for(cout)));
   const long long nseg = (long long)B * D * H * ((W + SEG - 1) / SEG);
   long long s = 2048 / nblk;
@@ -499,20 +500,24 @@ inline dim3 row_grid(int B, int C, long long V) {
 using namespace lea;
 using namespace lea::grad;
 
-extern "C" size_t lea_conv3d_wgrad_workspace_bytes(int B, int cin, int cout, int D, int H, int W, int k) {
+namespace lea {
+namespace grad {
+
+// K split over nsplit workgroups per (chunk, cout block); kd = k (3D) or 1 (2D 3x3)
+size_t wgrad_ws_bytes(int B, int cin, int cout, int D, int H, int W, int k, int kd) {
   if (B <= 0 || cin <= 0 || cout <= 0 || D <= 0 || H <= 0 || W <= 0 || (k != 1 && k != 3)) return 0;
-  const int ns = nsplit_for(B, cin, cout, D, H, W, k);
-  return ((size_t)ns * NWAVE + kSumGroups) * cout * cin * k * k * k * sizeof(float);
+  const int ns = nsplit_for(B, cin, cout, D, H, W, k, kd);
+  return ((size_t)ns * NWAVE + kSumGroups) * cout * cin * kd * k * k * sizeof(float);
 }
 
-extern "C" int lea_conv3d_wgrad(const float* x, const float* dz, float* dw, void* workspace, size_t ws_bytes, int B,
-                                int cin, int cout, int D, int H, int W, int k, void* stream) {
-  LEA_CHECK_ARG(x && dz && dw && workspace, "lea_conv3d_wgrad: null pointer");
-  LEA_CHECK_ARG(B > 0 && cin > 0 && cout > 0 && D > 0 && H > 0 && W > 0, "lea_conv3d_wgrad: bad shape");
-  LEA_CHECK_ARG(k == 1 || k == 3, "lea_conv3d_wgrad: k=%d unsupported", k);
-  LEA_CHECK_ARG((long long)D * H <= (1LL << 30) / B, "lea_conv3d_wgrad: volume too large");
-  const size_t need = lea_conv3d_wgrad_workspace_bytes(B, cin, cout, D, H, W, k);
-  LEA_CHECK_ARG(ws_bytes >= need, "lea_conv3d_wgrad: workspace %zu < %zu bytes", ws_bytes, need);
+int wgrad(const char* what, const float* x, const float* dz, float* dw, void* workspace, size_t ws_bytes, int B,
+          int cin, int cout, int D, int H, int W, int k, int kd, void* stream) {
+  LEA_CHECK_ARG(x && dz && dw && workspace, "%s: null pointer", what);
+  LEA_CHECK_ARG(B > 0 && cin > 0 && cout > 0 && D > 0 && H > 0 && W > 0, "%s: bad shape", what);
+  LEA_CHECK_ARG(k == 1 || k == 3, "%s: k=%d unsupported", what, k);
+  LEA_CHECK_ARG((long long)D * H <= (1LL << 30) / B, "%s: volume too large", what);
+  const size_t need = wgrad_ws_bytes(B, cin, cout, D, H, W, k, kd);
+  LEA_CHECK_ARG(ws_bytes >= need, "%s: workspace %zu < %zu bytes", what, ws_bytes, need);
   hipStream_t st = as_stream(stream);
   WArgs a;
   a.x = x;
@@ -526,25 +531,48 @@ extern "C" int lea_conv3d_wgrad(const float* x, const float* dz, float* dw, void
   a.W = W;
   a.nwseg = (W + SEG - 1) / SEG;
   a.nseg = B * D * H * a.nwseg;
-  a.nsplit = nsplit_for(B, cin, cout, D, H, W, k);
+  a.nsplit = nsplit_for(B, cin, cout, D, H, W, k, kd);
   const int mt = mt_for(cout);
   const int ci = k == 3 ? WCfg<3>::CI : WCfg<1>::CI;
   const dim3 grid((unsigned)a.nsplit, (unsigned)((cin + ci - 1) / ci), (unsigned)((cout + 16 * mt - 1) / (16 * mt)));
-  LEA_CHECK_ARG(grid.y <= 65535 && grid.z <= 65535, "lea_conv3d_wgrad: grid too large");
-#define LEA_WGRAD(KS, MT) \
-  if (k == KS && mt == MT) wgrad_kernel<KS, MT><<<grid, 256, 0, st>>>(a);
-  LEA_WGRAD(3, 1) LEA_WGRAD(3, 2) LEA_WGRAD(1, 1) LEA_WGRAD(1, 2)
+  LEA_CHECK_ARG(grid.y <= 65535 && grid.z <= 65535, "%s: grid too large", what);
+#define LEA_WGRAD(KS, KD, MT) \
+  if (k == KS && kd == KD && mt == MT) wgrad_kernel<KS, KD, MT><<<grid, 256, 0, st>>>(a);
+  LEA_WGRAD(3, 3, 1) LEA_WGRAD(3, 3, 2) LEA_WGRAD(1, 1, 1) LEA_WGRAD(1, 1, 2) LEA_WGRAD(3, 1, 1) LEA_WGRAD(3, 1, 2)
 #undef LEA_WGRAD
-  int rc = launch_status("lea_conv3d_wgrad");
+  int rc = launch_status(what);
   if (rc) return rc;
-  const long long n = (long long)cout * cin * k * k * k;
+  const long long n = (long long)cout * cin * kd * k * k;
   const int np = a.nsplit * NWAVE, G = std::min(kSumGroups, np);
   float* const part2 = a.part + (long long)np * n;
   sum_partials_stage1<<<dim3((unsigned)((n + 63) / 64), (unsigned)G), 256, 0, st>>>(a.part, part2, n, np);
-  rc = launch_status("lea_conv3d_wgrad(sum 1)");
+  rc = launch_status(what);
   if (rc) return rc;
   sum_partials_stage2<<<grid_for(n), 256, 0, st>>>(part2, dw, n, G);
-  return launch_status("lea_conv3d_wgrad(sum 2)");
+  return launch_status(what);
+}
+
+}  // namespace grad
+}  // namespace lea
+
+extern "C" size_t lea_conv3d_wgrad_workspace_bytes(int B, int cin, int cout, int D, int H, int W, int k) {
+  return wgrad_ws_bytes(B, cin, cout, D, H, W, k, k);
+}
+
+extern "C" int lea_conv3d_wgrad(const float* x, const float* dz, float* dw, void* workspace, size_t ws_bytes, int B,
+                                int cin, int cout, int D, int H, int W, int k, void* stream) {
+  clear_error();
+  return wgrad("lea_conv3d_wgrad", x, dz, dw, workspace, ws_bytes, B, cin, cout, D, H, W, k, k, stream);
+}
+
+extern "C" size_t lea_conv2d_wgrad_workspace_bytes(int B, int cin, int cout, int H, int W) {
+  return wgrad_ws_bytes(B, cin, cout, 1, H, W, 3, 1);
+}
+
+extern "C" int lea_conv2d_wgrad(const float* x, const float* dz, float* dw, void* workspace, size_t ws_bytes, int B,
+                                int cin, int cout, int H, int W, void* stream) {
+  clear_error();
+  return wgrad("lea_conv2d_wgrad", x, dz, dw, workspace, ws_bytes, B, cin, cout, 1, H, W, 3, 1, stream);
 }
 
 extern "C" int lea_conv3d_flip_weights(const float* w, float* wt, int cout, int cin, int k, void* stream) {

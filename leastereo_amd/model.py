@@ -98,12 +98,21 @@ def _head_modules(mod, initial_fm, dims, last3_bn_relu):
 
 class _ExecutorCache:
     """Kernel-side parameters (packed weights, folded BN) built on first use and
-    dropped whenever the weights may have changed (load_state_dict, .to(), ...)."""
+    dropped whenever the weights may have changed: load_state_dict, .to(), and any
+    in-place update of a parameter or buffer (an optimizer step, train-mode running
+    statistics -- train.py alternates training with evaluation), seen through the
+    tensors' version counters."""
 
     _executor_cls = None
 
     def invalidate(self):
         self._executor = None
+        self._versioned = None
+
+    def _weights_version(self):
+        if getattr(self, "_versioned", None) is None:
+            self._versioned = list(self.parameters()) + list(self.buffers())
+        return sum(t._version for t in self._versioned)
 
     def _apply(self, fn, *a, **kw):
         self.invalidate()
@@ -114,9 +123,12 @@ class _ExecutorCache:
         return super()._load_from_state_dict(*a, **kw)
 
     def executor(self):
+        if self._executor is not None and self._executor_version != self._weights_version():
+            self.invalidate()
         if self._executor is None:
             from . import executor
             self._executor = getattr(executor, self._executor_cls)(self)
+            self._executor_version = self._weights_version()
         return self._executor
 
 
@@ -233,6 +245,12 @@ class LEAStereo(nn.Module):
         if not x.is_cuda:
             raise RuntimeError("leastereo_amd.LEAStereo runs the matching net on a ROCm device only")
         self.check_shape(x.shape[2], x.shape[3])
+        if self.training or (torch.is_grad_enabled() and (x.requires_grad or y.requires_grad)):
+            # train.py:150-158: model.train(); model(input1, input2); loss.backward() -- the
+            # differentiable path (train-mode BN, unfused op order, autograd through the
+            # library's backward kernels); eval-mode inference takes the executors below
+            from .training import leastereo_forward_train
+            return leastereo_forward_train(self, x, y)
         # LEAStereo.py:31-32 runs the feature net twice; every layer is per-sample
         # (eval-mode BN), so one call on the stacked pair halves the launch count (the
         # fused stem reads x and y directly into the stacked stem1 maps)

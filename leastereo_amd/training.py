@@ -84,18 +84,86 @@ def _conv(x: torch.Tensor, w: torch.Tensor, relu: bool = False) -> torch.Tensor:
     return kernels.conv3d_bnrelu(x, kernels.pack_conv_weight(w), cout, k, None, None, relu=relu)
 
 
-class _ConvBR3dFn(torch.autograd.Function):
+def conv2d_wgrad(x: torch.Tensor, dz: torch.Tensor) -> torch.Tensor:
+    """Weight gradient of a Conv2d 3x3 / stride 1 / pad 1 on [B, C, 1, H, W] views:
+    x [B, cin, 1, H, W], dz [B, cout, 1, H, W] -> dw [cout, cin, 3, 3]."""
+    kernels._require_cuda(x, dz)
+    x, dz = x.contiguous(), dz.contiguous()
+    b, cin, _, h, w = x.shape
+    cout = dz.shape[1]
+    lib = _lib.load()
+    nws = lib.lea_conv2d_wgrad_workspace_bytes(b, cin, cout, h, w)
+    if nws == 0:
+        raise ValueError(f"conv2d_wgrad: unsupported shape {tuple(x.shape)} -> {cout}")
+    ws = torch.empty(nws // 4, device=x.device, dtype=torch.float32)
+    dw = torch.empty((cout, cin, 3, 3), device=x.device, dtype=torch.float32)
+    check(lib.lea_conv2d_wgrad(x.data_ptr(), dz.data_ptr(), dw.data_ptr(), ws.data_ptr(), nws, b, cin, cout, h, w,
+                               _stream()), "lea_conv2d_wgrad")
+    return dw
+
+
+def conv2d_s3_backward(x: torch.Tensor, dz: torch.Tensor, w: torch.Tensor, need_dx: bool, need_dw: bool):
+    """Gradients of the stride-3 stem conv (new_model_2d.py:94): x [B, cin, 1, Hi, Wi],
+    dz [B, cout, 1, Ho, Wo], w [cout, cin, 3, 3] -> (dx, dw)."""
+    kernels._require_cuda(x, dz, w)
+    x, dz, w = x.contiguous(), dz.contiguous(), w.detach().contiguous()
+    b, cin, _, hi, wi = x.shape
+    cout = w.shape[0]
+    lib = _lib.load()
+    dx = dw = None
+    if need_dx:
+        dx = torch.empty_like(x)
+        check(lib.lea_conv2d_s3_backward_data(dz.data_ptr(), w.data_ptr(), dx.data_ptr(), b, cin, cout, hi, wi,
+                                              _stream()), "lea_conv2d_s3_backward_data")
+    if need_dw:
+        nws = lib.lea_conv2d_s3_wgrad_workspace_bytes(b, cin, cout, hi, wi)
+        ws = torch.empty(nws // 4, device=x.device, dtype=torch.float32)
+        dw = torch.empty((cout, cin, 3, 3), device=x.device, dtype=torch.float32)
+        check(lib.lea_conv2d_s3_wgrad(x.data_ptr(), dz.data_ptr(), dw.data_ptr(), ws.data_ptr(), nws, b, cin, cout,
+                                      hi, wi, _stream()), "lea_conv2d_s3_wgrad")
+    return dx, dw
+
+
+# conv kinds of the ConvBR autograd function: "3d" (Conv3d k in {1, 3}, stride 1),
+# "2d" (Conv2d 3x3 / s1 / p1 on [B, C, 1, H, W] views), "s3" (Conv2d 3x3 / s3 / p1)
+def _conv_forward(kind, x, w, relu=False):
+    if kind == "3d":
+        return _conv(x, w, relu=relu)
+    if kind == "2d":
+        return kernels.conv2d_bnrelu(x, kernels.pack_conv2d_weight(w), w.shape[0], None, None, relu=relu)
+    return kernels.conv2d_s3_bnrelu(x, w, None, None, relu=relu)
+
+
+def _conv_backward(kind, x, w, dz, need_dx, need_dw):
+    if kind == "s3":
+        return conv2d_s3_backward(x, dz, w, need_dx, need_dw)
+    dx = dw = None
+    if kind == "3d":
+        if need_dx:
+            dx = _conv(dz, flip_weights(w))
+        if need_dw:
+            dw = conv3d_wgrad(x, dz, w.shape[-1])
+        return dx, dw
+    if need_dx:  # flipped along (kh, kw), [cin, cout, 3, 3]: the transposed conv's weight
+        wt = w.detach().flip(2, 3).transpose(0, 1).contiguous()
+        dx = kernels.conv2d_bnrelu(dz, kernels.pack_conv2d_weight(wt), w.shape[1], None, None, relu=False)
+    if need_dw:
+        dw = conv2d_wgrad(x, dz)
+    return dx, dw
+
+
+class _ConvBRFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, gamma, beta, running_mean, running_var, training, momentum, eps, use_bn,
-                relu):
+                relu, kind="3d"):
         kernels._require_cuda(x, weight)
         x = x.contiguous()
-        b, cin, d, h, w = x.shape
-        cout, k = weight.shape[0], weight.shape[-1]
+        b, cin = x.shape[:2]
+        cout = weight.shape[0]
         if weight.shape[1] != cin:
-            raise ValueError(f"ConvBR3d: weight {tuple(weight.shape)} does not take {cin} channels")
-        z = _conv(x, weight, relu=not use_bn and relu)
-        v = d * h * w
+            raise ValueError(f"ConvBR: weight {tuple(weight.shape)} does not take {cin} channels")
+        z = _conv_forward(kind, x, weight, relu=not use_bn and relu)
+        v = z.shape[2] * z.shape[3] * z.shape[4]
         lib = _lib.load()
         if use_bn:
             y = torch.empty_like(z)
@@ -111,13 +179,13 @@ class _ConvBR3dFn(torch.autograd.Function):
             mean = torch.zeros(cout, device=x.device, dtype=torch.float32)
             invstd = torch.ones_like(mean)
         ctx.save_for_backward(x, weight, gamma, z, y, mean, invstd)
-        ctx.cfg = (bool(training) and use_bn, use_bn, relu, k)
+        ctx.cfg = (bool(training) and use_bn, use_bn, relu, kind)
         return y
 
     @staticmethod
     def backward(ctx, dy):
         x, weight, gamma, z, y, mean, invstd = ctx.saved_tensors
-        train, use_bn, relu, k = ctx.cfg
+        train, use_bn, relu, kind = ctx.cfg
         dy = dy.contiguous()
         b, cout = dy.shape[:2]
         v = dy.shape[2] * dy.shape[3] * dy.shape[4]
@@ -131,13 +199,12 @@ class _ConvBR3dFn(torch.autograd.Function):
             _ptr(gamma) if use_bn else None, mean.data_ptr(), invstd.data_ptr(), 1 if train else 0,
             LEA_RELU if relu else 0, _ptr(dgamma), _ptr(dbeta), ws.data_ptr(), _stream()),
             "lea_bn_backward_f32")
-        dx = dw = None
-        if ctx.needs_input_grad[0]:
-            dx = _conv(dz, flip_weights(weight))
-        if ctx.needs_input_grad[1]:
-            dw = conv3d_wgrad(x, dz, k)
+        dx, dw = _conv_backward(kind, x, weight, dz, ctx.needs_input_grad[0], ctx.needs_input_grad[1])
         return (dx, dw, dgamma if ctx.needs_input_grad[2] else None,
-                dbeta if ctx.needs_input_grad[3] else None) + (None,) * 7
+                dbeta if ctx.needs_input_grad[3] else None) + (None,) * 8
+
+
+_ConvBR3dFn = _ConvBRFn  # the round-3 name (tests, tools)
 
 
 def resample3d_backward(dy: torch.Tensor, in_size, align_corners: bool = True) -> torch.Tensor:
@@ -226,10 +293,11 @@ def build_cost_volume(fl: torch.Tensor, fr: torch.Tensor, maxdisp: int) -> torch
     return _CostVolumeFn.apply(fl, fr, int(maxdisp))
 
 
-def convbr3d(x, weight, bn: nn.BatchNorm3d | None, relu: bool = True, training: bool = False):
-    """Functional form: ConvBR3d of x with ``weight`` and (optionally) ``bn``."""
+def convbr3d(x, weight, bn: nn.Module | None, relu: bool = True, training: bool = False, kind: str = "3d"):
+    """Functional form: ConvBR of x with ``weight`` and (optionally) ``bn``; ``kind``
+    "2d" / "s3" for the feature net's Conv2d 3x3 (stride 1 / 3) on [B, C, 1, H, W] views."""
     if bn is None:
-        return _ConvBR3dFn.apply(x, weight, None, None, None, None, False, 0.0, 1e-5, False, relu)
+        return _ConvBRFn.apply(x, weight, None, None, None, None, False, 0.0, 1e-5, False, relu, kind)
     track = bn.track_running_stats and bn.running_mean is not None
     use_batch = training or not track
     if use_batch and x.shape[0] * x.shape[2] * x.shape[3] * x.shape[4] == 1:
@@ -239,9 +307,9 @@ def convbr3d(x, weight, bn: nn.BatchNorm3d | None, relu: bool = True, training: 
         bn.num_batches_tracked.add_(1)
         if bn.momentum is None:  # cumulative moving average (torch's momentum=None)
             momentum = 1.0 / float(bn.num_batches_tracked.item())
-    return _ConvBR3dFn.apply(x, weight, bn.weight, bn.bias, bn.running_mean if (track and training) or not use_batch
-                             else None, bn.running_var if (track and training) or not use_batch else None,
-                             use_batch, momentum, bn.eps, True, relu)
+    return _ConvBRFn.apply(x, weight, bn.weight, bn.bias, bn.running_mean if (track and training) or not use_batch
+                           else None, bn.running_var if (track and training) or not use_batch else None,
+                           use_batch, momentum, bn.eps, True, relu, kind)
 
 
 class ConvBR3d(nn.Module):
@@ -268,14 +336,23 @@ class ConvBR3d(nn.Module):
 
 # ------------------------------------------------- the matching net's training forward
 def _convbr(m, x, training):
-    """A ``model.ConvBR`` parameter container (operations_3d.py:31-47) through the
-    differentiable HIP op."""
-    return convbr3d(x, m.conv.weight, m.bn if m.use_bn else None, m.relu, training)
+    """A ``model.ConvBR`` parameter container (operations_3d.py:31-47, or
+    operations_2d.py:31-47 on a [B, C, 1, H, W] view) through the differentiable HIP op."""
+    w, bn = m.conv.weight, (m.bn if m.use_bn else None)
+    if w.dim() == 5:
+        return convbr3d(x, w, bn, m.relu, training)
+    if w.shape[-1] == 1:  # Conv2d 1x1 = Conv3d 1x1x1 on the one-plane view
+        return convbr3d(x, w.view(w.shape[0], w.shape[1], 1, 1, 1), bn, m.relu, training)
+    if (m.stride, m.padding) not in ((1, 1), (3, 1)):
+        raise NotImplementedError(f"Conv2d 3x3 stride={m.stride} padding={m.padding}")
+    return convbr3d(x, w, bn, m.relu, training, kind="s3" if m.stride == 3 else "2d")
 
 
 def _cell(cell, s0, s1, training):
-    """Cell.forward, retrain/skip_model_3d.py:41-75 (pairwise sums and the cat stay
-    torch autograd glue; every conv, BN, ReLU and resample runs on the HIP library)."""
+    """Cell.forward, retrain/skip_model_3d.py:41-75 and new_model_2d.py:41-75 (a 2D cell's
+    maps are [B, C, 1, H, W] views: its bilinear resize is the trilinear one with an
+    identity D axis, scale_dimension(1, s) = 1).  Pairwise sums and the cat stay torch
+    autograd glue; every conv, BN, ReLU and resample runs on the HIP library."""
     from .arch import scale_dimension
     prev_input = s1
     if cell.downup_sample != 0:
@@ -339,3 +416,52 @@ def cost_to_disparity_train(model, fl: torch.Tensor, fr: torch.Tensor) -> torch.
     volume -> matching net (BN in the model's train/eval mode) -> Disp."""
     cost = build_cost_volume(fl, fr, model.maxdisp)
     return disparity_regression(matching_forward(model.matching, cost, model.training), model.maxdisp)
+
+
+# ------------------------------------------------- the feature net and the whole model
+def feature_forward(net, x: torch.Tensor, training: bool = True) -> torch.Tensor:
+    """newFeature.forward (retrain/new_model_2d.py:140-165) on ``net`` (``model.NewFeature``'s
+    parameters) with gradients: x [B, 3, H, W] -> [B, 32, H3, W3], the reference's op order,
+    BN in train mode when ``training``."""
+    if x.dim() != 4:
+        raise ValueError("x must be [B, 3, H, W]")
+    stem0 = _convbr(net.stem0, x.unsqueeze(2), training)
+    stem1 = _convbr(net.stem1, stem0, training)
+    stem2 = _convbr(net.stem2, stem1, training)
+    out = (stem1, stem2)
+    for cell in net.cells:
+        out = _cell(cell, out[0], out[1], training)
+    last = out[-1]
+    h, w = stem2.shape[3:]
+    full, half, quarter = (1, h, w), (1, h // 2, w // 2), (1, h // 4, w // 4)
+    lh = last.shape[3]
+    if lh == h:
+        y = last
+    elif lh == h // 2:
+        y = interpolate3d(_convbr(net.last_6, last, training), full)
+    elif lh == h // 4:
+        y = interpolate3d(_convbr(net.last_6, interpolate3d(_convbr(net.last_12, last, training), half),
+                                  training), full)
+    elif lh == h // 8:
+        y = interpolate3d(_convbr(net.last_24, last, training), quarter)
+        y = interpolate3d(_convbr(net.last_12, y, training), half)
+        y = interpolate3d(_convbr(net.last_6, y, training), full)
+    else:
+        # the reference raises UnboundLocalError here (new_model_2d.py:156-165)
+        raise ValueError(f"feature size {tuple(x.shape[2:])} is not legal for the feature net")
+    return _convbr(net.last_3, y, training).squeeze(2)
+
+
+def leastereo_forward_train(model, x: torch.Tensor, y: torch.Tensor) -> torch.Tensor:
+    """LEAStereo.forward (retrain/LEAStereo.py:30-52) with gradients, as train.py:150-158
+    runs it (``model.train()``, ``model(input1, input2)``, ``loss.backward()``): the feature
+    net once per image (train-mode BN normalises each image batch by its own statistics and
+    updates the running stats twice, as the reference's two calls do), the cost volume,
+    the matching net and Disp, every op on the HIP library."""
+    if model.precision != "f32":
+        raise NotImplementedError("training runs in f32 (the reference's arithmetic)")
+    training = model.training
+    fx = feature_forward(model.feature, x, training)
+    fy = feature_forward(model.feature, y, training)
+    cost = build_cost_volume(fx, fy, model.maxdisp)
+    return disparity_regression(matching_forward(model.matching, cost, training), model.maxdisp)

@@ -276,3 +276,222 @@ def test_matching_train_step_vs_reference_golden():
         assert rel <= bar, f"{k}: {rel:.3e} > {bar:.3e} (reference fp32 noise {noise[k]:.3e})"
     print(f"disp max |d| {derr:.2e} px (reference fp32: {noise['disp']:.2e}); relative error / reference "
           "fp32 noise per tensor:", {k: f"{v[0]:.1e}/{v[1]:.1e}" for k, v in sorted(worst.items())})
+
+
+# ---- the feature net's 2D ops (retrain/new_model_2d.py:93-95, models/operations_2d.py:31-47)
+CASES_2D = [
+    # B, cin, cout, H, W, kind, training, bn, relu
+    (2, 16, 16, 12, 70, "2d", True, True, True),    # cell 3x3 op, ragged W segments
+    (1, 3, 16, 20, 33, "2d", True, True, True),     # stem0 on the image (cin 3), dx wanted
+    (1, 32, 32, 9, 17, "2d", False, True, True),    # stem2 shape, eval mode
+    (1, 8, 8, 5, 130, "2d", True, True, False),     # 8-channel cell op, BN without ReLU
+    (2, 16, 32, 29, 50, "s3", True, True, True),    # stem1, H/W not multiples of 3
+    (1, 16, 32, 30, 48, "s3", True, True, True),
+    (1, 5, 40, 7, 8, "s3", False, True, True),      # partial channel chunk, three cout blocks
+]
+
+
+@pytest.mark.parametrize("case", CASES_2D, ids=lambda c: "x".join(map(str, c[:5])) + f"-{c[5]}-t{int(c[6])}r{int(c[8])}")
+def test_convbr2d_forward_backward_vs_fp64(case):
+    """Conv2d 3x3 (stride 1 or 3, pad 1) -> BatchNorm2d -> ReLU on [B, C, 1, H, W] views,
+    forward and every gradient against torch autograd in float64."""
+    from leastereo_amd.training import _ConvBRFn
+    b, cin, cout, h, w, kind, training, use_bn, relu = case
+    stride = 3 if kind == "s3" else 1
+    gen = torch.Generator().manual_seed(11 + cin * 7 + cout + h)
+    x = torch.randn(b, cin, h, w, generator=gen)
+    wt = torch.randn(cout, cin, 3, 3, generator=gen) * (2.0 / (cin * 9)) ** 0.5
+    g = 1 + 0.2 * torch.randn(cout, generator=gen)
+    bt = 0.1 * torch.randn(cout, generator=gen)
+    rm = 0.1 * torch.randn(cout, generator=gen)
+    rv = 1 + torch.rand(cout, generator=gen)
+    ho, wo = (h - 1) // stride + 1, (w - 1) // stride + 1
+    dy = torch.randn(b, cout, ho, wo, generator=gen)
+    momentum, eps = 0.1, 1e-5
+    xr = x.double().requires_grad_(True)
+    wr = wt.double().requires_grad_(True)
+    gr, br = g.double().requires_grad_(True), bt.double().requires_grad_(True)
+    rmr, rvr = rm.double().clone(), rv.double().clone()
+    z = F.conv2d(xr, wr, stride=stride, padding=1)
+    z = F.batch_norm(z, rmr, rvr, gr, br, training, momentum, eps)
+    z = F.relu(z) if relu else z
+    z.backward(dy.double())
+
+    xd = x.to(DEV).unsqueeze(2).requires_grad_(True)
+    wd = wt.to(DEV).requires_grad_(True)
+    gd, bd = g.to(DEV).requires_grad_(True), bt.to(DEV).requires_grad_(True)
+    rmd, rvd = rm.to(DEV), rv.to(DEV)
+    y = _ConvBRFn.apply(xd, wd, gd, bd, rmd, rvd, training, momentum, eps, use_bn, relu, kind)
+    y.backward(dy.to(DEV).unsqueeze(2))
+    torch.cuda.synchronize()
+    _close(y.squeeze(2), z.detach(), "y")
+    _close(xd.grad.squeeze(2), xr.grad, "dx")
+    _close(wd.grad, wr.grad, "dw")
+    _close(gd.grad, gr.grad, "dgamma")
+    _close(bd.grad, br.grad, "dbeta")
+    assert torch.allclose(rmd.cpu().double(), rmr, rtol=1e-5, atol=1e-6)
+    assert torch.allclose(rvd.cpu().double(), rvr, rtol=1e-5, atol=1e-6)
+
+
+def test_conv2d_wgrads_deterministic_at_c2_feature_size():
+    """The feature net's weight gradients at C2's map size (stem2: 32 -> 32 on 192 x 320;
+    stem1: 16 -> 32 stride 3 from 576 x 960) against float64 torch (1e-4 of the scale),
+    bit-identical across two calls."""
+    from leastereo_amd.training import conv2d_s3_backward, conv2d_wgrad
+    gen = torch.Generator(device=DEV).manual_seed(5)
+    x = torch.randn(1, 32, 1, 192, 320, device=DEV, generator=gen)
+    dz = torch.randn(1, 32, 1, 192, 320, device=DEV, generator=gen)
+    a, b = conv2d_wgrad(x, dz), conv2d_wgrad(x, dz)
+    assert torch.equal(a, b)
+    r = torch.nn.grad.conv2d_weight(x[:, :, 0].double().cpu(), (32, 32, 3, 3), dz[:, :, 0].double().cpu(), padding=1)
+    assert float((a.double().cpu() - r).abs().max()) <= 1e-4 * float(r.abs().max())
+    xs = torch.randn(1, 16, 1, 576, 960, device=DEV, generator=gen)
+    dzs = torch.randn(1, 32, 1, 192, 320, device=DEV, generator=gen)
+    w = torch.randn(32, 16, 3, 3, device=DEV, generator=gen)
+    (dx1, dw1), (dx2, dw2) = conv2d_s3_backward(xs, dzs, w, True, True), conv2d_s3_backward(xs, dzs, w, True, True)
+    assert torch.equal(dw1, dw2) and torch.equal(dx1, dx2)
+    r = torch.nn.grad.conv2d_weight(xs[:, :, 0].double().cpu(), (32, 16, 3, 3), dzs[:, :, 0].double().cpu(),
+                                    stride=3, padding=1)
+    assert float((dw1.double().cpu() - r).abs().max()) <= 1e-4 * float(r.abs().max())
+
+
+def test_whole_model_train_step_vs_reference_golden():
+    """train.py:150-158 through the drop-in's public API: ``model.train()``,
+    ``disp = model(input1, input2)`` with inputs that require grad (train.py:136),
+    smooth_l1 over the validity mask, ``loss.backward()`` -- the feature net twice (its own
+    train-mode BN statistics per image), the cost volume, newMatching, Disp, every op on
+    the HIP library -- against the reference model itself run in float64
+    (tests/golden/train_step_full.npz, tools/gen_golden_train_full.py) at 96 x 192 D48.
+    Bars: 3x the reference's own fp32-vs-fp64 difference per quantity (``noise/*``:
+    disparity 4.6e-2 px, gradients 1.3-3.9 % of their scale) plus 1e-4 of the scale."""
+    import numpy as np
+    from leastereo_amd.config import LEAStereoArgs, default_arch_args
+    from leastereo_amd.model import LEAStereo
+    from leastereo_amd.weights import seeded_normal
+    from tests.golden_util import golden, state_dict
+    g = golden("train_step_full")
+    m = LEAStereo(default_arch_args(LEAStereoArgs(maxdisp=48)), DEV)
+    m.load_state_dict(state_dict(), strict=True)
+    m = m.to(DEV)
+    for mod in m.modules():
+        if isinstance(mod, (torch.nn.BatchNorm2d, torch.nn.BatchNorm3d)):
+            mod.momentum = 1.0
+    m.train()
+    left = torch.from_numpy(seeded_normal(311, (1, 3, 96, 192))).to(DEV).requires_grad_(True)
+    right = torch.from_numpy(seeded_normal(312, (1, 3, 96, 192))).to(DEV).requires_grad_(True)
+    target = torch.from_numpy(seeded_normal(313, (1, 96, 192))).to(DEV) * 4 + 20
+    disp = m(left, right)
+    mask = (target < 48) & (target > 0.001)
+    loss = F.smooth_l1_loss(disp[mask], target[mask], reduction="mean")
+    loss.backward()
+    torch.cuda.synchronize()
+    noise = {k[6:]: float(v) for k, v in g.items() if k.startswith("noise/")}
+    derr = float((disp.detach().cpu().double() - torch.from_numpy(g["disp"]).double()).abs().max())
+    assert derr <= 3 * noise["disp"] + 1e-4, (derr, noise["disp"])
+    lrel = abs(loss.item() - float(g["loss"])) / abs(float(g["loss"]))
+    assert lrel <= 3 * noise["loss"] + 1e-6, (lrel, noise["loss"])
+    got = {"d_left_rows32": left.grad[:, :, :32]}
+    params, bufs = dict(m.named_parameters()), dict(m.named_buffers())
+    for k in g:
+        if k.startswith("grad/"):
+            name = k[5:]
+            t = params[name].grad
+            got[k] = t[:8] if name in ("matching.stem0.conv.weight", "matching.conv1.conv.weight") else t
+        elif k.startswith("mean/") or k.startswith("var/"):
+            got[k] = bufs[k.split("/", 1)[1] + (".running_mean" if k.startswith("mean/") else ".running_var")]
+    worst = {}
+    for k, t in got.items():
+        r = torch.from_numpy(np.asarray(g[k], dtype=np.float64))
+        a = t.detach().double().cpu()
+        assert a.shape == r.shape, k
+        rel = float((a - r).abs().max()) / max(float(r.abs().max()), 1e-12)
+        bar = 3 * noise[k] + (1e-6 if k.startswith(("mean/", "var/")) else 1e-4)
+        worst[k] = (rel, noise[k])
+        assert rel <= bar, f"{k}: {rel:.3e} > {bar:.3e} (reference fp32 noise {noise[k]:.3e})"
+    print(f"disp max |d| {derr:.2e} px (reference fp32: {noise['disp']:.2e}); relative error / reference "
+          "fp32 noise per tensor:", {k: f"{v[0]:.1e}/{v[1]:.1e}" for k, v in sorted(worst.items())})
+
+
+def test_whole_model_eval_mode_gradients_vs_oracle_fp64():
+    """Gradients through the drop-in in eval mode (running-statistics BN, inputs that
+    require grad: the differentiable path) against torch autograd of the oracle
+    (oracle/torch_ref.py, the reference's aten op sequence) in float64 on the CPU, same
+    weights and inputs, at 96 x 192 D48: disparity within 1e-3 px, the input and every
+    parameter gradient within 2e-3 of its scale (eval mode has no batch-statistics
+    amplification: the forward's fp32 noise is 5e-6 px)."""
+    import numpy as np
+    from oracle import torch_ref as ref
+    from leastereo_amd.config import ARCH_DIR, LEAStereoArgs, default_arch_args
+    from leastereo_amd.model import LEAStereo
+    from tests.golden_util import state_dict
+    import os
+    sd = state_dict()
+    m = LEAStereo(default_arch_args(LEAStereoArgs(maxdisp=48)), DEV)
+    m.load_state_dict(sd, strict=True)
+    m = m.to(DEV).eval()
+    gen = torch.Generator().manual_seed(31)
+    left, right = torch.randn(1, 3, 96, 192, generator=gen), torch.randn(1, 3, 96, 192, generator=gen)
+    dout = torch.randn(1, 96, 192, generator=gen)
+    ld, rd = left.to(DEV).requires_grad_(True), right.to(DEV).requires_grad_(True)
+    disp = m(ld, rd)
+    disp.backward(dout.to(DEV))
+    torch.cuda.synchronize()
+    arch = {k: np.load(os.path.join(ARCH_DIR, f)) for k, f in (
+        ("net_arch_fea", "feature_network_path.npy"), ("cell_arch_fea", "feature_genotype.npy"),
+        ("net_arch_mat", "matching_network_path.npy"), ("cell_arch_mat", "matching_genotype.npy"))}
+    sd64 = {k: torch.as_tensor(np.asarray(v)).double().requires_grad_(k.endswith(("conv.weight", "bn.weight",
+                                                                                   "bn.bias")))
+            if np.asarray(v).dtype.kind == "f" else torch.as_tensor(np.asarray(v)) for k, v in sd.items()}
+    lr, rr = left.double().requires_grad_(True), right.double().requires_grad_(True)
+    want = ref.leastereo_forward(sd64, lr, rr, 48, arch)
+    want.backward(dout.double())
+    assert float((disp.detach().cpu().double() - want.detach()).abs().max()) <= 1e-3
+    params = dict(m.named_parameters())
+    checked = 0
+    for k, t in list(sd64.items()) + [("left", lr), ("right", rr)]:
+        if not (isinstance(t, torch.Tensor) and t.requires_grad) or t.grad is None:
+            continue
+        got = (ld.grad if k == "left" else rd.grad if k == "right" else params[k].grad)
+        assert got is not None, k
+        r = t.grad
+        err = float((got.detach().double().cpu() - r).abs().max())
+        assert err <= 2e-3 * float(r.abs().max()) + 1e-9, f"{k}: {err:.3e} vs scale {float(r.abs().max()):.3e}"
+        checked += 1
+    assert checked > 300, checked
+
+
+def test_whole_model_sgd_steps_then_eval_uses_updated_weights():
+    """train.py's loop (zero_grad, forward in train mode, smooth_l1, backward, step) for
+    three steps, then evaluation: the inference executors were built before training
+    (an eval pass) and must see the optimizer's in-place updates (version counters)."""
+    from leastereo_amd.config import LEAStereoArgs, default_arch_args
+    from leastereo_amd.model import LEAStereo
+    from tests.golden_util import state_dict
+    m = LEAStereo(default_arch_args(LEAStereoArgs(maxdisp=48)), DEV)
+    m.load_state_dict(state_dict(), strict=True)
+    m = m.to(DEV).eval()
+    gen = torch.Generator().manual_seed(21)
+    left = torch.randn(1, 3, 96, 192, generator=gen).to(DEV)
+    right = torch.randn(1, 3, 96, 192, generator=gen).to(DEV)
+    with torch.no_grad():
+        before = m(left, right).clone()      # builds and caches the executors
+    m.train()
+    opt = torch.optim.SGD(m.parameters(), lr=1e-3, momentum=0.9)
+    losses = []
+    for _ in range(3):
+        target = (torch.rand(1, 96, 192, generator=gen) * 40 + 1).to(DEV)
+        opt.zero_grad()
+        loss = F.smooth_l1_loss(m(left, right), target, reduction="mean")
+        loss.backward()
+        opt.step()
+        losses.append(loss.item())
+    assert all(v == v and abs(v) < 1e6 for v in losses), losses
+    m.eval()
+    with torch.no_grad():
+        after = m(left, right)
+        # the eval path equals the differentiable path in eval mode on the updated weights
+        ld = left.clone().requires_grad_(True)
+    with torch.enable_grad():
+        diff_path = m(ld, right)
+    assert not torch.equal(after, before)
+    assert float((after - diff_path.detach()).abs().max()) <= 1e-3

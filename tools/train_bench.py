@@ -87,12 +87,15 @@ def main():
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--impl", default="hip,torch")
+    ap.add_argument("--whole", type=int, default=0, help="1: time only the whole-model train step")
     ap.add_argument("--torch-modes", default="default,benchmark",
                     help="MIOpen modes for the torch leg: default (immediate mode) and/or benchmark "
                          "(torch.backends.cudnn.benchmark=True: MIOpen's find per shape, more warm-up)")
     args = ap.parse_args()
     torch.backends.cudnn.allow_tf32 = False
     dev = "cuda"
+    if args.whole:
+        return whole_model(args, dev)
     gen = torch.Generator(device=dev).manual_seed(0)
     # ConvBR3d forward + backward at the hot shapes (C2's L0 8->8 cell, L1 16->16, conv1)
     for name, (cin, cout, d, h, w) in {"L0_8to8": (8, 8, 64, 192, 320), "L1_16to16": (16, 16, 32, 96, 160),
@@ -121,6 +124,30 @@ def main():
                               "ms": round(ms, 2), "warmup_steps": warm,
                               "wall_s": round(time.perf_counter() - t0, 1),
                               "peak_gb": round(torch.cuda.max_memory_allocated() / 2 ** 30, 1)}), flush=True)
+
+
+def whole_model(args, dev):
+    """train.py:150-158 on the drop-in: model.train(), model(left, right) with inputs that
+    require grad, smooth_l1, backward, SGD step -- the whole model (feature net twice,
+    cost volume, matching net, Disp) on the HIP library."""
+    model = LEAStereo(default_arch_args(LEAStereoArgs(maxdisp=args.maxdisp)), dev).to(dev).train()
+    opt = torch.optim.SGD(model.parameters(), lr=1e-4, momentum=0.9)
+    gen = torch.Generator(device=dev).manual_seed(1)
+    left = torch.randn(1, 3, args.height, args.width, device=dev, generator=gen).requires_grad_(True)
+    right = torch.randn(1, 3, args.height, args.width, device=dev, generator=gen).requires_grad_(True)
+    target = torch.rand(1, args.height, args.width, device=dev, generator=gen) * (args.maxdisp - 1)
+
+    def step():
+        opt.zero_grad()
+        disp = model(left, right)
+        mask = (target < args.maxdisp) & (target > 0.001)
+        F.smooth_l1_loss(disp[mask], target[mask], reduction="mean").backward()
+        opt.step()
+    torch.cuda.reset_peak_memory_stats()
+    ms = timed(step, args.steps, args.warmup)
+    print(json.dumps({"what": "whole_model_train_step", "impl": "hip", "height": args.height, "width": args.width,
+                      "maxdisp": args.maxdisp, "ms": round(ms, 2),
+                      "peak_gb": round(torch.cuda.max_memory_allocated() / 2 ** 30, 1)}), flush=True)
 
 
 if __name__ == "__main__":
