@@ -366,8 +366,9 @@ int lea_conv2d_wgrad(const float* x, const float* dz, float* dw, void* workspace
                      int B, int cin, int cout, int H, int W, void* stream);
 
 /* Backward of lea_conv2d_s3_bnrelu's convolution (stem1, new_model_2d.py:94; stride 3,
- * pad 1, 3x3: every input pixel is read by exactly one output tap), w: [cout, cin, 3, 3]:
+ * pad 1, 3x3: every input pixel is read by at most one output tap), w: [cout, cin, 3, 3]:
  *   dx[b][ci][y][x] = sum_co w[co][ci][(y+1)%3][(x+1)%3] * dz[b][co][(y+1)/3][(x+1)/3]
+ *   (0 where (y+1)/3 = Ho or (x+1)/3 = Wo: the last row / column when Hi / Wi % 3 == 0)
  *   dw[co][ci][kh][kw] = sum_{b,oy,ox} dz[b][co][oy][ox] * x[b][ci][3oy+kh-1][3ox+kw-1]
  * x/dx: [B, cin, Hi, Wi]; dz: [B, cout, (Hi-1)/3+1, (Wi-1)/3+1]; contiguous fp32.
  * workspace: lea_conv2d_s3_wgrad_workspace_bytes(...) bytes (per-slice partials, summed

@@ -71,7 +71,8 @@ __global__ __launch_bounds__(256) void conv2d_s3_kernel(const float* __restrict_
 // input row y is read only by output row oy = (y + 1) / 3 at kernel row kh = (y + 1) % 3
 // (columns alike), so
 //   dx[b][ci][y][x] = sum_co w[co][ci][kh(y)][kw(x)] * dz[b][co][oy(y)][ox(x)]
-// and oy <= Ho - 1 for every y < Hi.  One thread per input pixel and 16 channels.
+// (0 where oy = Ho: the last row when Hi % 3 == 0 is read by no output; columns alike).
+// One thread per input pixel and 16 channels.
 constexpr int kS3CiBlock = 16;
 
 __global__ __launch_bounds__(256) void conv2d_s3_dgrad_kernel(const float* __restrict__ dz, const float* __restrict__ w,
@@ -82,12 +83,13 @@ __global__ __launch_bounds__(256) void conv2d_s3_dgrad_kernel(const float* __res
   if (pix >= (long long)Hi * Wi) return;
   const int y = (int)(pix / Wi), x = (int)(pix - (long long)y * Wi);
   const int oy = (y + 1) / 3, ox = (x + 1) / 3, t = ((y + 1) % 3) * 3 + (x + 1) % 3;
-  const float* g = dz + ((long long)b * cout * Ho + oy) * Wo + ox;
+  const bool read = oy < Ho && ox < Wo;
+  const float* g = dz + ((long long)b * cout * Ho + (read ? oy : 0)) * Wo + (read ? ox : 0);
   const long long HWo = (long long)Ho * Wo;
   float acc[kS3CiBlock];
 #pragma unroll
   for (int j = 0; j < kS3CiBlock; ++j) acc[j] = 0.f;
-  for (int co = 0; co < cout; ++co) {
+  for (int co = 0; co < (read ? cout : 0); ++co) {
     const float gv = g[co * HWo];
     const float* wc = w + (long long)co * cin * 9 + t;
 #pragma unroll
