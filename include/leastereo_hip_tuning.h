@@ -76,6 +76,11 @@ int lea_conv3d_wino2_set_walk(int spw);
  * kernel name "..., 2, false>"), 0 = dword pieces ("..., 1, false>"). */
 int lea_conv3d_wino2_set_halo16(int on);
 
+/* 1 (default) = the W x D engine's per-lane 16-cout tile stages its halo as 16-byte
+ * LDS-DMA pieces with interleaved row sets (bank-conflict-free; kernel name
+ * "conv3d_wino2_kernel<8, 1, 1, 4, 2, 4, false>"), 0 = dword pieces ("..., 0, false>"). */
+int lea_conv3d_wino2_set_lane_halo16(int on);
+
 /* 1 (default) = the 16-byte-halo W x D tile runs as the one-barrier pipeline
  * ("conv3d_wino2p_kernel": item i's MFMAs interleaved with item i + 1's transform pass,
  * weights loaded per lane from the packed buffer's lane-major copy), 0 = the two-barrier

@@ -90,6 +90,7 @@ SIGNATURES = {
     "lea_conv3d_wino_set_variant": (_i, [_i]),
     "lea_conv3d_wino2_set_walk": (_i, [_i]),
     "lea_conv3d_wino2_set_halo16": (_i, [_i]),
+    "lea_conv3d_wino2_set_lane_halo16": (_i, [_i]),
     "lea_conv3d_wino2_set_pipeline": (_i, [_i]),
     "lea_conv3d_wino_set_epi_buf": (_i, [_i]),
     "lea_conv3d_set_rs_gather": (_i, [_i]),
@@ -159,6 +160,7 @@ def load():
 # in the library), e.g. LEASTEREO_WINO2_WALK=1 to disable the depth walk
 TUNING_ENV = {"LEASTEREO_WINO2_WALK": "lea_conv3d_wino2_set_walk",
               "LEASTEREO_HALO16": "lea_conv3d_wino2_set_halo16",
+              "LEASTEREO_LANE_HALO16": "lea_conv3d_wino2_set_lane_halo16",
               "LEASTEREO_WINO2_PIPE": "lea_conv3d_wino2_set_pipeline",
               "LEASTEREO_EPI_BUF": "lea_conv3d_wino_set_epi_buf",
               "LEASTEREO_RS_GATHER": "lea_conv3d_set_rs_gather",

@@ -73,7 +73,16 @@ struct Cfg2 {
     }
     return base;
   }
-  static constexpr int XS = PV == 2 ? (cb2(CIN_B - 1) + IMGA + 3) / 4 * 4 : CIN_B * CIS;
+  // PV = 4 (r04, per-lane V, the 16-cout tiles): 16-byte halo pieces (PIECES16 = 7 per
+  // channel, 28 per item) into channel regions CS4 = 0x702 floats apart (>= 7 whole pieces, so
+  // the partial last piece's surplus lanes land in the region's pad; 2 mod 64), bases odd so
+  // column w0 - 1 sits at an even dword; with the lane group's two rows RH / 2 - 1 = 4 tile
+  // rows apart (160 floats = 32 mod 64) every 32-lane half of a ds_read_b64 reads 64
+  // distinct banks (exhaustive check); adjacent rows (40 apart) were 2-way
+  static constexpr int CS4 = PIECES16 * 256 + ((2 - (PIECES16 * 256) % 64) % 64 + 64) % 64;
+  static constexpr int cb4(int c) { return 1 + c * CS4; }
+  static constexpr int XS = PV == 2 ? (cb2(CIN_B - 1) + IMGA + 3) / 4 * 4
+                          : PV == 4 ? (cb4(CIN_B) + 3) / 4 * 4 : CIN_B * CIS;
   static constexpr int WS = 27 * CIN_B * COP;    // g[kd*3+kh][kw][ci][co] of one chunk
   static constexpr int WSLOTS = (WS + 255) / 256;
   static constexpr int STAGE = XS + 256 * WSLOTS;
@@ -95,13 +104,16 @@ struct Cfg2 {
   // floats per channel: 0 mod 64 (PV = 1: the pass's 16-lane b128 writes pair rows,
   // TRS = 4 mod 8 apart; PV = 2: see above)
   static constexpr int TCS = (RH * TRS + 63) / 64 * 64;
-  static constexpr int TS = PV ? CIN_B * TCS : 0;
+  static constexpr int TS = (PV == 1 || PV == 2) ? CIN_B * TCS : 0;
+  static constexpr bool VPASS = PV == 1 || PV == 2;  // V formed by a per-chunk pass into LDS
   static constexpr int NUNIT = CIN_B * RH * Q;   // (channel, row, group) transforms per chunk
   static constexpr int WG_PER_CU = 4 * OCC / NW;
   static_assert(WG_PER_CU >= 1, "occupancy");
   static_assert(XS % 4 == 0 && WS % 4 == 0 && RW % 2 == 0 && PLANE % 2 == 0, "aligned LDS regions");
   static_assert(PV != 2 || (TW == 32 && NW % PIECES16 == 0 && cb2(1) % 64 == 3 && cb2(2) % 64 == 33 &&
                             cb2(3) % 64 == 35), "16-byte halo map");
+  static_assert(PV != 4 || (Q == 8 && WC == 1 && MTE == 1 && NW == 4 && CS4 % 64 == 2 && (4 * RWA) % 64 == 32 &&
+                            (PLANEA % 2) == 0 && RH == 2 * NW + 2), "PV = 4 halo map");
   static_assert((2 * STAGE + TS) * 4 * WG_PER_CU <= 160 * 1024, "double-buffered stages fit the LDS");
 };
 
@@ -247,7 +259,34 @@ __global__ __launch_bounds__(NW * 64, OCC) void conv3d_wino2_kernel(const ConvAr
       pln16 = p - 1;
     }
   }
+  // PV = 4: this wave's 7 pieces of the item are P = wave + 4 k (k < 7) of the 28 (channel
+  // P / 7, slot P % 7): their (plane, h, w) once, the plane per pair
+  constexpr int K4 = PV == 4 ? CIN_B * PIECES16 / NW : 1;
+  unsigned hwo4[K4], voff4[K4];
+  int pln4[K4];
+  if constexpr (PV == 4) {
+    static_assert(CIN_B * PIECES16 % NW == 0, "whole pieces per wave");
+#pragma unroll
+    for (int k = 0; k < K4; ++k) {
+      const int e = 64 * ((wave + NW * k) % PIECES16) + lane;
+      const int pl = e / (C::RH * (C::RWA / 4)), r = e - pl * (C::RH * (C::RWA / 4));
+      const int rr = r / (C::RWA / 4), blk = r - rr * (C::RWA / 4);
+      const int h = h0 + rr - 1, w = w0 - 4 + 4 * blk;  // W % 4 == 0: a block is all in or all out
+      const bool ok = e < C::BLK16 && (unsigned)h < (unsigned)a.H && (unsigned)w < (unsigned)a.W;
+      hwo4[k] = ok ? (unsigned)(h * a.W + w) * 4u : 0xFFFFFFF0u;  // surplus lanes: zeros into the pad
+      pln4[k] = ok ? pl - 1 : -1000;
+      voff4[k] = 0xFFFFFFF0u;
+    }
+  }
   auto set_pair = [&](int d0) {  // DMA offsets of the pair at output planes d0, d0 + 1
+    if constexpr (PV == 4) {
+#pragma unroll
+      for (int k = 0; k < K4; ++k) {
+        const int d = d0 + pln4[k];
+        voff4[k] = (unsigned)d < (unsigned)a.D ? hwo4[k] + (unsigned)d * (unsigned)HW * 4u : 0xFFFFFFF0u;
+      }
+      return;
+    }
     if constexpr (PV == 2) {
       const int d = d0 + pln16;
       voff16 = (hwo16 != 0xFFFFFFF0u && (unsigned)d < (unsigned)a.D) ? hwo16 + (unsigned)d * (unsigned)HW * 4u
@@ -283,6 +322,21 @@ __global__ __launch_bounds__(NW * 64, OCC) void conv3d_wino2_kernel(const ConvAr
     }
     const long long cvol = CV ? (long long)HW : (long long)HW * a.D;  // channel stride
     const unsigned crec = CV ? (unsigned)HW * 4u : nrec;
+    if constexpr (PV == 4) {
+      static_assert(!CV, "16-byte halo: plain volumes only");
+#pragma unroll
+      for (int k = 0; k < K4; ++k) {
+        const int P = wave + NW * k, ci = P / PIECES16, j = P - ci * PIECES16;
+        const int c = ch * CIN_B + ci;
+        const float* base = c < a.cin1 ? a.x + (long long)b * a.xbs + (long long)c * cvol
+                                       : a.x2 + (long long)b * a.x2bs + (long long)(c - a.cin1) * cvol;
+        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)base, 0, crec, 0x00020000);
+#ifndef LEA_EXP_NOHALO
+        dma_dwordx4_buf(rs, voff4[k], lds0 + 4 * (unsigned)(st - smem + C::cb4(0) + ci * C::CS4 + j * 256));
+#endif
+      }
+      return;
+    }
     if constexpr (PV == 2) {
       static_assert(!CV || PV != 2, "16-byte halo: plain volumes only");
 #pragma unroll
@@ -322,7 +376,9 @@ __global__ __launch_bounds__(NW * 64, OCC) void conv3d_wino2_kernel(const ConvAr
 
   const int ci = lane >> 4, p = lane & 15;
   const int pq = p % Q, pr = p / Q;  // output group within the row, row within the lane group
-  const int xoff = ci * C::CIS + (wr * C::RPG + pr) * C::RW + F * pq;
+  // tile row of the lane: PV = 4 interleaves the row sets (rows wr, wr + WR: bank map above)
+  const int trow = PV == 4 ? wr + C::WR * pr : wr * C::RPG + pr;
+  const int xoff = PV == 4 ? C::cb4(ci) + trow * C::RWA + 3 + F * pq : ci * C::CIS + trow * C::RW + F * pq;
   const int toff = ci * C::TCS + (wr * C::RPG + pr) * C::TRS + C::GS * pq;
   int woff[MTE];
 #pragma unroll
@@ -358,7 +414,7 @@ __global__ __launch_bounds__(NW * 64, OCC) void conv3d_wino2_kernel(const ConvAr
 #endif
   const long long DHW = (long long)HW * a.D;
   const int w = w0 + F * pq;
-  const int h = h0 + wr * C::RPG + pr;
+  const int h = h0 + trow;
   const int nv = min(F, a.W - w);  // valid outputs of this group
   const bool ebuf = a.flags & kEpiBuf;
   constexpr int NST = MTE * 4 * C::TD;  // buffer stores per epilogue
@@ -491,7 +547,7 @@ __global__ __launch_bounds__(NW * 64, OCC) void conv3d_wino2_kernel(const ConvAr
     LEA_STAMP(2);
     const float* xs = smem + (it & 1) * C::STAGE;
     const float* ws = xs + C::XS;
-    if constexpr (PV) {
+    if constexpr (C::VPASS) {
       // the workgroup transforms the chunk's halo once: unit (ci, row, group) reads
       // 4 planes x 6 inputs and writes its 24 V values
       static_assert(PV == 2 || (C::RW % 64 == 34 && C::CIS % 64 == 32 && C::RH % 2 == 0 && Q == 8),
@@ -551,19 +607,20 @@ __global__ __launch_bounds__(NW * 64, OCC) void conv3d_wino2_kernel(const ConvAr
     // one kh step: the inputs (4 planes x 6 staged values as float2s, or the 24
     // pre-transformed V as float4s) and the 9 g values (kd, kw) per cout tile
     struct Raw {
-      float2 x2[PV ? 1 : C::PLANES][3];
-      float4 v4[PV ? 6 : 1];
+      float2 x2[C::VPASS ? 1 : C::PLANES][3];
+      float4 v4[C::VPASS ? 6 : 1];
       float g[9][MTE];
     };
+    constexpr int XPL = PV == 4 ? C::PLANEA : C::PLANE, XRW = PV == 4 ? C::RWA : C::RW;
     auto load_step = [&](int kh, Raw& o) {
-      if constexpr (PV) {
+      if constexpr (C::VPASS) {
         const float4* tp = reinterpret_cast<const float4*>(tv + toff + kh * C::TRS);
 #pragma unroll
         for (int k = 0; k < 6; ++k) o.v4[k] = tp[k];
       } else {
 #pragma unroll
         for (int pl = 0; pl < C::PLANES; ++pl) {
-          const float* sp = xs + xoff + pl * C::PLANE + kh * C::RW;
+          const float* sp = xs + xoff + pl * XPL + kh * XRW;
 #pragma unroll
           for (int q = 0; q < 3; ++q)
 #ifdef LEA_EXP_NOLDSRD
@@ -590,7 +647,7 @@ __global__ __launch_bounds__(NW * 64, OCC) void conv3d_wino2_kernel(const ConvAr
       float u[NX][NE][MTE];
     };
     auto xform = [&](const Raw& o, Xf& T) {
-      if constexpr (PV) {
+      if constexpr (C::VPASS) {
 #pragma unroll
         for (int k = 0; k < 6; ++k) {
           const float e4[4] = {o.v4[k].x, o.v4[k].y, o.v4[k].z, o.v4[k].w};
@@ -1076,6 +1133,7 @@ int run2(const Plan2& p, ConvArgs a, int B, hipStream_t st, bool cv) {
   } else {
     LEA_WINO2_TILES(false)
     LEA_WINO2_CASE(8, 2, 1, 4, 2, 2, false)
+    LEA_WINO2_CASE(8, 1, 1, 4, 2, 4, false)
     if (p.q == 8 && p.wc == 2 && p.mte == 1 && p.nw == 4 && p.occ == 2 && p.pv == 3) {
       using C_ = Cfg2<8, 2, 1, 4, 2, 2>;
       a.ncob = (a.cout + C_::COP - 1) / C_::COP;

@@ -69,6 +69,18 @@ def _conv_params(mod, w=None, folded=None):
 class CellGraphExecutor:
     """Shared machinery: parameter packing, ConvBR dispatch, the searched cell."""
 
+    # stage capture for the per-stage parity checks (tests): tap(name, f32 NCDHW copy) at
+    # the stages oracle/torch_ref.matching_forward names; None (the default) costs nothing
+    tap = None
+
+    def _emit(self, name, t):
+        if self.tap is not None:
+            self.tap(name, self._as_f32(t))
+
+    @staticmethod
+    def _as_f32(t):
+        return t.detach().clone()
+
     # fp32: a down-sampled s1 that the next cell reads again as its s0 (same tensor, same
     # size) feeds one stacked 1x1 conv for both cells (the bf16 executors memoise every
     # resample instead); LEASTEREO_SHARE_DOWNSAMPLE=0 keeps two passes
@@ -322,19 +334,30 @@ class MatchingExecutor(CellGraphExecutor):
         return kernels.pack_conv2d_weight(wl), kernels.pack_conv2d_weight(wr)
 
     def _from_stem0(self, stem0):
+        out = self._matching_body(stem0)
+        if self.tap is not None:  # the head's output is f32 NCDHW in every executor
+            self.tap("matching", out.detach().clone())
+        return out
+
+    def _matching_body(self, stem0):
         d, h, w = self._volume(stem0)
+        self._emit("stem0", stem0)
         stem1 = self.conv("stem1", stem0)
+        self._emit("stem1", stem1)
         outs = []
         prev = (stem0, stem1)
         n = len(self.m.cells)
         for i in range(n):
             if i == 5 and n == 12:   # :150-151, cat read in place by the conv
                 fused = self.conv("conv1", outs[1][1], x2=outs[4][1])
+                self._emit("conv1", fused)
                 prev = (outs[4][0], fused)
             elif i == 9 and n == 12:  # :155-156
                 fused = self.conv("conv2", outs[4][1], x2=outs[8][1])
+                self._emit("conv2", fused)
                 prev = (outs[8][0], fused)
             o = self.cell(i, prev[0], prev[1])
+            self._emit(f"cell{i}", o[1])
             outs.append(o)
             prev = o
         last = outs[-1][1]
@@ -458,6 +481,10 @@ class _C8Layout:
 
     def _empty(self, b, c, size, like):
         return torch.empty((b, c // 8) + tuple(size) + (8,), device=like.device, dtype=torch.bfloat16)
+
+    @staticmethod
+    def _as_f32(t):
+        return kernels.from_c8(t)
 
     @staticmethod
     def _channels(t, c0, c1):

@@ -184,28 +184,38 @@ def feature_forward(sd, x, net_arch_fea, cell_arch_fea):
     return conv_br(y, sd, "feature.last_3", bn=False, relu=False)
 
 
-def matching_forward(sd, x, net_arch_mat, cell_arch_mat):
-    """newMatching.forward, retrain/skip_model_3d.py:140-174."""
+def matching_forward(sd, x, net_arch_mat, cell_arch_mat, tap=None):
+    """newMatching.forward, retrain/skip_model_3d.py:140-174.  ``tap(name, tensor)``, when
+    given, sees each stage's output (stem0, stem1, conv1, conv2, cell{i}, matching): the
+    per-stage parity checks compare the HIP executors' stages against these."""
+    tap = tap or (lambda name, t: None)
     space = network_layer_to_space(net_arch_mat)
     levels = cell_levels(space)
     prims = _primitives(cell_arch_mat, ["skip", "conv"])  # genotypes_3d.py:5-8
     stem0 = conv_br(x, sd, "matching.stem0")
+    tap("stem0", stem0)
     stem1 = conv_br(stem0, sd, "matching.stem1")
+    tap("stem1", stem1)
     outs = []
     prev = (stem0, stem1)
     for i, (_, downup) in enumerate(levels):
         if i == 5:   # :150-151
             fused = conv_br(torch.cat((outs[1][-1], outs[4][-1]), 1), sd, "matching.conv1")
+            tap("conv1", fused)
             prev = (outs[4][0], fused)
         elif i == 9:  # :155-156
             fused = conv_br(torch.cat((outs[4][-1], outs[8][-1]), 1), sd, "matching.conv2")
+            tap("conv2", fused)
             prev = (outs[8][0], fused)
         o = cell_forward(sd, f"matching.cells.{i}", prev[0], prev[1], downup, cell_arch_mat, prims)
+        tap(f"cell{i}", o[-1])
         outs.append(o)
         prev = o
     last = outs[-1][-1]
     y = _head(sd, "matching", last, x.shape[2:], 3)
-    return conv_br(y, sd, "matching.last_3", bn=False, relu=False)
+    out = conv_br(y, sd, "matching.last_3", bn=False, relu=False)
+    tap("matching", out)
+    return out
 
 
 def build_cost_volume(fl, fr, maxdisp):
@@ -240,16 +250,20 @@ def disp_forward(cost, maxdisp):
     return torch.sum(p * d, 1)
 
 
-def leastereo_forward(sd, left, right, maxdisp, arch, return_stages=False):
+def leastereo_forward(sd, left, right, maxdisp, arch, return_stages=False, tap=None):
     """LEAStereo.forward, retrain/LEAStereo.py:30-52.
 
     ``arch`` = dict with net_arch_fea, cell_arch_fea, net_arch_mat, cell_arch_mat
-    (the four .npy arrays, LEAStereo.py:16-17).
+    (the four .npy arrays, LEAStereo.py:16-17).  ``tap``: see matching_forward (plus
+    fea_l / fea_r, the feature maps).
     """
     fl = feature_forward(sd, left, arch["net_arch_fea"], arch["cell_arch_fea"])
     fr = feature_forward(sd, right, arch["net_arch_fea"], arch["cell_arch_fea"])
+    if tap is not None:
+        tap("fea_l", fl)
+        tap("fea_r", fr)
     cost = build_cost_volume(fl, fr, maxdisp)
-    mat = matching_forward(sd, cost, arch["net_arch_mat"], arch["cell_arch_mat"])
+    mat = matching_forward(sd, cost, arch["net_arch_mat"], arch["cell_arch_mat"], tap)
     disp = disp_forward(mat, maxdisp)
     if return_stages:
         return {"fea_l": fl, "fea_r": fr, "cost": cost, "matching": mat, "disp": disp}

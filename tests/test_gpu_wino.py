@@ -435,3 +435,42 @@ def test_wd_halo16_is_bit_identical_to_dword_pieces(b, cin, c1, cout, shape, mod
             lib.lea_conv3d_wino2_set_pipeline(1)
     assert torch.equal(outs[(1, 1)], outs[(0, 1)]) and torch.equal(outs[(1, 0)], outs[(0, 1)])
     np.testing.assert_allclose(outs[(1, 1)].cpu().double().numpy(), want.numpy(), rtol=1e-4, atol=1e-4)
+
+
+@pytest.mark.parametrize("b,cin,c1,cout,shape,mode", [
+    (1, 16, 16, 16, (11, 20, 40), "acc"), (2, 16, 16, 16, (5, 9, 36), "res"),
+    (1, 32, 16, 16, (4, 13, 68), None), (1, 16, 16, 16, (1, 1, 4), None),
+    (2, 64, 64, 16, (3, 8, 32), "acc"), (1, 16, 16, 16, (7, 33, 164), "res"),
+    (1, 16, 16, 12, (6, 10, 44), "acc")])
+def test_lane_halo16_is_bit_identical_to_dword_pieces(b, cin, c1, cout, shape, mode):
+    """The per-lane 16-cout W x D tile with its halo staged as 16-byte pieces into the
+    interleaved-row, bank-conflict-free layout (PV = 4, r04; lea_conv3d_wino2_set_lane_halo16)
+    equals the dword-piece tile (PV = 0) bit for bit -- same staged values, same transforms,
+    same accumulation order -- and float64 torch at the engine bar: ragged H (partial 8-row
+    tiles), odd D, W not a multiple of 32, one item, two sources, couts padding the block,
+    every epilogue."""
+    lib = _lib.load()
+    g = torch.Generator().manual_seed(cin * 3 + cout + shape[2])
+    x = torch.randn((b, cin) + shape, generator=g)
+    w = torch.randn(cout, cin, 3, 3, 3, generator=g) / np.sqrt(cin * 27)
+    scale = torch.rand(cout, generator=g) + 0.5
+    shift = torch.randn(cout, generator=g) * 0.1
+    r = torch.randn((b, cout) + shape, generator=g)
+    want = _ref(x, w, scale, shift, True, r if mode else None)
+    xs = x.to(DEV)
+    x1, x2 = (xs[:, :c1].contiguous(), xs[:, c1:].contiguous()) if c1 < cin else (xs, None)
+    pw = kernels.pack_conv_weight_wino(w.to(DEV))
+    outs = {}
+    for on in (1, 0):
+        assert lib.lea_conv3d_wino2_set_lane_halo16(on) == 0
+        try:
+            name = kernels.wino_kernel_name(b, cout, *shape, cin=cin)
+            assert name == "conv3d_wino2_kernel<8, 1, 1, 4, 2, %d, false>" % (4 if on else 0), name
+            out = r.to(DEV).clone() if mode == "acc" else None
+            outs[on] = kernels.conv3d_bnrelu_wino(x1, pw, cout, scale.to(DEV), shift.to(DEV), relu=True, out=out,
+                                                  accumulate=mode == "acc", x2=x2,
+                                                  residual=r.to(DEV) if mode == "res" else None)
+        finally:
+            lib.lea_conv3d_wino2_set_lane_halo16(1)
+    assert torch.equal(outs[1], outs[0])
+    np.testing.assert_allclose(outs[1].cpu().double().numpy(), want.numpy(), rtol=1e-4, atol=1e-4)
