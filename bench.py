@@ -73,6 +73,10 @@ CONFIGS = {
 # SURVEY.md §8d's roofline of the reference algorithm (direct convolutions, a
 # materialised cost volume): kept for comparison beside the issued-work roofline
 T_ROOF_REFERENCE_MS = {("c2", 1): 11.36, ("c3", 8): 10.91, ("c4", 8): 12.59, ("c5", 1): 43.1}
+# BASELINE.md §3's HBM-only time of the reference algorithm (its ConvBR-fused accounting: conv
+# in + out + weights once, resample in + out, one operand per cell sum; the materialised
+# cost volume excluded) -- the denominator BASELINE.md states the ">= 55 %" bar against
+HBM_ONLY_REFERENCE_MS = {("c2", 1): 2.67, ("c3", 8): 9.25, ("c4", 8): 10.68, ("c5", 1): 10.12}
 WORKLOADS = {"c2": "SceneFlow 576x960 D=192 fp32, batch 1 per GPU (BASELINE configs[1])",
              "c3": "KITTI2015 384x1248 D=192 bf16, batch 8 (BASELINE configs[2])",
              "c4": "SceneFlow 576x960 D=192 bf16, 8 pairs per GPU (BASELINE configs[3])",
@@ -587,6 +591,15 @@ def run(args, info):
                                                    "FLOPs for the same outputs; not a utilisation"}},
         "path_roofline": {"t_roof_ms": t_roof_ms, "frac": t_roof_ms / ms_step,
                           "hbm_only_ms": t_hbm_ms, "hbm_frac": t_hbm_ms / ms_step,
+                          "hbm_frac_rule": "bytes this implementation's kernels must move (each launch's "
+                                           "inputs + output + residual + weights once; the factored stem0 "
+                                           "and fused layers as run) / 8 TB/s, over the step",
+                          "hbm_frac_baseline_accounting": (
+                              None if HBM_ONLY_REFERENCE_MS.get((cfg, args.batch)) is None else
+                              HBM_ONLY_REFERENCE_MS[(cfg, args.batch)] / ms_step),
+                          "hbm_frac_baseline_rule": "BASELINE.md §3: the reference algorithm's ConvBR-fused "
+                                                    "bytes (C2 21.36 GB fp32, C3 74.0 / C4 85.4 GB per 8 "
+                                                    "pairs bf16) / 8 TB/s, over the step",
                           "matrix_only_ms": t_mat_ms, "launches": n_launch,
                           "source": "one eager forward: sum over its launches of max(issued MFMA FLOP / "
                                     "peak, VALU FLOP / fp32 peak, algorithmic bytes / 8 TB/s)",

@@ -875,6 +875,10 @@ def wino_eligible(cout: int, cin: int, k: int) -> bool:
 # below this the direct engine's smaller tiles fill the chip better (A/B override:
 # LEASTEREO_WINO_MIN_VOXELS)
 WINO_MIN_VOXELS = int(os.environ.get("LEASTEREO_WINO_MIN_VOXELS", "200000"))
+# ... except for 32-cout blocks on the one-barrier W x D tile down to this volume (r04
+# planner audit, profiles/r04_planner_sweep.txt: the C2 L2 32->32 cells, 61 K voxels, 34.6 us
+# on conv3d_wino2p_kernel vs 38.2 us direct; A/B override: LEASTEREO_WINO_SMALL32_MIN)
+WINO_SMALL32_MIN = int(os.environ.get("LEASTEREO_WINO_SMALL32_MIN", "32768"))
 
 
 def wino_preferred(b, cout, cin, d, h, w) -> bool:
@@ -882,9 +886,11 @@ def wino_preferred(b, cout, cin, d, h, w) -> bool:
     Winograd wins on the large volumes when the output channels fill its 16/32/48-row
     blocks (stem0, stem1, conv1/2, the L1 cells and sibling groups, the 8->24 L0
     group); on the small L2 volumes only the 96-channel sibling groups gain, the
-    32-channel cells stay on the direct engine."""
+    32-channel cells take the pipelined W x D tile down to WINO_SMALL32_MIN voxels (r04)."""
     if b * d * h * w < WINO_MIN_VOXELS:
-        return cout >= 64 and cout % 32 == 0  # small volumes: only wide blocks amortise the tile
+        # small volumes: only wide blocks amortise the tile; 32-cout blocks run the one-barrier
+        # pipelined tile (more than two 4-channel chunks per depth pair)
+        return cout % 32 == 0 and (cout >= 64 or (b * d * h * w >= WINO_SMALL32_MIN and cin > 8))
     return cout <= 8 or cout == 16 or cout == 24 or cout % 32 == 0 or cout % 48 == 0
 
 
