@@ -87,7 +87,16 @@ struct Cfg {
     return base;
   }
   static_assert(!H16 || (Q == 16 && F == 4), "16-byte halo: one tile row per lane group");
-  static constexpr int XS = H16 ? (cb2(CIN_B - 1) + IMGA + 3) / 4 * 4 : CIN_B * CIS;
+  // r04: channel regions of whole pieces (CSH = PIECES16 x 256 floats, 0 mod 64), every base
+  // 1 mod 64: column w0 - 1 sits 16-byte aligned, so a lane reads its 6 inputs per (plane,
+  // row) as two ds_read_b128, and each b128 lane group ({0-3,12-15,20-27}, ...: two channels'
+  // complementary 4-group runs of one row) reads 64 distinct banks.  The float2 reads the
+  // compiler paired into ds_read2_b64 (banked mod 32 over 16-lane groups) were 2-way
+  // conflicted on the 64-wide row (pq, pq + 8): 5.9 M of 17.7 M LDS cycles per L0 launch
+  static constexpr int CSH = PIECES16 * 256;
+  static constexpr int cbh(int c) { return 1 + c * CSH; }
+  static_assert(!H16 || (CSH % 64 == 0 && RWA % 4 == 0 && PLANEA % 4 == 0), "b128 halo map");
+  static constexpr int XS = H16 ? (cbh(CIN_B) + 3) / 4 * 4 : CIN_B * CIS;
   static constexpr int RWX = H16 ? RWA : RW;       // staged row / plane strides the steps read
   static constexpr int PLX = H16 ? PLANEA : PLANE;
   static constexpr int WS = NSTEP * 3 * CIN_B * COP;  // the chunk's weights g[step][kw][ci][co]
@@ -230,7 +239,7 @@ __global__ __launch_bounds__(kConvThreads, 2) void conv3d_wino_kernel(const Conv
         const float* base = c < a.cin1 ? a.x + (long long)b * a.xbs + (long long)c * cvol
                                        : a.x2 + (long long)b * a.x2bs + (long long)(c - a.cin1) * cvol;
         const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)base, 0, crec, 0x00020000);
-        const int cb = ci == 0 ? C::cb2(0) : ci == 1 ? C::cb2(1) : ci == 2 ? C::cb2(2) : C::cb2(3);
+        const int cb = C::cbh(0) + ci * C::CSH;
 #ifndef LEA_EXP_NOHALO  // ablation builds: outputs wrong, timing only
         if (ok16[t]) dma_dwordx4_buf(rs, voff16[t], lds0 + 4 * (unsigned)(st - smem + cb + (k % P16) * 256));
 #endif
@@ -268,8 +277,7 @@ __global__ __launch_bounds__(kConvThreads, 2) void conv3d_wino_kernel(const Conv
   int xoff[NP];  // staged input column F pq (w0 + F pq - 1) of tile row (wave NP + j) RPG + pr
 #pragma unroll
   for (int j = 0; j < NP; ++j)
-    xoff[j] = H16 ? (ci == 0 ? C::cb2(0) : ci == 1 ? C::cb2(1) : ci == 2 ? C::cb2(2) : C::cb2(3)) +
-                        ((wave * NP + j) * C::RPG + pr) * C::RWA + 3 + F * pq
+    xoff[j] = H16 ? C::cbh(ci) + ((wave * NP + j) * C::RPG + pr) * C::RWA + 3 + F * pq
                   : ci * C::CIS + ((wave * NP + j) * C::RPG + pr) * C::RW + F * pq;
   int woff[C::MTE];
 #pragma unroll
@@ -474,6 +482,16 @@ __global__ __launch_bounds__(kConvThreads, 2) void conv3d_wino_kernel(const Conv
 #pragma unroll
         for (int j = 0; j < NP; ++j) {
           const float* sp = xs + xoff[j] + (t + kd) * C::PLX + kh * C::RWX;
+          if constexpr (H16) {  // two 16-byte reads (bank map above); inputs 6, 7 unused
+            const float4 lo = *reinterpret_cast<const float4*>(sp);
+            // volatile keeps the whole second read (narrowed, it would pair into ds_read2_b64)
+            typedef const volatile __attribute__((address_space(3))) f32x4 lds_f32x4;
+            const f32x4 hi = *(lds_f32x4*)(sp + 4);
+            o.x2[t][j][0] = make_float2(lo.x, lo.y);
+            o.x2[t][j][1] = make_float2(lo.z, lo.w);
+            o.x2[t][j][2] = make_float2(hi[0], hi[1]);
+            continue;
+          }
 #pragma unroll
           for (int q = 0; q <= F / 2; ++q) o.x2[t][j][q] = *reinterpret_cast<const float2*>(sp + 2 * q);
         }

@@ -74,12 +74,15 @@ struct Cfg2 {
     return base;
   }
   // PV = 4 (r04, per-lane V, the 16-cout tiles): 16-byte halo pieces (PIECES16 = 7 per
-  // channel, 28 per item) into channel regions CS4 = 0x702 floats apart (>= 7 whole pieces, so
-  // the partial last piece's surplus lanes land in the region's pad; 2 mod 64), bases odd so
-  // column w0 - 1 sits at an even dword; with the lane group's two rows RH / 2 - 1 = 4 tile
-  // rows apart (160 floats = 32 mod 64) every 32-lane half of a ds_read_b64 reads 64
-  // distinct banks (exhaustive check); adjacent rows (40 apart) were 2-way
-  static constexpr int CS4 = PIECES16 * 256 + ((2 - (PIECES16 * 256) % 64) % 64 + 64) % 64;
+  // channel, 28 per item) into channel regions CS4 = 7 x 256 floats apart (whole pieces: the
+  // partial last piece's surplus lanes land in the region's pad), bases 1 mod 4 so column
+  // w0 - 1 sits 16-byte aligned: a lane reads its 6 inputs per (plane, row) as two
+  // ds_read_b128 (the compiler pairs float2 reads into ds_read2_b64, banked mod 32 over
+  // 16-lane groups: 2-way on this tile, 42 % of the LDS cycles in the r04 counters).  With the
+  // lane group's two rows 4 tile rows apart (rows wr, wr + 4) every b128 lane group
+  // ({0-3,12-15,20-27}, ...) reads 64 distinct banks (exhaustive check over the row sets,
+  // kh, planes and both reads)
+  static constexpr int CS4 = PIECES16 * 256;
   static constexpr int cb4(int c) { return 1 + c * CS4; }
   static constexpr int XS = PV == 2 ? (cb2(CIN_B - 1) + IMGA + 3) / 4 * 4
                           : PV == 4 ? (cb4(CIN_B) + 3) / 4 * 4 : CIN_B * CIS;
@@ -112,8 +115,8 @@ struct Cfg2 {
   static_assert(XS % 4 == 0 && WS % 4 == 0 && RW % 2 == 0 && PLANE % 2 == 0, "aligned LDS regions");
   static_assert(PV != 2 || (TW == 32 && NW % PIECES16 == 0 && cb2(1) % 64 == 3 && cb2(2) % 64 == 33 &&
                             cb2(3) % 64 == 35), "16-byte halo map");
-  static_assert(PV != 4 || (Q == 8 && WC == 1 && MTE == 1 && NW == 4 && CS4 % 64 == 2 && (4 * RWA) % 64 == 32 &&
-                            (PLANEA % 2) == 0 && RH == 2 * NW + 2), "PV = 4 halo map");
+  static_assert(PV != 4 || (Q == 8 && WC == 1 && MTE == 1 && NW == 4 && CS4 % 64 == 0 && (4 * RWA) % 64 == 32 &&
+                            PLANEA % 4 == 0 && RWA % 4 == 0 && RH == 2 * NW + 2), "PV = 4 halo map");
   static_assert((2 * STAGE + TS) * 4 * WG_PER_CU <= 160 * 1024, "double-buffered stages fit the LDS");
 };
 
@@ -607,8 +610,9 @@ __global__ __launch_bounds__(NW * 64, OCC) void conv3d_wino2_kernel(const ConvAr
     // one kh step: the inputs (4 planes x 6 staged values as float2s, or the 24
     // pre-transformed V as float4s) and the 9 g values (kd, kw) per cout tile
     struct Raw {
-      float2 x2[C::VPASS ? 1 : C::PLANES][3];
+      float2 x2[(C::VPASS || PV == 4) ? 1 : C::PLANES][3];
       float4 v4[C::VPASS ? 6 : 1];
+      float4 h4[PV == 4 ? C::PLANES : 1][2];  // PV = 4: inputs 0..7 of each plane (6, 7 unused)
       float g[9][MTE];
     };
     constexpr int XPL = PV == 4 ? C::PLANEA : C::PLANE, XRW = PV == 4 ? C::RWA : C::RW;
@@ -621,6 +625,15 @@ __global__ __launch_bounds__(NW * 64, OCC) void conv3d_wino2_kernel(const ConvAr
 #pragma unroll
         for (int pl = 0; pl < C::PLANES; ++pl) {
           const float* sp = xs + xoff + pl * XPL + kh * XRW;
+          if constexpr (PV == 4) {
+            o.h4[pl][0] = *reinterpret_cast<const float4*>(sp);
+            // volatile keeps the whole 16-byte read (inputs 6, 7 are unused: as a plain load
+            // the compiler narrows it to 8 bytes and pairs those into ds_read2_b64)
+            typedef const volatile __attribute__((address_space(3))) f32x4 lds_f32x4;
+            const f32x4 hi = *(lds_f32x4*)(sp + 4);
+            o.h4[pl][1] = make_float4(hi[0], hi[1], hi[2], hi[3]);
+            continue;
+          }
 #pragma unroll
           for (int q = 0; q < 3; ++q)
 #ifdef LEA_EXP_NOLDSRD
@@ -664,7 +677,12 @@ __global__ __launch_bounds__(NW * 64, OCC) void conv3d_wino2_kernel(const ConvAr
           for (int x = 0; x < NX; ++x) bw[pl][x] = e6[x];
         }
 #else
-          bw4(o.x2[pl][0].x, o.x2[pl][0].y, o.x2[pl][1].x, o.x2[pl][1].y, o.x2[pl][2].x, o.x2[pl][2].y, bw[pl]);
+        {
+          if constexpr (PV == 4)
+            bw4(o.h4[pl][0].x, o.h4[pl][0].y, o.h4[pl][0].z, o.h4[pl][0].w, o.h4[pl][1].x, o.h4[pl][1].y, bw[pl]);
+          else
+            bw4(o.x2[pl][0].x, o.x2[pl][0].y, o.x2[pl][1].x, o.x2[pl][1].y, o.x2[pl][2].x, o.x2[pl][2].y, bw[pl]);
+        }
 #endif
 #pragma unroll
         for (int x = 0; x < NX; ++x) {
