@@ -659,7 +659,7 @@ int g_block48 = 1;
 int g_epibuf = 1;  // lea_conv3d_wino_set_epi_buf
 int g_halo16 = 1;  // lea_conv3d_wino2_set_halo16
 int g_pipe = 1;    // lea_conv3d_wino2_set_pipeline
-int g_lane16 = 1;  // lea_conv3d_wino2_set_lane_halo16
+int g_lane16 = 1;  // lea_conv3d_wino2_set_lane_halo16 (2: the fenced step schedule, PV = 5)
 inline int host_mt(int cout) {
   if (g_small16 && cout <= 8) return 1;
   const int mt = mt_of(cout);
@@ -765,7 +765,7 @@ inline void plan_halo16(Plan& p, bool cv, int W, const ConvArgs* a, int cin = 0)
     // the per-lane 16-cout tile (the L1 cells): 16-byte pieces, interleaved row sets (r04)
     if (g_lane16 && p.p2.pv == 0 && p.p2.q == 8 && p.p2.wc == 1 && p.p2.mte == 1 && p.p2.nw == 4 &&
         p.p2.occ == 2)
-      p.p2.pv = 4;
+      p.p2.pv = g_lane16 == 2 ? 5 : 4;
   } else if (p.mt == 0 && p.f == 4 && p.q == 16 && p.np == 1 && p.td == 2) {
     p.h16 = true;  // the depth-paired 64-wide tile (the L0 8-channel cell ops)
   }
@@ -940,7 +940,7 @@ extern "C" int lea_conv3d_wino2_set_pipeline(int on) {
 
 extern "C" int lea_conv3d_wino2_set_lane_halo16(int on) {
   clear_error();
-  LEA_CHECK_ARG(on == 0 || on == 1, "lea_conv3d_wino2_set_lane_halo16: on=%d", on);
+  LEA_CHECK_ARG(on >= 0 && on <= 2, "lea_conv3d_wino2_set_lane_halo16: on=%d", on);
   wino::g_lane16 = on;
   return 0;
 }

@@ -82,10 +82,11 @@ struct Cfg2 {
   // lane group's two rows 4 tile rows apart (rows wr, wr + 4) every b128 lane group
   // ({0-3,12-15,20-27}, ...) reads 64 distinct banks (exhaustive check over the row sets,
   // kh, planes and both reads)
+  static constexpr bool H4 = PV == 4 || PV == 5;  // PV = 5: PV = 4 with the fenced step schedule
   static constexpr int CS4 = PIECES16 * 256;
   static constexpr int cb4(int c) { return 1 + c * CS4; }
   static constexpr int XS = PV == 2 ? (cb2(CIN_B - 1) + IMGA + 3) / 4 * 4
-                          : PV == 4 ? (cb4(CIN_B) + 3) / 4 * 4 : CIN_B * CIS;
+                          : H4 ? (cb4(CIN_B) + 3) / 4 * 4 : CIN_B * CIS;
   static constexpr int WS = 27 * CIN_B * COP;    // g[kd*3+kh][kw][ci][co] of one chunk
   static constexpr int WSLOTS = (WS + 255) / 256;
   static constexpr int STAGE = XS + 256 * WSLOTS;
@@ -115,7 +116,7 @@ struct Cfg2 {
   static_assert(XS % 4 == 0 && WS % 4 == 0 && RW % 2 == 0 && PLANE % 2 == 0, "aligned LDS regions");
   static_assert(PV != 2 || (TW == 32 && NW % PIECES16 == 0 && cb2(1) % 64 == 3 && cb2(2) % 64 == 33 &&
                             cb2(3) % 64 == 35), "16-byte halo map");
-  static_assert(PV != 4 || (Q == 8 && WC == 1 && MTE == 1 && NW == 4 && CS4 % 64 == 0 && (4 * RWA) % 64 == 32 &&
+  static_assert(!H4 || (Q == 8 && WC == 1 && MTE == 1 && NW == 4 && CS4 % 64 == 0 && (4 * RWA) % 64 == 32 &&
                             PLANEA % 4 == 0 && RWA % 4 == 0 && RH == 2 * NW + 2), "PV = 4 halo map");
   static_assert((2 * STAGE + TS) * 4 * WG_PER_CU <= 160 * 1024, "double-buffered stages fit the LDS");
 };
@@ -264,10 +265,10 @@ __global__ __launch_bounds__(NW * 64, OCC) void conv3d_wino2_kernel(const ConvAr
   }
   // PV = 4: this wave's 7 pieces of the item are P = wave + 4 k (k < 7) of the 28 (channel
   // P / 7, slot P % 7): their (plane, h, w) once, the plane per pair
-  constexpr int K4 = PV == 4 ? CIN_B * PIECES16 / NW : 1;
+  constexpr int K4 = C::H4 ? CIN_B * PIECES16 / NW : 1;
   unsigned hwo4[K4], voff4[K4];
   int pln4[K4];
-  if constexpr (PV == 4) {
+  if constexpr (C::H4) {
     static_assert(CIN_B * PIECES16 % NW == 0, "whole pieces per wave");
 #pragma unroll
     for (int k = 0; k < K4; ++k) {
@@ -282,7 +283,7 @@ __global__ __launch_bounds__(NW * 64, OCC) void conv3d_wino2_kernel(const ConvAr
     }
   }
   auto set_pair = [&](int d0) {  // DMA offsets of the pair at output planes d0, d0 + 1
-    if constexpr (PV == 4) {
+    if constexpr (C::H4) {
 #pragma unroll
       for (int k = 0; k < K4; ++k) {
         const int d = d0 + pln4[k];
@@ -325,7 +326,7 @@ __global__ __launch_bounds__(NW * 64, OCC) void conv3d_wino2_kernel(const ConvAr
     }
     const long long cvol = CV ? (long long)HW : (long long)HW * a.D;  // channel stride
     const unsigned crec = CV ? (unsigned)HW * 4u : nrec;
-    if constexpr (PV == 4) {
+    if constexpr (C::H4) {
       static_assert(!CV, "16-byte halo: plain volumes only");
 #pragma unroll
       for (int k = 0; k < K4; ++k) {
@@ -380,8 +381,8 @@ __global__ __launch_bounds__(NW * 64, OCC) void conv3d_wino2_kernel(const ConvAr
   const int ci = lane >> 4, p = lane & 15;
   const int pq = p % Q, pr = p / Q;  // output group within the row, row within the lane group
   // tile row of the lane: PV = 4 interleaves the row sets (rows wr, wr + WR: bank map above)
-  const int trow = PV == 4 ? wr + C::WR * pr : wr * C::RPG + pr;
-  const int xoff = PV == 4 ? C::cb4(ci) + trow * C::RWA + 3 + F * pq : ci * C::CIS + trow * C::RW + F * pq;
+  const int trow = C::H4 ? wr + C::WR * pr : wr * C::RPG + pr;
+  const int xoff = C::H4 ? C::cb4(ci) + trow * C::RWA + 3 + F * pq : ci * C::CIS + trow * C::RW + F * pq;
   const int toff = ci * C::TCS + (wr * C::RPG + pr) * C::TRS + C::GS * pq;
   int woff[MTE];
 #pragma unroll
@@ -610,12 +611,12 @@ __global__ __launch_bounds__(NW * 64, OCC) void conv3d_wino2_kernel(const ConvAr
     // one kh step: the inputs (4 planes x 6 staged values as float2s, or the 24
     // pre-transformed V as float4s) and the 9 g values (kd, kw) per cout tile
     struct Raw {
-      float2 x2[(C::VPASS || PV == 4) ? 1 : C::PLANES][3];
+      float2 x2[(C::VPASS || C::H4) ? 1 : C::PLANES][3];
       float4 v4[C::VPASS ? 6 : 1];
-      float4 h4[PV == 4 ? C::PLANES : 1][2];  // PV = 4: inputs 0..7 of each plane (6, 7 unused)
+      float4 h4[C::H4 ? C::PLANES : 1][2];  // PV = 4: inputs 0..7 of each plane (6, 7 unused)
       float g[9][MTE];
     };
-    constexpr int XPL = PV == 4 ? C::PLANEA : C::PLANE, XRW = PV == 4 ? C::RWA : C::RW;
+    constexpr int XPL = C::H4 ? C::PLANEA : C::PLANE, XRW = C::H4 ? C::RWA : C::RW;
     auto load_step = [&](int kh, Raw& o) {
       if constexpr (C::VPASS) {
         const float4* tp = reinterpret_cast<const float4*>(tv + toff + kh * C::TRS);
@@ -625,7 +626,7 @@ __global__ __launch_bounds__(NW * 64, OCC) void conv3d_wino2_kernel(const ConvAr
 #pragma unroll
         for (int pl = 0; pl < C::PLANES; ++pl) {
           const float* sp = xs + xoff + pl * XPL + kh * XRW;
-          if constexpr (PV == 4) {
+          if constexpr (C::H4) {
             o.h4[pl][0] = *reinterpret_cast<const float4*>(sp);
             // volatile keeps the whole 16-byte read (inputs 6, 7 are unused: as a plain load
             // the compiler narrows it to 8 bytes and pairs those into ds_read2_b64)
@@ -678,7 +679,7 @@ __global__ __launch_bounds__(NW * 64, OCC) void conv3d_wino2_kernel(const ConvAr
         }
 #else
         {
-          if constexpr (PV == 4)
+          if constexpr (C::H4)
             bw4(o.h4[pl][0].x, o.h4[pl][0].y, o.h4[pl][0].z, o.h4[pl][0].w, o.h4[pl][1].x, o.h4[pl][1].y, bw[pl]);
           else
             bw4(o.x2[pl][0].x, o.x2[pl][0].y, o.x2[pl][1].x, o.x2[pl][1].y, o.x2[pl][2].x, o.x2[pl][2].y, bw[pl]);
@@ -736,6 +737,25 @@ __global__ __launch_bounds__(NW * 64, OCC) void conv3d_wino2_kernel(const ConvAr
     Xf xf[2];
     // scheduler hint: interleave the step's LDS reads / VALU transforms with the MFMAs
     // (same-box sweep r02: -1 to -4 % per layer; iglp_opt(1) and s_setprio gained less)
+    if constexpr (PV == 5) {
+      // fenced schedule (r04 experiment): at most one step's inputs in flight beside one
+      // step's operands -- load(k + 1) | mfmas(k) | xform(k + 1) -- so the live set
+      // (96 accumulators + 48 operands + 41 inputs) leaves the scheduler room; sched_barrier
+      // keeps each step's LDS reads above the previous step's MFMAs
+      load_step(0, raw[0]);
+      xform(raw[0], xf[0]);
+      load_step(1, raw[1]);
+      __builtin_amdgcn_sched_barrier(0);
+      mfmas(xf[0]);
+      __builtin_amdgcn_sched_barrier(0);
+      xform(raw[1], xf[1]);
+      load_step(2, raw[0]);
+      __builtin_amdgcn_sched_barrier(0);
+      mfmas(xf[1]);
+      __builtin_amdgcn_sched_barrier(0);
+      xform(raw[0], xf[0]);
+      mfmas(xf[0]);
+    } else {
     __builtin_amdgcn_iglp_opt(0);
     load_step(0, raw[0]);
     load_step(1, raw[1]);
@@ -746,6 +766,7 @@ __global__ __launch_bounds__(NW * 64, OCC) void conv3d_wino2_kernel(const ConvAr
     xform(raw[0], xf[0]);
     mfmas(xf[1]);
     mfmas(xf[0]);
+    }
     LEA_STAMP(5);
     if (ch == nchunks - 1) {  // the pair's last chunk: its epilogue, fresh accumulators
       if (ebuf)
@@ -1152,6 +1173,7 @@ int run2(const Plan2& p, ConvArgs a, int B, hipStream_t st, bool cv) {
     LEA_WINO2_TILES(false)
     LEA_WINO2_CASE(8, 2, 1, 4, 2, 2, false)
     LEA_WINO2_CASE(8, 1, 1, 4, 2, 4, false)
+    LEA_WINO2_CASE(8, 1, 1, 4, 2, 5, false)
     if (p.q == 8 && p.wc == 2 && p.mte == 1 && p.nw == 4 && p.occ == 2 && p.pv == 3) {
       using C_ = Cfg2<8, 2, 1, 4, 2, 2>;
       a.ncob = (a.cout + C_::COP - 1) / C_::COP;

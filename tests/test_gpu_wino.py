@@ -461,16 +461,16 @@ def test_lane_halo16_is_bit_identical_to_dword_pieces(b, cin, c1, cout, shape, m
     x1, x2 = (xs[:, :c1].contiguous(), xs[:, c1:].contiguous()) if c1 < cin else (xs, None)
     pw = kernels.pack_conv_weight_wino(w.to(DEV))
     outs = {}
-    for on in (1, 0):
+    for on in (1, 2, 0):
         assert lib.lea_conv3d_wino2_set_lane_halo16(on) == 0
         try:
             name = kernels.wino_kernel_name(b, cout, *shape, cin=cin)
-            assert name == "conv3d_wino2_kernel<8, 1, 1, 4, 2, %d, false>" % (4 if on else 0), name
+            assert name == "conv3d_wino2_kernel<8, 1, 1, 4, 2, %d, false>" % {1: 4, 2: 5, 0: 0}[on], name
             out = r.to(DEV).clone() if mode == "acc" else None
             outs[on] = kernels.conv3d_bnrelu_wino(x1, pw, cout, scale.to(DEV), shift.to(DEV), relu=True, out=out,
                                                   accumulate=mode == "acc", x2=x2,
                                                   residual=r.to(DEV) if mode == "res" else None)
         finally:
             lib.lea_conv3d_wino2_set_lane_halo16(1)
-    assert torch.equal(outs[1], outs[0])
+    assert torch.equal(outs[1], outs[0]) and torch.equal(outs[2], outs[0])
     np.testing.assert_allclose(outs[1].cpu().double().numpy(), want.numpy(), rtol=1e-4, atol=1e-4)
