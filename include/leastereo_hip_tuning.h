@@ -76,14 +76,22 @@ int lea_conv3d_wino2_set_walk(int spw);
  * kernel name "..., 2, false>"), 0 = dword pieces ("..., 1, false>"). */
 int lea_conv3d_wino2_set_halo16(int on);
 
-/* 1 (default) = the W x D engine's per-lane 16-cout tile stages its halo as 16-byte
- * LDS-DMA pieces with interleaved row sets (bank-conflict-free; kernel name
- * "conv3d_wino2_kernel<8, 1, 1, 4, 2, 4, false>"), 0 = dword pieces ("..., 0, false>"). */
+/* The W x D engine's per-lane 16-cout tile: 2 (default) = 16-byte LDS-DMA halo pieces
+ * in interleaved row sets (bank-conflict-free) with the fenced step schedule (kernel name
+ * "conv3d_wino2_kernel<8, 1, 1, 4, 2, 5, false>"), 1 = the same halo with the compiler's
+ * schedule ("..., 4, false>"), 0 = dword pieces ("..., 0, false>").  Bit-identical. */
 int lea_conv3d_wino2_set_lane_halo16(int on);
+
+/* Fenced step schedules (each step's MFMAs issued as one block between sched_barriers),
+ * bit mask, 0 (default) = the compiler's interleaved schedules; bit 0: the 1-D engine's
+ * depth-paired 16-byte-halo tile (the L0 8 -> 8 cell ops; kernel name
+ * "conv3d_wino_kernel<4, 16, 0, 1, 2, false, true, true>"), bit 1: the pipelined W x D tile
+ * ("conv3d_wino2p_fenced_kernel").  Bit-identical. */
+int lea_conv3d_wino_set_fence(int on);
 
 /* 1 (default) = the 16-byte-halo W x D tile runs as the one-barrier pipeline
  * ("conv3d_wino2p_kernel": item i's MFMAs interleaved with item i + 1's transform pass,
- * weights loaded per lane from the packed buffer's lane-major copy), 0 = the two-barrier
+ * weights loaded per lane from the packed buffer's per-lane copy), 0 = the two-barrier
  * tile (PV = 2).  Same packed weights. */
 int lea_conv3d_wino2_set_pipeline(int on);
 

@@ -106,7 +106,7 @@ struct Cfg {
   static_assert(2 * STAGE * 4 * 2 <= 160 * 1024, "two double-buffered workgroups per CU");
 };
 
-template <int F, int Q, int MT, int NP, int TD, bool CV, bool H16 = false>
+template <int F, int Q, int MT, int NP, int TD, bool CV, bool H16 = false, bool FENCE = false>
 __global__ __launch_bounds__(kConvThreads, 2) void conv3d_wino_kernel(const ConvArgs a) {
   using C = Cfg<F, Q, MT, NP, TD, H16>;
   static_assert(!(CV && H16), "16-byte halo: plain volumes only");
@@ -560,6 +560,21 @@ __global__ __launch_bounds__(kConvThreads, 2) void conv3d_wino_kernel(const Conv
     // step ahead, so a step's VALU runs under the previous step's MFMAs
     StepOps ops[2];
     Xf xf[2];
+    if constexpr (FENCE) {
+      // fenced schedule (r04, as the W x D per-lane tile's PV = 5): each step's MFMAs
+      // issue as one block, then the next step's transforms and the LDS reads two ahead
+      load_step(0, ops[0]);
+      xform(ops[0], xf[0]);
+      load_step(1, ops[1]);
+#pragma unroll
+      for (int step = 0; step < C::NSTEP; ++step) {
+        __builtin_amdgcn_sched_barrier(0);
+        mfmas(xf[step & 1]);
+        __builtin_amdgcn_sched_barrier(0);
+        if (step + 1 < C::NSTEP) xform(ops[(step + 1) & 1], xf[(step + 1) & 1]);
+        if (step + 2 < C::NSTEP) load_step(step + 2, ops[step & 1]);
+      }
+    } else {
     // scheduler hint: interleave the step's LDS reads / VALU transforms with the MFMAs
     // (same-box sweep r02: -1 to -4 % per layer; iglp_opt(1) and s_setprio gained less)
     __builtin_amdgcn_iglp_opt(0);
@@ -571,6 +586,7 @@ __global__ __launch_bounds__(kConvThreads, 2) void conv3d_wino_kernel(const Conv
       if (step + 1 < C::NSTEP) xform(ops[(step + 1) & 1], xf[(step + 1) & 1]);
       if (step + 2 < C::NSTEP) load_step(step + 2, ops[step & 1]);
       mfmas(xf[step & 1]);
+    }
     }
     if (ch == nchunks - 1) {  // the depth group's last chunk: its epilogue, fresh accumulators
       if (ebuf)
@@ -659,7 +675,8 @@ int g_block48 = 1;
 int g_epibuf = 1;  // lea_conv3d_wino_set_epi_buf
 int g_halo16 = 1;  // lea_conv3d_wino2_set_halo16
 int g_pipe = 1;    // lea_conv3d_wino2_set_pipeline
-int g_lane16 = 1;  // lea_conv3d_wino2_set_lane_halo16 (2: the fenced step schedule, PV = 5)
+int g_fence = 0;   // lea_conv3d_wino_set_fence: the depth-paired 16-byte-halo tile's fenced schedule
+int g_lane16 = 2;  // lea_conv3d_wino2_set_lane_halo16 (2: the fenced step schedule, PV = 5; r04 default)
 inline int host_mt(int cout) {
   if (g_small16 && cout <= 8) return 1;
   const int mt = mt_of(cout);
@@ -805,7 +822,10 @@ int run(const Plan& p, ConvArgs a, int B, hipStream_t st, bool cv) {
     const long long n_ = (long long)a.ntiles * ((a.ndz + a.spw - 1) / a.spw) * B * a.ncob;
     LEA_CHECK_ARG(n_ < (1LL << 31), "lea_conv3d(wino): grid too large");
     a.nblk = (int)n_;
-    conv3d_wino_kernel<4, 16, 0, 1, 2, false, true><<<dim3((unsigned)n_), kConvThreads, 0, st>>>(a);
+    if (g_fence & 1)
+      conv3d_wino_kernel<4, 16, 0, 1, 2, false, true, true><<<dim3((unsigned)n_), kConvThreads, 0, st>>>(a);
+    else
+      conv3d_wino_kernel<4, 16, 0, 1, 2, false, true><<<dim3((unsigned)n_), kConvThreads, 0, st>>>(a);
     return launch_status("lea_conv3d(wino)");
   }
   if (cv) {
@@ -822,7 +842,7 @@ thread_local char g_name[96];
 const char* name(const Plan& p, bool cv) {
   if (p.d2) return name2(p.p2, cv);
   snprintf(g_name, sizeof(g_name), "conv3d_wino_kernel<%d, %d, %d, %d, %d, %s%s>", p.f, p.q, p.mt, p.np,
-           p.td, cv ? "true" : "false", p.h16 ? ", true" : "");
+           p.td, cv ? "true" : "false", p.h16 ? ((g_fence & 1) ? ", true, true" : ", true") : "");
   return g_name;
 }
 
@@ -860,7 +880,7 @@ extern "C" size_t lea_conv3d_wino_packed_floats(int cout, int cin) {
   if (cout <= 0 || cin <= 0 || cin % wino::CIN_B != 0) return 0;
   const int mt = wino::host_mt(cout), cop = wino::cop_of(mt), nstep = mt == 0 ? 12 : 9;
   // + one 256-float tail: the kernel stages whole 256-float pieces per chunk; 32-cout
-  // blocks append the lane-major copy the one-barrier W x D tile loads (PV = 3)
+  // blocks append the per-lane copy (16-byte slices) the one-barrier W x D tile loads (PV = 3)
   return (size_t)((cout + cop - 1) / cop) * (cin / wino::CIN_B) * nstep * 3 * wino::CIN_B * cop + 256 +
          (mt == 2 ? (size_t)wino::lane_weights_floats(cout, cin) : 0);
 }
@@ -935,6 +955,13 @@ extern "C" int lea_conv3d_wino2_set_pipeline(int on) {
   clear_error();
   LEA_CHECK_ARG(on == 0 || on == 1, "lea_conv3d_wino2_set_pipeline: on=%d", on);
   wino::g_pipe = on;
+  return 0;
+}
+
+extern "C" int lea_conv3d_wino_set_fence(int on) {
+  clear_error();
+  LEA_CHECK_ARG(on >= 0 && on <= 3, "lea_conv3d_wino_set_fence: on=%d", on);
+  wino::g_fence = on;
   return 0;
 }
 

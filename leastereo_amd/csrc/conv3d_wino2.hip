@@ -738,7 +738,7 @@ __global__ __launch_bounds__(NW * 64, OCC) void conv3d_wino2_kernel(const ConvAr
     // scheduler hint: interleave the step's LDS reads / VALU transforms with the MFMAs
     // (same-box sweep r02: -1 to -4 % per layer; iglp_opt(1) and s_setprio gained less)
     if constexpr (PV == 5) {
-      // fenced schedule (r04 experiment): at most one step's inputs in flight beside one
+      // fenced schedule (r04; L1 16 -> 16 cells 46.1 -> 44.2 us same box): at most one step's inputs in flight beside one
       // step's operands -- load(k + 1) | mfmas(k) | xform(k + 1) -- so the live set
       // (96 accumulators + 48 operands + 41 inputs) leaves the scheduler room; sched_barrier
       // keeps each step's LDS reads above the previous step's MFMAs
@@ -807,12 +807,13 @@ __global__ __launch_bounds__(NW * 64, OCC) void conv3d_wino2_kernel(const ConvAr
 //            step 0's transforms so the compiler's wait for g(i) never covers it
 //   g(i + 1) -> registers after the last U of item i (7 dwordx4 per lane)
 // The weights never touch LDS: each lane loads its (cout, channel)'s 27 taps of a chunk
-// from the lane-major copy lea_conv3d_wino_pack_weights appends for 32-cout blocks.
+// from the per-lane copy (16-byte slices) lea_conv3d_wino_pack_weights appends for 32-cout blocks.
 // Ablations of the two-barrier tile (tools/wino2_ablate.sh, conv1/2: 858 us) put its
 // V-pass at 118 us and the weight DMA at 49 us, serialised with the MFMAs.
-constexpr int kGL = 28;  // floats per lane and chunk in the lane-major weights (27 taps + pad)
+constexpr int kGL = 28;  // floats per lane and chunk in the per-lane weights (27 taps + pad)
 
-__global__ __launch_bounds__(256, 2) void conv3d_wino2p_kernel(const ConvArgs a) {
+template <bool FENCE>
+__device__ __forceinline__ void wino2p_body(const ConvArgs& a) {
   using C = Cfg2<8, 2, 1, 4, 2, 2>;  // the PV = 2 tile's geometry and maps (tv, V-pass banks)
   constexpr int Q = 8, WC = 2, F = 4, NX = 6, NE = 4, TD = 2;
   // halo channels 1024 floats apart (the PV = 2 map's bases mod 64): every lane of the 4
@@ -852,9 +853,9 @@ __global__ __launch_bounds__(256, 2) void conv3d_wino2p_kernel(const ConvArgs a)
   const int HW = a.H * a.W;
   const unsigned nrec = (unsigned)(HW * a.D) * 4u;
   const long long cvol = (long long)HW * a.D;
-  // lane-major weights: after the staged copy (ncob * nchunks * WS floats + 256 pad)
+  // per-lane weights (slice-major, see pack_wino_lane_kernel): after the staged copy (ncob * nchunks * WS floats + 256 pad)
   const float* wl = a.wp + (long long)a.ncob * nchunks * C::WS + 256 +
-                    ((long long)cob * nchunks * WC + wc) * 64 * kGL + lane * kGL;
+                    ((long long)cob * nchunks * WC + wc) * 64 * kGL + lane * 4;
 
   // 16-byte halo pieces: block slot j16 = wave of every channel (4 per wave per item);
   // lanes past the halo (e16 >= BLK16) read out of range: zeros into the channel's pad
@@ -895,7 +896,7 @@ __global__ __launch_bounds__(256, 2) void conv3d_wino2p_kernel(const ConvArgs a)
     for (int k = 0; k < kGL / 4; ++k) gw[k] = make_float4(1.f, 0.5f, 0.25f, (float)item);
 #else
 #pragma unroll
-    for (int k = 0; k < kGL / 4; ++k) gw[k] = src[k];
+    for (int k = 0; k < kGL / 4; ++k) gw[k] = src[64 * k];
 #endif
   };
   // V-pass of one item: unit u = (group g, channel c, halo row r), as PV = 2; branch-free:
@@ -1067,6 +1068,27 @@ __global__ __launch_bounds__(256, 2) void conv3d_wino2p_kernel(const ConvArgs a)
     };
     Raw raw[2];
     Xf xf[2];
+    if constexpr (FENCE) {
+      // fenced schedule (r04 experiment, as the per-lane tile's PV = 5): each step's 24
+      // MFMAs issue as one block; the transforms, the V-pass and the loads between them
+      load_step(0, raw[0]);
+      xform(0, raw[0], xf[0]);
+      load_step(1, raw[1]);
+      issue_halo(min(it + 2, nitems - 1), it & 1);
+      __builtin_amdgcn_sched_barrier(0);
+      mfmas(xf[0]);
+      __builtin_amdgcn_sched_barrier(0);
+      xform(1, raw[1], xf[1]);
+      load_step(2, raw[0]);
+      __builtin_amdgcn_sched_barrier(0);
+      mfmas(xf[1]);
+      __builtin_amdgcn_sched_barrier(0);
+      vpass((it + 1) & 1);
+      xform(2, raw[0], xf[0]);
+      load_g(min(it + 1, nitems - 1));
+      __builtin_amdgcn_sched_barrier(0);
+      mfmas(xf[0]);
+    } else {
     __builtin_amdgcn_iglp_opt(0);
     load_step(0, raw[0]);
     load_step(1, raw[1]);
@@ -1085,6 +1107,7 @@ __global__ __launch_bounds__(256, 2) void conv3d_wino2p_kernel(const ConvArgs a)
     load_g(min(it + 1, nitems - 1));
     mfmas(xf[1]);
     mfmas(xf[0]);
+    }
     after_epi = false;
     if (ch == nchunks - 1) {
       epilogue((pz0 + it / nchunks) * TD);
@@ -1099,16 +1122,22 @@ __global__ __launch_bounds__(256, 2) void conv3d_wino2p_kernel(const ConvArgs a)
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
-// lane-major weights of the PV = 3 tile, appended after the staged copy: per (cout block
-// of 32, chunk, cout tile wc, lane = 16 ci + n): the 27 taps [kh][kd][kw] of cout
-// 32 cb + 16 wc + n and input channel 4 chunk + ci, then one zero
+__global__ __launch_bounds__(256, 2) void conv3d_wino2p_kernel(const ConvArgs a) { wino2p_body<false>(a); }
+__global__ __launch_bounds__(256, 2) void conv3d_wino2p_fenced_kernel(const ConvArgs a) { wino2p_body<true>(a); }
+
+// per-lane weights of the pipelined tile, appended after the staged copy: per (cout block
+// of 32, chunk, cout tile wc) seven 256-float slices; slice s holds, per lane = 16 ci + n,
+// taps 4 s .. 4 s + 3 of [kh][kd][kw] (27 taps, then one zero) of cout 32 cb + 16 wc + n
+// and input channel 4 chunk + ci as one 16-byte word: a wave's float4 load of a slice is
+// one contiguous KB (r04; the lane-major form, 112 B between lanes, made each of the seven
+// loads touch 56 cache lines instead of 8)
 __global__ void pack_wino_lane_kernel(const float* __restrict__ w, float* __restrict__ out, int cout, int cin,
                                       int nchunks, long long total) {
   for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
        i += (long long)gridDim.x * blockDim.x) {
     long long q = i;
-    const int k = (int)(q % kGL); q /= kGL;
-    const int ln = (int)(q % 64); q /= 64;
+    const int e = (int)(q % (64 * kGL)); q /= 64 * kGL;
+    const int k = (e / 256) * 4 + (e & 3), ln = (e & 255) >> 2;
     const int wc = (int)(q % 2); q /= 2;
     const int ch = (int)(q % nchunks);
     const int cb = (int)(q / nchunks);
@@ -1184,7 +1213,10 @@ int run2(const Plan2& p, ConvArgs a, int B, hipStream_t st, bool cv) {
       const long long n_ = (long long)a.ntiles * ((a.ndz + a.spw - 1) / a.spw) * B * a.ncob;
       LEA_CHECK_ARG(n_ < (1LL << 31), "lea_conv3d(wino2): grid too large");
       a.nblk = (int)n_;
-      conv3d_wino2p_kernel<<<dim3((unsigned)n_), 256, 0, st>>>(a);
+      if (g_fence & 2)
+        conv3d_wino2p_fenced_kernel<<<dim3((unsigned)n_), 256, 0, st>>>(a);
+      else
+        conv3d_wino2p_kernel<<<dim3((unsigned)n_), 256, 0, st>>>(a);
       return launch_status("lea_conv3d(wino2p)");
     }
   }
@@ -1194,7 +1226,7 @@ int run2(const Plan2& p, ConvArgs a, int B, hipStream_t st, bool cv) {
 }
 
 const char* name2(const Plan2& p, bool cv) {
-  if (p.pv == 3 && !cv) return "conv3d_wino2p_kernel";
+  if (p.pv == 3 && !cv) return (g_fence & 2) ? "conv3d_wino2p_fenced_kernel" : "conv3d_wino2p_kernel";
   snprintf(g_name2, sizeof(g_name2), "conv3d_wino2_kernel<%d, %d, %d, %d, %d, %d, %s>", p.q, p.wc, p.mte,
            p.nw, p.occ, p.pv, cv ? "true" : "false");
   return g_name2;

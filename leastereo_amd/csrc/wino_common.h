@@ -137,12 +137,14 @@ inline int auto_walk(const ConvArgs& a, int B, int wg_per_cu) {
 }
 
 int run2(const Plan2& p, ConvArgs a, int B, hipStream_t st, bool cv);
-// the PV = 3 tile's lane-major weight copy (appended to the packed weights of 32-cout
+// the PV = 3 tile's per-lane weight copy (16-byte slices) (appended to the packed weights of 32-cout
 // blocks by lea_conv3d_wino_pack_weights), in floats, and its packer
 long long lane_weights_floats(int cout, int cin);
 __global__ void pack_wino_lane_kernel(const float* __restrict__ w, float* __restrict__ out, int cout, int cin,
                                       int nchunks, long long total);
 const char* name2(const Plan2& p, bool cv);
+// fenced step schedules, bit mask (lea_conv3d_wino_set_fence; defined in conv3d_wino.hip)
+extern int g_fence;
 
 }  // namespace wino
 }  // namespace lea

@@ -399,8 +399,9 @@ def test_buffer_epilogue_is_bit_identical(b, cin, cout, shape, small, variant):
 def test_wd_halo16_is_bit_identical_to_dword_pieces(b, cin, c1, cout, shape, mode):
     """The transform-pass W x D tile with its halo staged as 16-byte pieces (rows of whole
     16-byte blocks: W % 4 == 0) -- as the one-barrier pipeline (conv3d_wino2p_kernel, weights
-    from the lane-major copy, the default) and as the two-barrier tile (PV = 2) -- and the
-    depth-paired 1-D kernel with 16-byte pieces equal the dword-piece staging bit for bit
+    from the per-lane copy, the default), its fenced-schedule form and the two-barrier tile
+    (PV = 2) -- and the depth-paired 1-D kernel with 16-byte pieces (and its fenced schedule)
+    equal the dword-piece staging bit for bit
     (same values in LDS, same transforms, same accumulation order) and float64 torch at the
     engine bar; ragged H / D / W tiles (W = 36, 68, 4, 124, 60, 188: partial rows), a single
     item (cin 4, one pair), two sources (cin1 = c1), every epilogue."""
@@ -416,25 +417,30 @@ def test_wd_halo16_is_bit_identical_to_dword_pieces(b, cin, c1, cout, shape, mod
     x1, x2 = (xs[:, :c1].contiguous(), xs[:, c1:].contiguous()) if c1 < cin else (xs, None)
     pw = kernels.pack_conv_weight_wino(w.to(DEV))
     outs = {}
-    for on, pipe in ((1, 1), (1, 0), (0, 1)):
+    for on, pipe, fence in ((1, 1, 0), (1, 0, 0), (0, 1, 0), (1, 1, 3)):
         assert lib.lea_conv3d_wino2_set_halo16(on) == 0 and lib.lea_conv3d_wino2_set_pipeline(pipe) == 0
+        assert lib.lea_conv3d_wino_set_fence(fence) == 0
         try:
             name = kernels.wino_kernel_name(b, cout, *shape, cin=cin)
             if cout <= 8:
-                assert name == "conv3d_wino_kernel<4, 16, 0, 1, 2, false%s>" % (", true" if on else ""), name
+                want_name = "conv3d_wino_kernel<4, 16, 0, 1, 2, false%s>" % (
+                    (", true, true" if fence else ", true") if on else "")
+                assert name == want_name, name
             elif on and pipe and cin > 8:  # (one or two chunks per pair: the two-barrier tile)
-                assert name == "conv3d_wino2p_kernel", name
+                assert name == ("conv3d_wino2p_fenced_kernel" if fence else "conv3d_wino2p_kernel"), name
             else:
                 assert name.startswith("conv3d_wino2_kernel<8, 2, 1, 4, 2, %d," % (2 if on else 1)), name
             out = r.to(DEV).clone() if mode == "acc" else None
-            outs[(on, pipe)] = kernels.conv3d_bnrelu_wino(x1, pw, cout, scale.to(DEV), shift.to(DEV), relu=True,
-                                                          out=out, accumulate=mode == "acc", x2=x2,
-                                                          residual=r.to(DEV) if mode == "res" else None)
+            outs[(on, pipe, fence)] = kernels.conv3d_bnrelu_wino(
+                x1, pw, cout, scale.to(DEV), shift.to(DEV), relu=True, out=out, accumulate=mode == "acc", x2=x2,
+                residual=r.to(DEV) if mode == "res" else None)
         finally:
             lib.lea_conv3d_wino2_set_halo16(1)
             lib.lea_conv3d_wino2_set_pipeline(1)
-    assert torch.equal(outs[(1, 1)], outs[(0, 1)]) and torch.equal(outs[(1, 0)], outs[(0, 1)])
-    np.testing.assert_allclose(outs[(1, 1)].cpu().double().numpy(), want.numpy(), rtol=1e-4, atol=1e-4)
+            lib.lea_conv3d_wino_set_fence(0)
+    base = outs[(0, 1, 0)]
+    assert all(torch.equal(o, base) for o in outs.values())
+    np.testing.assert_allclose(outs[(1, 1, 0)].cpu().double().numpy(), want.numpy(), rtol=1e-4, atol=1e-4)
 
 
 @pytest.mark.parametrize("b,cin,c1,cout,shape,mode", [
@@ -444,8 +450,8 @@ def test_wd_halo16_is_bit_identical_to_dword_pieces(b, cin, c1, cout, shape, mod
     (1, 16, 16, 12, (6, 10, 44), "acc")])
 def test_lane_halo16_is_bit_identical_to_dword_pieces(b, cin, c1, cout, shape, mode):
     """The per-lane 16-cout W x D tile with its halo staged as 16-byte pieces into the
-    interleaved-row, bank-conflict-free layout (PV = 4, r04; lea_conv3d_wino2_set_lane_halo16)
-    equals the dword-piece tile (PV = 0) bit for bit -- same staged values, same transforms,
+    interleaved-row, bank-conflict-free layout (PV = 4, r04; lea_conv3d_wino2_set_lane_halo16),
+    and its fenced-schedule form (PV = 5, the default) equal the dword-piece tile (PV = 0) bit for bit -- same staged values, same transforms,
     same accumulation order -- and float64 torch at the engine bar: ragged H (partial 8-row
     tiles), odd D, W not a multiple of 32, one item, two sources, couts padding the block,
     every epilogue."""
@@ -471,6 +477,6 @@ def test_lane_halo16_is_bit_identical_to_dword_pieces(b, cin, c1, cout, shape, m
                                                   accumulate=mode == "acc", x2=x2,
                                                   residual=r.to(DEV) if mode == "res" else None)
         finally:
-            lib.lea_conv3d_wino2_set_lane_halo16(1)
+            lib.lea_conv3d_wino2_set_lane_halo16(2)
     assert torch.equal(outs[1], outs[0]) and torch.equal(outs[2], outs[0])
     np.testing.assert_allclose(outs[1].cpu().double().numpy(), want.numpy(), rtol=1e-4, atol=1e-4)
