@@ -44,6 +44,11 @@ int lea_conv3d_bf16_set_stream1x1(int on);
  * (4 when up-sampling, else 1) (tools/resample_probe.py). */
 int lea_resample_bf16_set_batch(int k);
 
+/* fp32 trilinear resample kernel: 0 (default) = the separable form where the output rows
+ * are whole 16-byte words (W-lerped source rows in LDS), 1 = the row-staged form, 2 = the
+ * per-output gather.  Bit-identical. */
+int lea_resample_set_mode(int mode);
+
 /* Disparity regression: 1 (default) = the register kernel (D3 plane values in registers,
  * compile-time depth axis, no rescaling softmin) for the configured (D3, maxdisp) pairs
  * (4, 12), (8, 24), (16, 48), (32, 96), (64, 192); 0 = the online-softmin kernel for every
@@ -82,11 +87,10 @@ int lea_conv3d_wino2_set_halo16(int on);
  * schedule ("..., 4, false>"), 0 = dword pieces ("..., 0, false>").  Bit-identical. */
 int lea_conv3d_wino2_set_lane_halo16(int on);
 
-/* Fenced step schedules (each step's MFMAs issued as one block between sched_barriers),
- * bit mask, 0 (default) = the compiler's interleaved schedules; bit 0: the 1-D engine's
- * depth-paired 16-byte-halo tile (the L0 8 -> 8 cell ops; kernel name
- * "conv3d_wino_kernel<4, 16, 0, 1, 2, false, true, true>"), bit 1: the pipelined W x D tile
- * ("conv3d_wino2p_fenced_kernel").  Bit-identical. */
+/* 1 (default) = the 1-D engine's depth-paired 16-byte-halo tile (the L0 8 -> 8 cell ops)
+ * issues each step's MFMAs as one block between sched_barriers (kernel name
+ * "conv3d_wino_kernel<4, 16, 0, 1, 2, false, true, true>"), 0 = the compiler's interleaved
+ * schedule ("..., false, true>").  Bit-identical. */
 int lea_conv3d_wino_set_fence(int on);
 
 /* 1 (default) = the 16-byte-halo W x D tile runs as the one-barrier pipeline

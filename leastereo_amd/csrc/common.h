@@ -18,7 +18,7 @@
      defined(LEA_EXP_NORES) || defined(LEA_EXP_NOSTORE) || defined(LEA_EXP_NOBAR1) ||    \
      defined(LEA_EXP_NOBAR2) || defined(LEA_EXP_NOVPASS) || defined(LEA_EXP_NOLDSRD) ||  \
      defined(LEA_EXP_NOXF) || defined(LEA_EXP_NOMFMA) || defined(LEA_EXP_NOWAIT) ||      \
-     defined(LEA_EXP_STAGGER))
+     defined(LEA_EXP_STAGGER) || defined(LEA_EXP_NOUXF))
 #error "LEA_EXP_* ablation switches give wrong outputs: build them only with -DLEA_ABLATION_BUILD"
 #endif
 

@@ -675,7 +675,7 @@ int g_block48 = 1;
 int g_epibuf = 1;  // lea_conv3d_wino_set_epi_buf
 int g_halo16 = 1;  // lea_conv3d_wino2_set_halo16
 int g_pipe = 1;    // lea_conv3d_wino2_set_pipeline
-int g_fence = 0;   // lea_conv3d_wino_set_fence: the depth-paired 16-byte-halo tile's fenced schedule
+int g_fence = 1;   // lea_conv3d_wino_set_fence: the depth-paired 16-byte-halo tile's fenced schedule (r04 default)
 int g_lane16 = 2;  // lea_conv3d_wino2_set_lane_halo16 (2: the fenced step schedule, PV = 5; r04 default)
 inline int host_mt(int cout) {
   if (g_small16 && cout <= 8) return 1;
@@ -822,7 +822,7 @@ int run(const Plan& p, ConvArgs a, int B, hipStream_t st, bool cv) {
     const long long n_ = (long long)a.ntiles * ((a.ndz + a.spw - 1) / a.spw) * B * a.ncob;
     LEA_CHECK_ARG(n_ < (1LL << 31), "lea_conv3d(wino): grid too large");
     a.nblk = (int)n_;
-    if (g_fence & 1)
+    if (g_fence)
       conv3d_wino_kernel<4, 16, 0, 1, 2, false, true, true><<<dim3((unsigned)n_), kConvThreads, 0, st>>>(a);
     else
       conv3d_wino_kernel<4, 16, 0, 1, 2, false, true><<<dim3((unsigned)n_), kConvThreads, 0, st>>>(a);
@@ -842,7 +842,7 @@ thread_local char g_name[96];
 const char* name(const Plan& p, bool cv) {
   if (p.d2) return name2(p.p2, cv);
   snprintf(g_name, sizeof(g_name), "conv3d_wino_kernel<%d, %d, %d, %d, %d, %s%s>", p.f, p.q, p.mt, p.np,
-           p.td, cv ? "true" : "false", p.h16 ? ((g_fence & 1) ? ", true, true" : ", true") : "");
+           p.td, cv ? "true" : "false", p.h16 ? (g_fence ? ", true, true" : ", true") : "");
   return g_name;
 }
 
@@ -960,7 +960,7 @@ extern "C" int lea_conv3d_wino2_set_pipeline(int on) {
 
 extern "C" int lea_conv3d_wino_set_fence(int on) {
   clear_error();
-  LEA_CHECK_ARG(on >= 0 && on <= 3, "lea_conv3d_wino_set_fence: on=%d", on);
+  LEA_CHECK_ARG(on == 0 || on == 1, "lea_conv3d_wino_set_fence: on=%d", on);
   wino::g_fence = on;
   return 0;
 }

@@ -812,8 +812,7 @@ __global__ __launch_bounds__(NW * 64, OCC) void conv3d_wino2_kernel(const ConvAr
 // V-pass at 118 us and the weight DMA at 49 us, serialised with the MFMAs.
 constexpr int kGL = 28;  // floats per lane and chunk in the per-lane weights (27 taps + pad)
 
-template <bool FENCE>
-__device__ __forceinline__ void wino2p_body(const ConvArgs& a) {
+__global__ __launch_bounds__(256, 2) void conv3d_wino2p_kernel(const ConvArgs a) {
   using C = Cfg2<8, 2, 1, 4, 2, 2>;  // the PV = 2 tile's geometry and maps (tv, V-pass banks)
   constexpr int Q = 8, WC = 2, F = 4, NX = 6, NE = 4, TD = 2;
   // halo channels 1024 floats apart (the PV = 2 map's bases mod 64): every lane of the 4
@@ -1043,6 +1042,12 @@ __device__ __forceinline__ void wino2p_body(const ConvArgs& a) {
         for (int i = 0; i < 4; ++i) T.v[(4 * k + i) % NX][(4 * k + i) / NX] = e4[i];
       }
       const float* g = reinterpret_cast<const float*>(gw) + kh * 9;
+#ifdef LEA_EXP_NOUXF  // ablation: U read straight from the taps (no transform VALU)
+#pragma unroll
+      for (int x = 0; x < NX; ++x)
+#pragma unroll
+        for (int e = 0; e < NE; ++e) T.u[x][e] = g[(x * NE + e) % 9];
+#else
       float uw[3][NX];
 #pragma unroll
       for (int kd = 0; kd < 3; ++kd) gw4(g[kd * 3], g[kd * 3 + 1], g[kd * 3 + 2], uw[kd]);
@@ -1054,6 +1059,7 @@ __device__ __forceinline__ void wino2p_body(const ConvArgs& a) {
         T.u[x][2] = s - uw[1][x];
         T.u[x][3] = uw[2][x];
       }
+#endif
     };
     auto mfmas = [&](const Xf& T) {
 #pragma unroll
@@ -1068,27 +1074,6 @@ __device__ __forceinline__ void wino2p_body(const ConvArgs& a) {
     };
     Raw raw[2];
     Xf xf[2];
-    if constexpr (FENCE) {
-      // fenced schedule (r04 experiment, as the per-lane tile's PV = 5): each step's 24
-      // MFMAs issue as one block; the transforms, the V-pass and the loads between them
-      load_step(0, raw[0]);
-      xform(0, raw[0], xf[0]);
-      load_step(1, raw[1]);
-      issue_halo(min(it + 2, nitems - 1), it & 1);
-      __builtin_amdgcn_sched_barrier(0);
-      mfmas(xf[0]);
-      __builtin_amdgcn_sched_barrier(0);
-      xform(1, raw[1], xf[1]);
-      load_step(2, raw[0]);
-      __builtin_amdgcn_sched_barrier(0);
-      mfmas(xf[1]);
-      __builtin_amdgcn_sched_barrier(0);
-      vpass((it + 1) & 1);
-      xform(2, raw[0], xf[0]);
-      load_g(min(it + 1, nitems - 1));
-      __builtin_amdgcn_sched_barrier(0);
-      mfmas(xf[0]);
-    } else {
     __builtin_amdgcn_iglp_opt(0);
     load_step(0, raw[0]);
     load_step(1, raw[1]);
@@ -1107,7 +1092,6 @@ __device__ __forceinline__ void wino2p_body(const ConvArgs& a) {
     load_g(min(it + 1, nitems - 1));
     mfmas(xf[1]);
     mfmas(xf[0]);
-    }
     after_epi = false;
     if (ch == nchunks - 1) {
       epilogue((pz0 + it / nchunks) * TD);
@@ -1122,8 +1106,6 @@ __device__ __forceinline__ void wino2p_body(const ConvArgs& a) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
-__global__ __launch_bounds__(256, 2) void conv3d_wino2p_kernel(const ConvArgs a) { wino2p_body<false>(a); }
-__global__ __launch_bounds__(256, 2) void conv3d_wino2p_fenced_kernel(const ConvArgs a) { wino2p_body<true>(a); }
 
 // per-lane weights of the pipelined tile, appended after the staged copy: per (cout block
 // of 32, chunk, cout tile wc) seven 256-float slices; slice s holds, per lane = 16 ci + n,
@@ -1213,10 +1195,7 @@ int run2(const Plan2& p, ConvArgs a, int B, hipStream_t st, bool cv) {
       const long long n_ = (long long)a.ntiles * ((a.ndz + a.spw - 1) / a.spw) * B * a.ncob;
       LEA_CHECK_ARG(n_ < (1LL << 31), "lea_conv3d(wino2): grid too large");
       a.nblk = (int)n_;
-      if (g_fence & 2)
-        conv3d_wino2p_fenced_kernel<<<dim3((unsigned)n_), 256, 0, st>>>(a);
-      else
-        conv3d_wino2p_kernel<<<dim3((unsigned)n_), 256, 0, st>>>(a);
+      conv3d_wino2p_kernel<<<dim3((unsigned)n_), 256, 0, st>>>(a);
       return launch_status("lea_conv3d(wino2p)");
     }
   }
@@ -1226,7 +1205,7 @@ int run2(const Plan2& p, ConvArgs a, int B, hipStream_t st, bool cv) {
 }
 
 const char* name2(const Plan2& p, bool cv) {
-  if (p.pv == 3 && !cv) return (g_fence & 2) ? "conv3d_wino2p_fenced_kernel" : "conv3d_wino2p_kernel";
+  if (p.pv == 3 && !cv) return "conv3d_wino2p_kernel";
   snprintf(g_name2, sizeof(g_name2), "conv3d_wino2_kernel<%d, %d, %d, %d, %d, %d, %s>", p.q, p.wc, p.mte,
            p.nw, p.occ, p.pv, cv ? "true" : "false");
   return g_name2;

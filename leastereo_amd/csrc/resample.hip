@@ -130,7 +130,85 @@ __global__ __launch_bounds__(256) void resample3d_rows_f32(
   }
 }
 
+// Separable variant (r04; the default when Wo % 4 == 0): trilerp's innermost terms are the
+// W-lerps of the four source rows, aw.l0 * row[aw.i0] + aw.l1 * row[aw.i1], so a workgroup
+// first forms the W-lerped rows of its <= nrmax source rows of both source planes at every
+// output column (each thread owns columns: one W axis per column, loads straight from
+// global), then every output quad combines four float4s of them with the H and D weights
+// in trilerp's own expression tree -- bit-identical to the row-staged and gather kernels.
+// Per output value: ~1.25 W-lerps (the rows two output rows share are lerped once) and one
+// 16-byte LDS read per source-row pair, instead of 4 W-lerps and 8 LDS reads.
+__global__ __launch_bounds__(256) void resample3d_sep_f32(
+    const float* __restrict__ x, long long xbs, float* __restrict__ y, long long ybs, int C, int Di,
+    int Hi, int Wi, int Do, int Ho, int Wo, float rd, float rh, float rw, int ac, int R, int nrmax,
+    const float* __restrict__ scale, const float* __restrict__ shift, unsigned flags) {
+#pragma clang fp contract(off)
+  extern __shared__ float wrows[];  // [2][nrmax][Wo]: W-lerped source rows
+  const int plane = blockIdx.y;
+  const int od = plane % Do;
+  const int bc = plane / Do;
+  const int b = bc / C, c = bc - b * C;
+  const int oh0 = blockIdx.x * R;
+  const int oh1 = min(oh0 + R, Ho);
+  const Axis ad = axis_index(rd, od, Di, Do, ac);
+  const int r_lo = axis_index(rh, oh0, Hi, Ho, ac).i0;
+  const int r_hi = axis_index(rh, oh1 - 1, Hi, Ho, ac).i1;
+  const int nr = min(r_hi - r_lo + 1, nrmax);  // (host bound: r_hi - r_lo < nrmax)
+  const long long HWi = (long long)Hi * Wi;
+  const float* xc = x + (long long)b * xbs + (long long)c * Di * HWi + (long long)r_lo * Wi;
+  const float* src0 = xc + ad.i0 * HWi;
+  const float* src1 = xc + ad.i1 * HWi;
+  for (int xo = threadIdx.x; xo < Wo; xo += blockDim.x) {
+    const Axis aw = axis_index(rw, xo, Wi, Wo, ac);
+    for (int r = 0; r < nr; ++r) {
+      const float* q0 = src0 + (long long)r * Wi;
+      const float* q1 = src1 + (long long)r * Wi;
+      wrows[r * Wo + xo] = aw.l0 * q0[aw.i0] + aw.l1 * q0[aw.i1];
+      wrows[(nrmax + r) * Wo + xo] = aw.l0 * q1[aw.i0] + aw.l1 * q1[aw.i1];
+    }
+  }
+  __syncthreads();
+  float* yp = y + (long long)b * ybs + ((long long)c * Do + od) * Ho * Wo;
+  const float sc = scale ? scale[c] : 1.f;
+  const float sh = scale ? shift[c] : 0.f;
+  const bool relu = flags & LEA_RELU;
+  const int wq = Wo / 4;
+  const int cells = (oh1 - oh0) * wq;
+  const float4* w4 = reinterpret_cast<const float4*>(wrows);
+  for (int t = threadIdx.x; t < cells; t += blockDim.x) {
+    const int oh = oh0 + t / wq;
+    const int q = t % wq;
+    const Axis ah = axis_index(rh, oh, Hi, Ho, ac);
+    const int r0 = ah.i0 - r_lo, r1 = ah.i1 - r_lo;
+    const float4 a00 = w4[r0 * wq + q], a01 = w4[r1 * wq + q];
+    const float4 a10 = w4[(nrmax + r0) * wq + q], a11 = w4[(nrmax + r1) * wq + q];
+    const float p00[4] = {a00.x, a00.y, a00.z, a00.w}, p01[4] = {a01.x, a01.y, a01.z, a01.w};
+    const float p10[4] = {a10.x, a10.y, a10.z, a10.w}, p11[4] = {a11.x, a11.y, a11.z, a11.w};
+    float v[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      float r = ad.l0 * (ah.l0 * p00[e] + ah.l1 * p01[e]) + ad.l1 * (ah.l0 * p10[e] + ah.l1 * p11[e]);
+      if (scale) r = r * sc + sh;
+      if (relu) r = fmaxf(r, 0.f);
+      v[e] = r;
+    }
+    *reinterpret_cast<float4*>(yp + (long long)oh * Wo + 4 * q) = make_float4(v[0], v[1], v[2], v[3]);
+  }
+}
+
+int g_resample_mode = 0;  // lea_resample_set_mode: 0 auto, 1 row-staged, 2 gather
+
 }  // namespace lea
+
+extern "C" int lea_resample_set_mode(int mode) {
+  lea::clear_error();
+  if (mode < 0 || mode > 2) {
+    lea::set_error("lea_resample_set_mode: mode=%d", mode);
+    return LEA_E_INVALID;
+  }
+  lea::g_resample_mode = mode;
+  return 0;
+}
 
 extern "C" int lea_resample3d_trilinear(const void* x, int64_t x_bstride, void* y, int64_t y_bstride,
                                         int B, int C, int Di, int Hi, int Wi, int Do, int Ho, int Wo,
@@ -158,9 +236,22 @@ extern "C" int lea_resample3d_trilinear(const void* x, int64_t x_bstride, void* 
   const int gx = (int)((cells + threads * 8 - 1) / (threads * 8));
   dim3 grid(gx, B * C * Do);
   const float rd = axis_ratio(Di, Do, ac), rh = axis_ratio(Hi, Ho, ac), rw = axis_ratio(Wi, Wo, ac);
+  // Separable kernel (16-byte outputs) when R output rows' W-lerped source rows fit 64 KB
+  if (vec && g_resample_mode == 0) {
+    for (int R = 16; R >= 2; R /= 2) {
+      const int nrmax = (int)floorf((float)(R - 1) * rh) + 3;  // +1: fp rounding margin
+      const size_t lds = (size_t)2 * nrmax * Wo * sizeof(float);
+      if (lds > 65536) continue;
+      dim3 g((Ho + R - 1) / R, B * C * Do);
+      resample3d_sep_f32<<<g, threads, lds, as_stream(stream)>>>(
+          (const float*)x, x_bstride, (float*)y, y_bstride, C, Di, Hi, Wi, Do, Ho, Wo, rd, rh, rw, ac, R, nrmax,
+          scale, shift, flags);
+      return launch_status("lea_resample3d_trilinear");
+    }
+  }
   // Row-staged kernel when R output rows' sources fit 64 KB of LDS: R = 16 rows
   // (20 KB of output per workgroup at Wo = 320), fewer for wide rows.
-  for (int R = 16; R >= 2; R /= 2) {
+  for (int R = 16; R >= 2 && g_resample_mode != 2; R /= 2) {
     const int nrmax = (int)floorf((float)(R - 1) * rh) + 3;  // +1: fp rounding margin
     const size_t lds = (size_t)2 * nrmax * Wi * sizeof(float);
     if (lds > 65536) continue;

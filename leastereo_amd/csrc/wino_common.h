@@ -143,8 +143,6 @@ long long lane_weights_floats(int cout, int cin);
 __global__ void pack_wino_lane_kernel(const float* __restrict__ w, float* __restrict__ out, int cout, int cin,
                                       int nchunks, long long total);
 const char* name2(const Plan2& p, bool cv);
-// fenced step schedules, bit mask (lea_conv3d_wino_set_fence; defined in conv3d_wino.hip)
-extern int g_fence;
 
 }  // namespace wino
 }  // namespace lea

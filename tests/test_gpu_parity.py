@@ -304,6 +304,34 @@ def test_resample_vs_torch_random_sizes():
             np.testing.assert_allclose(y.numpy(), refy.numpy(), atol=3e-6, rtol=0)
 
 
+@pytest.mark.parametrize("src,dst,ac,epi", [
+    ((32, 96, 160), (64, 192, 320), True, True), ((16, 48, 80), (32, 96, 160), True, False),
+    ((5, 9, 13), (3, 5, 8), False, True), ((4, 6, 8), (8, 12, 16), False, False),
+    ((3, 70, 9), (6, 141, 20), True, True), ((8, 40, 100), (4, 20, 52), True, False)])
+def test_resample_kernels_are_bit_identical(src, dst, ac, epi):
+    """The separable resample (W-lerped source rows in LDS, the default for 16-byte output
+    rows), the row-staged and the gather kernels give the same bits -- trilerp's expression
+    tree in each -- with and without the BN/ReLU epilogue, up- and down-sampling, ragged
+    row blocks (H 141), and match torch."""
+    lib = _lib.load()
+    g = torch.Generator().manual_seed(sum(dst))
+    x = torch.randn((2, 3) + src, generator=g)
+    scale = (torch.rand(3, generator=g) + 0.5).to(DEV) if epi else None
+    shift = (torch.randn(3, generator=g) * 0.1).to(DEV) if epi else None
+    outs = []
+    try:
+        for mode in (0, 1, 2):
+            assert lib.lea_resample_set_mode(mode) == 0
+            outs.append(kernels.resample_trilinear(x.to(DEV), dst, ac, None, scale, shift, relu=epi).cpu())
+    finally:
+        lib.lea_resample_set_mode(0)
+    assert torch.equal(outs[0], outs[1]) and torch.equal(outs[0], outs[2])
+    want = F.interpolate(x, dst, mode="trilinear", align_corners=ac)
+    if epi:
+        want = torch.relu(want * scale.cpu().view(1, -1, 1, 1, 1) + shift.cpu().view(1, -1, 1, 1, 1))
+    np.testing.assert_allclose(outs[0].numpy(), want.numpy(), atol=3e-6, rtol=0)
+
+
 def test_disparity_vs_oracle_sizes():
     g = torch.Generator().manual_seed(5)
     for shape, md in [((1, 1, 64, 12, 20), 192), ((2, 1, 88, 5, 9), 264), ((1, 1, 16, 7, 4), 48)]:

@@ -126,7 +126,7 @@ def test_wino_matches_the_direct_engine_at_full_size():
 
 
 @pytest.mark.parametrize("mode,name", [
-    (0, "conv3d_wino_kernel<4, 16, 0, 1, 2, false, true>"),
+    (0, "conv3d_wino_kernel<4, 16, 0, 1, 2, false, true, true>"),
     (1, "conv3d_wino2_kernel<16, 1, 1, 4, 2, 0, false>")])
 def test_small_cout_tiles_match_the_direct_engine_at_full_size(mode, name):
     """The L0 8->8 cell op at config 2 (8 channels, 64x192x320) on both small-cout forms
@@ -399,8 +399,8 @@ def test_buffer_epilogue_is_bit_identical(b, cin, cout, shape, small, variant):
 def test_wd_halo16_is_bit_identical_to_dword_pieces(b, cin, c1, cout, shape, mode):
     """The transform-pass W x D tile with its halo staged as 16-byte pieces (rows of whole
     16-byte blocks: W % 4 == 0) -- as the one-barrier pipeline (conv3d_wino2p_kernel, weights
-    from the per-lane copy, the default), its fenced-schedule form and the two-barrier tile
-    (PV = 2) -- and the depth-paired 1-D kernel with 16-byte pieces (and its fenced schedule)
+    from the per-lane copy, the default) and the two-barrier tile (PV = 2) -- and the
+    depth-paired 1-D kernel with 16-byte pieces (fenced schedule, the default, and the compiler's)
     equal the dword-piece staging bit for bit
     (same values in LDS, same transforms, same accumulation order) and float64 torch at the
     engine bar; ragged H / D / W tiles (W = 36, 68, 4, 124, 60, 188: partial rows), a single
@@ -417,7 +417,7 @@ def test_wd_halo16_is_bit_identical_to_dword_pieces(b, cin, c1, cout, shape, mod
     x1, x2 = (xs[:, :c1].contiguous(), xs[:, c1:].contiguous()) if c1 < cin else (xs, None)
     pw = kernels.pack_conv_weight_wino(w.to(DEV))
     outs = {}
-    for on, pipe, fence in ((1, 1, 0), (1, 0, 0), (0, 1, 0), (1, 1, 3)):
+    for on, pipe, fence in ((1, 1, 1), (1, 0, 1), (0, 1, 1), (1, 1, 0)):
         assert lib.lea_conv3d_wino2_set_halo16(on) == 0 and lib.lea_conv3d_wino2_set_pipeline(pipe) == 0
         assert lib.lea_conv3d_wino_set_fence(fence) == 0
         try:
@@ -427,7 +427,7 @@ def test_wd_halo16_is_bit_identical_to_dword_pieces(b, cin, c1, cout, shape, mod
                     (", true, true" if fence else ", true") if on else "")
                 assert name == want_name, name
             elif on and pipe and cin > 8:  # (one or two chunks per pair: the two-barrier tile)
-                assert name == ("conv3d_wino2p_fenced_kernel" if fence else "conv3d_wino2p_kernel"), name
+                assert name == "conv3d_wino2p_kernel", name
             else:
                 assert name.startswith("conv3d_wino2_kernel<8, 2, 1, 4, 2, %d," % (2 if on else 1)), name
             out = r.to(DEV).clone() if mode == "acc" else None
@@ -437,10 +437,10 @@ def test_wd_halo16_is_bit_identical_to_dword_pieces(b, cin, c1, cout, shape, mod
         finally:
             lib.lea_conv3d_wino2_set_halo16(1)
             lib.lea_conv3d_wino2_set_pipeline(1)
-            lib.lea_conv3d_wino_set_fence(0)
-    base = outs[(0, 1, 0)]
+            lib.lea_conv3d_wino_set_fence(1)
+    base = outs[(0, 1, 1)]
     assert all(torch.equal(o, base) for o in outs.values())
-    np.testing.assert_allclose(outs[(1, 1, 0)].cpu().double().numpy(), want.numpy(), rtol=1e-4, atol=1e-4)
+    np.testing.assert_allclose(outs[(1, 1, 1)].cpu().double().numpy(), want.numpy(), rtol=1e-4, atol=1e-4)
 
 
 @pytest.mark.parametrize("b,cin,c1,cout,shape,mode", [

@@ -1,6 +1,7 @@
 #!/usr/bin/env python3
-"""Every conv launch of one forward, in launch order: kernel, (B, cin, cout, D, H, W, k),
-HIP-event microseconds (median over --reps forwards), direct-conv TFLOP/s.
+"""Every probed launch of one forward, in launch order: kernel, (B, cin, cout, D, H, W, k),
+HIP-event microseconds (median over --reps forwards), direct-conv TFLOP/s and algorithmic
+GB/s (the probe's bytes: inputs + output + weights [+ residual]).
 
     python tools/layer_list.py [--config c2|c3|c4|c5] [--reps 5]
 """
@@ -40,14 +41,15 @@ def main():
             with kernels.KernelProbe() as probe:
                 model(left, right)
             torch.cuda.synchronize()
-            runs.append([(n, f, s, e0.elapsed_time(e1)) for n, f, _, e0, e1, _, s in probe.records])
+            runs.append([(n, f, s, e0.elapsed_time(e1), nb) for n, f, nb, e0, e1, _, s in probe.records])
     total = 0.0
     for i, rec in enumerate(runs[0]):
         us = statistics.median(r[i][3] for r in runs) * 1e3
         total += us
         name, flops, shp = rec[0], rec[1], rec[2]
         tf = flops / us / 1e6 if us > 0 else 0.0
-        print(f"{i:3d} {us:8.1f} us {tf:7.1f} TF/s  {str(shp):34s} {name}")
+        gbs = rec[4] / us / 1e3 if us > 0 else 0.0
+        print(f"{i:3d} {us:8.1f} us {tf:7.1f} TF/s {gbs:7.1f} GB/s  {str(shp):34s} {name}")
     print(f"conv launches {len(runs[0])}, {total / 1e3:.3f} ms")
 
 
