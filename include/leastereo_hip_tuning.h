@@ -49,6 +49,14 @@ int lea_resample_bf16_set_batch(int k);
  * per-output gather.  Bit-identical. */
 int lea_resample_set_mode(int mode);
 
+/* 1 (default) = lea_conv2d_bnrelu runs convs with cin <= 16 and cout <= 32 (the feature
+ * net's cell ops) on the few-channel VALU tile ("conv2d_small_kernel<CIN4, NG>"), 0 = the
+ * DMA / MFMA engine for every shape. */
+int lea_conv2d_set_small(int on);
+
+/* lea_conv2d_kernel_name with the input channel count (the few-channel tile depends on it). */
+const char* lea_conv2d_kernel_name_cin(int B, int cin, int cout, int H, int W);
+
 /* Disparity regression: 1 (default) = the register kernel (D3 plane values in registers,
  * compile-time depth axis, no rescaling softmin) for the configured (D3, maxdisp) pairs
  * (4, 12), (8, 24), (16, 48), (32, 96), (64, 192); 0 = the online-softmin kernel for every

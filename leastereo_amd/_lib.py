@@ -93,6 +93,8 @@ SIGNATURES = {
     "lea_conv3d_wino2_set_lane_halo16": (_i, [_i]),
     "lea_conv3d_wino_set_fence": (_i, [_i]),
     "lea_resample_set_mode": (_i, [_i]),
+    "lea_conv2d_set_small": (_i, [_i]),
+    "lea_conv2d_kernel_name_cin": (ctypes.c_char_p, [_i, _i, _i, _i, _i]),
     "lea_conv3d_wino2_set_pipeline": (_i, [_i]),
     "lea_conv3d_wino_set_epi_buf": (_i, [_i]),
     "lea_conv3d_set_rs_gather": (_i, [_i]),
@@ -165,6 +167,7 @@ TUNING_ENV = {"LEASTEREO_WINO2_WALK": "lea_conv3d_wino2_set_walk",
               "LEASTEREO_LANE_HALO16": "lea_conv3d_wino2_set_lane_halo16",
               "LEASTEREO_WINO_FENCE": "lea_conv3d_wino_set_fence",
               "LEASTEREO_RESAMPLE_MODE": "lea_resample_set_mode",
+              "LEASTEREO_CONV2D_SMALL": "lea_conv2d_set_small",
               "LEASTEREO_WINO2_PIPE": "lea_conv3d_wino2_set_pipeline",
               "LEASTEREO_EPI_BUF": "lea_conv3d_wino_set_epi_buf",
               "LEASTEREO_RS_GATHER": "lea_conv3d_set_rs_gather",

@@ -924,9 +924,10 @@ extern "C" int lea_conv2d_bnrelu(const void* x, int64_t x_bstride, const float* 
     set_error("lea_conv2d: dtype %d unsupported", dtype);
     return LEA_E_UNSUPPORTED;
   }
+  hipStream_t st = as_stream(stream);
+  if (conv2d_small_ok(cin, cout)) return run_conv2d_small(a, B, st);
   const Plan p = make_plan_2d(B, cout, H, W);
   a.ncob = (cout + p.mt * 16 - 1) / (p.mt * 16);
-  hipStream_t st = as_stream(stream);
   switch (p.mt) {
     case 1: return run_dma2d_mt1(p, a, B, st);
     case 2: return run_dma2d_mt2(p, a, B, st);

@@ -538,6 +538,9 @@ LEA_DMA_DECL_CV(3)
 LEA_DMA_DECL_CV(4)
 #undef LEA_DMA_DECL_CV
 int run_dma_dp(const Plan& p, const ConvArgs& a, int B, hipStream_t st);  // conv3d_dma_mt1.hip
+// the few-channel 2D 3x3 tile (conv2d_small.hip): eligibility and launch
+bool conv2d_small_ok(int cin, int cout);
+int run_conv2d_small(const ConvArgs& a, int B, hipStream_t st);
 LEA_DMA_DECL(1)
 LEA_DMA_DECL(2)
 LEA_DMA_DECL(3)

@@ -284,8 +284,10 @@ def conv3d_bnrelu_resampled(x: torch.Tensor, size, packed: torch.Tensor, cout: i
 # Feature-net activations travel as NCDHW views with D = 1 ([B, C, 1, H, W]), so the
 # 1x1 convs and bilinear resizes are the 3D entry points on a single plane.
 
-def conv2d_kernel_name(b, cout, h, w):
-    name = _lib.load().lea_conv2d_kernel_name(b, cout, h, w)
+def conv2d_kernel_name(b, cout, h, w, cin=None):
+    lib = _lib.load()
+    name = (lib.lea_conv2d_kernel_name(b, cout, h, w) if cin is None
+            else lib.lea_conv2d_kernel_name_cin(b, cin, cout, h, w))
     return name.decode() if name else None
 
 
@@ -318,7 +320,7 @@ def conv2d_bnrelu(x: torch.Tensor, packed: torch.Tensor, cout: int,
     rptr, rbs = _residual(out, accumulate, residual, ybs)
     flags = (LEA_RELU if relu else 0) | (LEA_RESIDUAL if rptr is not None else 0)
     rec = None if _probe is None else _probe_launch(
-        conv2d_kernel_name(b, cout, h, w), 2.0 * b * h * w * cout * cin * 9,
+        conv2d_kernel_name(b, cout, h, w, cin), 2.0 * b * h * w * cout * cin * 9,
         4.0 * b * h * w * (cin + cout * (2 if rptr is not None else 1)) + 36.0 * cout * cin)
     check(_lib.load().lea_conv2d_bnrelu(
         x.data_ptr(), xbs, packed.data_ptr(),

@@ -411,6 +411,48 @@ def test_conv2d_random_vs_torch(b, cin, cout, hw, res):
     np.testing.assert_allclose(y.squeeze(2).cpu().double().numpy(), refy.numpy(), rtol=1e-4, atol=1e-4)
 
 
+@pytest.mark.parametrize("b,cin,cout,hw,res", [
+    (2, 8, 8, (192, 320), "acc"), (2, 8, 16, (192, 320), None), (2, 16, 16, (96, 160), "res"),
+    (2, 16, 32, (96, 160), "slice"), (1, 3, 16, (31, 45), None), (1, 12, 24, (17, 100), "acc"),
+    (2, 5, 20, (9, 70), "res"), (1, 16, 8, (1, 1), None), (3, 4, 32, (33, 31), "slice")])
+def test_conv2d_few_channel_tile_vs_torch(b, cin, cout, hw, res):
+    """The few-channel 2D tile (cin <= 16, cout <= 32: the feature net's cell ops, r04) and
+    the DMA / MFMA engine it replaces there, against float64 torch: the 1/3 and 1/6
+    resolution cell shapes, ragged tiles, cin not a multiple of 4, the cell-sum epilogues
+    (accumulate, residual) and an output slice of a wider tensor (the cell's channel slot)."""
+    lib = _lib.load()
+    g = torch.Generator().manual_seed(cin * 11 + cout + hw[1])
+    x = torch.randn((b, cin) + hw, generator=g)
+    w = torch.randn(cout, cin, 3, 3, generator=g) / np.sqrt(cin * 9)
+    scale = torch.rand(cout, generator=g) + 0.5
+    shift = torch.randn(cout, generator=g) * 0.1
+    r = torch.randn((b, cout) + hw, generator=g)
+    refy = F.conv2d(x.double(), w.double(), None, 1, 1)
+    refy = torch.relu(refy * scale.double().view(1, -1, 1, 1) + shift.double().view(1, -1, 1, 1))
+    if res in ("acc", "res"):
+        refy = refy + r.double()
+    pw = kernels.pack_conv2d_weight(w.to(DEV))
+    ys = {}
+    try:
+        for small in (1, 0):
+            assert lib.lea_conv2d_set_small(small) == 0
+            name = kernels.conv2d_kernel_name(b, cout, hw[0], hw[1], cin)
+            assert name.startswith("conv2d_small_kernel<") == bool(small), name
+            big = torch.full((b, cout + 16, 1) + hw, 7.0, device=DEV)
+            out = (r.to(DEV).clone().unsqueeze(2) if res == "acc" else
+                   big[:, 8:8 + cout] if res == "slice" else None)
+            y = kernels.conv2d_bnrelu(x.to(DEV).unsqueeze(2), pw, cout, scale.to(DEV), shift.to(DEV),
+                                      relu=True, out=out, accumulate=res == "acc",
+                                      residual=r.to(DEV).unsqueeze(2) if res == "res" else None)
+            if res == "slice":
+                assert torch.all(big[:, :8] == 7.0) and torch.all(big[:, 8 + cout:] == 7.0)
+            ys[small] = y.squeeze(2).cpu().double().numpy()
+    finally:
+        lib.lea_conv2d_set_small(1)
+    for small, y in ys.items():
+        np.testing.assert_allclose(y, refy.numpy(), rtol=1e-4, atol=1e-4, err_msg=f"small={small}")
+
+
 @pytest.mark.parametrize("b,cin,cout,hw", [(2, 16, 32, (96, 192)), (1, 5, 20, (31, 46)),
                                            (1, 16, 32, (4, 3))])
 def test_conv2d_stride3_vs_torch(b, cin, cout, hw):
