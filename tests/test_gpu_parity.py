@@ -304,20 +304,22 @@ def test_resample_vs_torch_random_sizes():
             np.testing.assert_allclose(y.numpy(), refy.numpy(), atol=3e-6, rtol=0)
 
 
-@pytest.mark.parametrize("src,dst,ac,epi", [
-    ((32, 96, 160), (64, 192, 320), True, True), ((16, 48, 80), (32, 96, 160), True, False),
-    ((5, 9, 13), (3, 5, 8), False, True), ((4, 6, 8), (8, 12, 16), False, False),
-    ((3, 70, 9), (6, 141, 20), True, True), ((8, 40, 100), (4, 20, 52), True, False)])
-def test_resample_kernels_are_bit_identical(src, dst, ac, epi):
+@pytest.mark.parametrize("src,dst,ac,epi,ch", [
+    ((32, 96, 160), (64, 192, 320), True, True, 3), ((16, 48, 80), (32, 96, 160), True, False, 3),
+    ((5, 9, 13), (3, 5, 8), False, True, 3), ((4, 6, 8), (8, 12, 16), False, False, 3),
+    ((3, 70, 9), (6, 141, 20), True, True, 3), ((8, 40, 100), (4, 20, 52), True, False, 3),
+    ((16, 48, 80), (32, 96, 160), False, True, 3), ((40, 24, 36), (13, 48, 72), True, False, 3),
+    ((48, 20, 40), (24, 40, 80), True, True, 16), ((9, 33, 20), (19, 64, 40), False, False, 24)])
+def test_resample_kernels_are_bit_identical(src, dst, ac, epi, ch):
     """The separable resample (W-lerped source rows in LDS, the default for 16-byte output
     rows), the row-staged and the gather kernels give the same bits -- trilerp's expression
     tree in each -- with and without the BN/ReLU epilogue, up- and down-sampling, ragged
-    row blocks (H 141), and match torch."""
+    row blocks (H 141), 3 to 24 channels, and match torch."""
     lib = _lib.load()
     g = torch.Generator().manual_seed(sum(dst))
-    x = torch.randn((2, 3) + src, generator=g)
-    scale = (torch.rand(3, generator=g) + 0.5).to(DEV) if epi else None
-    shift = (torch.randn(3, generator=g) * 0.1).to(DEV) if epi else None
+    x = torch.randn((2, ch) + src, generator=g)
+    scale = (torch.rand(ch, generator=g) + 0.5).to(DEV) if epi else None
+    shift = (torch.randn(ch, generator=g) * 0.1).to(DEV) if epi else None
     outs = []
     try:
         for mode in (0, 1, 2):
@@ -325,7 +327,7 @@ def test_resample_kernels_are_bit_identical(src, dst, ac, epi):
             outs.append(kernels.resample_trilinear(x.to(DEV), dst, ac, None, scale, shift, relu=epi).cpu())
     finally:
         lib.lea_resample_set_mode(0)
-    assert torch.equal(outs[0], outs[1]) and torch.equal(outs[0], outs[2])
+    assert all(torch.equal(outs[0], o) for o in outs[1:])
     want = F.interpolate(x, dst, mode="trilinear", align_corners=ac)
     if epi:
         want = torch.relu(want * scale.cpu().view(1, -1, 1, 1, 1) + shift.cpu().view(1, -1, 1, 1, 1))
