@@ -87,7 +87,10 @@ class CellGraphExecutor:
     SHARE_DOWNSAMPLE = os.environ.get("LEASTEREO_SHARE_DOWNSAMPLE", "1") != "0"
     # a three-op sibling group of 16-channel 3D ops (the L1 cells: 16 -> 48) as a 32-cout
     # launch on the pipelined W x D kernel plus a 16-cout one (r03: 66 + 43 us vs 124 us on
-    # the 1-D 48-row engine); the f32 Winograd matching executor only
+    # the 1-D 48-row engine); the f32 Winograd matching executor only.  Split as step 0's op
+    # (head, 16 couts) + steps 1, 2 (the 32-cout group).  (r04: running op0 (s0 -> step 0)
+    # on a side stream beside s1's preprocess and this group, the head accumulating after
+    # the join, measured 140.6 -> 138.1 pairs/s at C2 in graph replay: not kept)
     SPLIT_S1_GROUP48 = False
 
     def __init__(self, net):
@@ -103,6 +106,7 @@ class CellGraphExecutor:
             # with cout = n*C over channels [.., ..) of the cell output (their weights
             # and folded BN stacked along cout).  The remaining ops accumulate.
             self.s1_group = {}
+            self.s1_split = set()
             for i, cell in enumerate(net.cells):
                 group = []
                 for k, terms in enumerate(cell.plan):
@@ -118,7 +122,7 @@ class CellGraphExecutor:
                 mods = [cell._ops[op] for _, op in group]
                 split = (self.SPLIT_S1_GROUP48 and WINOGRAD and len(mods) == 3 and cell.c_out == 16
                          and mods[0].conv.weight.dim() == 5 and mods[0].conv.weight.shape[2] == 3)
-                for key, part in ((("s1_group", mods[:2]), ("s1_group_tail", mods[2:])) if split
+                for key, part in ((("s1_group_head", mods[:1]), ("s1_group", mods[1:])) if split
                                   else (("s1_group", mods),)):
                     w = torch.cat([m.conv.weight for m in part], 0)
                     folded = [m.folded_bn() for m in part]
@@ -126,6 +130,8 @@ class CellGraphExecutor:
                     shift = torch.cat([f[1] for f in folded]).contiguous()
                     self.p[f"cells.{i}.{key}"] = _conv_params(part[0], w, (scale, shift))
                 self.s1_group[i] = group
+                if split:
+                    self.s1_split.add(i)
             # a cell that resamples s1, followed by a same-level cell: the next cell's s0
             # is this s1 (Cell.forward returns prev_input, skip_model_3d.py:75) at the same
             # size, so both 1x1 convs run as one stacked conv over one read of it (down:
@@ -186,11 +192,11 @@ class CellGraphExecutor:
             for name, p in self.p.items():
                 if p.kind != "3d" or not kernels.wino_eligible(p.cout, p.cin, p.k):
                     continue
-                if name.endswith("s1_group") or name.endswith("s1_group_tail"):
+                if name.endswith("s1_group") or name.endswith("s1_group_head"):
                     i = int(name.split(".")[1])
                     mods = [self.m.cells[i]._ops[op] for _, op in self.s1_group[i]]
-                    if f"cells.{i}.s1_group_tail" in self.p:
-                        mods = mods[2:] if name.endswith("_tail") else mods[:2]
+                    if i in self.s1_split:
+                        mods = mods[:1] if name.endswith("_head") else mods[1:]
                     w = torch.cat([m.conv.weight for m in mods], 0)
                 else:
                     w = self.m.get_submodule(name).conv.weight
@@ -244,6 +250,7 @@ class CellGraphExecutor:
             out = self._empty(b, bm * c, size, s1)
         slot = {idx: self._channels(out, k * c, (k + 1) * c)
                 for k, idx in enumerate(range(n_states - bm, n_states))}
+        group = self.s1_group.get(i, [])
         if memo is not None and memo[0] is s0 and memo[1] == size:
             s0 = memo[2]  # computed by the previous cell's stacked conv
             if 0 in slot:
@@ -262,17 +269,16 @@ class CellGraphExecutor:
         else:
             s1 = self.conv(f"cells.{i}.preprocess", s1, out=slot.get(1), size=size)
         states = [s0, s1]
-        group = self.s1_group.get(i, [])
         written = set()
+        done = set(group)
         if group:  # ops on s1 of every step, one launch, straight into their slots
             k0 = 2 + group[0][0] - (n_states - bm)
-            if f"cells.{i}.s1_group_tail" in self.p:
-                self.conv(f"cells.{i}.s1_group", s1, out=self._channels(out, k0 * c, (k0 + 2) * c))
-                self.conv(f"cells.{i}.s1_group_tail", s1, out=self._channels(out, (k0 + 2) * c, (k0 + 3) * c))
+            if i in self.s1_split:
+                self.conv(f"cells.{i}.s1_group", s1, out=self._channels(out, (k0 + 1) * c, (k0 + 3) * c))
+                self.conv(f"cells.{i}.s1_group_head", s1, out=self._channels(out, k0 * c, (k0 + 1) * c))
             else:
                 self.conv(f"cells.{i}.s1_group", s1, out=self._channels(out, k0 * c, (k0 + len(group)) * c))
             written = {k for k, _ in group}
-        done = set(group)
         for step, terms in enumerate(cell.plan):
             dst = slot.get(len(states))
             if dst is None:
