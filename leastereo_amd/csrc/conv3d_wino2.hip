@@ -1020,15 +1020,22 @@ __global__ __launch_bounds__(256, 2) void conv3d_wino2p_kernel(const ConvArgs a)
       asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NST) : "memory");
     else
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#ifndef LEA_EXP_NOBAR1
     __syncthreads();
+#endif
     const float* tv = tvb + (it & 1) * TS;
     struct Raw {
       float4 v4[6];
     };
     auto load_step = [&](int kh, Raw& o) {
       const float4* tp = reinterpret_cast<const float4*>(tv + toff + kh * C::TRS);
+#ifdef LEA_EXP_NOLDSRD  // ablation: V operands from registers (no LDS reads)
+      for (int k = 0; k < 6; ++k) o.v4[k] = make_float4(0.5f * kh, 0.25f, (float)k, 1.f);
+      (void)tp;
+#else
 #pragma unroll
       for (int k = 0; k < 6; ++k) o.v4[k] = tp[k];
+#endif
     };
     struct Xf {
       float v[NX][NE];
