@@ -30,11 +30,25 @@ __global__ __launch_bounds__(TW * TH) void feature_stem_kernel(
   const int hi0 = 3 * ho0 - 2, wi0 = 3 * wo0 - 2;
   const float* xb = x + (long long)b * xbs;
   const long long HWi = (long long)Hi * Wi;
-  for (int e = threadIdx.x; e < CIN * PH * PW; e += TW * TH) {
-    const int c = e / (PH * PW), r = (e / PW) % PH, q = e % PW;
-    const int h = hi0 + r, w = wi0 + q;
-    patch[c][r][q] = ((unsigned)h < (unsigned)Hi && (unsigned)w < (unsigned)Wi)
-                         ? xb[(long long)c * HWi + (long long)h * Wi + w] : 0.f;
+  {
+    // every load of the patch in flight before the first LDS write (r04: the rolled loop
+    // waited for each of its 32 loads in turn); branch-free, clamped in-range addresses
+    constexpr int N = CIN * PH * PW, NST = (N + TW * TH - 1) / (TW * TH);
+    float v[NST];
+#pragma unroll
+    for (int k = 0; k < NST; ++k) {
+      const int e = min((int)threadIdx.x + k * TW * TH, N - 1);
+      const int c = e / (PH * PW), r = (e / PW) % PH, q = e % PW;
+      const int h = hi0 + r, w = wi0 + q;
+      const bool ok = (unsigned)h < (unsigned)Hi && (unsigned)w < (unsigned)Wi;
+      const float t = xb[(long long)c * HWi + (long long)min(max(h, 0), Hi - 1) * Wi + min(max(w, 0), Wi - 1)];
+      v[k] = ok ? t : 0.f;
+    }
+#pragma unroll
+    for (int k = 0; k < NST; ++k) {
+      const int e = (int)threadIdx.x + k * TW * TH;
+      if (e < N) (&patch[0][0][0])[e] = v[k];
+    }
   }
   __syncthreads();
   const int tx = threadIdx.x % TW, ty = threadIdx.x / TW;

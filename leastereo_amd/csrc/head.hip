@@ -195,9 +195,23 @@ __global__ __launch_bounds__(256) void tapsum_hwpass_rows_f32(
   const long long HWi = (long long)Hi * Wi;
   const float* yp = ws + (long long)plane * 9 * HWi + (long long)r_lo * Wi;
   const int n1 = nr * Wi;
-  for (int e = threadIdx.x; e < 9 * n1; e += blockDim.x) {
-    const int k = e / n1, r = e - k * n1;
-    rows[k * nrmax * Wi + r] = yp[(long long)k * HWi + r];
+  // eight loads in flight per batch (r04: the rolled loop waited for each load in turn)
+  for (int e0 = threadIdx.x; e0 < 9 * n1; e0 += 8 * blockDim.x) {
+    float v[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int e = min(e0 + j * (int)blockDim.x, 9 * n1 - 1);
+      const int k = e / n1, r = e - k * n1;
+      v[j] = yp[(long long)k * HWi + r];
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int e = e0 + j * (int)blockDim.x;
+      if (e < 9 * n1) {
+        const int k = e / n1, r = e - k * n1;
+        rows[k * nrmax * Wi + r] = v[j];
+      }
+    }
   }
   __syncthreads();
   const float sc = scale ? scale[co] : 1.f, sh = scale ? shift[co] : 0.f;
