@@ -8,8 +8,9 @@
 // dot product over a 5x5x3 image patch, folded BN, ReLU; zero where the pixel lies in
 // stem1's padding) channel by channel and accumulates them straight into its C1 stem1
 // outputs: no stem0 pixel is computed twice and its 16 x 4 B per pixel never reach HBM
-// (70 MB per stereo pair at 576x960).  A workgroup stages its image patch in LDS with
-// coalesced loads; the weights are wave-uniform scalar loads.
+// (70 MB per stereo pair at 576x960).  A workgroup stages its image patch and the weights
+// (c0-major) in LDS with coalesced loads, all in flight at once; the weights are read as
+// wave-uniform LDS broadcasts.
 #include "common.h"
 
 namespace lea {
@@ -25,6 +26,11 @@ __global__ __launch_bounds__(TW * TH) void feature_stem_kernel(
     const float* __restrict__ sh0, const float* __restrict__ w1, const float* __restrict__ sc1,
     const float* __restrict__ sh1, void* __restrict__ y, long long ybs, int Hi, int Wi, int Ho, int Wo) {
   __shared__ float patch[CIN][PH][PW];
+  // the weights, c0-major, staged once (r04; read as wave-uniform scalar loads, each c0
+  // iteration waited on ~70 of them): w0s[c0][c][3][3] as given, w1s[c0][o][3][3]
+  __shared__ __attribute__((aligned(16))) float w0s[C0 * CIN * 9 + 1];
+  __shared__ __attribute__((aligned(16))) float w1s[C0 * C1 * 9];
+  __shared__ float bn0[2][C0];  // stem0's folded BN (scale, shift)
   const int b = blockIdx.z;
   const int ho0 = blockIdx.y * TH, wo0 = blockIdx.x * TW;
   const int hi0 = 3 * ho0 - 2, wi0 = 3 * wo0 - 2;
@@ -44,10 +50,33 @@ __global__ __launch_bounds__(TW * TH) void feature_stem_kernel(
       const float t = xb[(long long)c * HWi + (long long)min(max(h, 0), Hi - 1) * Wi + min(max(w, 0), Wi - 1)];
       v[k] = ok ? t : 0.f;
     }
+    constexpr int N0 = C0 * CIN * 9, N1 = C0 * C1 * 9;
+    constexpr int NW = (N0 + N1 + TW * TH - 1) / (TW * TH);
+    float wv[NW];
+#pragma unroll
+    for (int k = 0; k < NW; ++k) {
+      const int e = min((int)threadIdx.x + k * TW * TH, N0 + N1 - 1);
+      if (e < N0) {
+        wv[k] = w0[e];
+      } else {  // w1s index (c0, o, t) <- w1[(o * C0 + c0) * 9 + t]
+        const int f = e - N0, c0 = f / (C1 * 9), o = (f / 9) % C1, t = f % 9;
+        wv[k] = w1[(o * C0 + c0) * 9 + t];
+      }
+    }
 #pragma unroll
     for (int k = 0; k < NST; ++k) {
       const int e = (int)threadIdx.x + k * TW * TH;
       if (e < N) (&patch[0][0][0])[e] = v[k];
+    }
+#pragma unroll
+    for (int k = 0; k < NW; ++k) {
+      const int e = (int)threadIdx.x + k * TW * TH;
+      if (e < N0) w0s[e] = wv[k];
+      else if (e < N0 + N1) w1s[e - N0] = wv[k];
+    }
+    if (threadIdx.x < 2 * C0) {
+      const int c0 = threadIdx.x % C0;
+      bn0[threadIdx.x / C0][c0] = sc0 ? (threadIdx.x < C0 ? sc0[c0] : sh0[c0]) : (threadIdx.x < C0 ? 1.f : 0.f);
     }
   }
   __syncthreads();
@@ -72,7 +101,7 @@ __global__ __launch_bounds__(TW * TH) void feature_stem_kernel(
 #pragma unroll
   for (int o = 0; o < C1; ++o) acc[o] = 0.f;
   for (int c0 = 0; c0 < C0; ++c0) {
-    const float s0 = sc0 ? sc0[c0] : 1.f, t0 = sc0 ? sh0[c0] : 0.f;
+    const float s0 = bn0[0][c0], t0 = bn0[1][c0];
     float s[3][3];
 #pragma unroll
     for (int kh = 0; kh < 3; ++kh)
@@ -84,7 +113,7 @@ __global__ __launch_bounds__(TW * TH) void feature_stem_kernel(
 #pragma unroll
           for (int i = 0; i < 3; ++i)
 #pragma unroll
-            for (int j = 0; j < 3; ++j) v = fmaf(w0[((c0 * CIN + c) * 3 + i) * 3 + j], in[c][kh + i][kw + j], v);
+            for (int j = 0; j < 3; ++j) v = fmaf(w0s[((c0 * CIN + c) * 3 + i) * 3 + j], in[c][kh + i][kw + j], v);
         v = fmaxf(v * s0 + t0, 0.f);  // stem0's BN + ReLU (new_model_2d.py:93)
         s[kh][kw] = valid[kh][kw] ? v : 0.f;
       }
@@ -93,7 +122,7 @@ __global__ __launch_bounds__(TW * TH) void feature_stem_kernel(
 #pragma unroll
       for (int kh = 0; kh < 3; ++kh)
 #pragma unroll
-        for (int kw = 0; kw < 3; ++kw) acc[o] = fmaf(w1[((o * C0 + c0) * 3 + kh) * 3 + kw], s[kh][kw], acc[o]);
+        for (int kw = 0; kw < 3; ++kw) acc[o] = fmaf(w1s[(c0 * C1 + o) * 9 + kh * 3 + kw], s[kh][kw], acc[o]);
   }
   if (ho >= Ho || wo >= Wo) return;
   const long long HWo = (long long)Ho * Wo, pix = (long long)ho * Wo + wo;
