@@ -311,9 +311,18 @@ __global__ __launch_bounds__(NW * 64, OCC) void conv3d_wino2_kernel(const ConvAr
     }
   };
 
-  auto issue = [&](int item, float* st) {
-    const int ch = item % nchunks;
-    if (ch == 0) set_pair((pz0 + item / nchunks) * C::TD);
+  // H4 halo bases: channel c's = (c < cin1 ? xa : x2s) + c * cvol floats (x2s = x2's base cin1
+  // channels down), byte addresses: a compare, select and add per piece, no 64-bit products
+  const unsigned long long cvolb = (unsigned long long)HW * a.D * 4u;
+  const unsigned long long xa = (unsigned long long)(a.x + (long long)b * a.xbs);
+  const unsigned long long x2s =
+      a.x2 ? (unsigned long long)(a.x2 + (long long)b * a.x2bs) - (unsigned long long)a.cin1 * cvolb : xa;
+  unsigned long long coff4[K4];  // piece k's channel offset within the chunk
+#pragma unroll
+  for (int k = 0; k < K4; ++k) coff4[k] = (unsigned long long)((wave + NW * k) / PIECES16) * cvolb;
+  // item = (chunk ch, depth pair pr) of this workgroup's walk (the caller's counters)
+  auto issue = [&](int ch, int pr, float* st) {
+    if (ch == 0) set_pair((pz0 + pr) * C::TD);
     const float* wsrc = wp + (long long)ch * C::WS;
     float* wdst = st + C::XS;
 #pragma unroll
@@ -328,12 +337,12 @@ __global__ __launch_bounds__(NW * 64, OCC) void conv3d_wino2_kernel(const ConvAr
     const unsigned crec = CV ? (unsigned)HW * 4u : nrec;
     if constexpr (C::H4) {
       static_assert(!CV, "16-byte halo: plain volumes only");
+      const unsigned long long cbase = (unsigned long long)(ch * CIN_B) * cvolb;
 #pragma unroll
       for (int k = 0; k < K4; ++k) {
         const int P = wave + NW * k, ci = P / PIECES16, j = P - ci * PIECES16;
         const int c = ch * CIN_B + ci;
-        const float* base = c < a.cin1 ? a.x + (long long)b * a.xbs + (long long)c * cvol
-                                       : a.x2 + (long long)b * a.x2bs + (long long)(c - a.cin1) * cvol;
+        const unsigned long long base = (c < a.cin1 ? xa : x2s) + cbase + coff4[k];
         const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)base, 0, crec, 0x00020000);
 #ifndef LEA_EXP_NOHALO
         dma_dwordx4_buf(rs, voff4[k], lds0 + 4 * (unsigned)(st - smem + C::cb4(0) + ci * C::CS4 + j * 256));
@@ -537,17 +546,19 @@ __global__ __launch_bounds__(NW * 64, OCC) void conv3d_wino2_kernel(const ConvAr
   unsigned long long st_prev = stamp();
   const unsigned long long st_begin = st_prev;
 #endif
-  issue(0, smem);
+  issue(0, 0, smem);
   LEA_STAMP(2);
+  int ich = 0, ipr = 0;  // item it = (chunk, depth pair)
   for (int it = 0; it < nitems; ++it) {
-    const int ch = it % nchunks;
+    const int ch = ich;
+    const bool wrap = ich + 1 == nchunks;  // item it + 1 starts the next pair
     wait_item<NST>(ebuf && ch == 0 && it > 0);  // this wave's pieces of item it landed
     LEA_STAMP(0);
 #ifndef LEA_EXP_NOBAR1  // ablation builds (tools/wino2_ablate.sh): outputs wrong, timing only
     __syncthreads();  // ... and everyone's; item it-1's stage is free
 #endif
     LEA_STAMP(1);
-    if (it + 1 < nitems) issue(it + 1, smem + ((it + 1) & 1) * C::STAGE);
+    if (it + 1 < nitems) issue(wrap ? 0 : ich + 1, wrap ? ipr + 1 : ipr, smem + ((it + 1) & 1) * C::STAGE);
     LEA_STAMP(2);
     const float* xs = smem + (it & 1) * C::STAGE;
     const float* ws = xs + C::XS;
@@ -770,9 +781,9 @@ __global__ __launch_bounds__(NW * 64, OCC) void conv3d_wino2_kernel(const ConvAr
     LEA_STAMP(5);
     if (ch == nchunks - 1) {  // the pair's last chunk: its epilogue, fresh accumulators
       if (ebuf)
-        epilogue_buf((pz0 + it / nchunks) * C::TD);
+        epilogue_buf((pz0 + ipr) * C::TD);
       else
-        epilogue((pz0 + it / nchunks) * C::TD);
+        epilogue((pz0 + ipr) * C::TD);
 #pragma unroll
       for (int x = 0; x < NX; ++x)
 #pragma unroll
@@ -781,6 +792,8 @@ __global__ __launch_bounds__(NW * 64, OCC) void conv3d_wino2_kernel(const ConvAr
           for (int m = 0; m < MTE; ++m) acc[x][e][m] = f32x4{0.f, 0.f, 0.f, 0.f};
       LEA_STAMP(6);
     }
+    ich = wrap ? 0 : ich + 1;
+    ipr += wrap;
   }
 #ifdef LEA_EXP_STAMPS
   st_sum[7] = stamp() - st_begin;
@@ -871,16 +884,22 @@ __global__ __launch_bounds__(256, 2) void conv3d_wino2p_kernel(const ConvArgs a)
       pln16 = p - 1;
     }
   }
-  auto issue_halo = [&](int item, int buf) {  // branch-free: every lane, every channel
-    const int ch = item % nchunks;
-    const int d = (pz0 + item / nchunks) * TD + pln16;
+  // channel c's base = (c < cin1 ? xa : x2s) + c * cvol floats, x2s = x2's base cin1 channels down
+  // (byte addresses: one compare, select and add per channel instead of two 64-bit products)
+  const unsigned long long cvolb = (unsigned long long)cvol * 4u;
+  const unsigned long long xa = (unsigned long long)(a.x + (long long)b * a.xbs);
+  const unsigned long long x2s =
+      a.x2 ? (unsigned long long)(a.x2 + (long long)b * a.x2bs) - (unsigned long long)a.cin1 * cvolb : xa;
+  // item = (chunk ch, depth pair pr) of this workgroup's walk (counters, no divisions in the loop)
+  auto issue_halo = [&](int ch, int pr, int buf) {  // branch-free: every lane, every channel
+    const int d = (pz0 + pr) * TD + pln16;
     const unsigned vo = (hwo16 != 0xFFFFFFF0u && (unsigned)d < (unsigned)a.D)
                             ? hwo16 + (unsigned)d * (unsigned)HW * 4u : 0xFFFFFFF0u;
+    const unsigned long long cb = (unsigned long long)(ch * CIN_B) * cvolb;
 #pragma unroll
     for (int ci = 0; ci < CIN_B; ++ci) {
       const int c = ch * CIN_B + ci;
-      const float* base = c < a.cin1 ? a.x + (long long)b * a.xbs + (long long)c * cvol
-                                     : a.x2 + (long long)b * a.x2bs + (long long)(c - a.cin1) * cvol;
+      const unsigned long long base = (c < a.cin1 ? xa : x2s) + cb + (unsigned long long)ci * cvolb;
       const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)base, 0, nrec, 0x00020000);
       constexpr int cbs[4] = {CB0, CB1, CB2, CB3};
 #ifndef LEA_EXP_NOHALO
@@ -889,10 +908,10 @@ __global__ __launch_bounds__(256, 2) void conv3d_wino2p_kernel(const ConvArgs a)
     }
   };
   float4 gw[kGL / 4];  // this lane's taps of the current chunk: [kh][kd][kw]
-  auto load_g = [&](int item) {
-    const float4* src = reinterpret_cast<const float4*>(wl + (long long)(item % nchunks) * WC * 64 * kGL);
+  auto load_g = [&](int ch) {
+    const float4* src = reinterpret_cast<const float4*>(wl + (long long)ch * WC * 64 * kGL);
 #ifdef LEA_EXP_NOWDMA
-    for (int k = 0; k < kGL / 4; ++k) gw[k] = make_float4(1.f, 0.5f, 0.25f, (float)item);
+    for (int k = 0; k < kGL / 4; ++k) gw[k] = make_float4(1.f, 0.5f, 0.25f, (float)ch);
 #else
 #pragma unroll
     for (int k = 0; k < kGL / 4; ++k) gw[k] = src[64 * k];
@@ -1002,10 +1021,10 @@ __global__ __launch_bounds__(256, 2) void conv3d_wino2p_kernel(const ConvArgs a)
   };
 
   // prologue: halo(0), g(0), halo(1); V(0)
-  issue_halo(0, 0);
+  issue_halo(0, 0, 0);
   load_g(0);
   if (nitems > 1) {
-    issue_halo(1, 1);
+    issue_halo(1 % nchunks, 1 / nchunks, 1);
     asm volatile("s_waitcnt vmcnt(4)" ::: "memory");  // all but halo(1)'s four pieces
   } else {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1013,8 +1032,10 @@ __global__ __launch_bounds__(256, 2) void conv3d_wino2p_kernel(const ConvArgs a)
   __syncthreads();
   vpass(0);
   bool after_epi = false;
+  int ich = 0, ipr = 0;  // item it = (chunk, depth pair)
+  // item min(it + 2, nitems - 1), the halo the loop issues
+  int hch = min(2, nitems - 1) % nchunks, hpr = min(2, nitems - 1) / nchunks;
   for (int it = 0; it < nitems; ++it) {
-    const int ch = it % nchunks;
     // halo(it + 1) and g(it) landed (only an epilogue's stores may stay in flight)
     if (after_epi)
       asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NST) : "memory");
@@ -1088,7 +1109,7 @@ __global__ __launch_bounds__(256, 2) void conv3d_wino2p_kernel(const ConvArgs a)
     // halo(it + 2) into the buffer V-pass(it) read (after g(it)'s first use: see above);
     // past the last item the DMA / V-pass / loads repeat the last one (nothing reads
     // them), so the body is one basic block the scheduler can interleave with the MFMAs
-    issue_halo(min(it + 2, nitems - 1), it & 1);
+    issue_halo(hch, hpr, it & 1);
     load_step(2, raw[0]);
     xform(1, raw[1], xf[1]);
     mfmas(xf[0]);
@@ -1096,17 +1117,26 @@ __global__ __launch_bounds__(256, 2) void conv3d_wino2p_kernel(const ConvArgs a)
     vpass((it + 1) & 1);
 #endif
     xform(2, raw[0], xf[0]);
-    load_g(min(it + 1, nitems - 1));
+    // g(min(it + 1, nitems - 1)): the last item's chunk is nchunks - 1 = ich
+    load_g(it + 1 < nitems ? (ich + 1 == nchunks ? 0 : ich + 1) : ich);
     mfmas(xf[1]);
     mfmas(xf[0]);
     after_epi = false;
-    if (ch == nchunks - 1) {
-      epilogue((pz0 + it / nchunks) * TD);
+    if (ich == nchunks - 1) {
+      epilogue((pz0 + ipr) * TD);
       after_epi = true;
 #pragma unroll
       for (int x = 0; x < NX; ++x)
 #pragma unroll
         for (int e = 0; e < NE; ++e) acc[x][e] = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+    if (++ich == nchunks) {
+      ich = 0;
+      ++ipr;
+    }
+    if (it + 3 < nitems && ++hch == nchunks) {
+      hch = 0;
+      ++hpr;
     }
   }
   // the last iterations' repeated DMA still writes this workgroup's LDS: let it land
