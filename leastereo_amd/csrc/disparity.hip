@@ -59,6 +59,19 @@ __device__ __forceinline__ float dexp(float x) {
     return expf(x);
 }
 
+// expf(x) for x that cannot overflow (the register form's m - U <= rounding above 0):
+// the device library's sequence -- x log2(e) split hi / lo, exp2 of the reduced
+// argument, ldexp, the underflow select -- without its overflow select (bit-identical)
+__device__ __forceinline__ float exp_noovf(float x) {
+#pragma clang fp contract(off)
+  const float ph = x * 0x1.715476p+0f;
+  float pl = fmaf(x, 0x1.715476p+0f, -ph);
+  pl = fmaf(x, 0x1.4ae0bep-26f, pl);
+  const float rn = __builtin_rintf(ph);
+  const float r = __builtin_ldexpf(__builtin_amdgcn_exp2f((ph - rn) + pl), (int)rn);
+  return x < -0x1.9fe368p+6f ? 0.f : r;
+}
+
 template <bool FAST>
 __global__ __launch_bounds__(kDispThreads) void disparity_f32(const float* __restrict__ cost,
                                                               float* __restrict__ disp, int D3,
@@ -157,7 +170,7 @@ __global__ __launch_bounds__(kDispThreads) void disparity_reg_f32(const float* _
   for (int od = 0; od < MD; ++od) {
     const AxisW ad = src_axis(rd, od, D3, MD);  // constants after unrolling
     const float u = ad.l0 * v[ad.i0] + ad.l1 * v[ad.i1];
-    const float e = dexp<FAST>(m - u);
+    const float e = FAST ? dexp<true>(m - u) : exp_noovf(m - u);
     s += e;
     t += (float)od * e;
   }
