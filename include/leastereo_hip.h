@@ -126,6 +126,18 @@ int lea_conv2d_bnrelu(const void* x, int64_t x_bstride, const float* w_packed,
 /* Kernel instantiation lea_conv2d_bnrelu launches for this shape. */
 const char* lea_conv2d_kernel_name(int B, int cout, int H, int W);
 
+/* Two ConvBR2d 3x3 s1 p1 of the same input in one launch (a feature-net cell's two ops
+ * on s0, retrain/new_model_2d.py:41-75 -- the reference runs them as two convs): weights
+ * and folded BN of both stacked along cout (w_packed: lea_conv2d_pack_weights of the
+ * [cout, cin, 3, 3] stack), couts [0, c1) written to y with the residual (flags as for
+ * lea_conv2d_bnrelu), couts [c1, cout) to y2 without it.  cin <= 16, cout <= 32 and
+ * c1 % 8 == 0 (the few-channel tile; LEA_E_UNSUPPORTED beyond it); fp32. */
+int lea_conv2d_bnrelu_pair(const void* x, int64_t x_bstride, const float* w_packed,
+                           const float* scale, const float* shift, const void* residual,
+                           int64_t r_bstride, void* y, int64_t y_bstride, void* y2,
+                           int64_t y2_bstride, int B, int cin, int cout, int c1, int H, int W,
+                           unsigned flags, void* stream);
+
 /* Feature-net stem1: Conv2d 3x3, stride 3, pad 1 -> BN -> ReLU (new_model_2d.py:94).
  * w: the raw [cout, cin, 3, 3] weight (no packing).  x: [B, cin, Hi, Wi];
  * y: [B, cout, (Hi-1)/3+1, (Wi-1)/3+1]. */

@@ -95,6 +95,8 @@ SIGNATURES = {
     "lea_resample_set_mode": (_i, [_i]),
     "lea_conv2d_set_small": (_i, [_i]),
     "lea_conv2d_kernel_name_cin": (ctypes.c_char_p, [_i, _i, _i, _i, _i]),
+    "lea_conv2d_bnrelu_pair": (_i, [_p, _i64, _p, _p, _p, _p, _i64, _p, _i64, _p, _i64, _i, _i, _i, _i, _i,
+                                    _i, _u, _p]),
     "lea_conv3d_wino2_set_pipeline": (_i, [_i]),
     "lea_conv3d_wino_set_epi_buf": (_i, [_i]),
     "lea_conv3d_set_rs_gather": (_i, [_i]),

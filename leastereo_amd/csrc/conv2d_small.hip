@@ -98,7 +98,9 @@ __global__ __launch_bounds__(256) void conv2d_small_kernel(const ConvArgs a) {
     }
   }
   const int h = h0 + ty, w = w0 + tx;
-  const bool relu = a.flags & LEA_RELU, resid = a.flags & LEA_RESIDUAL;
+  // lea_conv2d_bnrelu_pair: this wave's 8 couts belong to the second conv (uniform: csplit % 8 == 0)
+  const bool second = a.csplit > 0 && cg * 8 >= a.csplit;
+  const bool relu = a.flags & LEA_RELU, resid = (a.flags & LEA_RESIDUAL) && !second;
   const long long pix = (long long)min(h, a.H - 1) * a.W + min(w, a.W - 1);
   // the residuals' loads all issued before the first use (clamped, in range)
   float rv[8], sc[8], sh[8];
@@ -118,7 +120,7 @@ __global__ __launch_bounds__(256) void conv2d_small_kernel(const ConvArgs a) {
   }
   // stores last: none of the loads above may be ordered after one (y may alias them)
   if (h >= a.H || w >= a.W) return;
-  float* yp = a.y + (long long)b * a.ybs + pix;
+  float* yp = second ? a.y2 + (long long)b * a.y2bs + pix - (long long)a.csplit * HW : a.y + (long long)b * a.ybs + pix;
   if (cg * 8 + 8 <= a.cout) {  // (uniform) the whole group: one block of 8 stores
 #pragma unroll
     for (int j = 0; j < 8; ++j) yp[(cg * 8 + j) * HW] = acc[j];
@@ -169,6 +171,48 @@ extern "C" int lea_conv2d_set_small(int on) {
   }
   lea::g_conv2d_small = on;
   return 0;
+}
+
+extern "C" int lea_conv2d_bnrelu_pair(const void* x, int64_t x_bstride, const float* w_packed,
+                                      const float* scale, const float* shift, const void* residual,
+                                      int64_t r_bstride, void* y, int64_t y_bstride, void* y2, int64_t y2_bstride,
+                                      int B, int cin, int cout, int c1, int H, int W, unsigned flags,
+                                      void* stream) {
+  using namespace lea;
+  clear_error();
+  ConvArgs a{};
+  a.x = (const float*)x;
+  a.xbs = x_bstride;
+  a.cin1 = cin;
+  a.wp = w_packed;
+  a.scale = scale;
+  a.shift = shift;
+  a.res = (const float*)residual;
+  a.rbs = r_bstride;
+  a.y = (float*)y;
+  a.ybs = y_bstride;
+  a.y2 = (float*)y2;
+  a.y2bs = y2_bstride;
+  a.csplit = c1;
+  a.cin = cin;
+  a.cout = cout;
+  a.D = 1;
+  a.H = H;
+  a.W = W;
+  a.flags = flags;
+  LEA_CHECK_ARG(a.x && a.wp && a.y && a.y2, "lea_conv2d_bnrelu_pair: null pointer");
+  LEA_CHECK_ARG((a.scale == nullptr) == (a.shift == nullptr),
+                "lea_conv2d_bnrelu_pair: scale/shift must both be set or both NULL");
+  LEA_CHECK_ARG(!(flags & LEA_RESIDUAL) || a.res, "lea_conv2d_bnrelu_pair: LEA_RESIDUAL without residual");
+  LEA_CHECK_ARG(B > 0 && cin > 0 && H > 0 && W > 0 && c1 > 0 && c1 < cout && c1 % 8 == 0,
+                "lea_conv2d_bnrelu_pair: bad shape B=%d cin=%d cout=%d c1=%d H=%d W=%d", B, cin, cout, c1, H, W);
+  LEA_CHECK_ARG((long long)(cout + 63) * H * W < (1LL << 31), "lea_conv2d_bnrelu_pair: plane too large");
+  LEA_CHECK_ARG(a.x != a.y && a.x != a.y2, "lea_conv2d_bnrelu_pair: input aliases an output");
+  if (cin > 16 || cout > 32) {  // the few-channel tile only (conv2d_small_ok's shapes, always on here)
+    set_error("lea_conv2d_bnrelu_pair: cin=%d cout=%d beyond the few-channel tile", cin, cout);
+    return LEA_E_UNSUPPORTED;
+  }
+  return run_conv2d_small(a, B, as_stream(stream));
 }
 
 extern "C" const char* lea_conv2d_kernel_name_cin(int B, int cin, int cout, int H, int W) {

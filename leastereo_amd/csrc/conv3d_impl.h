@@ -76,6 +76,10 @@ struct ConvArgs {
   unsigned flags;
   int spw;                 // W x D Winograd engine: depth pairs walked per workgroup (0 = 1)
   unsigned* dbg;           // diagnostic builds only (LEA_EXP_STAMPS): per-wave phase cycles
+  // lea_conv2d_bnrelu_pair (few-channel 2D tile): couts [csplit, cout) go to y2 (no residual)
+  float* y2;
+  long long y2bs;
+  int csplit;
 };
 
 // KD = kernel depth: KS for the 3D convs, 1 for the feature net's 2D 3x3 convs

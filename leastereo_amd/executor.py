@@ -92,6 +92,10 @@ class CellGraphExecutor:
     # on a side stream beside s1's preprocess and this group, the head accumulating after
     # the join, measured 140.6 -> 138.1 pairs/s at C2 in graph replay: not kept)
     SPLIT_S1_GROUP48 = False
+    # the feature net's 2D cells: their two conv ops on s0 (op0 -> step 0 with the skip term as
+    # its residual, op4 -> step 2 before op5 accumulates) as one launch writing two slots
+    # (lea_conv2d_bnrelu_pair; r04).  The f32 feature executor only; LEASTEREO_PAIR_S0=0: two launches
+    PAIR_S0 = False
 
     def __init__(self, net):
         from .model import ConvBR
@@ -132,6 +136,28 @@ class CellGraphExecutor:
                 self.s1_group[i] = group
                 if split:
                     self.s1_split.add(i)
+            self.s0_pair = {}
+            for i, cell in enumerate(net.cells) if self.PAIR_S0 else ():
+                pair = [(k, op) for k, terms in enumerate(cell.plan) for op, j in terms
+                        if j == 0 and cell.op_kinds[op] == "conv"]
+                first_cat_state = 2 + cell.steps - cell.block_multiplier
+                if (len(pair) != 2 or getattr(cell, "dims", 3) != 2 or 2 + pair[0][0] < first_cat_state
+                        or cell.c_out % 8 or 2 * cell.c_out > 32):
+                    continue
+                (k0, op0), (k1, op1) = pair
+                m0, m1 = cell._ops[op0], cell._ops[op1]
+                other = [(o, j) for o, j in cell.plan[k1] if o != op1]
+                # op1 writes its step first (the other term a conv that accumulates after it)
+                if (m0.relu != m1.relu or m0.conv.weight.dim() != 4 or m0.conv.weight.shape[-1] != 3
+                        or m0.stride != 1 or m1.stride != 1 or cell.plan[k1][0][0] != op1
+                        or not other or cell.op_kinds[other[0][0]] != "conv"):
+                    continue
+                w = torch.cat([m0.conv.weight, m1.conv.weight], 0)
+                folded = [m0.folded_bn(), m1.folded_bn()]
+                self.p[f"cells.{i}.s0_pair"] = _conv_params(
+                    m0, w, (torch.cat([f[0] for f in folded]).contiguous(),
+                            torch.cat([f[1] for f in folded]).contiguous()))
+                self.s0_pair[i] = pair
             # a cell that resamples s1, followed by a same-level cell: the next cell's s0
             # is this s1 (Cell.forward returns prev_input, skip_model_3d.py:75) at the same
             # size, so both 1x1 convs run as one stacked conv over one read of it (down:
@@ -271,6 +297,18 @@ class CellGraphExecutor:
         states = [s0, s1]
         written = set()
         done = set(group)
+        consumed = set()  # steps whose skip term went in as an epilogue residual already
+        pair = self.s0_pair.get(i)
+        if pair is not None and self._nchannels(s0) == c and self._volume(s0) == size:
+            (k0, op0), (k1, op1) = pair
+            skips0 = [states[j] for o, j in cell.plan[k0] if cell.op_kinds[o] != "conv"]
+            p = self.p[f"cells.{i}.s0_pair"]
+            kernels.conv2d_bnrelu_pair(s0, p.packed, c, 2 * c, p.scale, p.shift, p.relu,
+                                       slot[2 + k0], slot[2 + k1], skips0[-1] if skips0 else None)
+            done |= {(k0, op0), (k1, op1)}
+            written |= {k0, k1}
+            if skips0:
+                consumed.add(k0)
         if group:  # ops on s1 of every step, one launch, straight into their slots
             k0 = 2 + group[0][0] - (n_states - bm)
             if i in self.s1_split:
@@ -284,6 +322,8 @@ class CellGraphExecutor:
             if dst is None:
                 dst = self._empty(b, c, size, s1)
             skips = [states[j] for k, j in terms if cell.op_kinds[k] != "conv"]
+            if step in consumed:
+                skips.pop()
             for k, j in terms:
                 if (step, k) in done or cell.op_kinds[k] != "conv":
                     continue
@@ -430,6 +470,7 @@ class FeatureExecutor(CellGraphExecutor):
     # stems 0 and 1 as one kernel (csrc/feature_stem.hip); LEASTEREO_FEATURE_STEM=0 runs
     # them as two convs
     FUSED_STEM = os.environ.get("LEASTEREO_FEATURE_STEM", "1") != "0"
+    PAIR_S0 = os.environ.get("LEASTEREO_PAIR_S0", "1") != "0"
 
     def _stems(self, x, c8=False, x2=None):
         """new_model_2d.py:93-94 (stem1(stem0(x))), fused where the kernel is instantiated;
@@ -653,6 +694,7 @@ class FeatureExecutorBF16(_C8Layout, FeatureExecutor):
     stride-3 stem1 stay f32; from stem2 on the maps are c8 and the 3x3 convs run on
     the bf16 engine's 2D tiles.  Returns c8 feature maps [N, 32/8, 1, H3, W3, 8],
     which the bf16 matching net reads directly."""
+    PAIR_S0 = False  # (the pair launch is the f32 few-channel tile's)
 
     def __init__(self, feature):
         super().__init__(feature)

@@ -332,6 +332,41 @@ def conv2d_bnrelu(x: torch.Tensor, packed: torch.Tensor, cout: int,
     return out
 
 
+def conv2d_bnrelu_pair(x: torch.Tensor, packed: torch.Tensor, c1: int, cout: int,
+                       scale: torch.Tensor | None, shift: torch.Tensor | None, relu: bool,
+                       out1: torch.Tensor, out2: torch.Tensor,
+                       residual: torch.Tensor | None = None) -> None:
+    """Two ConvBR2d 3x3/s1/p1 of x [B, cin, 1, H, W] in one launch (lea_conv2d_bnrelu_pair):
+    ``packed`` holds both weight stacks along cout; couts [0, c1) go to ``out1`` (plus the
+    ``residual``, the cell's skip term), [c1, cout) to ``out2`` ([B, cout - c1, 1, H, W] views,
+    e.g. two non-adjacent slots of a cell's cat buffer)."""
+    _require_cuda(x, packed, scale, shift, out1, out2, residual)
+    b, cin, d, h, w = x.shape
+    if d != 1:
+        raise ValueError("conv2d_bnrelu_pair takes [B, C, 1, H, W] views")
+    xbs = _check_volume_view(x, "x")
+    if tuple(out1.shape) != (b, c1, 1, h, w) or tuple(out2.shape) != (b, cout - c1, 1, h, w):
+        raise ValueError(f"conv2d_bnrelu_pair: outputs {tuple(out1.shape)} / {tuple(out2.shape)}")
+    y1bs, y2bs = _check_volume_view(out1, "out1"), _check_volume_view(out2, "out2")
+    rptr, rbs = None, 0
+    if residual is not None:
+        if tuple(residual.shape) != tuple(out1.shape):
+            raise ValueError(f"conv2d_bnrelu_pair: residual {tuple(residual.shape)}")
+        rbs = _check_volume_view(residual, "residual")
+        rptr = residual.data_ptr()
+    flags = (LEA_RELU if relu else 0) | (LEA_RESIDUAL if rptr is not None else 0)
+    rec = None if _probe is None else _probe_launch(
+        conv2d_kernel_name(b, cout, h, w, cin), 2.0 * b * h * w * cout * cin * 9,
+        4.0 * b * h * w * (cin + cout + (c1 if rptr is not None else 0)) + 36.0 * cout * cin)
+    check(_lib.load().lea_conv2d_bnrelu_pair(
+        x.data_ptr(), xbs, packed.data_ptr(),
+        scale.data_ptr() if scale is not None else None,
+        shift.data_ptr() if shift is not None else None,
+        rptr, rbs, out1.data_ptr(), y1bs, out2.data_ptr(), y2bs, b, cin, cout, c1, h, w, flags, _stream()),
+        "lea_conv2d_bnrelu_pair")
+    _probe_end(rec)
+
+
 def feature_stem(x: torch.Tensor, w0: torch.Tensor, scale0, shift0, w1: torch.Tensor, scale1, shift1,
                  c8: bool = False, x2: torch.Tensor | None = None) -> torch.Tensor:
     """new_model_2d.py:93-94 fused (ConvBR 3x3 s1 then ConvBR 3x3 s3, BN + ReLU each):

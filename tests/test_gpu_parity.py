@@ -470,6 +470,52 @@ def test_conv2d_stride3_vs_torch(b, cin, cout, hw):
     np.testing.assert_allclose(y.squeeze(2).cpu().double().numpy(), refy.numpy(), rtol=1e-5, atol=1e-5)
 
 
+@pytest.mark.parametrize("b,cin,c,hw,res", [
+    (2, 8, 8, (192, 320), True), (2, 16, 16, (96, 160), True), (1, 8, 8, (33, 70), False),
+    (3, 5, 16, (17, 9), True), (1, 12, 8, (1, 1), False)])
+def test_conv2d_pair_is_the_two_convs(b, cin, c, hw, res):
+    """lea_conv2d_bnrelu_pair (a feature cell's two ops on s0 in one launch, r04): both halves
+    equal their own lea_conv2d_bnrelu bit for bit -- the first with the residual (the skip
+    term), the second without -- into two non-adjacent channel slots of one cat buffer, the
+    slot between and the edges untouched."""
+    g = torch.Generator().manual_seed(cin * 7 + c + hw[1])
+    x = torch.randn((b, cin, 1) + hw, generator=g).to(DEV)
+    w = (torch.randn(2 * c, cin, 3, 3, generator=g) / np.sqrt(cin * 9)).to(DEV)
+    scale = (torch.rand(2 * c, generator=g) + 0.5).to(DEV)
+    shift = (torch.randn(2 * c, generator=g) * 0.1).to(DEV)
+    r = torch.randn((b, c, 1) + hw, generator=g).to(DEV) if res else None
+    buf = torch.full((b, 4 * c, 1) + hw, 7.0, device=DEV)
+    kernels.conv2d_bnrelu_pair(x, kernels.pack_conv2d_weight(w), c, 2 * c, scale, shift, True,
+                               buf[:, 0:c], buf[:, 2 * c:3 * c], r)
+    y0 = kernels.conv2d_bnrelu(x, kernels.pack_conv2d_weight(w[:c].contiguous()), c, scale[:c].contiguous(),
+                               shift[:c].contiguous(), relu=True, residual=r)
+    y1 = kernels.conv2d_bnrelu(x, kernels.pack_conv2d_weight(w[c:].contiguous()), c, scale[c:].contiguous(),
+                               shift[c:].contiguous(), relu=True)
+    assert torch.equal(buf[:, 0:c], y0) and torch.equal(buf[:, 2 * c:3 * c], y1)
+    assert torch.all(buf[:, c:2 * c] == 7.0) and torch.all(buf[:, 3 * c:] == 7.0)
+
+
+def test_feature_net_pair_launch_is_bit_identical():
+    """The feature executor with each cell's two s0 ops as one launch (the default) and as two
+    launches (FeatureExecutor.PAIR_S0 = False) give the same feature maps bit for bit."""
+    from leastereo_amd import executor
+    m = _model(48)
+    x = normal(78, (2, 3, 96, 192)).to(DEV)
+    outs = {}
+    old = executor.FeatureExecutor.PAIR_S0
+    try:
+        for pair in (True, False):
+            executor.FeatureExecutor.PAIR_S0 = pair
+            m.feature._executor = None
+            with torch.no_grad():
+                outs[pair] = m.feature(x)
+            assert bool(m.feature.executor().s0_pair) == pair
+    finally:
+        executor.FeatureExecutor.PAIR_S0 = old
+        m.feature._executor = None
+    assert torch.equal(outs[True], outs[False])
+
+
 def test_feature_net_golden():
     """HIP feature net vs the reference's own feature map (e2e fixture)."""
     m = _model(48)
