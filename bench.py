@@ -26,10 +26,11 @@ Extras in the JSON line:
                  VALU FLOP / peak, algorithmic bytes / 8 TB/s), for the algorithms
                  actually run, over the measured step time; plus the HBM-only fraction
   pair_epe_px    per pair of every rank's shard: |HIP - a second HIP path| (f32: the
-                 matching net on the direct-conv engine over the in-place cost volume and
-                 the LDS disparity kernel -- the feature net is the same code in both;
-                 bf16: the f32 path), all-gathered over ranks (the data path's one
-                 collective)
+                 matching net on the direct-conv engine over the in-place cost volume, the
+                 feature net's 3x3 convs on the DMA/MFMA engine with unfused stems, the
+                 gather resample and the LDS disparity kernel -- only the streamed 1x1
+                 kernel is common; bf16: the f32 path on those engines), all-gathered
+                 over ranks (the data path's one collective)
   epe_px         per rank: HIP vs the reference's own fp32 output (golden e2e case)
   cpu_baseline   the CPU oracle (oracle/torch_ref.py, the reference's aten op sequence
                  restated) on the host's physical cores, rank 0, N = 1: C2 (this
@@ -39,6 +40,7 @@ Extras in the JSON line:
 from __future__ import annotations
 
 import argparse
+import contextlib
 import json
 import os
 import platform
@@ -144,6 +146,33 @@ def launch(n: int, argv) -> int:
 
 
 # ------------------------------------------------------------------------ models
+@contextlib.contextmanager
+def independent_check_engines():
+    """The per-pair check's engines (bench.py's pair_epe_px): every switchable kernel the timed
+    path runs swapped for its alternative -- the feature net's few-channel 3x3 tile and pair
+    launch (lea_conv2d_set_small(0), FeatureExecutor.PAIR_S0), the fused stems (FUSED_STEM),
+    the separable resample (lea_resample_set_mode(2): the per-output gather) and the register
+    disparity kernel (the online-softmin LDS kernel).  The process-wide settings go back to
+    what the LEASTEREO_* environment (or the default) set afterwards."""
+    from leastereo_amd import _lib, executor
+    lib = _lib.load()
+    fe = executor.FeatureExecutor
+    saved = (fe.FUSED_STEM, fe.PAIR_S0)
+    env = lambda var, default: int(os.environ.get(var) or default)  # noqa: E731
+    switches = (("lea_disparity_set_register_form", 0, "LEASTEREO_DISP_REG", 1),
+                ("lea_conv2d_set_small", 0, "LEASTEREO_CONV2D_SMALL", 1),
+                ("lea_resample_set_mode", 2, "LEASTEREO_RESAMPLE_MODE", 0))
+    try:
+        for fn, value, _, _ in switches:
+            _lib.check(getattr(lib, fn)(value), fn)
+        fe.FUSED_STEM, fe.PAIR_S0 = False, False
+        yield
+    finally:
+        fe.FUSED_STEM, fe.PAIR_S0 = saved
+        for fn, _, var, default in switches:
+            _lib.check(getattr(lib, fn)(env(var, default)), fn)
+
+
 def build_model(maxdisp, device, precision="f32"):
     args = default_arch_args(LEAStereoArgs(maxdisp=maxdisp))
     model = LEAStereo(args, device, precision=precision)
@@ -498,25 +527,22 @@ def run(args, info):
     pair = None
     if args.pair_check:
         ref_prec = "f32_direct" if args.precision == "f32" else "f32"
-        from leastereo_amd import _lib
-        lib = _lib.load()
-        # the check's disparity regression runs on the online-softmin LDS kernel (the
-        # timed forward uses the register form for the configured depths)
-        _lib.check(lib.lea_disparity_set_register_form(0), "lea_disparity_set_register_form")
-        try:
+        with independent_check_engines():
             with torch.no_grad():
                 check = build_model(args.maxdisp, device, ref_prec)(left, right)
                 torch.cuda.synchronize()
-        finally:
-            _lib.check(lib.lea_disparity_set_register_form(1), "lea_disparity_set_register_form")
         e = (out.double() - check.double()).abs().mean(dim=(1, 2)).float()
         del check
         per_pair = [float(v) for v in parallel.gather_per_pair(e).cpu()]
-        pair = {"vs": ("HIP f32 with the matching net on the direct-conv engine over the in-place cost "
-                       "volume (no Winograd, no factored stem0) and the online-softmin LDS disparity "
-                       "kernel; the feature net's engine is shared with the timed path"
-                       if args.precision == "f32" else
-                       "HIP f32 path, same weights, online-softmin LDS disparity kernel"),
+        pair = {"vs": ("HIP f32 on engines the timed path does not run: the matching net on the "
+                       "direct-conv engine over the in-place cost volume (no Winograd, no factored "
+                       "stem0), the feature net's 3x3 convs on the DMA/MFMA engine (no few-channel "
+                       "tile, no pair launch) with unfused stems, the per-output gather resample and "
+                       "the online-softmin LDS disparity kernel; only the streamed 1x1 conv kernel "
+                       "is common to both" if args.precision == "f32" else
+                       "HIP f32 path, same weights, the feature net's 3x3 convs on the DMA/MFMA engine "
+                       "with unfused stems, the per-output gather resample, online-softmin LDS "
+                       "disparity kernel"),
                 "pairs": world * args.batch, "max": max(per_pair), "mean": sum(per_pair) / len(per_pair),
                 "per_pair": per_pair}
     epe = None

@@ -68,6 +68,13 @@ int lea_disparity_set_register_form(int on);
  * the L1.  Identical bits. */
 int lea_tapsum_set_rows(int on);
 
+/* Host query (no GPU): the exact largest number of source rows a row-staged kernel's
+ * workgroup reads when it owns R output rows plus `halo` rows either side, for a
+ * trilinear axis Hi -> Ho (align_corners ac): the LDS bound of resample3d_rows/sep_f32
+ * (halo 0) and tapsum_hwpass_rows_f32 (halo 1).  A kernel that ever met more rows than
+ * this would write NaN rather than read rows it never staged. */
+int lea_staged_rows(int Hi, int Ho, int ac, int R, int halo);
+
 /* Winograd entries: tile override (np in {1, 2} tile rows per wave, td in {1, 2}
  * planes, f in {0 = planner, 2, 4, 8 = F(4,3) on 32-wide row pairs}; np = 0 resets;
  * depth-paired shapes keep np = 1, td = 2 and F(4,3)). */

@@ -70,6 +70,7 @@ SIGNATURES = {
     "lea_resample_bf16_set_batch": (_i, [_i]),
     "lea_disparity_set_register_form": (_i, [_i]),
     "lea_tapsum_set_rows": (_i, [_i]),
+    "lea_staged_rows": (_i, [_i, _i, _i, _i, _i]),
     "lea_conv1x1_resampled_bf16": (_i, [_p, _i64, _i, _i, _i, _p, _p, _p, _p, _i64, _i, _i, _i, _i, _i,
                                         _i, _u, _p]),
     "lea_to_c8_bf16": (_i, [_p, _i64, _p, _i64, _i, _i, _i64, _p]),

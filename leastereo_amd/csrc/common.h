@@ -85,6 +85,24 @@ __host__ __device__ __forceinline__ Axis axis_index(float ratio, int o, int in, 
   return a;
 }
 
+// Row-staged kernels (resample3d_rows/sep_f32, tapsum_hwpass_rows_f32): a workgroup owns
+// output rows h0 .. h0 + R - 1 and stages the source rows that rows h0 - halo .. h0 + R - 1 +
+// halo (clamped to the output) read.  The exact largest count over the blocks, from the
+// kernels' own index expression on the host (the same IEEE float ops, contraction off), sizes
+// their LDS; a kernel that ever sees more rows than this writes NaN instead of reading rows it
+// never staged (lea_staged_rows exports it for the host sweep test).
+__host__ inline int staged_rows(int Hi, int Ho, int ac, int R, int halo) {
+  const float rh = axis_ratio(Hi, Ho, ac);
+  int n = 0;
+  for (int h0 = 0; h0 < Ho; h0 += R) {
+    const int lo = axis_index(rh, h0 - halo > 0 ? h0 - halo : 0, Hi, Ho, ac).i0;
+    const int e = h0 + R - 1 + halo;
+    const int hi = axis_index(rh, e < Ho - 1 ? e : Ho - 1, Hi, Ho, ac).i1;
+    n = hi - lo + 1 > n ? hi - lo + 1 : n;
+  }
+  return n;
+}
+
 // p{dz}{hy}: row pointers of source plane d_{dz}, row h_{hy}; nested-lerp order of
 // aten's upsample_trilinear3d: t0*(h0*(w0*a + w1*b) + h1*(...)) + t1*(...)
 __device__ __forceinline__ float trilerp(const Axis& ad, const Axis& ah, const Axis& aw,

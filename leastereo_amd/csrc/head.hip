@@ -191,7 +191,9 @@ __global__ __launch_bounds__(256) void tapsum_hwpass_rows_f32(
   const int h1 = min(h0 + R, Ho);
   const int r_lo = axis_index(rh, max(h0 - 1, 0), Hi, Ho, 1).i0;
   const int r_hi = axis_index(rh, min(h1, Ho - 1), Hi, Ho, 1).i1;
-  const int nr = min(r_hi - r_lo + 1, nrmax);  // == the host's count; the min keeps LDS in bounds
+  // nrmax = the host's exact bound (staged_rows); past it: NaN outputs, never unstaged rows
+  const bool over = r_hi - r_lo + 1 > nrmax;
+  const int nr = over ? 0 : r_hi - r_lo + 1;
   const long long HWi = (long long)Hi * Wi;
   const float* yp = ws + (long long)plane * 9 * HWi + (long long)r_lo * Wi;
   const int n1 = nr * Wi;
@@ -236,15 +238,15 @@ __global__ __launch_bounds__(256) void tapsum_hwpass_rows_f32(
       for (int kh = 0; kh < 3; ++kh) {
         if (!hok[kh]) continue;
         const float* tm = rows + (kh * 3 + kw) * nrmax * Wi;
-        const float* r0 = tm + (ah[kh].i0 - r_lo) * Wi;
-        const float* r1 = tm + (ah[kh].i1 - r_lo) * Wi;
+        const float* r0 = tm + (over ? 0 : ah[kh].i0 - r_lo) * Wi;
+        const float* r1 = tm + (over ? 0 : ah[kh].i1 - r_lo) * Wi;
         acc += ah[kh].l0 * (aw.l0 * r0[aw.i0] + aw.l1 * r0[aw.i1]) +
                ah[kh].l1 * (aw.l0 * r1[aw.i0] + aw.l1 * r1[aw.i1]);
       }
     }
     if (scale) acc = acc * sc + sh;
     if (flags & LEA_RELU) acc = fmaxf(acc, 0.f);
-    y[(long long)b * ybs + (((long long)co * Do + d) * Ho + h) * Wo + w] = acc;
+    y[(long long)b * ybs + (((long long)co * Do + d) * Ho + h) * Wo + w] = over ? __builtin_nanf("") : acc;
   }
 }
 
@@ -266,15 +268,8 @@ static int hwpass(const float* ws, void* y, int64_t y_bstride, int B, int cout, 
   const float rh = axis_ratio(Hi, Ho, 1), rw = axis_ratio(Wi, Wo, 1);
   if (g_tapsum_rows) {
     for (int R = 8; R >= 2; R /= 2) {
-      // rows h0-1 .. h0+R of every block, from the kernel's own index expression on the
-      // host (the same IEEE float ops, contraction off): the exact largest row count
-      int nrmax = 0;
-      for (int h0 = 0; h0 < Ho; h0 += R) {
-        const int h1 = h0 + R < Ho ? h0 + R : Ho;
-        const int lo = axis_index(rh, h0 > 0 ? h0 - 1 : 0, Hi, Ho, 1).i0;
-        const int hi = axis_index(rh, h1 < Ho - 1 ? h1 : Ho - 1, Hi, Ho, 1).i1;
-        nrmax = hi - lo + 1 > nrmax ? hi - lo + 1 : nrmax;
-      }
+      // rows h0-1 .. h0+R of every block: the exact largest row count (common.h)
+      const int nrmax = staged_rows(Hi, Ho, 1, R, 1);
       const size_t lds = (size_t)9 * nrmax * Wi * sizeof(float);
       if (lds > 65536) continue;
       dim3 g((unsigned)((Ho + R - 1) / R), (unsigned)(B * cout * Do));

@@ -90,7 +90,9 @@ __global__ __launch_bounds__(256) void resample3d_rows_f32(
   const Axis ad = axis_index(rd, od, Di, Do, ac);
   const int r_lo = axis_index(rh, oh0, Hi, Ho, ac).i0;
   const int r_hi = axis_index(rh, oh1 - 1, Hi, Ho, ac).i1;
-  const int nr = r_hi - r_lo + 1;  // <= nrmax (host bound)
+  // nrmax = the host's exact bound (staged_rows); past it: NaN outputs, never unstaged rows
+  const bool over = r_hi - r_lo + 1 > nrmax;
+  const int nr = over ? 0 : r_hi - r_lo + 1;
   const long long HWi = (long long)Hi * Wi;
   const float* xc = x + (long long)b * xbs + (long long)c * Di * HWi + (long long)r_lo * Wi;
   const float* src[2] = {xc + ad.i0 * HWi, xc + ad.i1 * HWi};
@@ -113,7 +115,7 @@ __global__ __launch_bounds__(256) void resample3d_rows_f32(
     const int oh = oh0 + t / wq;
     const int q = t % wq;
     const Axis ah = axis_index(rh, oh, Hi, Ho, ac);
-    const int r0 = (ah.i0 - r_lo) * Wi, r1 = (ah.i1 - r_lo) * Wi;
+    const int r0 = over ? 0 : (ah.i0 - r_lo) * Wi, r1 = over ? 0 : (ah.i1 - r_lo) * Wi;
     float v[VEC ? 4 : 1];
 #pragma unroll
     for (int e = 0; e < (VEC ? 4 : 1); ++e) {
@@ -121,7 +123,7 @@ __global__ __launch_bounds__(256) void resample3d_rows_f32(
       float r = trilerp(ad, ah, aw, l0 + r0, l0 + r1, l1 + r0, l1 + r1);
       if (scale) r = r * sc + sh;
       if (relu) r = fmaxf(r, 0.f);
-      v[e] = r;
+      v[e] = over ? __builtin_nanf("") : r;
     }
     if constexpr (VEC)
       *reinterpret_cast<float4*>(yp + (long long)oh * Wo + 4 * q) = make_float4(v[0], v[1], v[2], v[3]);
@@ -153,7 +155,9 @@ __global__ __launch_bounds__(256) void resample3d_sep_f32(
   const Axis ad = axis_index(rd, od, Di, Do, ac);
   const int r_lo = axis_index(rh, oh0, Hi, Ho, ac).i0;
   const int r_hi = axis_index(rh, oh1 - 1, Hi, Ho, ac).i1;
-  const int nr = min(r_hi - r_lo + 1, nrmax);  // (host bound: r_hi - r_lo < nrmax)
+  // nrmax = the host's exact bound (staged_rows); past it: NaN outputs, never unstaged rows
+  const bool over = r_hi - r_lo + 1 > nrmax;
+  const int nr = over ? 0 : r_hi - r_lo + 1;
   const long long HWi = (long long)Hi * Wi;
   const float* xc = x + (long long)b * xbs + (long long)c * Di * HWi + (long long)r_lo * Wi;
   const float* src0 = xc + ad.i0 * HWi;
@@ -179,7 +183,7 @@ __global__ __launch_bounds__(256) void resample3d_sep_f32(
     const int oh = oh0 + t / wq;
     const int q = t % wq;
     const Axis ah = axis_index(rh, oh, Hi, Ho, ac);
-    const int r0 = ah.i0 - r_lo, r1 = ah.i1 - r_lo;
+    const int r0 = over ? 0 : ah.i0 - r_lo, r1 = over ? 0 : ah.i1 - r_lo;
     const float4 a00 = w4[r0 * wq + q], a01 = w4[r1 * wq + q];
     const float4 a10 = w4[(nrmax + r0) * wq + q], a11 = w4[(nrmax + r1) * wq + q];
     const float p00[4] = {a00.x, a00.y, a00.z, a00.w}, p01[4] = {a01.x, a01.y, a01.z, a01.w};
@@ -190,7 +194,7 @@ __global__ __launch_bounds__(256) void resample3d_sep_f32(
       float r = ad.l0 * (ah.l0 * p00[e] + ah.l1 * p01[e]) + ad.l1 * (ah.l0 * p10[e] + ah.l1 * p11[e]);
       if (scale) r = r * sc + sh;
       if (relu) r = fmaxf(r, 0.f);
-      v[e] = r;
+      v[e] = over ? __builtin_nanf("") : r;
     }
     *reinterpret_cast<float4*>(yp + (long long)oh * Wo + 4 * q) = make_float4(v[0], v[1], v[2], v[3]);
   }
@@ -208,6 +212,13 @@ extern "C" int lea_resample_set_mode(int mode) {
   }
   lea::g_resample_mode = mode;
   return 0;
+}
+
+extern "C" int lea_staged_rows(int Hi, int Ho, int ac, int R, int halo) {
+  lea::clear_error();
+  LEA_CHECK_ARG(Hi > 0 && Ho > 0 && R > 0 && halo >= 0 && (ac == 0 || ac == 1),
+                "lea_staged_rows: Hi=%d Ho=%d ac=%d R=%d halo=%d", Hi, Ho, ac, R, halo);
+  return lea::staged_rows(Hi, Ho, ac, R, halo);
 }
 
 extern "C" int lea_resample3d_trilinear(const void* x, int64_t x_bstride, void* y, int64_t y_bstride,
@@ -239,7 +250,7 @@ extern "C" int lea_resample3d_trilinear(const void* x, int64_t x_bstride, void* 
   // Separable kernel (16-byte outputs) when R output rows' W-lerped source rows fit 64 KB
   if (vec && g_resample_mode == 0) {
     for (int R = 16; R >= 2; R /= 2) {
-      const int nrmax = (int)floorf((float)(R - 1) * rh) + 3;  // +1: fp rounding margin
+      const int nrmax = staged_rows(Hi, Ho, ac, R, 0);  // exact (common.h)
       const size_t lds = (size_t)2 * nrmax * Wo * sizeof(float);
       if (lds > 65536) continue;
       dim3 g((Ho + R - 1) / R, B * C * Do);
@@ -252,7 +263,7 @@ extern "C" int lea_resample3d_trilinear(const void* x, int64_t x_bstride, void* 
   // Row-staged kernel when R output rows' sources fit 64 KB of LDS: R = 16 rows
   // (20 KB of output per workgroup at Wo = 320), fewer for wide rows.
   for (int R = 16; R >= 2 && g_resample_mode != 2; R /= 2) {
-    const int nrmax = (int)floorf((float)(R - 1) * rh) + 3;  // +1: fp rounding margin
+    const int nrmax = staged_rows(Hi, Ho, ac, R, 0);  // exact (common.h)
     const size_t lds = (size_t)2 * nrmax * Wi * sizeof(float);
     if (lds > 65536) continue;
     dim3 g((Ho + R - 1) / R, B * C * Do);

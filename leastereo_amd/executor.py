@@ -147,6 +147,10 @@ class CellGraphExecutor:
                 (k0, op0), (k1, op1) = pair
                 m0, m1 = cell._ops[op0], cell._ops[op1]
                 other = [(o, j) for o, j in cell.plan[k1] if o != op1]
+                # the s1 sibling group writes its steps' slots without accumulating, after
+                # the pair: a step both of them write would lose the pair's term
+                if {k for k, _ in self.s1_group.get(i, [])} & {k0, k1}:
+                    continue
                 # op1 writes its step first (the other term a conv that accumulates after it)
                 if (m0.relu != m1.relu or m0.conv.weight.dim() != 4 or m0.conv.weight.shape[-1] != 3
                         or m0.stride != 1 or m1.stride != 1 or cell.plan[k1][0][0] != op1
@@ -316,7 +320,7 @@ class CellGraphExecutor:
                 self.conv(f"cells.{i}.s1_group_head", s1, out=self._channels(out, k0 * c, (k0 + 1) * c))
             else:
                 self.conv(f"cells.{i}.s1_group", s1, out=self._channels(out, k0 * c, (k0 + len(group)) * c))
-            written = {k for k, _ in group}
+            written |= {k for k, _ in group}
         for step, terms in enumerate(cell.plan):
             dst = slot.get(len(states))
             if dst is None:

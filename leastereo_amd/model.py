@@ -283,6 +283,10 @@ class GraphedForward:
     def __init__(self, model: LEAStereo, batch: int, height: int, width: int):
         if not torch.cuda.is_available():
             raise RuntimeError("HIP graphs need a ROCm device")
+        if model.training:
+            # a train-mode forward is the differentiable path (batch-statistics BN, running
+            # statistics updated per call, autograd buffers): capture inference only
+            raise RuntimeError("graphed() captures the eval-mode forward: call model.eval() first")
         model.check_shape(height, width)
         dev = next(model.parameters()).device
         self.model = model
