@@ -102,6 +102,9 @@ def parse(argv=None):
                    help="torch-ROCm GPU-eager leg of the reference op sequence at C1 (BASELINE.md §4), "
                         "comma list of MIOpen modes: default (immediate mode) and/or benchmark "
                         "(torch.backends.cudnn.benchmark: MIOpen find per shape); empty to skip")
+    p.add_argument("--gpu-eager-c2", type=int, default=0,
+                   help="1: the GPU-eager leg at the timed workload too (first pair, 1 warm-up + 1 timed "
+                        "forward per mode)")
     p.add_argument("--epe", type=int, default=1, help="check EPE vs the reference golden disparity")
     p.add_argument("--pair-check", type=int, default=1,
                    help="per-pair EPE of every rank's shard vs an independent HIP path, all-gathered")
@@ -330,7 +333,11 @@ def cpu_baseline(args, model, left0, right0, disp0, hip_step_s, device):
             res["configs"][cfg] = entry
         modes = [m for m in args.gpu_eager.split(",") if m]
         if modes:
-            res["torch_gpu_eager"] = gpu_eager_baseline(sd, a, device, modes, args.cpu_timed)
+            c2 = None
+            if args.gpu_eager_c2:
+                c2 = (left0, right0, args.maxdisp, hip_step_s / args.batch, disp0,
+                      f"{args.height}x{args.width} D={args.maxdisp}")
+            res["torch_gpu_eager"] = gpu_eager_baseline(sd, a, device, modes, args.cpu_timed, c2)
     head = res["configs"].get("c2") or next(iter(res["configs"].values()))
     res["value"] = head["cpu_pairs_s"]
     res["sample"] = (f"oracle/torch_ref.py on torch CPU ({cores['model']}, {cores['threads']} threads = "
@@ -339,25 +346,39 @@ def cpu_baseline(args, model, left0, right0, disp0, hip_step_s, device):
     return res
 
 
-def gpu_eager_baseline(sd, arch, device, modes, timed):
+def gpu_eager_baseline(sd, arch, device, modes, timed, c2=None):
     """BASELINE.md §4's torch-ROCm GPU-eager column: the reference's aten op sequence
     (oracle/torch_ref.py, as predict.py:227-229 runs the model) on this GPU through
     MIOpen, fp32 (no TF32), at C1 -- the SceneFlow sample pair, 288x576 D96 -- beside
-    the HIP path on the same pair.  C2 eager is skipped: MIOpen's 3D convolutions at
-    576x960 D192 take minutes per forward in the default mode."""
+    the HIP path on the same pair.  ``c2`` = (left, right, maxdisp, hip_s, hip_out, tag):
+    the same at the timed workload's first pair (``--gpu-eager-c2 1``), 1 warm-up + 1 timed
+    forward per mode -- MIOpen's 3D convolutions at 576x960 D192 take seconds per forward."""
     from oracle import torch_ref as ref
     from tests.golden_util import c1_inputs
     l, r = (t.to(device) for t in c1_inputs())
-    md = 96
     sd_dev = {k: v.to(device) for k, v in sd.items()}
-    hip_s, hip_out = _time_hip(build_model(md, device, "f32"), l, r)
-    out = {"workload": "SceneFlow sample pair 0001 (predict.py preprocessing), 288x576 D=96, B=1 fp32",
-           "hip_pairs_s": 1.0 / hip_s, "modes": {}}
+    hip_s, hip_out = _time_hip(build_model(96, device, "f32"), l, r)
+    out = _eager_modes(ref, sd_dev, arch, l, r, 96, hip_s, hip_out, modes, timed)
+    out["workload"] = "SceneFlow sample pair 0001 (predict.py preprocessing), 288x576 D=96, B=1 fp32"
+    if c2 is not None:
+        l2, r2, md2, hip2_s, hip2_out, tag = c2
+        out["c2"] = _eager_modes(ref, sd_dev, arch, l2, r2, md2, hip2_s, hip2_out, modes, 1, warm_default=1,
+                                 warm_benchmark=1)
+        out["c2"]["workload"] = tag + ", the timed workload's first pair, B=1 fp32"
+    del sd_dev
+    torch.cuda.empty_cache()
+    return out
+
+
+def _eager_modes(ref, sd_dev, arch, l, r, md, hip_s, hip_out, modes, timed, warm_default=1, warm_benchmark=3):
+    out = {"hip_pairs_s": 1.0 / hip_s, "modes": {}}
     prev = torch.backends.cudnn.benchmark
     try:
         for mode in modes:
             torch.backends.cudnn.benchmark = mode == "benchmark"
-            warm = 1 if mode == "default" else 3  # benchmark: MIOpen's find on the first call(s)
+            # benchmark: MIOpen's find on the first call(s)
+            warm = warm_default if mode == "default" else warm_benchmark
+            log(f"gpu-eager {tuple(l.shape)} D{md} mode={mode}: {warm} warm-up + {timed} timed")
             t0 = time.perf_counter()
             with torch.no_grad():
                 for _ in range(warm):
@@ -377,8 +398,6 @@ def gpu_eager_baseline(sd, arch, device, modes, timed):
             del want
     finally:
         torch.backends.cudnn.benchmark = prev
-    del sd_dev
-    torch.cuda.empty_cache()
     return out
 
 

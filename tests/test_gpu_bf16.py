@@ -152,8 +152,10 @@ def test_bf16_e2e_vs_reference_fixture():
 
 def _bf16_noise(cfg):
     """The reference network's own bf16 noise at this config (tests/golden/bf16_noise.json,
-    tools/gen_bf16_noise.py: the oracle with bf16 nets vs the oracle in f32, EPE px of each
-    of the 8 pairs the test runs, and pair 0's relative L2 distance per stage)."""
+    tools/gen_bf16_noise.py: /root/reference's LEAStereo imported and run with bf16 feature +
+    matching nets and an f32 Disp vs itself in f32, EPE px of each of the 8 pairs the test
+    runs, and pair 0's relative L2 distance per stage; the oracle restatement gives the same
+    figures bit for bit, bf16_noise_oracle.json / agreement_with_oracle)."""
     import json
     import os
     from tests.golden_util import GOLD
