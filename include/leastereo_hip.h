@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define LEA_ABI_VERSION 11
+#define LEA_ABI_VERSION 12
 
 #define LEA_F32 0
 #define LEA_BF16 1
@@ -43,6 +43,15 @@ extern "C" {
 #define LEA_RELU 1u     /* ReLU after the BN affine (operations_3d.py:45-46)          */
 #define LEA_RESIDUAL 2u /* y = act(...) + residual: the cell's `sum(new_states)`
                            (skip_model_3d.py:69); residual may alias y               */
+#define LEA_PAIR_SUM 4u /* two ConvBRs summed, a cell step of two conv terms
+                           (skip_model_3d.py:57-69): y = act(BN_a(conv_a(x))) +
+                           act(BN_b(conv_b(x2))) -- input channels [0, cin - cin2) are
+                           conv_a's, [cin - cin2, cin) conv_b's (the weights packed as one
+                           conv over the concatenation), scale/shift hold 2 * cout values
+                           (a's, then b's); exclusive with LEA_RESIDUAL.  Where an engine
+                           supports it (lea_conv3d_bnrelu_wino: cout <= 32, W % 4 == 0;
+                           lea_conv3d_bnrelu_bf16: the D-streaming 3x3x3 layers), else
+                           LEA_E_UNSUPPORTED                                           */
 
 int lea_abi_version(void);
 const char* lea_last_error(void);

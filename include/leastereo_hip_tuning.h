@@ -44,6 +44,13 @@ int lea_conv3d_bf16_set_stream1x1(int on);
  * (4 when up-sampling, else 1) (tools/resample_probe.py). */
 int lea_resample_bf16_set_batch(int k);
 
+/* c8 resample up-samplings: 1 (default) = the column-walking kernel (a wave walks R = 8 output
+ * rows of 64 columns, each source row W-lerped once into registers, the next row's words
+ * loaded one row ahead; "resample_c8_cols_kernel<8>"), 2 = the same with R = 16, 0 = the
+ * per-output gather ("resample_c8_kernel<K>", also what a nonzero lea_resample_bf16_set_batch
+ * selects).  Bit-identical. */
+int lea_resample_bf16_set_cols(int on);
+
 /* fp32 trilinear resample kernel: 0 (default) = the separable form where the output rows
  * are whole 16-byte words (W-lerped source rows in LDS), 1 = the row-staged form, 2 = the
  * per-output gather.  Bit-identical. */
@@ -74,6 +81,11 @@ int lea_tapsum_set_rows(int on);
  * (halo 0) and tapsum_hwpass_rows_f32 (halo 1).  A kernel that ever met more rows than
  * this would write NaN rather than read rows it never staged. */
 int lea_staged_rows(int Hi, int Ho, int ac, int R, int halo);
+
+/* 1 = the Winograd entries run 16-cout layers (the L1 cells' 16 -> 16 ops) on the F(2,3) along W
+ * x F(2,3) along D tile with the packer's U and four waves per SIMD ("conv3d_wino22_kernel",
+ * csrc/conv3d_wino22.hip); 0 = the F(4,3) x F(2,3) per-lane tile.  Same packed weights. */
+int lea_conv3d_wino_set_w22(int on);
 
 /* Winograd entries: tile override (np in {1, 2} tile rows per wave, td in {1, 2}
  * planes, f in {0 = planner, 2, 4, 8 = F(4,3) on 32-wide row pairs}; np = 0 resets;

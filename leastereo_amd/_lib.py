@@ -12,11 +12,12 @@ LIB_PATH = os.environ.get(
     "LEASTEREO_HIP_LIB",
     os.path.join(os.path.dirname(os.path.abspath(__file__)), "libleastereo_hip.so"))
 
-ABI_VERSION = 11
+ABI_VERSION = 12
 LEA_F32 = 0
 LEA_BF16 = 1
 LEA_RELU = 1
 LEA_RESIDUAL = 2
+LEA_PAIR_SUM = 4
 LEA_E_INVALID = 1001
 
 _p = ctypes.c_void_p
@@ -68,6 +69,8 @@ SIGNATURES = {
     "lea_resample3d_trilinear_bf16": (_i, [_p, _i64, _p, _i64, _i, _i, _i, _i, _i, _i, _i, _i,
                                            _i, _p, _p, _u, _p]),
     "lea_resample_bf16_set_batch": (_i, [_i]),
+    "lea_resample_bf16_set_cols": (_i, [_i]),
+    "lea_conv3d_wino_set_w22": (_i, [_i]),
     "lea_disparity_set_register_form": (_i, [_i]),
     "lea_tapsum_set_rows": (_i, [_i]),
     "lea_staged_rows": (_i, [_i, _i, _i, _i, _i]),
@@ -176,6 +179,8 @@ TUNING_ENV = {"LEASTEREO_WINO2_WALK": "lea_conv3d_wino2_set_walk",
               "LEASTEREO_RS_GATHER": "lea_conv3d_set_rs_gather",
               "LEASTEREO_BF16_1X1": "lea_conv3d_bf16_set_stream1x1",
               "LEASTEREO_RESAMPLE_K": "lea_resample_bf16_set_batch",
+              "LEASTEREO_RESAMPLE_COLS": "lea_resample_bf16_set_cols",
+              "LEASTEREO_W22": "lea_conv3d_wino_set_w22",
               "LEASTEREO_DISP_REG": "lea_disparity_set_register_form",
               "LEASTEREO_TAPSUM_ROWS": "lea_tapsum_set_rows"}
 

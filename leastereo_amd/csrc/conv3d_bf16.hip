@@ -384,6 +384,90 @@ __global__ __launch_bounds__(256) void resample_c8_kernel(
   }
 }
 
+// Up-sampling form (r05; the default when the output volume is the larger): a wave owns 64
+// consecutive output columns of R consecutive output rows of one output plane and walks
+// down the rows.  Each source row it needs is loaded once per wave (the two corner words
+// of each column in both source planes) and W-lerped into registers (aw.l0 * x[i0] +
+// aw.l1 * x[i1], trilerp's innermost terms); consecutive output rows of an up-sampling share
+// their source rows, so a row is lerped once for ~2 output rows.  Per output word: ~2
+// 16-byte loads instead of the gather kernel's 8, ~5 lerp ops per channel instead of 7, the
+// same expression tree (fp contraction off): bit-identical to resample_c8_kernel.
+template <int R>
+__global__ __launch_bounds__(256) void resample_c8_cols_kernel(
+    const __bf16* __restrict__ x, long long xbs, __bf16* __restrict__ y, long long ybs, int CB,
+    int Di, int Hi, int Wi, int Do, int Ho, int Wo, float rd, float rh, float rw, int ac,
+    const float* __restrict__ scale, const float* __restrict__ shift, unsigned flags, int ctiles) {
+#pragma clang fp contract(off)
+  const int plane = blockIdx.y;  // (b * CB + cb) * Do + od
+  const int od = plane % Do;
+  const int bcb = plane / Do;
+  const int b = bcb / CB, cb = bcb % CB;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+  const int ct = blockIdx.x % ctiles, rblk = blockIdx.x / ctiles;
+  const int oh0 = (rblk * 4 + wave) * R;
+  if (oh0 >= Ho) return;  // whole waves only
+  const int oh1 = min(oh0 + R, Ho);
+  const int ow = ct * 64 + lane;
+  const bool active = ow < Wo;
+  const Axis ad = axis_index(rd, od, Di, Do, ac);
+  const Axis aw = axis_index(rw, active ? ow : Wo - 1, Wi, Wo, ac);
+  const long long HWi = (long long)Hi * Wi;
+  const bf16x8* xc = reinterpret_cast<const bf16x8*>(x + (long long)b * xbs) + (long long)cb * Di * HWi;
+  bf16x8* yp = reinterpret_cast<bf16x8*>(y + (long long)b * ybs) + ((long long)cb * Do + od) * Ho * Wo;
+  const bf16x8* p0 = xc + ad.i0 * HWi;
+  const bf16x8* p1 = xc + ad.i1 * HWi;
+  const bool relu = flags & LEA_RELU;
+  float sc[8], sh[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    sc[j] = scale ? scale[cb * 8 + j] : 1.f;
+    sh[j] = scale ? shift[cb * 8 + j] : 0.f;
+  }
+  // walk the source rows r_lo .. r_hi the wave's output rows read, the next row's four corner
+  // words loaded one row ahead; after row r is W-lerped, every output row whose upper source
+  // row (ah.i1) is r is complete: its lower row is r - 1 (or r itself at the last row)
+  const long long rs = (long long)Wi;
+  auto load_row = [&](int r, bf16x8* q) {
+    const long long o = (long long)r * rs;
+    q[0] = p0[o + aw.i0];
+    q[1] = p0[o + aw.i1];
+    q[2] = p1[o + aw.i0];
+    q[3] = p1[o + aw.i1];
+  };
+  Axis ah = axis_index(rh, oh0, Hi, Ho, ac);
+  const int r_lo = ah.i0, r_hi = axis_index(rh, oh1 - 1, Hi, Ho, ac).i1;
+  bf16x8 nxt[4];
+  load_row(r_lo, nxt);
+  float lo[2][8], hi[2][8];  // W-lerped rows r - 1 and r, both source planes
+  int oh = oh0;
+  for (int r = r_lo; r <= r_hi; ++r) {  // wave-uniform
+    bf16x8 cur[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) cur[k] = nxt[k];
+    if (r < r_hi) load_row(r + 1, nxt);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      lo[0][j] = hi[0][j];
+      lo[1][j] = hi[1][j];
+      hi[0][j] = aw.l0 * (float)cur[0][j] + aw.l1 * (float)cur[1][j];
+      hi[1][j] = aw.l0 * (float)cur[2][j] + aw.l1 * (float)cur[3][j];
+    }
+    for (; oh < oh1 && ah.i1 == r; ah = axis_index(rh, ++oh, Hi, Ho, ac)) {
+      const bool same = ah.i0 == r;  // the last source row pairs with itself
+      bf16x8 o;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float a0 = same ? hi[0][j] : lo[0][j], a1 = same ? hi[1][j] : lo[1][j];
+        float v = ad.l0 * (ah.l0 * a0 + ah.l1 * hi[0][j]) + ad.l1 * (ah.l0 * a1 + ah.l1 * hi[1][j]);
+        if (scale) v = v * sc[j] + sh[j];
+        if (relu) v = fmaxf(v, 0.f);
+        o[j] = (__bf16)v;
+      }
+      if (active) yp[(long long)oh * Wo + ow] = o;
+    }
+  }
+}
+
 // ---- 1x1 conv of a trilinearly resampled c8 input (align_corners=True): the cell
 // preprocess after a level change (skip_model_3d.py:44-53) without materialising the
 // resampled tensor.  A gather-GEMM: lane (g, n) of a wave forms its own B fragment of
@@ -1126,6 +1210,16 @@ extern "C" int lea_from_c8_bf16(const void* x, int64_t x_bstride, float* y, int6
 // resample words per thread (lea_resample_bf16_set_batch; 0 = up-sampling 4, else 1)
 static int g_resample_k = 0;
 
+// 1 (default) = up-samplings on the column-walking kernel (lea_resample_bf16_set_cols)
+static int g_resample_cols = 1;
+
+extern "C" int lea_resample_bf16_set_cols(int on) {
+  clear_error();
+  LEA_CHECK_ARG(on >= 0 && on <= 2, "lea_resample_bf16_set_cols: %d", on);
+  g_resample_cols = on;
+  return 0;
+}
+
 extern "C" int lea_resample_bf16_set_batch(int k) {
   clear_error();
   LEA_CHECK_ARG(k == 0 || k == 1 || k == 2 || k == 4, "lea_resample_bf16_set_batch: k=%d", k);
@@ -1147,7 +1241,21 @@ extern "C" int lea_resample3d_trilinear_bf16(const void* x, int64_t x_bstride, v
                 "lea_resample3d_trilinear_bf16: bad shape");
   const int ac = align_corners ? 1 : 0;
   const long long cells = (long long)Ho * Wo;
-  const int k = g_resample_k > 0 ? g_resample_k : ((long long)Do * Ho * Wo > (long long)Di * Hi * Wi ? 4 : 1);
+  const bool up = (long long)Do * Ho * Wo > (long long)Di * Hi * Wi;
+  if (up && g_resample_cols && g_resample_k == 0) {
+    const int R = g_resample_cols == 2 ? 16 : 8;  // output rows per wave; 4 waves per workgroup
+    const int ctiles = (Wo + 63) / 64, rblocks = (Ho + 4 * R - 1) / (4 * R);
+    dim3 g((unsigned)(ctiles * rblocks), B * (C / 8) * Do);
+#define LEA_RS_COLS(R_)                                                                                        \
+  if (R == R_)                                                                                                \
+    bf::resample_c8_cols_kernel<R_><<<g, 256, 0, as_stream(stream)>>>(                                         \
+        (const __bf16*)x, x_bstride, (__bf16*)y, y_bstride, C / 8, Di, Hi, Wi, Do, Ho, Wo, axis_ratio(Di, Do, ac), \
+        axis_ratio(Hi, Ho, ac), axis_ratio(Wi, Wo, ac), ac, scale, shift, flags, ctiles);
+    LEA_RS_COLS(8) LEA_RS_COLS(16)
+#undef LEA_RS_COLS
+    return launch_status("lea_resample3d_trilinear_bf16");
+  }
+  const int k = g_resample_k > 0 ? g_resample_k : (up ? 4 : 1);
   dim3 grid((unsigned)((cells + 256LL * k - 1) / (256LL * k)), B * (C / 8) * Do);
 #define LEA_RS_K(K_)                                                                                \
   if (k == K_)                                                                                     \

@@ -677,10 +677,25 @@ int g_halo16 = 1;  // lea_conv3d_wino2_set_halo16
 int g_pipe = 1;    // lea_conv3d_wino2_set_pipeline
 int g_fence = 1;   // lea_conv3d_wino_set_fence: the depth-paired 16-byte-halo tile's fenced schedule (r04 default)
 int g_lane16 = 2;  // lea_conv3d_wino2_set_lane_halo16 (2: the fenced step schedule, PV = 5; r04 default)
+// lea_conv3d_wino_set_w22: layers on the F(2,3) x F(2,3) tile (conv3d_wino22.hip): 0 none (LEA_PAIR_SUM
+// always), 1 the 16-cout layers, 2 every cout <= 32
+int g_w22 = 0;
 inline int host_mt(int cout) {
   if (g_small16 && cout <= 8) return 1;
   const int mt = mt_of(cout);
   return (mt == 3 && !g_block48) ? 2 : mt;
+}
+// the staged g rows of every (cout block, chunk) + one 256-float tail (the kernels stage
+// whole 256-float pieces per chunk), in floats
+inline long long staged_floats(int cout, int cin) {
+  const int mt = host_mt(cout), cop = cop_of(mt), nstep = mt == 0 ? 12 : 9;
+  return (long long)((cout + cop - 1) / cop) * (cin / CIN_B) * nstep * 3 * CIN_B * cop + 256;
+}
+// couts <= 32 also carry the F(2,3) x F(2,3) tile's U, after the staged rows and (32-cout
+// blocks) the per-lane copy
+inline bool has_u22(int cout) { return cout <= 32; }
+inline long long u22_offset(int cout, int cin) {
+  return staged_floats(cout, cin) + (host_mt(cout) == 2 ? lane_weights_floats(cout, cin) : 0);
 }
 
 // W x D engine tile for variant v (2..4), or nullptr-equivalent (q = 0) when the
@@ -866,6 +881,20 @@ int common(ConvArgs& a, int B, bool cv, int dtype, void* stream) {
     return LEA_E_UNSUPPORTED;
   }
   Plan p = make_plan(B, a.cout, a.D, a.H, a.W);
+  const bool pair = a.flags & LEA_PAIR_SUM;
+  if (pair) {
+    LEA_CHECK_ARG(!(a.flags & LEA_RESIDUAL) && a.cin1 > 0 && a.cin1 < a.cin && !cv,
+                  "lea_conv3d(wino): LEA_PAIR_SUM needs two sources and no residual");
+    if (!wino22_ok(a)) {
+      set_error("lea_conv3d(wino): LEA_PAIR_SUM unsupported for cout=%d W=%d (or unaligned operands)", a.cout, a.W);
+      return LEA_E_UNSUPPORTED;
+    }
+  }
+  if (pair || (g_w22 && !cv && (p.mt == 1 || g_w22 == 2) && g_variant == 0 && g_override[0] == 0 &&
+               wino22_ok(a))) {
+    a.uoff = u22_offset(a.cout, a.cin);
+    return run22(a, B, g_spw, as_stream(stream));
+  }
   plan_halo16(p, cv, a.W, &a);
   if (g_epibuf && epi_buf_ok(a)) a.flags |= kEpiBuf;
   return run(p, a, B, as_stream(stream), cv);
@@ -878,11 +907,9 @@ using namespace lea;
 
 extern "C" size_t lea_conv3d_wino_packed_floats(int cout, int cin) {
   if (cout <= 0 || cin <= 0 || cin % wino::CIN_B != 0) return 0;
-  const int mt = wino::host_mt(cout), cop = wino::cop_of(mt), nstep = mt == 0 ? 12 : 9;
-  // + one 256-float tail: the kernel stages whole 256-float pieces per chunk; 32-cout
-  // blocks append the per-lane copy (16-byte slices) the one-barrier W x D tile loads (PV = 3)
-  return (size_t)((cout + cop - 1) / cop) * (cin / wino::CIN_B) * nstep * 3 * wino::CIN_B * cop + 256 +
-         (mt == 2 ? (size_t)wino::lane_weights_floats(cout, cin) : 0);
+  // 32-cout blocks append the per-lane copy (16-byte slices) the one-barrier W x D tile loads
+  // (PV = 3), couts <= 32 the F(2,3) x F(2,3) tile's U (conv3d_wino22.hip)
+  return (size_t)wino::u22_offset(cout, cin) + (wino::has_u22(cout) ? (size_t)wino::u22_section(cout, cin) : 0);
 }
 
 extern "C" int lea_conv3d_wino_pack_weights(const float* w, float* packed, int cout, int cin,
@@ -894,16 +921,22 @@ extern "C" int lea_conv3d_wino_pack_weights(const float* w, float* packed, int c
   const long long total = (long long)lea_conv3d_wino_packed_floats(cout, cin);
   const int grid = (int)std::min<long long>((total + 255) / 256, 4096);
   hipStream_t st = as_stream(stream);
+  const long long staged = wino::staged_floats(cout, cin), uoff = wino::u22_offset(cout, cin);
   switch (wino::host_mt(cout)) {
-    case 0: wino::pack_wino_dp_kernel<<<grid, 256, 0, st>>>(w, packed, cout, cin, cin / wino::CIN_B, total); break;
-    case 1: wino::pack_wino_kernel<1><<<grid, 256, 0, st>>>(w, packed, cout, cin, cin / wino::CIN_B, total); break;
-    case 3: wino::pack_wino_kernel<3><<<grid, 256, 0, st>>>(w, packed, cout, cin, cin / wino::CIN_B, total); break;
+    case 0: wino::pack_wino_dp_kernel<<<grid, 256, 0, st>>>(w, packed, cout, cin, cin / wino::CIN_B, staged); break;
+    case 1: wino::pack_wino_kernel<1><<<grid, 256, 0, st>>>(w, packed, cout, cin, cin / wino::CIN_B, staged); break;
+    case 3: wino::pack_wino_kernel<3><<<grid, 256, 0, st>>>(w, packed, cout, cin, cin / wino::CIN_B, staged); break;
     default: {
-      const long long lane = wino::lane_weights_floats(cout, cin), staged = total - lane;
+      const long long lane = uoff - staged;
       wino::pack_wino_kernel<2><<<grid, 256, 0, st>>>(w, packed, cout, cin, cin / wino::CIN_B, staged);
       const int g2 = (int)std::min<long long>((lane + 255) / 256, 4096);
       wino::pack_wino_lane_kernel<<<g2, 256, 0, st>>>(w, packed + staged, cout, cin, cin / wino::CIN_B, lane);
     }
+  }
+  if (wino::has_u22(cout)) {  // the F(2,3) x F(2,3) tile's U
+    const long long u = total - uoff;
+    const int g2 = (int)std::min<long long>((u + 255) / 256, 4096);
+    wino::pack_wino22_kernel<<<g2, 256, 0, st>>>(w, packed + uoff, cout, cin, u);
   }
   return launch_status("lea_conv3d_wino_pack_weights");
 }
@@ -912,6 +945,9 @@ extern "C" const char* lea_conv3d_wino_kernel_name(int B, int cin, int cout, int
                                                    int costvolume) {
   if (B <= 0 || cout <= 0 || D <= 0 || H <= 0 || W <= 0) return nullptr;
   wino::Plan p = wino::make_plan(B, cout, D, H, W);
+  if (wino::g_w22 && !costvolume && (p.mt == 1 || (wino::g_w22 == 2 && cout <= 32)) && wino::g_variant == 0 &&
+      wino::g_override[0] == 0 && W % 4 == 0)
+    return "conv3d_wino22_kernel";  // (assumes 16-byte aligned sources)
   wino::plan_halo16(p, costvolume != 0, W, nullptr, cin);  // (assumes 16-byte aligned sources)
   return wino::name(p, costvolume != 0);
 }
@@ -983,6 +1019,13 @@ extern "C" int lea_conv3d_wino2_set_walk(int spw) {
   clear_error();
   LEA_CHECK_ARG(spw >= 0 && spw <= 64, "lea_conv3d_wino2_set_walk: spw=%d", spw);
   wino::g_spw = spw;
+  return 0;
+}
+
+extern "C" int lea_conv3d_wino_set_w22(int on) {
+  clear_error();
+  LEA_CHECK_ARG(on >= 0 && on <= 2, "lea_conv3d_wino_set_w22: on=%d", on);
+  wino::g_w22 = on;
   return 0;
 }
 

@@ -78,8 +78,11 @@ __device__ __forceinline__ int a_col(int m, int ci, int n, bool swz) { return ((
 // wait for its DMA with vmcnt(stores) -- loads, stores and LDS-DMA retire in issue
 // order (MI355X_MICROARCH.md, s_waitcnt) -- instead of for the stores as well.
 constexpr unsigned kEpiBuf = 1u << 16;  // internal ConvArgs::flags bit
+constexpr unsigned kPairSum = LEA_PAIR_SUM;
 constexpr unsigned kEpiOob = 0xFFFFFF00u;
 typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
+typedef unsigned u32x2_t __attribute__((ext_vector_type(2)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t block_rsrc(const float* base, long long bytes) {
   return __builtin_amdgcn_make_buffer_rsrc((void*)base, 0, (int)(unsigned)bytes, 0x00020000);
 }
@@ -143,6 +146,14 @@ long long lane_weights_floats(int cout, int cin);
 __global__ void pack_wino_lane_kernel(const float* __restrict__ w, float* __restrict__ out, int cout, int cin,
                                       int nchunks, long long total);
 const char* name2(const Plan2& p, bool cv);
+
+// F(2,3) x F(2,3) tile for the 16-cout layers (conv3d_wino22.hip): the U section the packer
+// appends for 16-cout blocks (floats), the host's shape / alignment check and the launch
+long long u22_section(int cout, int cin);
+bool wino22_ok(const ConvArgs& a);
+int run22(ConvArgs a, int B, int spw, hipStream_t st);
+__global__ void pack_wino22_kernel(const float* __restrict__ w, float* __restrict__ out, int cout, int cin,
+                                   long long total);
 
 }  // namespace wino
 }  // namespace lea

@@ -96,6 +96,12 @@ class CellGraphExecutor:
     # its residual, op4 -> step 2 before op5 accumulates) as one launch writing two slots
     # (lea_conv2d_bnrelu_pair; r04).  The f32 feature executor only; LEASTEREO_PAIR_S0=0: two launches
     PAIR_S0 = False
+    # a 3D cell whose every step sums two conv ops (the shipped matching genotype): each step
+    # as ONE LEA_PAIR_SUM launch, y = relu(BN_a(conv_a(s_ja))) + relu(BN_b(conv_b(s_jb))),
+    # reading the two states and writing the step's slot once (r05) -- instead of the s1
+    # sibling group plus an accumulating launch per remaining op (a read-modify-write of the
+    # slot each).  Executors whose engine takes LEA_PAIR_SUM set it
+    PAIR_STEPS = False
 
     def __init__(self, net):
         from .model import ConvBR
@@ -162,6 +168,22 @@ class CellGraphExecutor:
                     m0, w, (torch.cat([f[0] for f in folded]).contiguous(),
                             torch.cat([f[1] for f in folded]).contiguous()))
                 self.s0_pair[i] = pair
+            self.pair_steps = {}
+            for i, cell in enumerate(net.cells) if self.PAIR_STEPS else ():
+                terms = [[(op, j) for op, j in t] for t in cell.plan]
+                if (getattr(cell, "dims", 3) != 3 or not terms
+                        or any(len(t) != 2 or any(cell.op_kinds[op] != "conv" for op, _ in t) for t in terms)):
+                    continue
+                mods = [[cell._ops[op] for op, _ in t] for t in terms]
+                if any(m.conv.weight.shape[-1] != 3 or not m.relu for ms in mods for m in ms):
+                    continue
+                for k, (ma, mb) in enumerate(mods):
+                    folded = [ma.folded_bn(), mb.folded_bn()]
+                    self.p[f"cells.{i}.pair{k}"] = self._pair_params(
+                        ma, torch.cat([ma.conv.weight, mb.conv.weight], 1),
+                        (torch.cat([f[0] for f in folded]).contiguous(),
+                         torch.cat([f[1] for f in folded]).contiguous()))
+                self.pair_steps[i] = terms
             # a cell that resamples s1, followed by a same-level cell: the next cell's s0
             # is this s1 (Cell.forward returns prev_input, skip_model_3d.py:75) at the same
             # size, so both 1x1 convs run as one stacked conv over one read of it (down:
@@ -214,6 +236,21 @@ class CellGraphExecutor:
         return kernels.conv3d_bnrelu(x, p.packed, p.cout, p.k, p.scale, p.shift, p.relu, out,
                                      accumulate, x2, residual)
 
+    def _pair_params(self, mod, w, folded):
+        """ConvParams of a LEA_PAIR_SUM step: [W_a | W_b] along cin, BN (a's, then b's)."""
+        p = _conv_params(mod, w, folded)
+        p.cout = w.shape[0]
+        return p
+
+    def _pair_ok(self, x, x2, out):
+        """The f32 pair launch's shape / alignment rule (lea_conv3d_bnrelu_wino, LEA_PAIR_SUM:
+        the F(2,3) x F(2,3) tile, conv3d_wino22.hip)."""
+        return kernels.pair_sum_supported(x, x2, out)
+
+    def pair_conv(self, name, x, x2, out):
+        p = self.p[name]
+        return kernels.conv3d_bnrelu_wino(x, p.wino, p.cout, p.scale, p.shift, True, out, x2=x2, pair_sum=True)
+
     def _use_winograd(self):
         """Pack the eligible 3x3x3 layers for the Winograd engine (f32 executors)."""
         if not WINOGRAD:
@@ -222,7 +259,11 @@ class CellGraphExecutor:
             for name, p in self.p.items():
                 if p.kind != "3d" or not kernels.wino_eligible(p.cout, p.cin, p.k):
                     continue
-                if name.endswith("s1_group") or name.endswith("s1_group_head"):
+                if ".pair" in name:
+                    i, k = int(name.split(".")[1]), int(name.rsplit("pair", 1)[1])
+                    cell = self.m.cells[i]
+                    w = torch.cat([cell._ops[op].conv.weight for op, _ in self.pair_steps[i][k]], 1)
+                elif name.endswith("s1_group") or name.endswith("s1_group_head"):
                     i = int(name.split(".")[1])
                     mods = [self.m.cells[i]._ops[op] for _, op in self.s1_group[i]]
                     if i in self.s1_split:
@@ -299,6 +340,17 @@ class CellGraphExecutor:
         else:
             s1 = self.conv(f"cells.{i}.preprocess", s1, out=slot.get(1), size=size)
         states = [s0, s1]
+        pairs = self.pair_steps.get(i)
+        if pairs is not None:
+            dsts = [slot.get(2 + k) for k in range(len(pairs))]
+            if all(d is not None for d in dsts) and all(
+                    self._pair_ok(states[t[0][1]] if t[0][1] < 2 else dsts[t[0][1] - 2],
+                                  states[t[1][1]] if t[1][1] < 2 else dsts[t[1][1] - 2], dsts[k])
+                    for k, t in enumerate(pairs)):
+                for k, ((_, ja), (_, jb)) in enumerate(pairs):
+                    self.pair_conv(f"cells.{i}.pair{k}", states[ja], states[jb], dsts[k])
+                    states.append(dsts[k])
+                return prev_input, out
         written = set()
         done = set(group)
         consumed = set()  # steps whose skip term went in as an epilogue residual already
@@ -349,6 +401,9 @@ class CellGraphExecutor:
 
 class MatchingExecutor(CellGraphExecutor):
     SPLIT_S1_GROUP48 = os.environ.get("LEASTEREO_SPLIT_GROUP48", "1") != "0"
+    # the matching cells' steps as LEA_PAIR_SUM launches (LEASTEREO_PAIR_STEPS=0: the s1 group
+    # + accumulating launches); the f32 pair runs on the Winograd F(2,3) x F(2,3) tile
+    PAIR_STEPS = WINOGRAD and os.environ.get("LEASTEREO_PAIR_STEPS", "1") != "0"
 
     def run(self, x):
         """newMatching.forward (skip_model_3d.py:140-174): [B,64,D3,H3,W3] -> [B,1,D3,H3,W3]."""
@@ -461,6 +516,7 @@ class MatchingExecutorDirect(MatchingExecutor):
     per-pair cross-check of every rank's shard (precision "f32_direct")."""
 
     SPLIT_S1_GROUP48 = False
+    PAIR_STEPS = False
 
     def __init__(self, matching):
         super().__init__(matching)
@@ -605,6 +661,7 @@ class MatchingExecutorBF16(_C8Layout, MatchingExecutor):
     is f32 for the disparity regression.  Same graph as MatchingExecutor."""
 
     SPLIT_S1_GROUP48 = False
+    PAIR_STEPS = False
 
     def __init__(self, matching):
         from .model import ConvBR

@@ -12,7 +12,7 @@ import os
 import torch
 
 from . import _lib
-from ._lib import LEA_F32, LEA_RELU, LEA_RESIDUAL, check
+from ._lib import LEA_F32, LEA_PAIR_SUM, LEA_RELU, LEA_RESIDUAL, check
 
 
 def _stream():
@@ -935,7 +935,10 @@ def wino_mfma_scale(cout: int, name: str) -> float:
     """MFMA products issued per direct-convolution product: (F + 2) per 3F for the
     kernel's F (first template argument of ``name``), times the padding of cout to
     the engine's 16/32/48-row block.  The W x D engine (conv3d_wino2_kernel<Q, WC, MTE,
-    ...>) issues 24 products per 72: 1/3, with couts padded to 16 WC MTE."""
+    ...>) issues 24 products per 72: 1/3, with couts padded to 16 WC MTE; the F(2,3) x F(2,3)
+    tile (conv3d_wino22_kernel) 16 per 36: 4/9, couts padded to 16."""
+    if name.startswith("conv3d_wino22_kernel"):  # F(2,3) x F(2,3): 16 per (2 x 2 outputs x 9 taps)
+        return (-(-cout // 16) * 16) / cout * 4.0 / 9.0
     if name.startswith("conv3d_wino2p_kernel"):  # the one-barrier W x D tile: 32-cout blocks
         return (-(-cout // 32) * 32) / cout / 3.0
     if name.startswith("conv3d_wino2_kernel<"):
@@ -971,14 +974,30 @@ def pack_conv_weight_wino(w: torch.Tensor) -> torch.Tensor:
     return packed
 
 
+def pair_sum_supported(x: torch.Tensor, x2: torch.Tensor, out: torch.Tensor) -> bool:
+    """Whether conv3d_bnrelu_wino(..., pair_sum=True) takes these operands: the F(2,3) x F(2,3)
+    tile's rule (csrc/conv3d_wino22.hip wino22_ok) -- cout <= 32, W % 4 == 0, 16-byte aligned
+    sources with batch strides of whole 16-byte words, 8-byte aligned output."""
+    b, c, d, h, w = x.shape
+    ok = out.shape[1] <= 32 and w % 4 == 0 and x2.shape[2:] == x.shape[2:] and x.shape[1] % 4 == 0
+    for t, al in ((x, 16), (x2, 16), (out, 8)):
+        ok = ok and t.data_ptr() % al == 0 and t.stride(0) % (al // 4) == 0 and \
+            t.stride()[1:] == (d * h * w, h * w, w, 1)
+    return bool(ok and 16 * d * h * w * 4 < 0xFFFFFF00)
+
+
 def conv3d_bnrelu_wino(x: torch.Tensor, packed: torch.Tensor, cout: int,
                        scale: torch.Tensor | None, shift: torch.Tensor | None, relu: bool = True,
                        out: torch.Tensor | None = None, accumulate: bool = False,
                        x2: torch.Tensor | None = None,
-                       residual: torch.Tensor | None = None) -> torch.Tensor:
+                       residual: torch.Tensor | None = None, pair_sum: bool = False) -> torch.Tensor:
     """``conv3d_bnrelu`` (k = 3) on the Winograd engine: same semantics, weights
-    packed by ``pack_conv_weight_wino``."""
+    packed by ``pack_conv_weight_wino``.  ``pair_sum`` (LEA_PAIR_SUM): x's and x2's channels
+    feed two separate ConvBRs (the packed weight is [W_a | W_b] along cin, scale / shift
+    2 * cout values) whose activations are summed -- a matching-cell step."""
     _require_cuda(x, x2, packed, scale, shift, out)
+    if pair_sum and (x2 is None or accumulate or residual is not None):
+        raise ValueError("pair_sum takes two sources and no residual")
     b, cin, d, h, w = x.shape
     xbs = _check_volume_view(x, "x")
     cin2, x2bs = 0, 0
@@ -989,10 +1008,10 @@ def conv3d_bnrelu_wino(x: torch.Tensor, packed: torch.Tensor, cout: int,
         x2bs = _check_volume_view(x2, "x2")
     out, ybs = _conv_out(x.shape, cout, (d, h, w), out, accumulate, x.device, x.dtype)
     rptr, rbs = _residual(out, accumulate, residual, ybs)
-    flags = (LEA_RELU if relu else 0) | (LEA_RESIDUAL if rptr is not None else 0)
+    flags = (LEA_RELU if relu else 0) | (LEA_RESIDUAL if rptr is not None else 0) | (LEA_PAIR_SUM if pair_sum else 0)
     rec = None
     if _probe is not None:  # (the kernel-name query only when a probe listens)
-        name = wino_kernel_name(b, cout, d, h, w, cin=cin + cin2)
+        name = "conv3d_wino22_kernel" if pair_sum else wino_kernel_name(b, cout, d, h, w, cin=cin + cin2)
         rec = _probe_begin(b, cin + cin2, cout, d, h, w, 3, rptr is not None, b * d * h * w, False,
                            name=name, mfma_scale=wino_mfma_scale(cout, name))
     check(_lib.load().lea_conv3d_bnrelu_wino(

@@ -89,6 +89,30 @@ class FakeKernels:
         x = F.interpolate(x, size=tuple(size), mode="trilinear", align_corners=True)
         return self.conv3d_bnrelu(x, packed, cout, k, scale, shift, relu, out, accumulate)
 
+    @staticmethod
+    def pack_conv_weight_wino(w):
+        return w.detach().clone()
+
+    def conv3d_bnrelu_wino(self, x, packed, cout, scale, shift, relu=True, out=None, accumulate=False,
+                           x2=None, residual=None, pair_sum=False):
+        self.log.append(("wino", out.data_ptr() if out is not None else None, accumulate, pair_sum))
+        if not pair_sum:
+            return self.conv3d_bnrelu(x, packed, cout, 3, scale, shift, relu, out, accumulate, x2, residual)
+        ca = x.shape[1]
+        ya = _act(F.conv3d(x, packed[:, :ca].to(x.dtype), padding=1), scale[:cout], shift[:cout], relu)
+        yb = _act(F.conv3d(x2, packed[:, ca:].to(x.dtype), padding=1), scale[cout:], shift[cout:], relu)
+        return _emit(ya + yb, out, False, None)
+
+    def tapsum_upsample(self, q, cout, size, scale=None, shift=None, relu=False):
+        """sum over the 27 taps of the up-sampled per-tap partial sums, shifted by the tap
+        (channel co * 27 + tap): conv3x3x3(upsample(y)) by linearity."""
+        d, h, w = (int(v) for v in size)
+        up = F.pad(F.interpolate(q, size=(d, h, w), mode="trilinear", align_corners=True), (1, 1, 1, 1, 1, 1))
+        y = sum(up[:, co * 27 + (kd * 3 + kh) * 3 + kw::27 * cout][:, :1, kd:kd + d, kh:kh + h, kw:kw + w]
+                for co in range(cout) for kd in range(3) for kh in range(3) for kw in range(3)) \
+            if cout == 1 else None
+        return _act(y, scale, shift, relu)
+
     def resample_trilinear(self, x, size, align_corners=True, out=None, scale=None, shift=None,
                            relu=False):
         y = _act(F.interpolate(x, size=tuple(size), mode="trilinear", align_corners=align_corners),
@@ -100,7 +124,8 @@ class FakeKernels:
 def fake(monkeypatch):
     fk = FakeKernels()
     for name in ("pack_conv2d_weight", "pack_conv_weight", "conv2d_bnrelu", "conv2d_bnrelu_pair",
-                 "conv2d_s3_bnrelu", "conv3d_bnrelu", "conv3d_bnrelu_resampled", "resample_trilinear"):
+                 "conv2d_s3_bnrelu", "conv3d_bnrelu", "conv3d_bnrelu_resampled", "resample_trilinear",
+                 "pack_conv_weight_wino", "conv3d_bnrelu_wino", "tapsum_upsample"):
         monkeypatch.setattr(kernels, name, getattr(fk, name))
     # the stems as two convs (the fused stem kernel has no stand-in here)
     monkeypatch.setattr(ex.FeatureExecutor, "FUSED_STEM", False)
@@ -149,4 +174,45 @@ def test_feature_executor_plan_matches_oracle(tmp_path, fake, monkeypatch, geno,
     err = float((got - want).abs().max())
     # folded BN is f32 by design (model.ConvBR.folded_bn): ~1e-7 relative per layer; a plan
     # error (a dropped or doubled term) is O(1)
+    assert err <= 1e-5 * float(want.abs().max()), err
+
+
+# The matching net's cells (skip_model_3d.py:41-75): the shipped genotype (every step two conv
+# terms: LEA_PAIR_SUM launches when PAIR_STEPS) and one with a skip term (that cell keeps the
+# s1 group + accumulating launches)
+MATCHING_GENOTYPES = {"shipped": None, "with_skip": [[1, 1], [0, 1], [3, 1], [4, 0], [8, 1], [6, 1]]}
+
+
+@pytest.mark.parametrize("pair_steps", [True, False])
+@pytest.mark.parametrize("split48", [True, False])
+@pytest.mark.parametrize("geno", sorted(MATCHING_GENOTYPES))
+def test_matching_executor_plan_matches_oracle(tmp_path, fake, monkeypatch, geno, split48, pair_steps):
+    monkeypatch.setattr(ex.MatchingExecutor, "PAIR_STEPS", pair_steps)
+    monkeypatch.setattr(ex.MatchingExecutor, "SPLIT_S1_GROUP48", split48)
+    monkeypatch.setattr(ex, "CV_STEM", False)
+    args = LEAStereoArgs(maxdisp=48)
+    a = arch()
+    if MATCHING_GENOTYPES[geno] is not None:
+        a["cell_arch_mat"] = np.array(MATCHING_GENOTYPES[geno])
+        args.cell_arch_mat = str(tmp_path / "mat_geno.npy")
+        np.save(args.cell_arch_mat, a["cell_arch_mat"])
+    args = default_arch_args(args)
+    m = LEAStereo(args, "cpu")
+    sd = synthetic_state_dict({k: tuple(v.shape) for k, v in m.state_dict().items()}, bn_file=None)
+    m.load_state_dict(sd, strict=True)
+    m = m.double().eval()
+    me = ex.MatchingExecutor(m.matching)
+    if pair_steps and geno == "shipped":
+        assert len(me.pair_steps) == len(m.matching.cells), "every shipped cell runs as pair launches"
+    if geno == "with_skip":
+        assert 0 not in me.pair_steps  # every cell has the skip term at step 1
+    x = normal(903, (1, 64, 16, 32, 64)).double()  # the e2e case's cost volume shape (96x192 D48)
+    with torch.no_grad():
+        got = me.run(x)
+        sd64 = {k: (v.double() if v.is_floating_point() else v) for k, v in sd.items()}
+        want = ref.matching_forward(sd64, x, a["net_arch_mat"], a["cell_arch_mat"])
+    pairs = [e for e in fake.log if e[0] == "wino" and e[3]]
+    assert bool(pairs) == (pair_steps and geno == "shipped")
+    assert got.shape == want.shape
+    err = float((got - want).abs().max())
     assert err <= 1e-5 * float(want.abs().max()), err

@@ -119,6 +119,34 @@ def test_resample_bf16_is_the_f32_kernel_rounded(src, dst, ac):
     assert torch.equal(got, want.to(torch.bfloat16).float())
 
 
+@pytest.mark.parametrize("b,c,src,dst,ac", [(2, 24, (5, 7, 9), (9, 13, 17), True),
+                                            (1, 8, (32, 96, 160), (64, 192, 320), True),
+                                            (2, 16, (16, 48, 80), (32, 96, 160), True),
+                                            (1, 16, (8, 12, 20), (16, 24, 70), False),
+                                            (1, 8, (3, 40, 33), (5, 79, 130), True)])
+def test_resample_bf16_cols_kernel_is_the_gather_kernel(b, c, src, dst, ac):
+    """The up-sampling column walker (resample_c8_cols_kernel: source rows W-lerped once per
+    wave into registers) gives the per-output gather kernel's bits, into a channel slice too
+    (odd sizes, a partial last column tile, the last source row pairing with itself)."""
+    from leastereo_amd import _lib
+    lib = _lib.load()
+    g = torch.Generator().manual_seed(b * 100 + c)
+    x = kernels.to_c8(torch.randn((b, c) + src, generator=g).to(DEV))
+    scale = (torch.rand(c, generator=g) + 0.5).to(DEV)
+    shift = (torch.randn(c, generator=g) * 0.1).to(DEV)
+    outs = []
+    try:
+        for cols in (0, 1, 2):  # gather, column walker R = 8, R = 16
+            assert lib.lea_resample_bf16_set_cols(cols) == 0
+            big = torch.full((b, c // 8 + 2) + tuple(dst) + (8,), 7.0, device=DEV, dtype=torch.bfloat16)
+            kernels.resample_trilinear_bf16(x, dst, ac, big[:, 1:1 + c // 8], scale, shift, relu=True)
+            outs.append(big)
+    finally:
+        lib.lea_resample_bf16_set_cols(1)
+    assert torch.equal(outs[0], outs[1]) and torch.equal(outs[0], outs[2])
+    assert bool((outs[1][:, 0] == 7.0).all()) and bool((outs[1][:, -1] == 7.0).all())
+
+
 def test_tapsum_bf16_matches_f32_on_same_values():
     g = torch.Generator().manual_seed(9)
     q = _bf(torch.randn(1, 32, 8, 12, 20, generator=g)).to(DEV)  # 27 taps + 5 pad channels

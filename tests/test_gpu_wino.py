@@ -480,3 +480,61 @@ def test_lane_halo16_is_bit_identical_to_dword_pieces(b, cin, c1, cout, shape, m
             lib.lea_conv3d_wino2_set_lane_halo16(2)
     assert torch.equal(outs[1], outs[0]) and torch.equal(outs[2], outs[0])
     np.testing.assert_allclose(outs[1].cpu().double().numpy(), want.numpy(), rtol=1e-4, atol=1e-4)
+
+
+# ------------------------------------------------------------------ F(2,3) x F(2,3) tile
+@pytest.mark.parametrize("b,cin,cout,shape,mode,split", [
+    (1, 16, 16, (32, 96, 160), "acc", 0),    # the L1 cells' 16 -> 16 op at C2
+    (1, 16, 16, (16, 48, 80), "res", 0),     # a partial 32-column tile (W = 80)
+    (2, 16, 16, (5, 9, 20), None, 0),        # odd D, H not a multiple of 8, W < 32
+    (1, 32, 16, (4, 7, 36), "acc", 0),       # 8 chunks, W = 36 (a 4-column tail tile)
+    (1, 16, 12, (3, 10, 24), "res", 0),      # a partial cout block (12 of 16 rows)
+    (1, 16, 16, (6, 11, 40), "acc", 8),      # two sources (cat of 8 + 8 channels)
+    (1, 64, 16, (2, 3, 4), None, 0),         # one row, one column tile, one depth pair
+])
+def test_wino22_vs_torch(b, cin, cout, shape, mode, split):
+    """conv3d_wino22_kernel (16-cout blocks on F(2,3) x F(2,3), the packer's U, 4 waves per
+    SIMD) against float64 torch with the engines' tolerance, every epilogue, ragged tiles;
+    and the same layer on the default per-lane F(4,3) x F(2,3) tile within the same bar."""
+    lib = _lib.load()
+    g = torch.Generator().manual_seed(cin * 11 + cout + shape[2])
+    x = torch.randn((b, cin) + shape, generator=g)
+    w = torch.randn(cout, cin, 3, 3, 3, generator=g) / np.sqrt(cin * 27)
+    scale = torch.rand(cout, generator=g) + 0.5
+    shift = torch.randn(cout, generator=g) * 0.1
+    r = torch.randn((b, cout) + shape, generator=g)
+    want = _ref(x, w, scale, shift, True, r if mode else None).numpy()
+    packed = kernels.pack_conv_weight_wino(w.to(DEV))
+    xd = x.to(DEV)
+    x1, x2 = (xd[:, :split].contiguous(), xd[:, split:].contiguous()) if split else (xd, None)
+    got = {}
+    try:
+        for on in (1, 0):
+            assert lib.lea_conv3d_wino_set_w22(on) == 0
+            name = kernels.wino_kernel_name(b, cout, *shape)
+            assert (name == "conv3d_wino22_kernel") == bool(on), name
+            out = r.to(DEV).clone() if mode == "acc" else None
+            got[on] = kernels.conv3d_bnrelu_wino(x1, packed, cout, scale.to(DEV), shift.to(DEV), relu=True,
+                                                 out=out, accumulate=mode == "acc", x2=x2,
+                                                 residual=r.to(DEV) if mode == "res" else None)
+            np.testing.assert_allclose(got[on].cpu().double().numpy(), want, rtol=1e-4, atol=1e-4)
+    finally:
+        lib.lea_conv3d_wino_set_w22(0)
+
+
+def test_wino22_writes_only_its_channel_slice():
+    """Output into channels [16, 32) of a 48-channel buffer: the other channels untouched."""
+    lib = _lib.load()
+    g = torch.Generator().manual_seed(22)
+    x = torch.randn((1, 16, 4, 9, 40), generator=g).to(DEV)
+    w = (torch.randn(16, 16, 3, 3, 3, generator=g) / np.sqrt(16 * 27)).to(DEV)
+    big = torch.full((1, 48, 4, 9, 40), 3.0, device=DEV)
+    try:
+        assert lib.lea_conv3d_wino_set_w22(1) == 0
+        kernels.conv3d_bnrelu_wino(x, kernels.pack_conv_weight_wino(w), 16, None, None, relu=False,
+                                   out=big[:, 16:32])
+    finally:
+        lib.lea_conv3d_wino_set_w22(0)
+    want = F.conv3d(x.double(), w.double(), None, 1, 1)
+    np.testing.assert_allclose(big[:, 16:32].cpu().double().numpy(), want.cpu().numpy(), rtol=1e-4, atol=1e-4)
+    assert bool((big[:, :16] == 3.0).all()) and bool((big[:, 32:] == 3.0).all())
