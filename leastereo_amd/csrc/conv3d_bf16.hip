@@ -727,18 +727,22 @@ __global__ __launch_bounds__(kThreads, 2) void conv_bf16_stream_kernel(const Arg
 
   // DMA pieces of one plane: piece q = wave + 4t -> (block q / PIECES, words 64 (q % PIECES)
   // + lane); one buffer resource over the batch element's blocks (host: < 4 GiB)
+  // (LEA_PAIR_SUM: blocks [cb1, cin / 8) come from the second source, offsets relative to it)
   unsigned hwo[C::PPW];
   unsigned ldo[C::PPW];
+  bool src2[C::PPW];
 #pragma unroll
   for (int t = 0; t < C::PPW; ++t) {
     const int q = wave + 4 * t;
     const int blk = q / C::PIECES, e = (q % C::PIECES) * 64 + lane;
+    src2[t] = blk >= a.cb1;  // wave-uniform
+    const int sblk = src2[t] ? blk - a.cb1 : blk;
     unsigned v = 0xFFFFFFF0u;
     if (q < C::NBK * C::PIECES && e < C::PLANE && blk * 8 < a.cin) {
       const int rr = e / C::RW, cc = e % C::RW;
       const int h = h0 + rr - 1, w = w0 + cc - 1;
       if ((unsigned)h < (unsigned)a.H && (unsigned)w < (unsigned)a.W)
-        v = (unsigned)blk * (unsigned)DHW * 16u + (unsigned)(h * a.W + w) * 16u;
+        v = (unsigned)sblk * (unsigned)DHW * 16u + (unsigned)(h * a.W + w) * 16u;
     }
     hwo[t] = v;
     // padding pieces (q >= NBK * PIECES) land past the ring
@@ -746,7 +750,10 @@ __global__ __launch_bounds__(kThreads, 2) void conv_bf16_stream_kernel(const Arg
                                     : (unsigned)(C::RING * C::SLOTW + (q - C::NBK * C::PIECES) * 64);
   }
   const __amdgpu_buffer_rsrc_t xrs = __builtin_amdgcn_make_buffer_rsrc(
-      (void*)(a.x + (long long)b * a.xbs), 0, (unsigned)(a.cin / 8) * (unsigned)DHW * 16u, 0x00020000);
+      (void*)(a.x + (long long)b * a.xbs), 0, (unsigned)a.cb1 * (unsigned)DHW * 16u, 0x00020000);
+  const __amdgpu_buffer_rsrc_t x2rs = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(a.x2 ? a.x2 + (long long)b * a.x2bs : a.x), 0,
+      a.x2 ? (unsigned)(a.cin / 8 - a.cb1) * (unsigned)DHW * 16u : 0u, 0x00020000);
   auto load_plane = [&](int d) {  // plane d (zeros outside 0..D-1) -> ring slot d & 7
     const bool dv = (unsigned)d < (unsigned)a.D;
     const unsigned slot = (unsigned)(d & 7) * C::SLOTW;
@@ -754,7 +761,7 @@ __global__ __launch_bounds__(kThreads, 2) void conv_bf16_stream_kernel(const Arg
     for (int t = 0; t < C::PPW; ++t) {
       const unsigned vo = (dv && hwo[t] != 0xFFFFFFF0u) ? hwo[t] + (unsigned)d * (unsigned)HW * 16u : 0xFFFFFFF0u;
       const unsigned dst = ldo[t] < (unsigned)(C::RING * C::SLOTW) ? slot + ldo[t] : ldo[t];
-      dma_x4(xrs, vo, lds0 + 16u * dst);
+      dma_x4(src2[t] ? x2rs : xrs, vo, lds0 + 16u * dst);
     }
   };
 
@@ -802,14 +809,23 @@ __global__ __launch_bounds__(kThreads, 2) void conv_bf16_stream_kernel(const Arg
 #pragma unroll
       for (int m = 0; m < MT; ++m)
         av[c][ks][m] = wpv[((((long long)cob * NCH + c) * C::S + ks) * (WC * MT) + mtile0 + m) * 64 + g * 16 + n];
-  float sc[MT][4], sh[MT][4];
+  // LEA_PAIR_SUM: chunks [0, NCH / 2) are conv a's (BN at scale[co]), the rest conv b's
+  // (BN at scale[cout + co]); a's activation is kept in registers until b's epilogue
+  // (sc / sh: the final epilogue's BN -- conv b's under LEA_PAIR_SUM; sca / sha: conv a's; static
+  // indices only: a runtime-indexed register array is placed in scratch memory)
+  const bool pair = a.flags & LEA_PAIR_SUM;
+  float sc[MT][4], sh[MT][4], sca[MT][4], sha[MT][4];
 #pragma unroll
   for (int m = 0; m < MT; ++m)
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int co = cob * C::COB + (mtile0 + m) * 16 + 4 * g + r;
-      sc[m][r] = (a.scale && co < a.cout) ? a.scale[co] : 1.f;
-      sh[m][r] = (a.shift && co < a.cout) ? a.shift[co] : 0.f;
+      const bool cv = co < a.cout;
+      const int o = (pair ? a.cout : 0) + co;
+      sc[m][r] = (a.scale && cv) ? a.scale[o] : 1.f;
+      sh[m][r] = (a.shift && cv) ? a.shift[o] : 0.f;
+      sca[m][r] = (a.scale && cv && NCH % 2 == 0) ? a.scale[co] : 1.f;
+      sha[m][r] = (a.shift && cv && NCH % 2 == 0) ? a.shift[co] : 0.f;
     }
   const bool relu = a.flags & LEA_RELU;
 
@@ -830,8 +846,9 @@ __global__ __launch_bounds__(kThreads, 2) void conv_bf16_stream_kernel(const Arg
 #pragma unroll
       for (int i = 0; i < C::NV; ++i) acc[m][i] = f32x4{0.f, 0.f, 0.f, 0.f};
     const int base = 2 * s - 1;
+    float va[MT][C::NV][4];  // LEA_PAIR_SUM: conv a's activation
 #pragma unroll
-    for (int c = 0; c < NCH; ++c)
+    for (int c = 0; c < NCH; ++c) {
 #pragma unroll
       for (int ks = 0; ks < C::S; ++ks)
 #pragma unroll
@@ -844,6 +861,20 @@ __global__ __launch_bounds__(kThreads, 2) void conv_bf16_stream_kernel(const Arg
           for (int m = 0; m < MT; ++m)
             acc[m][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[c][ks][m], bv, acc[m][i], 0, 0, 0);
         }
+      if (NCH % 2 == 0 && c == NCH / 2 - 1 && pair) {
+#pragma unroll
+        for (int m = 0; m < MT; ++m)
+#pragma unroll
+          for (int i = 0; i < C::NV; ++i) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              float v = acc[m][i][r] * sca[m][r] + sha[m][r];
+              va[m][i][r] = relu ? fmaxf(v, 0.f) : v;
+            }
+            acc[m][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+          }
+      }
+    }
     const unsigned rslot = resbase + (unsigned)(s & 1) * C::RESW;
 #pragma unroll
     for (int m = 0; m < MT; ++m) {
@@ -860,6 +891,7 @@ __global__ __launch_bounds__(kThreads, 2) void conv_bf16_stream_kernel(const Arg
         for (int r = 0; r < 4; ++r) {
           v[r] = acc[m][i][r] * sc[m][r] + sh[m][r];
           if (relu) v[r] = fmaxf(v[r], 0.f);
+          if (NCH % 2 == 0 && pair) v[r] = va[m][i][r] + v[r];  // conv a's term + conv b's
         }
         if (resid) {
           // word ((m * 2 + 4g / 8) * NV + i) * 16 + n of this wave's slot, bf16 (4g) % 8 on
@@ -984,12 +1016,17 @@ int run(const Plan& p, Args a, int B, hipStream_t st, bool cv) {
     else conv1x1_c8_kernel<4><<<grid, 256, 0, st>>>(a, (int)tpw);
     return launch_status("lea_conv3d(bf16 1x1)");
   }
-  if (p.nsplit > 0 && !cv && a.cb1 * 8 == a.cin) {  // (one source: the ring walks one tensor)
+  // (one source, or LEA_PAIR_SUM's two: the ring walks the blocks of both)
+  if (p.nsplit > 0 && !cv && (a.cb1 * 8 == a.cin || (a.flags & LEA_PAIR_SUM))) {
     LEA_CHECK_ARG((long long)std::max(a.cin, a.cout + 7) / 8 * a.D * a.H * a.W * 16 < 0xFFFFFFF0LL,
                   "lea_conv3d(bf16 stream): volume too large");
     LEA_BFS_CASE(1, 8, 1, 1) LEA_BFS_CASE(2, 8, 1, 1) LEA_BFS_CASE(4, 8, 1, 1)
     LEA_BFS_CASE(1, 4, 2, 1) LEA_BFS_CASE(2, 4, 2, 1) LEA_BFS_CASE(4, 4, 2, 1)
-    LEA_BFS_CASE(1, 4, 2, 2) LEA_BFS_CASE(2, 4, 2, 2)
+    LEA_BFS_CASE(1, 4, 2, 2) LEA_BFS_CASE(2, 4, 2, 2) LEA_BFS_CASE(1, 8, 1, 2)
+  }
+  if (a.flags & LEA_PAIR_SUM) {
+    set_error("lea_conv3d(bf16): LEA_PAIR_SUM runs on the D-streaming kernel only (cout <= 16, D >= 4)");
+    return LEA_E_UNSUPPORTED;
   }
   if (cv) {
     LEA_BF_MT(3, 2, 2, true)
@@ -1115,7 +1152,18 @@ static int bf16_conv_common(bf::Args& a, int B, int k, bool cv, void* stream) {
   LEA_CHECK_ARG((long long)a.D * a.H * a.W * 16 < (1LL << 32), "lea_conv3d(bf16): volume too large");
   LEA_CHECK_ARG(a.x != (const __bf16*)a.y && a.x2 != (const __bf16*)a.y,
                 "lea_conv3d(bf16): input aliases output");
-  const bf::Plan p = bf::plan(B, a.cout, a.D, a.H, a.W, k, a.cin);
+  const bool pair = a.flags & LEA_PAIR_SUM;
+  bf::Plan p = bf::plan(B, a.cout, a.D, a.H, a.W, k, pair ? a.cb1 * 8 : a.cin);
+  if (pair) {
+    // two equal sources of one K chunk each (the L0 / L1 cell steps), one 16-cout block: the
+    // packed weight is conv a's chunk then conv b's
+    LEA_CHECK_ARG(!(a.flags & LEA_RESIDUAL) && a.x2 && 2 * a.cb1 * 8 == a.cin && k == 3 && !cv,
+                  "lea_conv3d(bf16): LEA_PAIR_SUM needs two equal sources and no residual");
+    if (a.cout > 16 || p.nsplit <= 0 || a.cb1 * 8 > 8 * p.nb) {
+      set_error("lea_conv3d(bf16): LEA_PAIR_SUM unsupported for cin=%d cout=%d D=%d", a.cin, a.cout, a.D);
+      return LEA_E_UNSUPPORTED;
+    }
+  }
   const int cobv = bf::cob_of(a.cout);
   a.ncob = (a.cout + cobv - 1) / cobv;
   a.nchunks = (a.cin / 8 + p.nb - 1) / p.nb;

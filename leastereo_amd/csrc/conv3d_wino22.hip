@@ -205,8 +205,9 @@ __global__ __launch_bounds__(512, 4) void conv3d_wino22_kernel(const ConvArgs a)
       const int cr = 4 * ci + r;
       const bool cv = lv && cr < nco;
       // BN: scale 1, shift 0 without a BN (out-of-range loads read 0)
-      const float sc = a.scale ? __builtin_amdgcn_raw_buffer_load_b32(srs, bn4 + (unsigned)cr * 4u, 0, 0) : 1.f;
-      const float sh = __builtin_amdgcn_raw_buffer_load_b32(hrs2, bn4 + (unsigned)cr * 4u, 0, 0);
+      const float sc = a.scale ? __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(srs, bn4 + (unsigned)cr * 4u, 0, 0))
+                               : 1.f;
+      const float sh = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(hrs2, bn4 + (unsigned)cr * 4u, 0, 0));
       unsigned off[2];
       f32x2 rv[2];
 #pragma unroll
@@ -312,11 +313,12 @@ int run22(ConvArgs a, int B, int spw, hipStream_t st) {
   a.tiles_w = (a.W + C::TW - 1) / C::TW;
   a.ntiles = a.tiles_w * ((a.H + C::TH - 1) / C::TH);
   a.ndz = (a.D + C::TD - 1) / C::TD;
-  // depth pairs per workgroup: while about two rounds of workgroups remain (2 per CU)
+  // depth pairs per workgroup: two when that leaves one round of workgroups (2 per CU) instead
+  // of two (r05 tools/w22_ab.py, C2 L1 16 -> 16: 960 workgroups 47 us, 480 walking 2 pairs 44 us;
+  // C5's 3696 workgroups equal either way)
   if (spw <= 0) {
     const long long base = (long long)a.ntiles * a.ndz * B * a.ncob;
-    spw = 1;
-    while (spw < 4 && base / (2 * spw) >= 2 * 512) spw *= 2;
+    spw = base > 512 && base <= 1024 ? 2 : 1;
   }
   a.spw = std::max(1, std::min(spw, a.ndz));
   const long long n = (long long)a.ntiles * ((a.ndz + a.spw - 1) / a.spw) * B * a.ncob;

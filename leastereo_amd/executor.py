@@ -102,6 +102,8 @@ class CellGraphExecutor:
     # sibling group plus an accumulating launch per remaining op (a read-modify-write of the
     # slot each).  Executors whose engine takes LEA_PAIR_SUM set it
     PAIR_STEPS = False
+    # the cells' channel counts that take the pair launches (A/B: LEASTEREO_PAIR_C=16,32 ...)
+    PAIR_C = tuple(int(c) for c in os.environ.get("LEASTEREO_PAIR_C", "8,16,32").split(",") if c)
 
     def __init__(self, net):
         from .model import ConvBR
@@ -171,7 +173,7 @@ class CellGraphExecutor:
             self.pair_steps = {}
             for i, cell in enumerate(net.cells) if self.PAIR_STEPS else ():
                 terms = [[(op, j) for op, j in t] for t in cell.plan]
-                if (getattr(cell, "dims", 3) != 3 or not terms
+                if (getattr(cell, "dims", 3) != 3 or not terms or cell.c_out not in self.PAIR_C
                         or any(len(t) != 2 or any(cell.op_kinds[op] != "conv" for op, _ in t) for t in terms)):
                     continue
                 mods = [[cell._ops[op] for op, _ in t] for t in terms]
@@ -403,7 +405,7 @@ class MatchingExecutor(CellGraphExecutor):
     SPLIT_S1_GROUP48 = os.environ.get("LEASTEREO_SPLIT_GROUP48", "1") != "0"
     # the matching cells' steps as LEA_PAIR_SUM launches (LEASTEREO_PAIR_STEPS=0: the s1 group
     # + accumulating launches); the f32 pair runs on the Winograd F(2,3) x F(2,3) tile
-    PAIR_STEPS = WINOGRAD and os.environ.get("LEASTEREO_PAIR_STEPS", "1") != "0"
+    PAIR_STEPS = WINOGRAD and os.environ.get("LEASTEREO_PAIR_STEPS", "0") != "0"
 
     def run(self, x):
         """newMatching.forward (skip_model_3d.py:140-174): [B,64,D3,H3,W3] -> [B,1,D3,H3,W3]."""
@@ -661,7 +663,9 @@ class MatchingExecutorBF16(_C8Layout, MatchingExecutor):
     is f32 for the disparity regression.  Same graph as MatchingExecutor."""
 
     SPLIT_S1_GROUP48 = False
-    PAIR_STEPS = False
+    # the L0 / L1 cells' steps (8 or 16 channels: one K chunk per conv) as LEA_PAIR_SUM
+    # launches of the D-streaming kernel; the L2 cells keep the group + accumulating launches
+    PAIR_STEPS = os.environ.get("LEASTEREO_PAIR_STEPS", "1") != "0"
 
     def __init__(self, matching):
         from .model import ConvBR
@@ -680,6 +684,12 @@ class MatchingExecutorBF16(_C8Layout, MatchingExecutor):
                     self.p[name] = ConvParams(kernels.pack_conv_weight_bf16(taps), None, None, ci,
                                               taps.shape[0], 1, False, "bf16")
                     continue
+                if ".pair" in name:
+                    i, k = int(name.split(".")[1]), int(name.rsplit("pair", 1)[1])
+                    wa, wb = (matching.cells[i]._ops[op].conv.weight for op, _ in self.pair_steps[i][k])
+                    packed = torch.cat([kernels.pack_conv_weight_bf16(wa), kernels.pack_conv_weight_bf16(wb)])
+                    self.p[name] = ConvParams(packed, p.scale, p.shift, p.cin, p.cout, p.k, p.relu, "bf16")
+                    continue
                 if name.endswith(".s1_group"):
                     i = int(name.split(".")[1])
                     mods = [matching.cells[i]._ops[op] for _, op in self.s1_group[i]]
@@ -695,6 +705,14 @@ class MatchingExecutorBF16(_C8Layout, MatchingExecutor):
 
     def _use_winograd(self):
         """bf16 layers stay on the bf16 engine."""
+
+    def _pair_ok(self, x, x2, out):
+        return kernels.pair_sum_supported_bf16(x, x2, out)
+
+    def pair_conv(self, name, x, x2, out):
+        p = self.p[name]
+        return kernels.conv3d_bnrelu_bf16(x, p.packed, p.cout, 3, p.scale, p.shift, True, out, x2=x2,
+                                          pair_sum=True)
 
     def _cv_stem_pack(self, wl, wr):
         return kernels.pack_conv2d_weight_bf16(wl), kernels.pack_conv2d_weight_bf16(wr)

@@ -578,10 +578,15 @@ def conv3d_bnrelu_bf16(x: torch.Tensor, packed: torch.Tensor, cout: int, k: int,
                        scale: torch.Tensor | None, shift: torch.Tensor | None, relu: bool = True,
                        out: torch.Tensor | None = None, accumulate: bool = False,
                        x2: torch.Tensor | None = None,
-                       residual: torch.Tensor | None = None) -> torch.Tensor:
-    """conv3d_bnrelu at dtype bf16 on c8 tensors (out may be a block slice)."""
+                       residual: torch.Tensor | None = None, pair_sum: bool = False) -> torch.Tensor:
+    """conv3d_bnrelu at dtype bf16 on c8 tensors (out may be a block slice).  ``pair_sum``
+    (LEA_PAIR_SUM, the D-streaming kernel): x's and x2's channels feed two ConvBRs whose
+    activations are summed; ``packed`` = pack_conv_weight_bf16(W_a) then (W_b) (one K chunk
+    each), scale / shift 2 * cout values."""
     _require_c8(x, x2, out, residual)
     _require_cuda(scale, shift)
+    if pair_sum and (x2 is None or accumulate or residual is not None):
+        raise ValueError("pair_sum takes two sources and no residual")
     b, cb, d, h, w, _ = x.shape
     xbs = _check_c8_view(x, "x")
     cin2, x2bs = 0, 0
@@ -606,10 +611,11 @@ def conv3d_bnrelu_bf16(x: torch.Tensor, packed: torch.Tensor, cout: int, k: int,
         rptr, rbs = residual.data_ptr(), _check_c8_view(residual, "residual")
     else:
         rptr, rbs = None, 0
-    flags = (LEA_RELU if relu else 0) | (LEA_RESIDUAL if rptr is not None else 0)
+    flags = (LEA_RELU if relu else 0) | (LEA_RESIDUAL if rptr is not None else 0) | (LEA_PAIR_SUM if pair_sum else 0)
     rec = None if _probe is None else _probe_begin(
         b, cb * 8 + cin2, cout, d, h, w, k, rptr is not None, b * d * h * w, False,
-        name=conv_kernel_name_bf16(b, cout, cb * 8 + cin2, d, h, w, k), esz=2)
+        name=(f"conv_bf16_stream_kernel<1, 1, {8 if cb == 1 else 4}, {cb}, 2>" if pair_sum else
+              conv_kernel_name_bf16(b, cout, cb * 8 + cin2, d, h, w, k)), esz=2)
     check(_lib.load().lea_conv3d_bnrelu_bf16(
         x.data_ptr(), xbs, x2.data_ptr() if x2 is not None else None, x2bs, cin2, packed.data_ptr(),
         scale.data_ptr() if scale is not None else None,
@@ -617,6 +623,13 @@ def conv3d_bnrelu_bf16(x: torch.Tensor, packed: torch.Tensor, cout: int, k: int,
         cb * 8 + cin2, cout, d, h, w, k, flags, _stream()), "lea_conv3d_bnrelu_bf16")
     _probe_end(rec)
     return out
+
+
+def pair_sum_supported_bf16(x: torch.Tensor, x2: torch.Tensor, out: torch.Tensor) -> bool:
+    """Whether conv3d_bnrelu_bf16(..., pair_sum=True) takes these c8 operands: two equal sources
+    of one K chunk each (8 or 16 channels), cout <= 16, D >= 4 (the D-streaming kernel)."""
+    return bool(x.shape[1] == x2.shape[1] and x.shape[1] in (1, 2) and out.shape[1] * 8 <= 16
+                and x.shape[2] >= 4 and tuple(x.shape[2:5]) == tuple(x2.shape[2:5]))
 
 
 def conv1x1_resampled_bf16(x: torch.Tensor, size, packed: torch.Tensor, cout: int, scale, shift,

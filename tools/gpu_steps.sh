@@ -7,7 +7,7 @@
 #   tests=EXPR               pytest -m gpu -k EXPR (EXPR: a -k expression)
 #   file=PATH[@EXPR]         pytest PATH [-k EXPR]
 #   bench=CFG[@ARGS]         bench.py --config CFG (ARGS: extra flags, '+' for ' ')
-#   ab=CFG@ENV_A@ENV_B       same-box A/B, two interleaved rounds (tools/gpu_ab.sh; ENV ',' for ' ')
+#   ab=CFG@ENV_A@ENV_B[@..]  same-box A/B/.., interleaved rounds (tools/gpu_ab.sh; ENV ',' for ' ', '-' none)
 #   layers                   per-launch conv list of the C2 forward (tools/layer_list.py)
 #   prof=TAG                 rocprofv3 kernel stats + forward breakdown of the default C2 bench
 #   py=SCRIPT[@ARGS]         python SCRIPT ARGS ('+' for ' ')
@@ -28,16 +28,15 @@ for step in "$@"; do
     suite) timeout -k 10 1000 $PYT tests -m gpu > $log 2>&1 ;;
     tests) timeout -k 10 900 $PYT tests -m gpu -k "$val" > $log 2>&1 ;;
     file)
-      f=${val%%@*}; k=""; [ "$f" != "$val" ] && k=${val#*@}
+      f=${val%%@*}; k=""; [ "$f" != "$val" ] && k=$(echo "${val#*@}" | tr "+" " ")
       if [ -n "$k" ]; then timeout -k 10 900 $PYT "$f" -k "$k" > $log 2>&1
       else timeout -k 10 900 $PYT "$f" > $log 2>&1; fi ;;
     bench)
       cfg=${val%%@*}; extra=""; [ "$cfg" != "$val" ] && extra=$(echo "${val#*@}" | tr '+' ' ')
       timeout -k 10 900 python3 bench.py --config $cfg $extra > $O/$tag.json 2> $log ;;
-    ab)
-      IFS=@ read -r cfg ea eb <<< "$val"
-      CONFIGS=$cfg ROUNDS=2 AB_A="$(echo $ea | tr ',' ' ')" AB_B="$(echo $eb | tr ',' ' ')" \
-        timeout -k 10 900 bash tools/gpu_ab.sh > $log 2>&1 ;;
+    ab)  # ab=CFG@VARIANT@VARIANT[@...]: each variant a ','-separated env list ('-' = none)
+      cfg=${val%%@*}; vars=$(echo "${val#*@}" | tr '@' ';' | sed 's/^-;/;/; s/;-;/;;/g; s/;-$/;/')
+      CONFIGS=$cfg ROUNDS=${ROUNDS:-2} AB_VARIANTS="$vars" timeout -k 10 1100 bash tools/gpu_ab.sh > $log 2>&1 ;;
     layers) timeout -k 10 300 python3 -u tools/layer_list.py --reps 5 > $log 2>&1 ;;
     prof)
       timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_$val -o run -- \
@@ -49,7 +48,7 @@ for step in "$@"; do
     *) echo "unknown step $step"; exit 2 ;;
   esac
   rc=$?
-  tail -4 $log
+  tail -${TAIL:-4} $log
   [ -f $O/$tag.json ] && python3 -c "import json,sys; d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); print('value', round(d['value'],2), 'ms', round(d['ms_per_step'],3), 'pair', d.get('pair_epe_px',{}) and d['pair_epe_px'].get('max'))" $O/$tag.json 2>/dev/null
   [ $rc -eq 0 ] || { echo "step $step rc=$rc"; exit $rc; }
 done

@@ -26,11 +26,12 @@ def main():
     ap.add_argument("--iters", type=int, default=50)
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--walks", default="0", help="depth pairs per workgroup for the w22 tile (0 = planner)")
+    ap.add_argument("--only", default="", help="substring of the shape names to run (_ for a space)")
     a = ap.parse_args()
     lib = _lib.load()
     dev = "cuda"
     for name, cin, cout, (d, h, w), acc in SHAPES:
-        if w % 4:
+        if w % 4 or (a.only and a.only.replace("_", " ") not in name):
             continue
         g = torch.Generator(device=dev).manual_seed(0)
         x = torch.randn(1, cin, d, h, w, device=dev, generator=g)
