@@ -71,6 +71,7 @@ SIGNATURES = {
     "lea_resample_bf16_set_batch": (_i, [_i]),
     "lea_resample_bf16_set_cols": (_i, [_i]),
     "lea_conv3d_wino_set_w22": (_i, [_i]),
+    "lea_conv3d_bf16_set_pair_split": (_i, [_i]),
     "lea_disparity_set_register_form": (_i, [_i]),
     "lea_tapsum_set_rows": (_i, [_i]),
     "lea_staged_rows": (_i, [_i, _i, _i, _i, _i]),
@@ -181,6 +182,7 @@ TUNING_ENV = {"LEASTEREO_WINO2_WALK": "lea_conv3d_wino2_set_walk",
               "LEASTEREO_RESAMPLE_K": "lea_resample_bf16_set_batch",
               "LEASTEREO_RESAMPLE_COLS": "lea_resample_bf16_set_cols",
               "LEASTEREO_W22": "lea_conv3d_wino_set_w22",
+              "LEASTEREO_PAIR_SPLIT": "lea_conv3d_bf16_set_pair_split",
               "LEASTEREO_DISP_REG": "lea_disparity_set_register_form",
               "LEASTEREO_TAPSUM_ROWS": "lea_tapsum_set_rows"}
 

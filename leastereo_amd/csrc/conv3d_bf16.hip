@@ -26,6 +26,7 @@ namespace bf {
 
 using bf16x8 = __attribute__((ext_vector_type(8))) __bf16;
 using bf16x4 = __attribute__((ext_vector_type(4))) __bf16;
+typedef unsigned u32x2_t __attribute__((ext_vector_type(2)));
 using f32x4 = __attribute__((__vector_size__(4 * sizeof(float)))) float;
 using lds_void = __attribute__((address_space(3))) void;
 constexpr int kThreads = 256;
@@ -912,6 +913,195 @@ __global__ __launch_bounds__(kThreads, 2) void conv_bf16_stream_kernel(const Arg
   wait_vm<0>();  // no LDS-DMA may outlive the workgroup
 }
 
+// LEA_PAIR_SUM (a matching-cell step: relu(BN_a(conv_a(xa))) + relu(BN_b(conv_b(xb))), one K chunk
+// per conv) on the D-streaming form with the two convs on separate wave halves (r05): 8 waves, waves
+// 0-3 run conv a and 4-7 conv b over the same 16 x TH x 2 tile rows (wave w and w + 4 on one
+// SIMD), so each wave holds ONE chunk's A fragments -- the single-wave-group form held both
+// (184 VGPRs: two waves per SIMD, 2.5 TB/s on the L1 steps).  Conv a's activation goes to LDS as
+// bf16 (the rounding the two-launch form applies to a's output), and the conv-b wave adds it in
+// its epilogue of step s, deferred to after the next step's barrier; the ring holds both
+// sources' planes (blocks a0..a(NB-1), b0..b(NB-1) per slot).
+template <int TH, int NB>
+struct PCfg {
+  static constexpr int TD = 2, VT = TH * TD, NV = VT / 4;     // 16-voxel rows per wave
+  static constexpr int T = 27, S = (T * NB + 3) / 4;          // k-steps of one conv
+  static constexpr int NBK = 2 * NB;                          // blocks per ring slot
+  static constexpr int RH = TH + 2, RW = 18, PLANE = RH * RW;
+  static constexpr int PIECES = (PLANE + 63) / 64, PLANEP = 64 * PIECES;
+  static constexpr int SLOTW = NBK * PLANEP;
+  static constexpr int PPW = (NBK * PIECES + 7) / 8;           // pieces per wave and plane
+  static constexpr int RING = 8;
+  static constexpr int RINGW = RING * SLOTW + 64 * (8 * PPW - NBK * PIECES);  // + padding pieces
+  static constexpr int XW = 4 * NV * 16 * 2;                   // a's activations per parity (16-B words)
+  static constexpr int LDSW = RINGW + 2 * XW;
+  static_assert(VT % 4 == 0, "rows per wave");
+  static_assert(2 * LDSW * 16 <= 160 * 1024, "two workgroups per CU");
+};
+
+template <int TH, int NB>
+__global__ __launch_bounds__(512, 2) void conv_bf16_pair_kernel(const Args a, int nsplit) {
+  using C = PCfg<TH, NB>;
+  extern __shared__ __attribute__((aligned(16))) bf16x8 smem[];  // ring + a's activations
+  const unsigned lds0 = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)(lds_void*)smem);
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int part = wave >> 2, wv = wave & 3;  // conv a (0) / b (1); rows wv * NV ..
+  const int g = lane >> 4, n = lane & 15;
+
+  const int xcd = blockIdx.x % 8, idx = blockIdx.x / 8;
+  const int q8 = a.nblk / 8, r8 = a.nblk % 8;
+  const int lin = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + idx;
+  const int sp = lin % nsplit;
+  const int tile = (lin / nsplit) % a.ntiles;
+  const int b = lin / (nsplit * a.ntiles);  // (one 16-cout block)
+  const int h0 = (tile / a.tiles_w) * TH, w0 = (tile % a.tiles_w) * 16;
+  const int HW = a.H * a.W;
+  const int DHW = HW * a.D;
+  const int nst = (a.D + 1) / 2;
+  const int s0 = sp * nst / nsplit, s1 = (sp + 1) * nst / nsplit;
+
+  // DMA pieces of one plane: piece q = wave + 8t -> (block q / PIECES, words 64 (q % PIECES) + lane);
+  // blocks [0, NB) from xa, [NB, 2NB) from xb
+  unsigned hwo[C::PPW], ldo[C::PPW];
+  bool src2[C::PPW];
+#pragma unroll
+  for (int t = 0; t < C::PPW; ++t) {
+    const int q = wave + 8 * t;
+    const int blk = q / C::PIECES, e = (q % C::PIECES) * 64 + lane;
+    src2[t] = blk >= NB;
+    const int sblk = src2[t] ? blk - NB : blk;
+    unsigned v = 0xFFFFFFF0u;
+    if (q < C::NBK * C::PIECES && e < C::PLANE) {
+      const int rr = e / C::RW, cc = e % C::RW;
+      const int h = h0 + rr - 1, w = w0 + cc - 1;
+      if ((unsigned)h < (unsigned)a.H && (unsigned)w < (unsigned)a.W)
+        v = (unsigned)sblk * (unsigned)DHW * 16u + (unsigned)(h * a.W + w) * 16u;
+    }
+    hwo[t] = v;
+    ldo[t] = q < C::NBK * C::PIECES ? (unsigned)(blk * C::PLANEP + (q % C::PIECES) * 64)
+                                    : (unsigned)(C::RING * C::SLOTW + (q - C::NBK * C::PIECES) * 64);
+  }
+  const unsigned srcb = (unsigned)NB * (unsigned)DHW * 16u;
+  const __amdgpu_buffer_rsrc_t xrs =
+      __builtin_amdgcn_make_buffer_rsrc((void*)(a.x + (long long)b * a.xbs), 0, srcb, 0x00020000);
+  const __amdgpu_buffer_rsrc_t x2rs =
+      __builtin_amdgcn_make_buffer_rsrc((void*)(a.x2 + (long long)b * a.x2bs), 0, srcb, 0x00020000);
+  auto load_plane = [&](int d) {  // plane d (zeros outside 0..D-1) -> ring slot d & 7
+    const bool dv = (unsigned)d < (unsigned)a.D;
+    const unsigned slot = (unsigned)(d & 7) * C::SLOTW;
+#pragma unroll
+    for (int t = 0; t < C::PPW; ++t) {
+      const unsigned vo = (dv && hwo[t] != 0xFFFFFFF0u) ? hwo[t] + (unsigned)d * (unsigned)HW * 16u : 0xFFFFFFF0u;
+      const unsigned dst = ldo[t] < (unsigned)(C::RING * C::SLOTW) ? slot + ldo[t] : ldo[t];
+      dma_x4(src2[t] ? x2rs : xrs, vo, lds0 + 16u * dst);
+    }
+  };
+
+  // this wave's K slots: k-step ks, lane group g -> tap, block of its conv's chunk
+  int kdv[C::S], koff[C::S];
+#pragma unroll
+  for (int ks = 0; ks < C::S; ++ks) {
+    const int slot = 4 * ks + g;
+    const int tap = min(slot / NB, C::T - 1);  // slots past the last tap carry zero weights
+    const int blk = slot % NB + part * NB;
+    kdv[ks] = tap / 9;
+    koff[ks] = blk * C::PLANEP + ((tap / 3) % 3) * C::RW + tap % 3;
+  }
+  // this wave's conv: chunk `part` of the pair's packed weights (conv a's pack, then b's)
+  const bf16x8* wpv = reinterpret_cast<const bf16x8*>(a.wp);
+  bf16x8 av[C::S];
+#pragma unroll
+  for (int ks = 0; ks < C::S; ++ks) av[ks] = wpv[((long long)part * C::S + ks) * 64 + g * 16 + n];
+  float sc[4], sh[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int co = 4 * g + r;
+    sc[r] = (a.scale && co < a.cout) ? a.scale[part * a.cout + co] : 1.f;
+    sh[r] = (a.shift && co < a.cout) ? a.shift[part * a.cout + co] : 0.f;
+  }
+  const bool relu = a.flags & LEA_RELU;
+  // a's activations: [parity][wv][row i][column n][16 couts] bf16, lane (g, n) owns couts 4g..4g+3
+  __bf16* xa_lds = reinterpret_cast<__bf16*>(smem + C::RINGW);
+  auto xoff = [&](int parity, int i) { return ((((parity * 4 + wv) * C::NV + i) * 16 + n) * 16 + 4 * g); };
+
+  // conv b's output through one buffer resource: every lane issues the same NV 8-byte stores
+  // per step (invalid ones at an out-of-range offset: dropped), so the waits below can count them
+  f32x4 prev[C::NV];  // conv b: the previous step's accumulators (epilogue after the next barrier)
+  const __amdgpu_buffer_rsrc_t yrs = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(a.y + (long long)b * a.ybs), 0, (unsigned)((a.cout + 7) / 8) * (unsigned)DHW * 16u, 0x00020000);
+  auto epilogue_b = [&](int s) {
+#pragma unroll
+    for (int i = 0; i < C::NV; ++i) {
+      const int qrow = wv * C::NV + i;
+      const int d = 2 * s + qrow / TH, h = h0 + qrow % TH, w = w0 + n;
+      const bf16x4 va = *reinterpret_cast<const bf16x4*>(xa_lds + xoff(s & 1, i));
+      const int co = 4 * g;
+      const bool ok = d < a.D && h < a.H && w < a.W && co < a.cout;
+      const unsigned off = ok ? (unsigned)(co / 8) * (unsigned)DHW * 16u + (unsigned)(co % 8) * 2u +
+                                    (unsigned)(d * HW + h * a.W + w) * 16u
+                              : 0xFFFFFFF0u;
+      bf16x4 out;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        float v = prev[i][r] * sc[r] + sh[r];
+        if (relu) v = fmaxf(v, 0.f);
+        out[r] = (__bf16)((float)va[r] + v);
+      }
+      __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2_t, out), yrs, off, 0, 0);
+    }
+  };
+
+  // Pipeline: after step s's barrier every wave issues planes 2s+5, 2s+6 (into the slots of
+  // planes 2s-3, 2s-2, which only step s-1 read) -- two steps of planes in flight during the
+  // MFMAs -- then conv b's waves store step s-1.  The top of step s+1 waits for all but the
+  // younger operations than planes 2s+3, 2s+4: planes 2s+5, 2s+6 and, on conv b's waves, the
+  // stores issued since (of steps s-2 and s-1: NV each; none for step s0 - 1)
+  for (int j = -1; j <= 4; ++j) load_plane(2 * s0 + j);
+  for (int s = s0; s < s1; ++s) {
+    if (part == 1 && s - s0 >= 3)
+      wait_vm<2 * C::PPW + 2 * C::NV>();
+    else if (part == 1 && s - s0 == 2)
+      wait_vm<2 * C::PPW + C::NV>();  // (step s0 stored nothing)
+    else
+      wait_vm<2 * C::PPW>();  // conv a; s0 (the prologue's planes 2s0+3, 2s0+4 may stay in flight)
+    __syncthreads();  // everyone's planes landed; step s-1 done (its activations in LDS)
+    load_plane(2 * s + 5);
+    load_plane(2 * s + 6);
+    if (part == 1 && s > s0) epilogue_b(s - 1);
+    f32x4 acc[C::NV];
+#pragma unroll
+    for (int i = 0; i < C::NV; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+    const int base = 2 * s - 1;
+#pragma unroll
+    for (int ks = 0; ks < C::S; ++ks)
+#pragma unroll
+      for (int i = 0; i < C::NV; ++i) {
+        const int qrow = wv * C::NV + i;
+        const int t = qrow / TH, r = qrow % TH;
+        const bf16x8 bv = smem[((base + t + kdv[ks]) & 7) * C::SLOTW + koff[ks] + r * C::RW + n];
+        acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[ks], bv, acc[i], 0, 0, 0);
+      }
+    if (part == 0) {
+#pragma unroll
+      for (int i = 0; i < C::NV; ++i) {
+        bf16x4 o;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          float v = acc[i][r] * sc[r] + sh[r];
+          o[r] = (__bf16)(relu ? fmaxf(v, 0.f) : v);
+        }
+        *reinterpret_cast<bf16x4*>(xa_lds + xoff(s & 1, i)) = o;
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < C::NV; ++i) prev[i] = acc[i];
+    }
+  }
+  wait_vm<0>();  // no LDS-DMA may outlive the workgroup
+  __syncthreads();
+  if (part == 1 && s1 > s0) epilogue_b(s1 - 1);
+}
+
 struct Plan {
   int ks, mt, wc, th, td, nb;
   int nsplit;  // > 0: the D-streaming kernel with nsplit column segments along D
@@ -921,6 +1111,7 @@ struct Plan {
 int g_override[3] = {0, 0, 0};  // th, td, mt (lea_conv3d_bf16_set_tile_override)
 int g_variant = 0;              // lea_conv3d_bf16_set_variant: 0 planner, 1 tile kernel only
 int g_stream1x1 = 1;            // lea_conv3d_bf16_set_stream1x1
+int g_pair_split = 1;           // lea_conv3d_bf16_set_pair_split: LEA_PAIR_SUM on the split-wave kernel
 
 inline Plan plan(int B, int cout, int D, int H, int W, int ks, int cin) {
   // r01 sweep (tools/conv_sweep.py --bf16, profiles/r01_conv_sweep_bf16.txt): one
@@ -1016,6 +1207,22 @@ int run(const Plan& p, Args a, int B, hipStream_t st, bool cv) {
     else conv1x1_c8_kernel<4><<<grid, 256, 0, st>>>(a, (int)tpw);
     return launch_status("lea_conv3d(bf16 1x1)");
   }
+  if ((a.flags & LEA_PAIR_SUM) && g_pair_split && p.nsplit > 0 && a.ncob == 1 && (a.nchunks == 2) &&
+      ((p.nb == 2 && p.th == 4) || (p.nb == 1 && p.th == 8))) {
+    // the split-wave pair kernel (conv a / conv b on separate wave halves)
+    a.tiles_w = (a.W + 15) / 16;
+    a.ntiles = a.tiles_w * ((a.H + p.th - 1) / p.th);
+    const long long nb_ = (long long)a.ntiles * p.nsplit * B;
+    LEA_CHECK_ARG(nb_ < (1LL << 31), "lea_conv3d(bf16 pair): grid too large");
+    LEA_CHECK_ARG((long long)(a.cin / 16 + 1) * a.D * a.H * a.W * 16 < 0xFFFFFFF0LL,
+                  "lea_conv3d(bf16 pair): volume too large");
+    a.nblk = (int)nb_;
+    if (p.nb == 2)
+      conv_bf16_pair_kernel<4, 2><<<dim3((unsigned)nb_), 512, PCfg<4, 2>::LDSW * 16, st>>>(a, p.nsplit);
+    else
+      conv_bf16_pair_kernel<8, 1><<<dim3((unsigned)nb_), 512, PCfg<8, 1>::LDSW * 16, st>>>(a, p.nsplit);
+    return launch_status("lea_conv3d(bf16 pair)");
+  }
   // (one source, or LEA_PAIR_SUM's two: the ring walks the blocks of both)
   if (p.nsplit > 0 && !cv && (a.cb1 * 8 == a.cin || (a.flags & LEA_PAIR_SUM))) {
     LEA_CHECK_ARG((long long)std::max(a.cin, a.cout + 7) / 8 * a.D * a.H * a.W * 16 < 0xFFFFFFF0LL,
@@ -1092,6 +1299,13 @@ extern "C" int lea_conv3d_bf16_set_stream1x1(int on) {
   clear_error();
   LEA_CHECK_ARG(on == 0 || on == 1, "lea_conv3d_bf16_set_stream1x1: on=%d", on);
   bf::g_stream1x1 = on;
+  return 0;
+}
+
+extern "C" int lea_conv3d_bf16_set_pair_split(int on) {
+  clear_error();
+  LEA_CHECK_ARG(on == 0 || on == 1, "lea_conv3d_bf16_set_pair_split: %d", on);
+  bf::g_pair_split = on;
   return 0;
 }
 

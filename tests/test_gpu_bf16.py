@@ -477,3 +477,36 @@ def test_stream_1x1_is_the_tile_kernel(b, cin, cout, shape, mode, cin2):
     if mode:
         want = want + r.double()
     _close(kernels.from_c8(outs[0]), want)
+
+
+@pytest.mark.parametrize("split", [1, 0])
+@pytest.mark.parametrize("c,shape", [(16, (6, 9, 40)), (8, (5, 12, 33)), (16, (4, 4, 16)), (8, (8, 20, 64))])
+def test_pair_sum_bf16_vs_torch(c, shape, split):
+    """LEA_PAIR_SUM on the bf16 engine (a matching-cell step: relu(BN_a(conv_a(xa))) +
+    relu(BN_b(conv_b(xb))) in one launch) -- the split-wave pair kernel and the D-streaming
+    kernel with both convs per wave -- against float64 torch on the same bf16 operands,
+    written into a block slice of a cat buffer; odd D / ragged H, W."""
+    from leastereo_amd import _lib
+    lib = _lib.load()
+    g = torch.Generator().manual_seed(c * 3 + shape[0])
+    xa, xb = _bf(torch.randn((2, c) + shape, generator=g)), _bf(torch.randn((2, c) + shape, generator=g))
+    wa = _bf(torch.randn(c, c, 3, 3, 3, generator=g) / np.sqrt(c * 27))
+    wb = _bf(torch.randn(c, c, 3, 3, 3, generator=g) / np.sqrt(c * 27))
+    sc, sh = torch.rand(2 * c, generator=g) + 0.5, torch.randn(2 * c, generator=g) * 0.1
+
+    def branch(x, w, s, t):
+        y = F.conv3d(x.double(), w.double(), None, 1, 1)
+        return torch.relu(y * s.double().view(1, -1, 1, 1, 1) + t.double().view(1, -1, 1, 1, 1))
+    want = branch(xa, wa, sc[:c], sh[:c]) + branch(xb, wb, sc[c:], sh[c:])
+    packed = torch.cat([kernels.pack_conv_weight_bf16(wa.to(DEV)), kernels.pack_conv_weight_bf16(wb.to(DEV))])
+    big = torch.full((2, c // 8 + 2) + shape + (8,), 5.0, device=DEV, dtype=torch.bfloat16)
+    out = big[:, 1:1 + c // 8]
+    xa8, xb8 = kernels.to_c8(xa.to(DEV)), kernels.to_c8(xb.to(DEV))
+    assert kernels.pair_sum_supported_bf16(xa8, xb8, out)
+    try:
+        assert lib.lea_conv3d_bf16_set_pair_split(split) == 0
+        kernels.conv3d_bnrelu_bf16(xa8, packed, c, 3, sc.to(DEV), sh.to(DEV), True, out, x2=xb8, pair_sum=True)
+    finally:
+        lib.lea_conv3d_bf16_set_pair_split(1)
+    _close(kernels.from_c8(out.contiguous()), want)
+    assert bool((big[:, 0] == 5.0).all()) and bool((big[:, -1] == 5.0).all())
