@@ -75,9 +75,11 @@ const char* lea_conv2d_kernel_name_cin(int B, int cin, int cout, int H, int W);
  * shape. */
 int lea_disparity_set_register_form(int on);
 
-/* Head tap-sum pass 2: 1 (default) = row-staged (R output rows' low-res source rows of the
- * 9 maps in LDS, when they fit 64 KB), 0 = one workgroup per output row gathering through
- * the L1.  Identical bits. */
+/* Head tap-sum: 2 (default, r05) = passes 1 + 2 in one launch (a workgroup computes the
+ * pass-1 values of its R output rows' low-res source rows straight into LDS; the workspace is
+ * not touched), 1 = pass 1 through the workspace, then the row-staged pass 2 (R output rows'
+ * low-res source rows of the 9 maps in LDS), each when those rows fit 64 KB; 0 = pass 1,
+ * then one workgroup per output row gathering through the L1.  Identical bits. */
 int lea_tapsum_set_rows(int on);
 
 /* Host query (no GPU): the exact largest number of source rows a row-staged kernel's

@@ -689,6 +689,13 @@ struct SCfg {
   static constexpr int RPW = RESW / 64;                          // residual pieces per wave
   static constexpr int RINGW = RING * SLOTW + 64 * (4 * PPW - NBK * PIECES);  // + padding pieces
   static constexpr int LDSW = RINGW + 4 * 2 * RESW;  // with two residual slots per wave (dynamic LDS)
+  // B-fragment prefetch distance in k-steps (r05): as deep as keeps 4 waves per SIMD (<= 128
+  // VGPRs) on the one-chunk 16-cout forms; 0 = the compiler's schedule (one MFMA pair ahead)
+#ifdef LEA_BF_PF
+  static constexpr int PF = LEA_BF_PF;
+#else
+  static constexpr int PF = (WC == 1 && MT == 1 && NCH == 1) ? (NB == 2 ? 3 : 2) : 0;
+#endif
   static_assert(RESW % 64 == 0, "whole residual pieces");
   static_assert(LDSW * 16 <= 96 * 1024, "ring + residual");
 };
@@ -829,18 +836,28 @@ __global__ __launch_bounds__(kThreads, 2) void conv_bf16_stream_kernel(const Arg
       sha[m][r] = (a.shift && cv && NCH % 2 == 0) ? a.shift[co] : 0.f;
     }
   const bool relu = a.flags & LEA_RELU;
+  // the output through one buffer resource: every lane issues the same MT * NV 8-byte stores
+  // per step (invalid ones at an out-of-range offset: dropped), so the waits can count them
+  const __amdgpu_buffer_rsrc_t yrs = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(a.y + (long long)b * a.ybs), 0, (unsigned)((a.cout + 7) / 8) * (unsigned)DHW * 16u, 0x00020000);
 
   // Pipeline (issue order = completion order for vmcnt): after step s's barrier the wave
-  // issues step s+1's residual into its slot (s+1) & 1; the end of step s issues planes
-  // 2s+5, 2s+6 (into the slots of planes 2s-3, 2s-2, which only step s-1 read); the top
-  // of step s+1 waits for all but those two planes -- i.e. for step s+1's planes (issued
-  // at the end of step s-1), its residual and step s's stores.
+  // issues step s+1's residual into its slot (s+1) & 1, then planes 2s+5, 2s+6 (into the
+  // slots of planes 2s-3, 2s-2, which only step s-1 read), and step s's MT * NV stores at
+  // its end (r05: the planes used to follow the stores, so the top of step s+1 waited for
+  // step s's stores).  The top of step s+1 waits for all but planes 2s+5, 2s+6 and the
+  // stores -- i.e. for step s+1's planes (issued after step s-1's barrier) and residual.
   if (resid) load_res(s0);
   for (int j = -1; j <= 4; ++j) load_plane(2 * s0 + j);
   for (int s = s0; s < s1; ++s) {
-    wait_vm<2 * C::PPW>();
+    if (s > s0)
+      wait_vm<2 * C::PPW + MT * C::NV>();
+    else
+      wait_vm<2 * C::PPW>();
     __syncthreads();  // everyone's planes landed; everyone done with step s-1
     if (resid && s + 1 < s1) load_res(s + 1);
+    load_plane(2 * s + 5);
+    load_plane(2 * s + 6);
     f32x4 acc[MT][C::NV];
 #pragma unroll
     for (int m = 0; m < MT; ++m)
@@ -850,18 +867,41 @@ __global__ __launch_bounds__(kThreads, 2) void conv_bf16_stream_kernel(const Arg
     float va[MT][C::NV][4];  // LEA_PAIR_SUM: conv a's activation
 #pragma unroll
     for (int c = 0; c < NCH; ++c) {
+      auto ldb = [&](int ks, int i) {
+        const int qrow = wv * C::NV + i;
+        const int t = qrow / TH, r = qrow % TH;
+        return smem[((base + t + kdv[ks]) & 7) * C::SLOTW + c * NB * C::PLANEP + koff[ks] + r * C::RW + n];
+      };
+      if constexpr (C::PF > 0) {
+        // B fragments PF k-steps ahead of their MFMAs, in that issue order
+        bf16x8 bq[C::S][C::NV];
 #pragma unroll
-      for (int ks = 0; ks < C::S; ++ks)
+        for (int ks = 0; ks < C::PF && ks < C::S; ++ks)
 #pragma unroll
-        for (int i = 0; i < C::NV; ++i) {
-          const int qrow = wv * C::NV + i;
-          const int t = qrow / TH, r = qrow % TH;
-          const int word = ((base + t + kdv[ks]) & 7) * C::SLOTW + c * NB * C::PLANEP + koff[ks] + r * C::RW + n;
-          const bf16x8 bv = smem[word];
+          for (int i = 0; i < C::NV; ++i) bq[ks][i] = ldb(ks, i);
 #pragma unroll
-          for (int m = 0; m < MT; ++m)
-            acc[m][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[c][ks][m], bv, acc[m][i], 0, 0, 0);
+        for (int ks = 0; ks < C::S; ++ks) {
+          if (ks + C::PF < C::S)
+#pragma unroll
+            for (int i = 0; i < C::NV; ++i) bq[ks + C::PF][i] = ldb(ks + C::PF, i);
+#pragma unroll
+          for (int i = 0; i < C::NV; ++i)
+#pragma unroll
+            for (int m = 0; m < MT; ++m)
+              acc[m][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[c][ks][m], bq[ks][i], acc[m][i], 0, 0, 0);
+          __builtin_amdgcn_sched_barrier(0);
         }
+      } else {
+#pragma unroll
+        for (int ks = 0; ks < C::S; ++ks)
+#pragma unroll
+          for (int i = 0; i < C::NV; ++i) {
+            const bf16x8 bv = ldb(ks, i);
+#pragma unroll
+            for (int m = 0; m < MT; ++m)
+              acc[m][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[c][ks][m], bv, acc[m][i], 0, 0, 0);
+          }
+      }
       if (NCH % 2 == 0 && c == NCH / 2 - 1 && pair) {
 #pragma unroll
         for (int m = 0; m < MT; ++m)
@@ -880,13 +920,14 @@ __global__ __launch_bounds__(kThreads, 2) void conv_bf16_stream_kernel(const Arg
 #pragma unroll
     for (int m = 0; m < MT; ++m) {
       const int co = cob * C::COB + (mtile0 + m) * 16 + 4 * g;
-      if (co >= a.cout) continue;
-      const long long cofs = (long long)(co / 8) * DHW * 8 + (co % 8);
 #pragma unroll
       for (int i = 0; i < C::NV; ++i) {
         const int qrow = wv * C::NV + i;
         const int d = 2 * s + qrow / TH, h = h0 + qrow % TH, w = w0 + n;
-        if (d >= a.D || h >= a.H || w >= a.W) continue;
+        const bool ok = d < a.D && h < a.H && w < a.W && co < a.cout;
+        const unsigned off = ok ? (unsigned)(co / 8) * (unsigned)DHW * 16u + (unsigned)(co % 8) * 2u +
+                                      (unsigned)(d * HW + h * a.W + w) * 16u
+                                : 0xFFFFFFF0u;
         float v[4];
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
@@ -904,11 +945,9 @@ __global__ __launch_bounds__(kThreads, 2) void conv_bf16_stream_kernel(const Arg
         bf16x4 out;
 #pragma unroll
         for (int r = 0; r < 4; ++r) out[r] = (__bf16)v[r];
-        *reinterpret_cast<bf16x4*>(a.y + (long long)b * a.ybs + cofs + ((long long)d * HW + h * a.W + w) * 8) = out;
+        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2_t, out), yrs, off, 0, 0);
       }
     }
-    load_plane(2 * s + 5);
-    load_plane(2 * s + 6);
   }
   wait_vm<0>();  // no LDS-DMA may outlive the workgroup
 }
@@ -934,6 +973,11 @@ struct PCfg {
   static constexpr int RINGW = RING * SLOTW + 64 * (8 * PPW - NBK * PIECES);  // + padding pieces
   static constexpr int XW = 4 * NV * 16 * 2;                   // a's activations per parity (16-B words)
   static constexpr int LDSW = RINGW + 2 * XW;
+#ifdef LEA_BF_PF
+  static constexpr int PF = LEA_BF_PF > 0 ? LEA_BF_PF : 1;
+#else
+  static constexpr int PF = NB == 2 ? 2 : 1;  // B-fragment prefetch distance (k-steps)
+#endif
   static_assert(VT % 4 == 0, "rows per wave");
   static_assert(2 * LDSW * 16 <= 160 * 1024, "two workgroups per CU");
 };
@@ -1072,15 +1116,27 @@ __global__ __launch_bounds__(512, 2) void conv_bf16_pair_kernel(const Args a, in
 #pragma unroll
     for (int i = 0; i < C::NV; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
     const int base = 2 * s - 1;
+    auto ldb = [&](int ks, int i) {
+      const int qrow = wv * C::NV + i;
+      const int t = qrow / TH, r = qrow % TH;
+      return smem[((base + t + kdv[ks]) & 7) * C::SLOTW + koff[ks] + r * C::RW + n];
+    };
+    // B fragments PF k-steps ahead of their MFMAs, in that issue order (as the stream kernel)
+    bf16x8 bq[C::S][C::NV];
 #pragma unroll
-    for (int ks = 0; ks < C::S; ++ks)
+    for (int ks = 0; ks < C::PF && ks < C::S; ++ks)
 #pragma unroll
-      for (int i = 0; i < C::NV; ++i) {
-        const int qrow = wv * C::NV + i;
-        const int t = qrow / TH, r = qrow % TH;
-        const bf16x8 bv = smem[((base + t + kdv[ks]) & 7) * C::SLOTW + koff[ks] + r * C::RW + n];
-        acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[ks], bv, acc[i], 0, 0, 0);
-      }
+      for (int i = 0; i < C::NV; ++i) bq[ks][i] = ldb(ks, i);
+#pragma unroll
+    for (int ks = 0; ks < C::S; ++ks) {
+      if (ks + C::PF < C::S)
+#pragma unroll
+        for (int i = 0; i < C::NV; ++i) bq[ks + C::PF][i] = ldb(ks + C::PF, i);
+#pragma unroll
+      for (int i = 0; i < C::NV; ++i)
+        acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[ks], bq[ks][i], acc[i], 0, 0, 0);
+      __builtin_amdgcn_sched_barrier(0);
+    }
     if (part == 0) {
 #pragma unroll
       for (int i = 0; i < C::NV; ++i) {
@@ -1378,6 +1434,10 @@ static int bf16_conv_common(bf::Args& a, int B, int k, bool cv, void* stream) {
       return LEA_E_UNSUPPORTED;
     }
   }
+  // the D-streaming kernels address one batch element's input, residual and output blocks
+  // through 32-bit buffer offsets
+  LEA_CHECK_ARG(p.nsplit <= 0 || (long long)std::max(a.cin, a.cout) / 8 * a.D * a.H * a.W * 16 < (1LL << 32),
+                "lea_conv3d(bf16): batch element too large for the D-streaming kernel");
   const int cobv = bf::cob_of(a.cout);
   a.ncob = (a.cout + cobv - 1) / cobv;
   a.nchunks = (a.cin / 8 + p.nb - 1) / p.nb;

@@ -172,6 +172,48 @@ __global__ __launch_bounds__(512) void tapsum_hwpass_f32(
   }
 }
 
+// pass 2's output phase: R output rows (h0..h1) of plane (b, co, d) from the staged rows
+// [9][nrmax][Wi] (low-res rows r_lo..), 36 LDS corner values per output
+__device__ __forceinline__ void tapsum_rows_out(const float* __restrict__ rows, float* __restrict__ y, long long ybs,
+                                                int b, int co, int d, int h0, int h1, int r_lo, bool over, int nrmax,
+                                                int Wi, int Do, int Ho, int Wo, float rh, float rw, int Hi,
+                                                const float* __restrict__ scale, const float* __restrict__ shift,
+                                                unsigned flags) {
+#pragma clang fp contract(off)
+  const float sc = scale ? scale[co] : 1.f, sh = scale ? shift[co] : 0.f;
+  const int cells = (h1 - h0) * Wo;
+  for (int t = threadIdx.x; t < cells; t += blockDim.x) {
+    const int h = h0 + t / Wo, w = t % Wo;
+    Axis ah[3];
+    bool hok[3];
+#pragma unroll
+    for (int kh = 0; kh < 3; ++kh) {
+      const int p = h + kh - 1;
+      hok[kh] = (unsigned)p < (unsigned)Ho;
+      ah[kh] = axis_index(rh, hok[kh] ? p : 0, Hi, Ho, 1);
+    }
+    float acc = 0.f;
+#pragma unroll
+    for (int kw = 0; kw < 3; ++kw) {
+      const int p = w + kw - 1;
+      if ((unsigned)p >= (unsigned)Wo) continue;
+      const Axis aw = axis_index(rw, p, Wi, Wo, 1);
+#pragma unroll
+      for (int kh = 0; kh < 3; ++kh) {
+        if (!hok[kh]) continue;
+        const float* tm = rows + (kh * 3 + kw) * nrmax * Wi;
+        const float* r0 = tm + (over ? 0 : ah[kh].i0 - r_lo) * Wi;
+        const float* r1 = tm + (over ? 0 : ah[kh].i1 - r_lo) * Wi;
+        acc += ah[kh].l0 * (aw.l0 * r0[aw.i0] + aw.l1 * r0[aw.i1]) +
+               ah[kh].l1 * (aw.l0 * r1[aw.i0] + aw.l1 * r1[aw.i1]);
+      }
+    }
+    if (scale) acc = acc * sc + sh;
+    if (flags & LEA_RELU) acc = fmaxf(acc, 0.f);
+    y[(long long)b * ybs + (((long long)co * Do + d) * Ho + h) * Wo + w] = over ? __builtin_nanf("") : acc;
+  }
+}
+
 // pass 2, row-staged (r03): a workgroup owns R output rows of one plane; the <= nrmax
 // low-res rows of the 9 (kh, kw) maps they read are copied into LDS once (coalesced),
 // then every output sums its 36 corner values from LDS instead of gathering them through
@@ -216,48 +258,116 @@ __global__ __launch_bounds__(256) void tapsum_hwpass_rows_f32(
     }
   }
   __syncthreads();
-  const float sc = scale ? scale[co] : 1.f, sh = scale ? shift[co] : 0.f;
-  const int cells = (h1 - h0) * Wo;
-  for (int t = threadIdx.x; t < cells; t += blockDim.x) {
-    const int h = h0 + t / Wo, w = t % Wo;
-    Axis ah[3];
-    bool hok[3];
+  tapsum_rows_out(rows, y, ybs, b, co, d, h0, h1, r_lo, over, nrmax, Wi, Do, Ho, Wo, rh, rw, Hi, scale, shift, flags);
+}
+
+// passes 1 + 2 in one launch (r05): a workgroup computes the pass-1 values of the <= nrmax
+// low-res rows its R output rows read, for all 9 (kh, kw) maps, straight into LDS (same
+// expression and kd order as tapsum_dpass_f32 / _c8: identical bits), then runs pass 2's
+// output phase -- the 9-map workspace never goes through HBM.  Workgroups walk d fastest
+// within (b, co, row block), XCD-contiguous, so the Q planes neighbouring d values share stay
+// in L2.  C8: q in the bf16 c8 layout; else f32 NCDHW (VEC: float4 along Wi).
+template <bool C8, bool VEC>
+__global__ __launch_bounds__(256) void tapsum_fused(const void* __restrict__ qv, long long qbs,
+                                                    float* __restrict__ y, long long ybs, int cout, int Di,
+                                                    int Hi, int Wi, int Do, int Ho, int Wo, float rd, float rh,
+                                                    float rw, const float* __restrict__ scale,
+                                                    const float* __restrict__ shift, unsigned flags, int R,
+                                                    int nrmax, int nhb, int nblk) {
+#pragma clang fp contract(off)
+  extern __shared__ float rows[];  // [9][nrmax][Wi]
+  const int xcd = blockIdx.x % 8, idx = blockIdx.x / 8;
+  const int q8 = nblk / 8, r8 = nblk % 8;
+  const int lin = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + idx;
+  const int d = lin % Do;
+  const int hb = (lin / Do) % nhb;
+  const int bc = lin / (Do * nhb);  // b * cout + co
+  const int co = bc % cout, b = bc / cout;
+  const int h0 = hb * R;
+  const int h1 = min(h0 + R, Ho);
+  const int r_lo = axis_index(rh, max(h0 - 1, 0), Hi, Ho, 1).i0;
+  const int r_hi = axis_index(rh, min(h1, Ho - 1), Hi, Ho, 1).i1;
+  const bool over = r_hi - r_lo + 1 > nrmax;
+  const int nr = over ? 0 : r_hi - r_lo + 1;
+  const long long HWi = (long long)Hi * Wi;
+  const long long vol = HWi * Di;
+  Axis ad[3];
+  bool dok[3];
 #pragma unroll
-    for (int kh = 0; kh < 3; ++kh) {
-      const int p = h + kh - 1;
-      hok[kh] = (unsigned)p < (unsigned)Ho;
-      ah[kh] = axis_index(rh, hok[kh] ? p : 0, Hi, Ho, 1);
+  for (int kd = 0; kd < 3; ++kd) {
+    const int pd = d + kd - 1;
+    dok[kd] = (unsigned)pd < (unsigned)Do;
+    ad[kd] = axis_index(rd, dok[kd] ? pd : 0, Di, Do, 1);
+  }
+  if constexpr (C8) {
+    const bf16x8_t* qw = reinterpret_cast<const bf16x8_t*>(reinterpret_cast<const __bf16*>(qv) + (long long)b * qbs);
+    for (int e = threadIdx.x; e < nr * Wi; e += blockDim.x) {
+      const long long pos = (long long)r_lo * Wi + e;  // (row r_lo + e / Wi, column e % Wi)
+      float acc[9] = {};
+#pragma unroll
+      for (int kd = 0; kd < 3; ++kd) {
+        if (!dok[kd]) continue;
+        const int cb = co * 27 + kd * 9;
+        const bf16x8_t* blk0 = qw + (long long)(cb / 8) * vol;
+        const bf16x8_t* blk1 = blk0 + vol;
+        const bf16x8_t a0 = blk0[ad[kd].i0 * HWi + pos], a1 = blk1[ad[kd].i0 * HWi + pos];
+        const bf16x8_t b0 = blk0[ad[kd].i1 * HWi + pos], b1 = blk1[ad[kd].i1 * HWi + pos];
+        switch (cb % 8) {
+          case 0: tapsum_acc9<0>(acc, a0, a1, b0, b1, ad[kd].l0, ad[kd].l1); break;
+          case 1: tapsum_acc9<1>(acc, a0, a1, b0, b1, ad[kd].l0, ad[kd].l1); break;
+          case 2: tapsum_acc9<2>(acc, a0, a1, b0, b1, ad[kd].l0, ad[kd].l1); break;
+          case 3: tapsum_acc9<3>(acc, a0, a1, b0, b1, ad[kd].l0, ad[kd].l1); break;
+          case 4: tapsum_acc9<4>(acc, a0, a1, b0, b1, ad[kd].l0, ad[kd].l1); break;
+          case 5: tapsum_acc9<5>(acc, a0, a1, b0, b1, ad[kd].l0, ad[kd].l1); break;
+          case 6: tapsum_acc9<6>(acc, a0, a1, b0, b1, ad[kd].l0, ad[kd].l1); break;
+          default: tapsum_acc9<7>(acc, a0, a1, b0, b1, ad[kd].l0, ad[kd].l1);
+        }
+      }
+#pragma unroll
+      for (int k = 0; k < 9; ++k) rows[k * nrmax * Wi + e] = acc[k];
     }
-    float acc = 0.f;
+  } else {
+    const float* qb = reinterpret_cast<const float*>(qv) + (long long)b * qbs + (long long)co * 27 * vol;
+    constexpr int V = VEC ? 4 : 1;
+    for (int e = threadIdx.x; e < nr * Wi / V; e += blockDim.x) {
+      const long long pos = (long long)r_lo * Wi + (long long)e * V;
 #pragma unroll
-    for (int kw = 0; kw < 3; ++kw) {
-      const int p = w + kw - 1;
-      if ((unsigned)p >= (unsigned)Wo) continue;
-      const Axis aw = axis_index(rw, p, Wi, Wo, 1);
+      for (int k = 0; k < 9; ++k) {
+        float acc[V] = {};
 #pragma unroll
-      for (int kh = 0; kh < 3; ++kh) {
-        if (!hok[kh]) continue;
-        const float* tm = rows + (kh * 3 + kw) * nrmax * Wi;
-        const float* r0 = tm + (over ? 0 : ah[kh].i0 - r_lo) * Wi;
-        const float* r1 = tm + (over ? 0 : ah[kh].i1 - r_lo) * Wi;
-        acc += ah[kh].l0 * (aw.l0 * r0[aw.i0] + aw.l1 * r0[aw.i1]) +
-               ah[kh].l1 * (aw.l0 * r1[aw.i0] + aw.l1 * r1[aw.i1]);
+        for (int kd = 0; kd < 3; ++kd) {
+          if (!dok[kd]) continue;
+          const float* q0 = qb + (long long)(kd * 9 + k) * vol + ad[kd].i0 * HWi + pos;
+          const float* q1 = qb + (long long)(kd * 9 + k) * vol + ad[kd].i1 * HWi + pos;
+          if constexpr (VEC) {
+            const float4 a = *reinterpret_cast<const float4*>(q0);
+            const float4 c = *reinterpret_cast<const float4*>(q1);
+            acc[0] += ad[kd].l0 * a.x + ad[kd].l1 * c.x;
+            acc[1] += ad[kd].l0 * a.y + ad[kd].l1 * c.y;
+            acc[2] += ad[kd].l0 * a.z + ad[kd].l1 * c.z;
+            acc[3] += ad[kd].l0 * a.w + ad[kd].l1 * c.w;
+          } else {
+            acc[0] += ad[kd].l0 * q0[0] + ad[kd].l1 * q1[0];
+          }
+        }
+#pragma unroll
+        for (int j = 0; j < V; ++j) rows[k * nrmax * Wi + e * V + j] = acc[j];
       }
     }
-    if (scale) acc = acc * sc + sh;
-    if (flags & LEA_RELU) acc = fmaxf(acc, 0.f);
-    y[(long long)b * ybs + (((long long)co * Do + d) * Ho + h) * Wo + w] = over ? __builtin_nanf("") : acc;
   }
+  __syncthreads();
+  tapsum_rows_out(rows, y, ybs, b, co, d, h0, h1, r_lo, over, nrmax, Wi, Do, Ho, Wo, rh, rw, Hi, scale, shift, flags);
 }
 
 }  // namespace lea
 
-// lea_tapsum_set_rows: 1 (default) = the row-staged pass 2 when R output rows' sources
-// fit 64 KB of LDS, 0 = one workgroup per output row gathering through the L1
-static int g_tapsum_rows = 1;
+// lea_tapsum_set_rows: 2 (default, r05) = passes 1 + 2 fused (tapsum_fused), 1 = the
+// row-staged pass 2 after pass 1 through the workspace, each when R output rows' sources fit
+// 64 KB of LDS; 0 = pass 1, then one workgroup per output row gathering through the L1
+static int g_tapsum_rows = 2;
 extern "C" int lea_tapsum_set_rows(int on) {
   lea::clear_error();
-  LEA_CHECK_ARG(on == 0 || on == 1, "lea_tapsum_set_rows: %d", on);
+  LEA_CHECK_ARG(on >= 0 && on <= 2, "lea_tapsum_set_rows: %d", on);
   g_tapsum_rows = on;
   return 0;
 }
@@ -312,19 +422,41 @@ extern "C" int lea_tapsum_upsample(const void* q, int64_t q_bstride, void* y, in
   hipStream_t st = as_stream(stream);
   float* ws = (float*)workspace;
   const long long HWi = (long long)Hi * Wi;
+  const float rd = axis_ratio(Di, Do, 1);
+  const bool vec = (HWi % 4) == 0 && ((uintptr_t)q % 16) == 0 && (q_bstride % 4) == 0 &&
+                   ((long long)Di * HWi) % 4 == 0 && ((uintptr_t)ws % 16) == 0;
+  if (g_tapsum_rows == 2) {
+    const float rh = axis_ratio(Hi, Ho, 1), rw = axis_ratio(Wi, Wo, 1);
+    for (int R = 8; R >= 2; R /= 2) {
+      const int nrmax = staged_rows(Hi, Ho, 1, R, 1);
+      const size_t lds = (size_t)9 * nrmax * Wi * sizeof(float);
+      if (lds > 65536) continue;
+      const int nhb = (Ho + R - 1) / R;
+      const long long nb = (long long)B * cout * Do * nhb;
+      if (nb >= (1LL << 31)) break;
+      const bool v4 = dtype == LEA_F32 && vec && Wi % 4 == 0;
+      const dim3 g((unsigned)nb);
+      if (dtype == LEA_BF16)
+        tapsum_fused<true, false><<<g, 256, lds, st>>>(q, q_bstride, (float*)y, y_bstride, cout, Di, Hi, Wi, Do,
+                                                       Ho, Wo, rd, rh, rw, scale, shift, flags, R, nrmax, nhb, (int)nb);
+      else if (v4)
+        tapsum_fused<false, true><<<g, 256, lds, st>>>(q, q_bstride, (float*)y, y_bstride, cout, Di, Hi, Wi, Do,
+                                                       Ho, Wo, rd, rh, rw, scale, shift, flags, R, nrmax, nhb, (int)nb);
+      else
+        tapsum_fused<false, false><<<g, 256, lds, st>>>(q, q_bstride, (float*)y, y_bstride, cout, Di, Hi, Wi, Do,
+                                                        Ho, Wo, rd, rh, rw, scale, shift, flags, R, nrmax, nhb, (int)nb);
+      return launch_status("lea_tapsum_upsample");
+    }
+  }
   if (dtype == LEA_BF16) {
     dim3 g1((unsigned)((HWi + 255) / 256), (unsigned)(B * cout * Do));
-    tapsum_dpass_c8<<<g1, 256, 0, st>>>((const __bf16*)q, q_bstride, ws, cout, Di, Hi, Wi, Do,
-                                        axis_ratio(Di, Do, 1));
+    tapsum_dpass_c8<<<g1, 256, 0, st>>>((const __bf16*)q, q_bstride, ws, cout, Di, Hi, Wi, Do, rd);
     const int rc = launch_status("lea_tapsum_upsample");
     if (rc) return rc;
     return hwpass(ws, y, y_bstride, B, cout, Hi, Wi, Do, Ho, Wo, scale, shift, flags, st);
   }
-  const bool vec = (HWi % 4) == 0 && ((uintptr_t)q % 16) == 0 && (q_bstride % 4) == 0 &&
-                   ((long long)Di * HWi) % 4 == 0 && ((uintptr_t)ws % 16) == 0;
   const long long n = vec ? HWi / 4 : HWi;
   dim3 g1((unsigned)((n + 255) / 256), (unsigned)(B * cout * Do * 9));
-  const float rd = axis_ratio(Di, Do, 1);
   if (vec)
     tapsum_dpass_f32<true><<<g1, 256, 0, st>>>((const float*)q, q_bstride, ws, cout, Di, Hi, Wi, Do, rd);
   else

@@ -248,20 +248,23 @@ def test_head_tapsum_upsample_vs_torch(cout, cin, src, dst):
 @pytest.mark.parametrize("b,cout,src,dst", [(1, 1, (32, 96, 160), (64, 192, 320)), (2, 2, (3, 5, 9), (5, 9, 17)),
                                            (1, 1, (4, 13, 7), (8, 26, 14)), (1, 1, (16, 48, 252), (32, 96, 504))])
 def test_head_tapsum_rows_pass_is_the_gather_pass(b, cout, src, dst):
-    """The row-staged pass 2 of the tap-sum head (the default) and the per-row gather pass
-    produce identical bits, f32 and bf16 (c8) partial sums alike."""
+    """The fused tap-sum head (passes 1 + 2 in one launch, the default since r05), the
+    row-staged pass 2 after pass 1 and the per-row gather pass produce identical bits, f32
+    and bf16 (c8) partial sums alike; a non-float4 f32 layout too (odd W)."""
     lib = _lib.load()
     g = torch.Generator().manual_seed(13)
     q = torch.randn((b, 27 * cout) + src, generator=g).to(DEV)
     qc = kernels.to_c8(torch.cat([q, torch.zeros((b, (-27 * cout) % 8) + src, device=DEV)], 1))
     out = {}
-    for on in (1, 0):
+    for on in (2, 1, 0):
         assert lib.lea_tapsum_set_rows(on) == 0
         try:
             out[on] = (kernels.tapsum_upsample(q, cout, dst), kernels.tapsum_upsample_bf16(qc, cout, dst))
         finally:
-            lib.lea_tapsum_set_rows(1)
-    assert torch.equal(out[1][0], out[0][0]) and torch.equal(out[1][1], out[0][1])
+            lib.lea_tapsum_set_rows(2)
+    for on in (1, 0):
+        assert torch.equal(out[2][0], out[on][0]) and torch.equal(out[2][1], out[on][1]), on
+    assert not torch.isnan(out[2][0]).any()
 
 
 def test_resample_affine_relu_epilogue_into_slice():
