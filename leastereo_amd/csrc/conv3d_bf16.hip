@@ -690,11 +690,13 @@ struct SCfg {
   static constexpr int RINGW = RING * SLOTW + 64 * (4 * PPW - NBK * PIECES);  // + padding pieces
   static constexpr int LDSW = RINGW + 4 * 2 * RESW;  // with two residual slots per wave (dynamic LDS)
   // B-fragment prefetch distance in k-steps (r05): as deep as keeps 4 waves per SIMD (<= 128
-  // VGPRs) on the one-chunk 16-cout forms; 0 = the compiler's schedule (one MFMA pair ahead)
+  // VGPRs) on the one-chunk 16-cout forms; 2 on the two-chunk forms (two waves per SIMD
+  // already: 204 / 240 VGPRs; same box C4 +1.3-2 %, 3 was no better); 0 = the compiler's
+  // schedule (one MFMA pair ahead)
 #ifdef LEA_BF_PF
   static constexpr int PF = LEA_BF_PF;
 #else
-  static constexpr int PF = (WC == 1 && MT == 1 && NCH == 1) ? (NB == 2 ? 3 : 2) : 0;
+  static constexpr int PF = (WC == 1 && MT == 1 && NCH == 1) ? (NB == 2 ? 3 : 2) : (NCH == 2 ? 2 : 0);
 #endif
   static_assert(RESW % 64 == 0, "whole residual pieces");
   static_assert(LDSW * 16 <= 96 * 1024, "ring + residual");
