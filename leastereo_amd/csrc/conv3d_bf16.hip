@@ -962,10 +962,19 @@ __global__ __launch_bounds__(kThreads, 2) void conv_bf16_stream_kernel(const Arg
 // bf16 (the rounding the two-launch form applies to a's output), and the conv-b wave adds it in
 // its epilogue of step s, deferred to after the next step's barrier; the ring holds both
 // sources' planes (blocks a0..a(NB-1), b0..b(NB-1) per slot).
-template <int TH, int NB>
+// PP (the 8 -> 8 steps, cout <= 8, NB = 1; r05): "plane-paired" M rows -- the MFMA's 16 rows are
+// the 8 couts of output plane 2s (rows 0-7) and of plane 2s+1 (rows 8-15), so one 16 x 16 tile
+// covers both planes of an H row and no row is the zero padding of an 8-cout block.  K runs over
+// the 4 input planes 2s-1 .. 2s+2 (36 (plane, kh, kw) slots = 9 k-steps instead of 7 per plane
+// pair's rows: 9 MFMAs and B reads per H row and step instead of 14); rows 0-7 take kd = plane - 0,
+// rows 8-15 kd = plane - 1 (zero outside 0..2).  Those A fragments are gathered once from the
+// ordinary packing (each is one of its 16-byte words, or zero), so the weights need no own layout.
+template <int TH, int NB, bool PP = false>
 struct PCfg {
-  static constexpr int TD = 2, VT = TH * TD, NV = VT / 4;     // 16-voxel rows per wave
-  static constexpr int T = 27, S = (T * NB + 3) / 4;          // k-steps of one conv
+  static constexpr int TD = 2, VT = TH * TD;
+  static constexpr int NV = PP ? TH / 4 : VT / 4;             // MFMA rows per wave (H rows if PP)
+  static constexpr int T = 27, S0 = (T * NB + 3) / 4;         // k-steps of one conv's packing
+  static constexpr int S = PP ? 9 : S0;                       // k-steps of the tile
   static constexpr int NBK = 2 * NB;                          // blocks per ring slot
   static constexpr int RH = TH + 2, RW = 18, PLANE = RH * RW;
   static constexpr int PIECES = (PLANE + 63) / 64, PLANEP = 64 * PIECES;
@@ -978,15 +987,15 @@ struct PCfg {
 #ifdef LEA_BF_PF
   static constexpr int PF = LEA_BF_PF > 0 ? LEA_BF_PF : 1;
 #else
-  static constexpr int PF = NB == 2 ? 2 : 1;  // B-fragment prefetch distance (k-steps)
+  static constexpr int PF = NB == 2 ? 2 : (PP ? 2 : 1);  // B-fragment prefetch distance (k-steps)
 #endif
-  static_assert(VT % 4 == 0, "rows per wave");
+  static_assert(VT % 4 == 0 && (!PP || (NB == 1 && TH % 4 == 0)), "rows per wave");
   static_assert(2 * LDSW * 16 <= 160 * 1024, "two workgroups per CU");
 };
 
-template <int TH, int NB>
+template <int TH, int NB, bool PP>
 __global__ __launch_bounds__(512, 2) void conv_bf16_pair_kernel(const Args a, int nsplit) {
-  using C = PCfg<TH, NB>;
+  using C = PCfg<TH, NB, PP>;
   extern __shared__ __attribute__((aligned(16))) bf16x8 smem[];  // ring + a's activations
   const unsigned lds0 = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)(lds_void*)smem);
   const int tid = threadIdx.x, lane = tid & 63;
@@ -1048,20 +1057,37 @@ __global__ __launch_bounds__(512, 2) void conv_bf16_pair_kernel(const Args a, in
 #pragma unroll
   for (int ks = 0; ks < C::S; ++ks) {
     const int slot = 4 * ks + g;
-    const int tap = min(slot / NB, C::T - 1);  // slots past the last tap carry zero weights
-    const int blk = slot % NB + part * NB;
-    kdv[ks] = tap / 9;
-    koff[ks] = blk * C::PLANEP + ((tap / 3) % 3) * C::RW + tap % 3;
+    if (PP) {  // slot = (input plane 2s-1 + j) x (kh, kw)
+      const int j = slot / 9, t2 = slot % 9;
+      kdv[ks] = j;
+      koff[ks] = part * C::PLANEP + (t2 / 3) * C::RW + t2 % 3;
+    } else {
+      const int tap = min(slot / NB, C::T - 1);  // slots past the last tap carry zero weights
+      const int blk = slot % NB + part * NB;
+      kdv[ks] = tap / 9;
+      koff[ks] = blk * C::PLANEP + ((tap / 3) % 3) * C::RW + tap % 3;
+    }
   }
   // this wave's conv: chunk `part` of the pair's packed weights (conv a's pack, then b's)
   const bf16x8* wpv = reinterpret_cast<const bf16x8*>(a.wp);
   bf16x8 av[C::S];
 #pragma unroll
-  for (int ks = 0; ks < C::S; ++ks) av[ks] = wpv[((long long)part * C::S + ks) * 64 + g * 16 + n];
+  for (int ks = 0; ks < C::S; ++ks) {
+    if (PP) {
+      // row n: cout n % 8 of output plane 2s + n / 8, whose kd for input plane 2s-1 + j is j - n / 8;
+      // its 8 channels of tap (kd, kh, kw) are word (tap / 4, tap % 4, cout) of the packing
+      const int slot = 4 * ks + g, j = slot / 9, t2 = slot % 9;
+      const int kd = j - n / 8, co = n % 8, tap = kd * 9 + t2;
+      const bool ok = kd >= 0 && kd <= 2 && co < a.cout;
+      av[ks] = ok ? wpv[((long long)part * C::S0 + tap / 4) * 64 + (tap % 4) * 16 + co] : bf16x8{};
+    } else {
+      av[ks] = wpv[((long long)part * C::S + ks) * 64 + g * 16 + n];
+    }
+  }
   float sc[4], sh[4];
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
-    const int co = 4 * g + r;
+    const int co = (PP ? 4 * (g % 2) : 4 * g) + r;  // PP: lane group g holds plane 2s + g / 2
     sc[r] = (a.scale && co < a.cout) ? a.scale[part * a.cout + co] : 1.f;
     sh[r] = (a.shift && co < a.cout) ? a.shift[part * a.cout + co] : 0.f;
   }
@@ -1079,9 +1105,9 @@ __global__ __launch_bounds__(512, 2) void conv_bf16_pair_kernel(const Args a, in
 #pragma unroll
     for (int i = 0; i < C::NV; ++i) {
       const int qrow = wv * C::NV + i;
-      const int d = 2 * s + qrow / TH, h = h0 + qrow % TH, w = w0 + n;
+      const int d = 2 * s + (PP ? g / 2 : qrow / TH), h = h0 + (PP ? qrow : qrow % TH), w = w0 + n;
       const bf16x4 va = *reinterpret_cast<const bf16x4*>(xa_lds + xoff(s & 1, i));
-      const int co = 4 * g;
+      const int co = PP ? 4 * (g % 2) : 4 * g;
       const bool ok = d < a.D && h < a.H && w < a.W && co < a.cout;
       const unsigned off = ok ? (unsigned)(co / 8) * (unsigned)DHW * 16u + (unsigned)(co % 8) * 2u +
                                     (unsigned)(d * HW + h * a.W + w) * 16u
@@ -1120,7 +1146,7 @@ __global__ __launch_bounds__(512, 2) void conv_bf16_pair_kernel(const Args a, in
     const int base = 2 * s - 1;
     auto ldb = [&](int ks, int i) {
       const int qrow = wv * C::NV + i;
-      const int t = qrow / TH, r = qrow % TH;
+      const int t = PP ? 0 : qrow / TH, r = PP ? qrow : qrow % TH;
       return smem[((base + t + kdv[ks]) & 7) * C::SLOTW + koff[ks] + r * C::RW + n];
     };
     // B fragments PF k-steps ahead of their MFMAs, in that issue order (as the stream kernel)
@@ -1169,7 +1195,8 @@ struct Plan {
 int g_override[3] = {0, 0, 0};  // th, td, mt (lea_conv3d_bf16_set_tile_override)
 int g_variant = 0;              // lea_conv3d_bf16_set_variant: 0 planner, 1 tile kernel only
 int g_stream1x1 = 1;            // lea_conv3d_bf16_set_stream1x1
-int g_pair_split = 1;           // lea_conv3d_bf16_set_pair_split: LEA_PAIR_SUM on the split-wave kernel
+int g_pair_split = 2;           // lea_conv3d_bf16_set_pair_split: LEA_PAIR_SUM on the split-wave kernel
+                                // (2: the plane-paired tile for the 8 -> 8 steps)
 
 inline Plan plan(int B, int cout, int D, int H, int W, int ks, int cin) {
   // r01 sweep (tools/conv_sweep.py --bf16, profiles/r01_conv_sweep_bf16.txt): one
@@ -1266,7 +1293,7 @@ int run(const Plan& p, Args a, int B, hipStream_t st, bool cv) {
     return launch_status("lea_conv3d(bf16 1x1)");
   }
   if ((a.flags & LEA_PAIR_SUM) && g_pair_split && p.nsplit > 0 && a.ncob == 1 && (a.nchunks == 2) &&
-      ((p.nb == 2 && p.th == 4) || (p.nb == 1 && p.th == 8))) {
+      ((p.nb == 2 && p.th == 4 && g_pair_split != 3) || (p.nb == 1 && p.th == 8))) {
     // the split-wave pair kernel (conv a / conv b on separate wave halves)
     a.tiles_w = (a.W + 15) / 16;
     a.ntiles = a.tiles_w * ((a.H + p.th - 1) / p.th);
@@ -1276,9 +1303,11 @@ int run(const Plan& p, Args a, int B, hipStream_t st, bool cv) {
                   "lea_conv3d(bf16 pair): volume too large");
     a.nblk = (int)nb_;
     if (p.nb == 2)
-      conv_bf16_pair_kernel<4, 2><<<dim3((unsigned)nb_), 512, PCfg<4, 2>::LDSW * 16, st>>>(a, p.nsplit);
+      conv_bf16_pair_kernel<4, 2, false><<<dim3((unsigned)nb_), 512, PCfg<4, 2>::LDSW * 16, st>>>(a, p.nsplit);
+    else if (g_pair_split >= 2 && a.cout <= 8)
+      conv_bf16_pair_kernel<8, 1, true><<<dim3((unsigned)nb_), 512, PCfg<8, 1, true>::LDSW * 16, st>>>(a, p.nsplit);
     else
-      conv_bf16_pair_kernel<8, 1><<<dim3((unsigned)nb_), 512, PCfg<8, 1>::LDSW * 16, st>>>(a, p.nsplit);
+      conv_bf16_pair_kernel<8, 1, false><<<dim3((unsigned)nb_), 512, PCfg<8, 1>::LDSW * 16, st>>>(a, p.nsplit);
     return launch_status("lea_conv3d(bf16 pair)");
   }
   // (one source, or LEA_PAIR_SUM's two: the ring walks the blocks of both)
@@ -1362,7 +1391,7 @@ extern "C" int lea_conv3d_bf16_set_stream1x1(int on) {
 
 extern "C" int lea_conv3d_bf16_set_pair_split(int on) {
   clear_error();
-  LEA_CHECK_ARG(on == 0 || on == 1, "lea_conv3d_bf16_set_pair_split: %d", on);
+  LEA_CHECK_ARG(on >= 0 && on <= 3, "lea_conv3d_bf16_set_pair_split: %d", on);
   bf::g_pair_split = on;
   return 0;
 }

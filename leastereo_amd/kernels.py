@@ -574,6 +574,16 @@ def conv_kernel_name_bf16(b, cout, cin, d, h, w, k, costvolume=False):
     return name.decode() if name else None
 
 
+def _pair_kernel_name_bf16(cb: int) -> str:
+    """The LEA_PAIR_SUM launch's kernel (conv3d_bf16.hip run(): the split-wave kernel unless
+    LEASTEREO_PAIR_SPLIT=0, the two-source D-streaming kernel otherwise) for the probe."""
+    th = 8 if cb == 1 else 4
+    split = os.environ.get("LEASTEREO_PAIR_SPLIT", "2")
+    if split != "0":
+        return f"conv_bf16_pair_kernel<{th}, {cb}, {'true' if split == '2' and cb == 1 else 'false'}>"
+    return f"conv_bf16_stream_kernel<1, 1, {th}, {cb}, 2>"
+
+
 def conv3d_bnrelu_bf16(x: torch.Tensor, packed: torch.Tensor, cout: int, k: int,
                        scale: torch.Tensor | None, shift: torch.Tensor | None, relu: bool = True,
                        out: torch.Tensor | None = None, accumulate: bool = False,
@@ -614,7 +624,7 @@ def conv3d_bnrelu_bf16(x: torch.Tensor, packed: torch.Tensor, cout: int, k: int,
     flags = (LEA_RELU if relu else 0) | (LEA_RESIDUAL if rptr is not None else 0) | (LEA_PAIR_SUM if pair_sum else 0)
     rec = None if _probe is None else _probe_begin(
         b, cb * 8 + cin2, cout, d, h, w, k, rptr is not None, b * d * h * w, False,
-        name=(f"conv_bf16_stream_kernel<1, 1, {8 if cb == 1 else 4}, {cb}, 2>" if pair_sum else
+        name=(_pair_kernel_name_bf16(cb) if pair_sum else
               conv_kernel_name_bf16(b, cout, cb * 8 + cin2, d, h, w, k)), esz=2)
     check(_lib.load().lea_conv3d_bnrelu_bf16(
         x.data_ptr(), xbs, x2.data_ptr() if x2 is not None else None, x2bs, cin2, packed.data_ptr(),
