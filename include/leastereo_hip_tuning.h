@@ -40,11 +40,12 @@ int lea_conv3d_bf16_set_variant(int variant);
  * bit-identical to the tile kernel), 0 = the tile kernel. */
 int lea_conv3d_bf16_set_stream1x1(int on);
 
-/* LEA_PAIR_SUM on the bf16 engine: 2 (default) = the split-wave pair kernel (8 waves, conv a on
- * waves 0-3 and conv b on 4-7, a's activation handed over in LDS; "conv_bf16_pair_kernel<TH, NB,
- * PP>"), with the 8 -> 8 steps (cout <= 8) on its plane-paired tile (PP: the MFMA rows are the
- * couts of both output planes); 1 = the split-wave kernel without PP; 0 = the D-streaming kernel
- * with both convs' weights in every wave. */
+/* LEA_PAIR_SUM on the bf16 engine: 3 (default) = the 8 -> 8 steps (cout <= 8) on the split-wave
+ * pair kernel's plane-paired tile ("conv_bf16_pair_kernel<8, 1, true>": 8 waves, conv a on waves
+ * 0-3 and conv b on 4-7, a's activation handed over in LDS; the MFMA rows are the couts of both
+ * output planes), the 16-channel steps on the D-streaming kernel with both convs' weights in every
+ * wave; 2 = the split-wave kernel for both (PP for the 8 -> 8 steps); 1 = the split-wave kernel
+ * without PP; 0 = the D-streaming kernel for both. */
 int lea_conv3d_bf16_set_pair_split(int on);
 
 /* Output words per thread of the c8 resample, k in {1, 2, 4}; 0 restores the default

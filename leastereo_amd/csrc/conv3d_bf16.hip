@@ -1195,8 +1195,9 @@ struct Plan {
 int g_override[3] = {0, 0, 0};  // th, td, mt (lea_conv3d_bf16_set_tile_override)
 int g_variant = 0;              // lea_conv3d_bf16_set_variant: 0 planner, 1 tile kernel only
 int g_stream1x1 = 1;            // lea_conv3d_bf16_set_stream1x1
-int g_pair_split = 2;           // lea_conv3d_bf16_set_pair_split: LEA_PAIR_SUM on the split-wave kernel
-                                // (2: the plane-paired tile for the 8 -> 8 steps)
+int g_pair_split = 3;           // lea_conv3d_bf16_set_pair_split: LEA_PAIR_SUM on the split-wave kernel
+                                // (2: the plane-paired tile for the 8 -> 8 steps; 3: that, and the
+                                // 16-channel steps on the two-source D-streaming kernel)
 
 inline Plan plan(int B, int cout, int D, int H, int W, int ks, int cin) {
   // r01 sweep (tools/conv_sweep.py --bf16, profiles/r01_conv_sweep_bf16.txt): one

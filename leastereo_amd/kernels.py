@@ -578,9 +578,9 @@ def _pair_kernel_name_bf16(cb: int) -> str:
     """The LEA_PAIR_SUM launch's kernel (conv3d_bf16.hip run(): the split-wave kernel unless
     LEASTEREO_PAIR_SPLIT=0, the two-source D-streaming kernel otherwise) for the probe."""
     th = 8 if cb == 1 else 4
-    split = os.environ.get("LEASTEREO_PAIR_SPLIT", "2")
-    if split != "0":
-        return f"conv_bf16_pair_kernel<{th}, {cb}, {'true' if split == '2' and cb == 1 else 'false'}>"
+    split = os.environ.get("LEASTEREO_PAIR_SPLIT", "3")
+    if split in ("1", "2") or (split == "3" and cb == 1):
+        return f"conv_bf16_pair_kernel<{th}, {cb}, {'true' if split != '1' and cb == 1 else 'false'}>"
     return f"conv_bf16_stream_kernel<1, 1, {th}, {cb}, 2>"
 
 

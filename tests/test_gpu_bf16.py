@@ -479,15 +479,16 @@ def test_stream_1x1_is_the_tile_kernel(b, cin, cout, shape, mode, cin2):
     _close(kernels.from_c8(outs[0]), want)
 
 
-@pytest.mark.parametrize("split", [2, 1, 0])
+@pytest.mark.parametrize("split", [3, 2, 1, 0])
 @pytest.mark.parametrize("c,shape", [(16, (6, 9, 40)), (8, (5, 12, 33)), (16, (4, 4, 16)), (8, (8, 20, 64)),
                                      (8, (4, 9, 17))])
 def test_pair_sum_bf16_vs_torch(c, shape, split):
     """LEA_PAIR_SUM on the bf16 engine (a matching-cell step: relu(BN_a(conv_a(xa))) +
-    relu(BN_b(conv_b(xb))) in one launch) -- the split-wave pair kernel (split 1; split 2 = the
-    default: the plane-paired tile for the 8 -> 8 steps) and the D-streaming kernel with both
-    convs per wave (split 0) -- against float64 torch on the same bf16 operands, written into a
-    block slice of a cat buffer; odd D / ragged H, W."""
+    relu(BN_b(conv_b(xb))) in one launch) -- the split-wave pair kernel (split 1; split 2 with
+    the plane-paired tile for the 8 -> 8 steps; split 3, the default: that tile for the 8 -> 8
+    steps, the 16-channel ones as split 0) and the D-streaming kernel with both convs per wave
+    (split 0) -- against float64 torch on the same bf16 operands, written into a block slice of
+    a cat buffer; odd D / ragged H, W."""
     from leastereo_amd import _lib
     lib = _lib.load()
     g = torch.Generator().manual_seed(c * 3 + shape[0])
@@ -509,6 +510,6 @@ def test_pair_sum_bf16_vs_torch(c, shape, split):
         assert lib.lea_conv3d_bf16_set_pair_split(split) == 0
         kernels.conv3d_bnrelu_bf16(xa8, packed, c, 3, sc.to(DEV), sh.to(DEV), True, out, x2=xb8, pair_sum=True)
     finally:
-        lib.lea_conv3d_bf16_set_pair_split(2)
+        lib.lea_conv3d_bf16_set_pair_split(3)
     _close(kernels.from_c8(out.contiguous()), want)
     assert bool((big[:, 0] == 5.0).all()) and bool((big[:, -1] == 5.0).all())

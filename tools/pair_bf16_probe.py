@@ -65,6 +65,7 @@ def main():
         y1b = y1.clone()
         lib.lea_conv3d_bf16_set_pair_split(2)
         t_pair, t_two = timed(pair, a.iters), timed(two, a.iters)
+        lib.lea_conv3d_bf16_set_pair_split(3)  # the default again
         print(f"{name:14s} pair (both convs per wave) {t_pair0:8.1f} us ({3 * (B * d * h * w * c * 2) / t_pair0 / 1e6:5.2f} TB/s)")
         print(f"{name:14s} pair (split, no PP)        {t_pair1:8.1f} us ({3 * (B * d * h * w * c * 2) / t_pair1 / 1e6:5.2f} TB/s)"
               f"   max|PP - no PP|/max {float((y1.float() - y1b.float()).abs().max() / y1b.float().abs().max()):.2e}")
