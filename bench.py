@@ -154,17 +154,19 @@ def independent_check_engines():
     """The per-pair check's engines (bench.py's pair_epe_px): every switchable kernel the timed
     path runs swapped for its alternative -- the feature net's few-channel 3x3 tile and pair
     launch (lea_conv2d_set_small(0), FeatureExecutor.PAIR_S0), the fused stems (FUSED_STEM),
-    the separable resample (lea_resample_set_mode(2): the per-output gather) and the register
-    disparity kernel (the online-softmin LDS kernel).  The process-wide settings go back to
+    the separable resample (lea_resample_set_mode(2): the per-output gather), the fused tap-sum
+    head (lea_tapsum_set_rows(0): pass 1 through the workspace, then the per-row gather pass)
+    and the row-staged disparity kernel (the online-softmin LDS kernel).  The process-wide settings go back to
     what the LEASTEREO_* environment (or the default) set afterwards."""
     from leastereo_amd import _lib, executor
     lib = _lib.load()
     fe = executor.FeatureExecutor
     saved = (fe.FUSED_STEM, fe.PAIR_S0)
     env = lambda var, default: int(os.environ.get(var) or default)  # noqa: E731
-    switches = (("lea_disparity_set_register_form", 0, "LEASTEREO_DISP_REG", 1),
+    switches = (("lea_disparity_set_register_form", 0, "LEASTEREO_DISP_REG", 2),
                 ("lea_conv2d_set_small", 0, "LEASTEREO_CONV2D_SMALL", 1),
-                ("lea_resample_set_mode", 2, "LEASTEREO_RESAMPLE_MODE", 0))
+                ("lea_resample_set_mode", 2, "LEASTEREO_RESAMPLE_MODE", 0),
+                ("lea_tapsum_set_rows", 0, "LEASTEREO_TAPSUM_ROWS", 2))
     try:
         for fn, value, _, _ in switches:
             _lib.check(getattr(lib, fn)(value), fn)

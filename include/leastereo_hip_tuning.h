@@ -72,10 +72,11 @@ int lea_conv2d_set_small(int on);
 /* lea_conv2d_kernel_name with the input channel count (the few-channel tile depends on it). */
 const char* lea_conv2d_kernel_name_cin(int B, int cin, int cout, int H, int W);
 
-/* Disparity regression: 1 (default) = the register kernel (D3 plane values in registers,
- * compile-time depth axis, no rescaling softmin) for the configured (D3, maxdisp) pairs
- * (4, 12), (8, 24), (16, 48), (32, 96), (64, 192); 0 = the online-softmin kernel for every
- * shape. */
+/* Disparity regression: 2 (default, r05) = the row-staged kernel (a workgroup's two source
+ * rows of every plane H-lerped into LDS, two passes over the planes, compile-time depth axis,
+ * no rescaling softmin) for the configured (D3, maxdisp) pairs (4, 12), (8, 24), (16, 48),
+ * (32, 96), (64, 192); 1 = the register kernel (D3 plane values in registers) for them; 0 = the
+ * online-softmin kernel for every shape. */
 int lea_disparity_set_register_form(int on);
 
 /* Head tap-sum: 2 (default, r05) = passes 1 + 2 in one launch (a workgroup computes the

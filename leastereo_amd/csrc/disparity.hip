@@ -177,15 +177,86 @@ __global__ __launch_bounds__(kDispThreads) void disparity_reg_f32(const float* _
   disp[((long long)b * Ho + oh) * Wo + ow] = t / s;
 }
 
+// Row-staged form (r05; the default for the configured depths): a workgroup owns 256
+// consecutive output columns of one output row, so its pixels read two source rows
+// (ah.i0, ah.i1) of every plane over <= kDispCols source columns.  Those are H-lerped once
+// into LDS, hl[dd][c] = ah.l0 * row0 + ah.l1 * row1 (coalesced loads, two per value), and
+// each thread forms v[dd] = aw.l0 * hl[dd][i0] + aw.l1 * hl[dd][i1] from LDS -- two LDS reads
+// per plane instead of four dependent global loads, ~110 fewer VGPRs than the register
+// form's load batches (two waves per SIMD there).  H before W: the bilinear weights are
+// applied in the other order than disparity_reg_f32 (same values up to fp32 rounding); the
+// depth axis and softmin are the register form's.
+constexpr int kDispCols = 96;  // >= the source columns of 256 outputs at x3 (88), + slack
+
+template <int D3, int MD, bool FAST>
+__global__ __launch_bounds__(kDispThreads, 4) void disparity_rows_f32(const float* __restrict__ cost,
+                                                                   float* __restrict__ disp, int H3, int W3,
+                                                                   float rh, float rw) {
+#pragma clang fp contract(off)
+  __shared__ float hl[D3 * kDispCols];
+  const int Ho = 3 * H3, Wo = 3 * W3;
+  const int ow0 = blockIdx.x * blockDim.x;
+  const int oh = blockIdx.y;
+  const int b = blockIdx.z;
+  const AxisW ah = src_axis(rh, oh, H3, Ho);
+  const int c_lo = src_axis(rw, ow0, W3, Wo).i0;
+  const int c_hi = src_axis(rw, min(ow0 + (int)blockDim.x - 1, Wo - 1), W3, Wo).i1;
+  const int ncol = min(c_hi - c_lo + 1, kDispCols);  // host: <= kDispCols (Wo = 3 W3)
+  const long long HW = (long long)H3 * W3;
+  const float* base = cost + (long long)b * D3 * HW + c_lo;
+  const float* r0 = base + (long long)ah.i0 * W3;
+  const float* r1 = base + (long long)ah.i1 * W3;
+  for (int e = threadIdx.x; e < D3 * ncol; e += blockDim.x) {
+    const int dd = e / ncol, c = e - dd * ncol;
+    const long long o = (long long)dd * HW + c;
+    hl[dd * kDispCols + c] = ah.l0 * r0[o] + ah.l1 * r1[o];
+  }
+  __syncthreads();
+  const int ow = ow0 + threadIdx.x;
+  if (ow >= Wo) return;  // no barrier below
+  const AxisW aw = src_axis(rw, ow, W3, Wo);
+  const int j0 = aw.i0 - c_lo, j1 = aw.i1 - c_lo;
+  auto plane = [&](int dd) { return aw.l0 * hl[dd * kDispCols + j0] + aw.l1 * hl[dd * kDispCols + j1]; };
+  // pass 1: the smallest plane value; pass 2 forms the planes again from LDS in depth order
+  // (the register form kept all D3 of them live: two waves per SIMD)
+  float m = plane(0);
+#pragma unroll
+  for (int dd = 1; dd < D3; ++dd) {
+    m = fminf(m, plane(dd));
+    if (dd % 8 == 7) __builtin_amdgcn_sched_barrier(0);
+  }
+  constexpr float rd = (float)D3 / (float)MD;
+  float s = 0.f, t = 0.f;
+  float vlo = plane(0), vhi = plane(D3 > 1 ? 1 : 0);
+  int k = 0;  // vlo = plane k, vhi = plane min(k + 1, D3 - 1): constants after unrolling
+#pragma unroll
+  for (int od = 0; od < MD; ++od) {
+    const AxisW ad = src_axis(rd, od, D3, MD);  // constants after unrolling
+    while (k < ad.i0) {
+      ++k;
+      vlo = vhi;
+      vhi = plane(k + 1 < D3 ? k + 1 : D3 - 1);
+    }
+    const float v1 = ad.i1 == k ? vlo : vhi;
+    const float u = ad.l0 * vlo + ad.l1 * v1;
+    const float e = FAST ? dexp<true>(m - u) : exp_noovf(m - u);
+    s += e;
+    t += (float)od * e;
+    if (od % 12 == 11) __builtin_amdgcn_sched_barrier(0);
+  }
+  disp[((long long)b * Ho + oh) * Wo + ow] = t / s;
+}
+
 }  // namespace lea
 
-// lea_disparity_set_register_form: 1 (default) = the register kernel for the configured
-// (D3, maxdisp), 0 = the online-softmin kernel everywhere (A/B and tests)
-static int g_disp_reg = 1;
+// lea_disparity_set_register_form: 2 (default, r05) = the row-staged kernel for the configured
+// (D3, maxdisp), 1 = the register kernel for them, 0 = the online-softmin kernel everywhere
+// (A/B and tests)
+static int g_disp_reg = 2;
 extern "C" int lea_disparity_set_register_form(int on) {
   using namespace lea;
   clear_error();
-  LEA_CHECK_ARG(on == 0 || on == 1, "lea_disparity_set_register_form: %d", on);
+  LEA_CHECK_ARG(on >= 0 && on <= 2, "lea_disparity_set_register_form: %d", on);
   g_disp_reg = on;
   return 0;
 }
@@ -216,6 +287,18 @@ extern "C" int lea_disparity_regression(const void* cost, float* disp, int B, in
     k_<<<grid, block, 0, as_stream(stream)>>>((const float*)cost, disp, H3, W3, rh, rw);                 \
     return launch_status("lea_disparity_regression");                                                  \
   }
+  // the row-staged form: 256 outputs of a row read <= kDispCols source columns (Wo = 3 W3)
+  const bool rows_ok = g_disp_reg == 2 && (256LL * W3 + Wo - 1) / Wo + 2 <= kDispCols;
+#define LEA_DISP_ROWS(D3_, MD_)                                                                         \
+  if (D3 == D3_ && maxdisp == MD_) {                                                                   \
+    auto k_ = fast ? disparity_rows_f32<D3_, MD_, true> : disparity_rows_f32<D3_, MD_, false>;          \
+    k_<<<grid, block, 0, as_stream(stream)>>>((const float*)cost, disp, H3, W3, rh, rw);                 \
+    return launch_status("lea_disparity_regression");                                                  \
+  }
+  if (rows_ok) {
+    LEA_DISP_ROWS(4, 12) LEA_DISP_ROWS(8, 24) LEA_DISP_ROWS(16, 48) LEA_DISP_ROWS(32, 96) LEA_DISP_ROWS(64, 192)
+  }
+#undef LEA_DISP_ROWS
   if (g_disp_reg) {
     // (88, 264) -- config 5 -- stays on the LDS kernel: its 88 plane values take all 256
     // VGPRs, one wave per SIMD (r03: 0.388 vs 0.380 ms); at (64, 192): 0.125 -> 0.081 ms

@@ -352,23 +352,26 @@ def test_disparity_vs_oracle_sizes():
 @pytest.mark.parametrize("shape,md", [((1, 1, 64, 12, 20), 192), ((2, 1, 32, 9, 13), 96), ((1, 1, 16, 7, 4), 48),
                                       ((1, 1, 8, 5, 6), 24)])
 def test_disparity_register_form_matches_the_lds_form(shape, md):
-    """The register disparity kernel (D3 plane values in registers, compile-time depth
+    """The row-staged disparity kernel (the default: source rows H-lerped into LDS, two passes
+    over the planes), the register kernel (D3 plane values in registers, compile-time depth
     axis, softmin shifted by the smallest plane value) and the online-softmin LDS kernel
-    agree to fp32 summation noise, and both meet the oracle at the 1e-3 px bar."""
+    agree to fp32 summation noise, f32 and fast-exp alike, and all meet the oracle at the
+    1e-3 px bar."""
     lib = _lib.load()
     g = torch.Generator().manual_seed(11)
     x = torch.randn(shape, generator=g) * 3
     refd = ref.disp_forward(x.double(), md).numpy()
-    out = {}
-    for on in (1, 0):
-        assert lib.lea_disparity_set_register_form(on) == 0
-        try:
-            out[on] = kernels.disparity_regression(x.to(DEV), md).cpu().double().numpy()
-        finally:
-            lib.lea_disparity_set_register_form(1)
-        err = np.abs(out[on] - refd)
-        assert err.max() < 2e-3 and err.mean() < 1e-4, (on, err.max(), err.mean())
-    assert np.abs(out[1] - out[0]).max() < 1e-3
+    for fast in (False, True):
+        out = {}
+        for on in (2, 1, 0):
+            assert lib.lea_disparity_set_register_form(on) == 0
+            try:
+                out[on] = kernels.disparity_regression(x.to(DEV), md, fast).cpu().double().numpy()
+            finally:
+                lib.lea_disparity_set_register_form(2)
+            err = np.abs(out[on] - refd)
+            assert err.max() < 2e-3 and err.mean() < 1e-4, (fast, on, err.max(), err.mean())
+        assert np.abs(out[1] - out[0]).max() < 1e-3 and np.abs(out[2] - out[1]).max() < 1e-3
 
 
 @pytest.mark.parametrize("b,c,cout,maxdisp,hw", [(2, 32, 32, 48, (12, 40)), (1, 4, 16, 27, (5, 7)),
