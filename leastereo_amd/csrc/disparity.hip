@@ -229,7 +229,7 @@ __global__ __launch_bounds__(kDispThreads, 4) void disparity_rows_f32(const floa
   float s = 0.f, t = 0.f;
   float vlo = plane(0), vhi = plane(D3 > 1 ? 1 : 0);
   int k = 0;  // vlo = plane k, vhi = plane min(k + 1, D3 - 1): constants after unrolling
-#pragma unroll
+#pragma clang loop unroll(full)
   for (int od = 0; od < MD; ++od) {
     const AxisW ad = src_axis(rd, od, D3, MD);  // constants after unrolling
     while (k < ad.i0) {
@@ -297,6 +297,7 @@ extern "C" int lea_disparity_regression(const void* cost, float* disp, int B, in
   }
   if (rows_ok) {
     LEA_DISP_ROWS(4, 12) LEA_DISP_ROWS(8, 24) LEA_DISP_ROWS(16, 48) LEA_DISP_ROWS(32, 96) LEA_DISP_ROWS(64, 192)
+    LEA_DISP_ROWS(88, 264)
   }
 #undef LEA_DISP_ROWS
   if (g_disp_reg) {

@@ -13,7 +13,8 @@ import torch
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from leastereo_amd import _lib, kernels  # noqa: E402
 
-SHAPES = [("C2", 1, 64, 192, 320, 192), ("C4", 8, 64, 192, 320, 192), ("C3", 8, 64, 128, 416, 192)]
+SHAPES = [("C2", 1, 64, 192, 320, 192), ("C4", 8, 64, 192, 320, 192), ("C3", 8, 64, 128, 416, 192),
+          ("C5", 1, 88, 336, 504, 264)]
 
 
 def main():
