@@ -17,6 +17,7 @@ namespace lea {
 namespace fstem {
 
 using bf16x8 = __attribute__((ext_vector_type(8))) __bf16;
+using f32x2 = __attribute__((ext_vector_type(2))) float;
 constexpr int TW = 64, TH = 4;                       // stem1 outputs per workgroup
 constexpr int PW = 3 * TW + 2, PH = 3 * TH + 2;      // image patch (input rows/cols 3ho-2 ..)
 
@@ -58,8 +59,8 @@ __global__ __launch_bounds__(TW * TH) void feature_stem_kernel(
       const int e = min((int)threadIdx.x + k * TW * TH, N0 + N1 - 1);
       if (e < N0) {
         wv[k] = w0[e];
-      } else {  // w1s index (c0, o, t) <- w1[(o * C0 + c0) * 9 + t]
-        const int f = e - N0, c0 = f / (C1 * 9), o = (f / 9) % C1, t = f % 9;
+      } else {  // w1s index (c0, t, o) <- w1[(o * C0 + c0) * 9 + t]
+        const int f = e - N0, c0 = f / (C1 * 9), t = (f / C1) % 9, o = f % C1;
         wv[k] = w1[(o * C0 + c0) * 9 + t];
       }
     }
@@ -97,12 +98,16 @@ __global__ __launch_bounds__(TW * TH) void feature_stem_kernel(
 #pragma unroll
     for (int kw = 0; kw < 3; ++kw)
       valid[kh][kw] = (unsigned)(3 * ho - 1 + kh) < (unsigned)Hi && (unsigned)(3 * wo - 1 + kw) < (unsigned)Wi;
-  float acc[C1];
+  // stem1 on packed f32 FMAs (r05): two couts per v_pk_fma_f32 (same stem0 value; w1s is
+  // [c0][tap][cout], so a cout pair is one 8-byte LDS word) -- each element sees the scalar
+  // form's fmaf sequence: identical bits (stem0 stays scalar: pairing its pixels or channels
+  // needs the input values broadcast into register pairs -- 256 VGPRs)
+  f32x2 acc[C1 / 2];
 #pragma unroll
-  for (int o = 0; o < C1; ++o) acc[o] = 0.f;
+  for (int o = 0; o < C1 / 2; ++o) acc[o] = f32x2{0.f, 0.f};
   for (int c0 = 0; c0 < C0; ++c0) {
     const float s0 = bn0[0][c0], t0 = bn0[1][c0];
-    float s[3][3];
+    float s[9];
 #pragma unroll
     for (int kh = 0; kh < 3; ++kh)
 #pragma unroll
@@ -115,20 +120,19 @@ __global__ __launch_bounds__(TW * TH) void feature_stem_kernel(
 #pragma unroll
             for (int j = 0; j < 3; ++j) v = fmaf(w0s[((c0 * CIN + c) * 3 + i) * 3 + j], in[c][kh + i][kw + j], v);
         v = fmaxf(v * s0 + t0, 0.f);  // stem0's BN + ReLU (new_model_2d.py:93)
-        s[kh][kw] = valid[kh][kw] ? v : 0.f;
+        s[kh * 3 + kw] = valid[kh][kw] ? v : 0.f;
       }
+    const f32x2* w1p = reinterpret_cast<const f32x2*>(w1s + c0 * 9 * C1);
 #pragma unroll
-    for (int o = 0; o < C1; ++o)
+    for (int o = 0; o < C1 / 2; ++o)
 #pragma unroll
-      for (int kh = 0; kh < 3; ++kh)
-#pragma unroll
-        for (int kw = 0; kw < 3; ++kw) acc[o] = fmaf(w1s[(c0 * C1 + o) * 9 + kh * 3 + kw], s[kh][kw], acc[o]);
+      for (int t = 0; t < 9; ++t) acc[o] = __builtin_elementwise_fma(w1p[t * (C1 / 2) + o], f32x2{s[t], s[t]}, acc[o]);
   }
   if (ho >= Ho || wo >= Wo) return;
   const long long HWo = (long long)Ho * Wo, pix = (long long)ho * Wo + wo;
   float r[C1];
 #pragma unroll
-  for (int o = 0; o < C1; ++o) r[o] = fmaxf(acc[o] * (sc1 ? sc1[o] : 1.f) + (sc1 ? sh1[o] : 0.f), 0.f);
+  for (int o = 0; o < C1; ++o) r[o] = fmaxf(acc[o / 2][o % 2] * (sc1 ? sc1[o] : 1.f) + (sc1 ? sh1[o] : 0.f), 0.f);
   if constexpr (C8) {  // bf16 c8: [B][C1/8][1][Ho][Wo][8]
     bf16x8* yp = reinterpret_cast<bf16x8*>(static_cast<__bf16*>(y) + (long long)b * ybs);
 #pragma unroll
