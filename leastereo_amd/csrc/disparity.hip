@@ -201,7 +201,9 @@ __global__ __launch_bounds__(kDispThreads, 4) void disparity_rows_f32(const floa
   const AxisW ah = src_axis(rh, oh, H3, Ho);
   const int c_lo = src_axis(rw, ow0, W3, Wo).i0;
   const int c_hi = src_axis(rw, min(ow0 + (int)blockDim.x - 1, Wo - 1), W3, Wo).i1;
-  const int ncol = min(c_hi - c_lo + 1, kDispCols);  // host: <= kDispCols (Wo = 3 W3)
+  // host: <= kDispCols (Wo = 3 W3); past it the staging is clamped and the outputs are NaN
+  const bool over = c_hi - c_lo + 1 > kDispCols;
+  const int ncol = min(c_hi - c_lo + 1, kDispCols);
   const long long HW = (long long)H3 * W3;
   const float* base = cost + (long long)b * D3 * HW + c_lo;
   const float* r0 = base + (long long)ah.i0 * W3;
@@ -215,7 +217,7 @@ __global__ __launch_bounds__(kDispThreads, 4) void disparity_rows_f32(const floa
   const int ow = ow0 + threadIdx.x;
   if (ow >= Wo) return;  // no barrier below
   const AxisW aw = src_axis(rw, ow, W3, Wo);
-  const int j0 = aw.i0 - c_lo, j1 = aw.i1 - c_lo;
+  const int j0 = min(aw.i0 - c_lo, kDispCols - 1), j1 = min(aw.i1 - c_lo, kDispCols - 1);
   auto plane = [&](int dd) { return aw.l0 * hl[dd * kDispCols + j0] + aw.l1 * hl[dd * kDispCols + j1]; };
   // pass 1: the smallest plane value; pass 2 forms the planes again from LDS in depth order
   // (the register form kept all D3 of them live: two waves per SIMD)
@@ -244,7 +246,7 @@ __global__ __launch_bounds__(kDispThreads, 4) void disparity_rows_f32(const floa
     t += (float)od * e;
     if (od % 12 == 11) __builtin_amdgcn_sched_barrier(0);
   }
-  disp[((long long)b * Ho + oh) * Wo + ow] = t / s;
+  disp[((long long)b * Ho + oh) * Wo + ow] = over ? __builtin_nanf("") : t / s;
 }
 
 }  // namespace lea
