@@ -1221,8 +1221,9 @@ inline Plan plan(int B, int cout, int D, int H, int W, int ks, int cin) {
     p.td = 4;
   }
   // r05: the deep-K 64-cout layers (conv1/2, cin 128) with two cout tiles per wave (each B
-  // fragment read from LDS by two waves instead of four): same-box C4 +1.2 %, C3 +1.1 % over
-  // four interleaved rounds (profiles/r05_conv12_mt2_ab.txt)
+  // fragment read from LDS by two waves instead of four): same-box C4 +0.35 %, C3 +0.55 % over
+  // four order-balanced rounds (profiles/r05_conv12_mt2_ab.txt; the first, fixed-order A/B
+  // read +1.2 % -- part of that was the second-run bias)
   if (ks == 3 && cin >= 64 && cobv == 64) {
     p.th = 8;
     p.td = 2;

@@ -8,7 +8,9 @@ mkdir -p gpurun_out
 if [ -n "${AB_VARIANTS:-}" ]; then IFS=';' read -r -a VARS <<< "$AB_VARIANTS"; else VARS=("${AB_A:-}" "${AB_B:-}"); fi
 for r in $(seq 1 ${ROUNDS:-2}); do
   for c in ${CONFIGS:-c2}; do
-    for i in "${!VARS[@]}"; do
+    # reverse the variant order on even rounds so a first-run/second-run bias cancels
+    idx=("${!VARS[@]}"); [ $((r % 2)) -eq 0 ] && idx=($(printf '%s\n' "${idx[@]}" | tac))
+    for i in "${idx[@]}"; do
       envs=$(echo "${VARS[$i]}" | tr ',' ' ')
       env $envs timeout -k 10 300 python3 bench.py --config $c --steps ${STEPS:-20} --warmup 5 --cpu-baseline 0 --epe 0 --pair-check 0 \
         > gpurun_out/ab_${i}_${c}_$r.json 2> gpurun_out/ab_${i}_${c}_$r.err
