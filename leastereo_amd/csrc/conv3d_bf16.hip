@@ -477,26 +477,28 @@ __global__ __launch_bounds__(256) void resample_c8_cols_kernel(
 // rounded to bf16 the same way), so no LDS; the A fragments (the k = 1 packing: one
 // k-step per 32-channel chunk) sit in registers.  Bit-identical to resample_c8 + the
 // 1x1 tile kernel; saves the resampled tensor's write and read.
-template <int MT>
+// NCH = cin / 32 at compile time (1, 2; 4 covers 96 and 128 with a runtime count) so the
+// corner words are sized to the layer, and a wave issues the corner loads of TU tiles before
+// their MFMAs (r05: 196 VGPRs at two waves per SIMD with one tile in flight before).
+template <int MT, int NCH, int TU>
 __global__ __launch_bounds__(256) void conv1x1_rs_c8_kernel(
     const __bf16* __restrict__ x, long long xbs, int Di, int Hi, int Wi, const bf16x8* __restrict__ wp,
     const float* __restrict__ scale, const float* __restrict__ shift, __bf16* __restrict__ y,
     long long ybs, int cin, int cout, int Do, int Ho, int Wo, float rd, float rh, float rw,
     unsigned flags, int tiles_per_wave) {
 #pragma clang fp contract(off)
-  constexpr int MAXCH = 4;  // cin <= 128 (host)
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int g = lane >> 4, n = lane & 15;
   const int b = blockIdx.y;
-  const int nch = cin / 32;
+  const int nch = NCH < 4 ? NCH : cin / 32;
   const long long HWi = (long long)Hi * Wi, vin = HWi * Di;
   const int HWo = Ho * Wo;
   const long long vout = (long long)HWo * Do;
   const bf16x8* xb = reinterpret_cast<const bf16x8*>(x + (long long)b * xbs);
   // A fragments of every chunk and cout tile (cob block of 16 MT couts: [chunk][s][mtile][g][16])
-  bf16x8 av[MAXCH][MT];
+  bf16x8 av[NCH][MT];
 #pragma unroll
-  for (int c = 0; c < MAXCH; ++c)
+  for (int c = 0; c < NCH; ++c)
 #pragma unroll
     for (int m = 0; m < MT; ++m) av[c][m] = c < nch ? wp[((c * MT + m) * 4 + g) * 16 + n] : bf16x8{};
   float sc[MT][4], sh[MT][4];
@@ -510,61 +512,74 @@ __global__ __launch_bounds__(256) void conv1x1_rs_c8_kernel(
     }
   const bool relu = flags & LEA_RELU;
   const long long tile0 = ((long long)blockIdx.x * 4 + wave) * tiles_per_wave;
-  for (int tt = 0; tt < tiles_per_wave; ++tt) {
-    const long long v0 = (tile0 + tt) * 16;
-    if (v0 >= vout) break;
-    const long long v = min(v0 + n, vout - 1);
-    const int od = (int)(v / HWo), rem = (int)(v - (long long)od * HWo);
-    const int oh = rem / Wo, ow = rem - oh * Wo;
-    const Axis ad = axis_index(rd, od, Di, Do, 1), ah = axis_index(rh, oh, Hi, Ho, 1),
-               aw = axis_index(rw, ow, Wi, Wo, 1);
-    const long long o00 = (long long)ad.i0 * HWi + (long long)ah.i0 * Wi, o01 = (long long)ad.i0 * HWi + (long long)ah.i1 * Wi;
-    const long long o10 = (long long)ad.i1 * HWi + (long long)ah.i0 * Wi, o11 = (long long)ad.i1 * HWi + (long long)ah.i1 * Wi;
-    bf16x8 cw[MAXCH][8];
+  for (int tt = 0; tt < tiles_per_wave; tt += TU) {
+    if ((tile0 + tt) * 16 >= vout) break;
+    bf16x8 cw[TU][NCH][8];
+    Axis ad[TU], ah[TU], aw[TU];
 #pragma unroll
-    for (int c = 0; c < MAXCH; ++c) {
-      if (c >= nch) break;
-      const bf16x8* xc = xb + (long long)(4 * c + g) * vin;
-      cw[c][0] = xc[o00 + aw.i0];
-      cw[c][1] = xc[o00 + aw.i1];
-      cw[c][2] = xc[o01 + aw.i0];
-      cw[c][3] = xc[o01 + aw.i1];
-      cw[c][4] = xc[o10 + aw.i0];
-      cw[c][5] = xc[o10 + aw.i1];
-      cw[c][6] = xc[o11 + aw.i0];
-      cw[c][7] = xc[o11 + aw.i1];
-    }
-    f32x4 acc[MT];
+    for (int u = 0; u < TU; ++u) {
+      // tiles past the wave's share or the volume load the last voxel's corners (never stored)
+      const long long v = min((tile0 + tt + u) * 16 + n, vout - 1);
+      const int od = (int)(v / HWo), rem = (int)(v - (long long)od * HWo);
+      const int oh = rem / Wo, ow = rem - oh * Wo;
+      ad[u] = axis_index(rd, od, Di, Do, 1);
+      ah[u] = axis_index(rh, oh, Hi, Ho, 1);
+      aw[u] = axis_index(rw, ow, Wi, Wo, 1);
+      const long long o00 = (long long)ad[u].i0 * HWi + (long long)ah[u].i0 * Wi;
+      const long long o01 = (long long)ad[u].i0 * HWi + (long long)ah[u].i1 * Wi;
+      const long long o10 = (long long)ad[u].i1 * HWi + (long long)ah[u].i0 * Wi;
+      const long long o11 = (long long)ad[u].i1 * HWi + (long long)ah[u].i1 * Wi;
 #pragma unroll
-    for (int m = 0; m < MT; ++m) acc[m] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int c = 0; c < MAXCH; ++c) {
-      if (c >= nch) break;
-      bf16x8 bv;
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const float r = ad.l0 * (ah.l0 * (aw.l0 * (float)cw[c][0][j] + aw.l1 * (float)cw[c][1][j]) +
-                                 ah.l1 * (aw.l0 * (float)cw[c][2][j] + aw.l1 * (float)cw[c][3][j])) +
-                        ad.l1 * (ah.l0 * (aw.l0 * (float)cw[c][4][j] + aw.l1 * (float)cw[c][5][j]) +
-                                 ah.l1 * (aw.l0 * (float)cw[c][6][j] + aw.l1 * (float)cw[c][7][j]));
-        bv[j] = (__bf16)r;
+      for (int c = 0; c < NCH; ++c) {
+        if (c >= nch) break;
+        const bf16x8* xc = xb + (long long)(4 * c + g) * vin;
+        cw[u][c][0] = xc[o00 + aw[u].i0];
+        cw[u][c][1] = xc[o00 + aw[u].i1];
+        cw[u][c][2] = xc[o01 + aw[u].i0];
+        cw[u][c][3] = xc[o01 + aw[u].i1];
+        cw[u][c][4] = xc[o10 + aw[u].i0];
+        cw[u][c][5] = xc[o10 + aw[u].i1];
+        cw[u][c][6] = xc[o11 + aw[u].i0];
+        cw[u][c][7] = xc[o11 + aw[u].i1];
       }
-#pragma unroll
-      for (int m = 0; m < MT; ++m) acc[m] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[c][m], bv, acc[m], 0, 0, 0);
     }
-    if (v0 + n >= vout) continue;
 #pragma unroll
-    for (int m = 0; m < MT; ++m) {
-      const int co = 16 * m + 4 * g;  // first of the lane's 4 couts
-      if (co >= cout) continue;
-      bf16x4 out;
+    for (int u = 0; u < TU; ++u) {
+      const long long v0 = (tile0 + tt + u) * 16;
+      if (tt + u >= tiles_per_wave || v0 >= vout) break;
+      f32x4 acc[MT];
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        float t = acc[m][r] * sc[m][r] + sh[m][r];
-        if (relu) t = fmaxf(t, 0.f);
-        out[r] = (__bf16)t;
+      for (int m = 0; m < MT; ++m) acc[m] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int c = 0; c < NCH; ++c) {
+        if (c >= nch) break;
+        bf16x8 bv;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const Axis &pd = ad[u], &ph = ah[u], &pw = aw[u];
+          const float r = pd.l0 * (ph.l0 * (pw.l0 * (float)cw[u][c][0][j] + pw.l1 * (float)cw[u][c][1][j]) +
+                                   ph.l1 * (pw.l0 * (float)cw[u][c][2][j] + pw.l1 * (float)cw[u][c][3][j])) +
+                          pd.l1 * (ph.l0 * (pw.l0 * (float)cw[u][c][4][j] + pw.l1 * (float)cw[u][c][5][j]) +
+                                   ph.l1 * (pw.l0 * (float)cw[u][c][6][j] + pw.l1 * (float)cw[u][c][7][j]));
+          bv[j] = (__bf16)r;
+        }
+#pragma unroll
+        for (int m = 0; m < MT; ++m) acc[m] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[c][m], bv, acc[m], 0, 0, 0);
       }
-      *reinterpret_cast<bf16x4*>(y + (long long)b * ybs + ((long long)(co / 8) * vout + v0 + n) * 8 + co % 8) = out;
+      if (v0 + n >= vout) continue;
+#pragma unroll
+      for (int m = 0; m < MT; ++m) {
+        const int co = 16 * m + 4 * g;  // first of the lane's 4 couts
+        if (co >= cout) continue;
+        bf16x4 out;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          float t = acc[m][r] * sc[m][r] + sh[m][r];
+          if (relu) t = fmaxf(t, 0.f);
+          out[r] = (__bf16)t;
+        }
+        *reinterpret_cast<bf16x4*>(y + (long long)b * ybs + ((long long)(co / 8) * vout + v0 + n) * 8 + co % 8) = out;
+      }
     }
   }
 }
@@ -575,13 +590,15 @@ __global__ __launch_bounds__(256) void conv1x1_rs_c8_kernel(
 // registers, the A fragments (the k = 1 packing) sit in registers, and a wave issues the
 // words of TU tiles before their MFMAs so TU * nch loads per lane are in flight.  Same
 // operands, order and epilogue as the tile kernel's k = 1 path: bit-identical.
-template <int MT>
+// NCH = the 32-channel chunk count at compile time (1, 2; 4 covers 3 and 4 at run time): r05,
+// 114 -> fewer VGPRs for the one- and two-chunk layers
+template <int MT, int NCH>
 __global__ __launch_bounds__(256) void conv1x1_c8_kernel(const Args a, int tpw) {
-  constexpr int MAXCH = 4, TU = 4;  // cin <= 128 (host); tiles per load group
+  constexpr int MAXCH = NCH, TU = 4;  // cin <= 128 (host); tiles per load group
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int g = lane >> 4, n = lane & 15;
   const int b = blockIdx.y / a.ncob, cob = blockIdx.y - b * a.ncob;
-  const int nch = (a.cin / 8 + 3) / 4;
+  const int nch = NCH < 4 ? NCH : (a.cin / 8 + 3) / 4;
   const long long vox = (long long)a.D * a.H * a.W;
   const bf16x8* wp = reinterpret_cast<const bf16x8*>(a.wp);
   bf16x8 av[MAXCH][MT];
@@ -1198,6 +1215,9 @@ int g_stream1x1 = 1;            // lea_conv3d_bf16_set_stream1x1
 int g_pair_split = 3;           // lea_conv3d_bf16_set_pair_split: LEA_PAIR_SUM on the split-wave kernel
                                 // (2: the plane-paired tile for the 8 -> 8 steps; 3: that, and the
                                 // 16-channel steps on the two-source D-streaming kernel)
+// conv1x1_rs_c8_kernel: tiles per wave (r05 probe at the C4 shapes, tools/rs_probe.py: two tiles'
+// corner loads in flight together 4-5 % faster than one; more tiles per wave slower)
+constexpr int g_rs_tpw = 2;
 
 inline Plan plan(int B, int cout, int D, int H, int W, int ks, int cin) {
   // r01 sweep (tools/conv_sweep.py --bf16, profiles/r01_conv_sweep_bf16.txt): one
@@ -1298,9 +1318,18 @@ int run(const Plan& p, Args a, int B, hipStream_t st, bool cv) {
     const long long gx = (tiles + 4 * tpw - 1) / (4 * tpw);
     LEA_CHECK_ARG(gx < (1LL << 31) && (long long)B * a.ncob <= 65535, "lea_conv3d(bf16 1x1): grid too large");
     const dim3 grid((unsigned)gx, B * a.ncob);
-    if (p.wc == 1) conv1x1_c8_kernel<1><<<grid, 256, 0, st>>>(a, (int)tpw);
-    else if (p.wc == 2) conv1x1_c8_kernel<2><<<grid, 256, 0, st>>>(a, (int)tpw);
-    else conv1x1_c8_kernel<4><<<grid, 256, 0, st>>>(a, (int)tpw);
+    // one-chunk layers and the two-chunk ones with >= 2 cout tiles on the specialised forms;
+    // the two-chunk single-tile layers measured 2 % slower at 6 waves per SIMD than at 4
+    // (r05 tools/rs_probe.py --one, profiles/r05_1x1_rs_probe.txt)
+    const int nch0 = (a.cin / 8 + 3) / 4, nch = (nch0 == 1 || (nch0 == 2 && p.wc >= 2)) ? nch0 : 4;
+#define LEA_1X1(MT_)                                                                            \
+  if (p.wc == MT_) {                                                                            \
+    if (nch == 1) conv1x1_c8_kernel<MT_, 1><<<grid, 256, 0, st>>>(a, (int)tpw);                 \
+    else if (nch == 2) conv1x1_c8_kernel<MT_, 2><<<grid, 256, 0, st>>>(a, (int)tpw);            \
+    else conv1x1_c8_kernel<MT_, 4><<<grid, 256, 0, st>>>(a, (int)tpw);                          \
+  }
+    LEA_1X1(1) LEA_1X1(2) LEA_1X1(4)
+#undef LEA_1X1
     return launch_status("lea_conv3d(bf16 1x1)");
   }
   if ((a.flags & LEA_PAIR_SUM) && g_pair_split && p.nsplit > 0 && a.ncob == 1 && (a.nchunks == 2) &&
@@ -1645,7 +1674,7 @@ extern "C" int lea_conv1x1_resampled_bf16(const void* x, int64_t x_bstride, int 
                 "lea_conv1x1_resampled_bf16: cin %% 32 (<= 128), cout %% 16 (<= 64) required, got %d/%d",
                 cin, cout);
   const long long vout = (long long)D * H * W;
-  const int tpw = 2;  // 16-voxel tiles per wave
+  const int tpw = bf::g_rs_tpw;  // 16-voxel tiles per wave
   const long long nblk = (vout + 64LL * tpw - 1) / (64LL * tpw);
   LEA_CHECK_ARG(nblk < (1LL << 31), "lea_conv1x1_resampled_bf16: grid too large");
   const dim3 grid((unsigned)nblk, B);
@@ -1654,12 +1683,16 @@ extern "C" int lea_conv1x1_resampled_bf16(const void* x, int64_t x_bstride, int 
   // (one block of cob_of(cout) couts: cout = 16 MT)
   LEA_CHECK_ARG(bf::cob_of(cout) == cout, "lea_conv1x1_resampled_bf16: cout %d is not one packing block", cout);
   const bf16x8_t* wp = reinterpret_cast<const bf16x8_t*>(w_packed);
-#define LEA_RS1(MT_)                                                                                 \
-  if (cout == 16 * MT_)                                                                              \
-    bf::conv1x1_rs_c8_kernel<MT_><<<grid, 256, 0, as_stream(stream)>>>(                              \
+  const int nchk = cin == 32 ? 1 : cin == 64 ? 2 : 4;
+  // TU tiles' corner loads in flight (1 for the three- and four-chunk layers: 222-256 VGPRs at 2)
+#define LEA_RS1(MT_, NCH_, TU_)                                                                      \
+  if (cout == 16 * MT_ && nchk == NCH_)                                                              \
+    bf::conv1x1_rs_c8_kernel<MT_, NCH_, TU_><<<grid, 256, 0, as_stream(stream)>>>(                   \
         (const __bf16*)x, x_bstride, Di, Hi, Wi, wp, scale, shift, (__bf16*)y, y_bstride, cin, cout, D, \
         H, W, rd, rh, rw, flags, tpw);
-  LEA_RS1(1) LEA_RS1(2) LEA_RS1(4)
+  LEA_RS1(1, 1, 2) LEA_RS1(1, 2, 2) LEA_RS1(1, 4, 1)
+  LEA_RS1(2, 1, 2) LEA_RS1(2, 2, 2) LEA_RS1(2, 4, 1)
+  LEA_RS1(4, 1, 2) LEA_RS1(4, 2, 2) LEA_RS1(4, 4, 1)
 #undef LEA_RS1
   return launch_status("lea_conv1x1_resampled_bf16");
 }

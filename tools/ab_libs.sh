@@ -6,7 +6,9 @@
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 for r in $(seq 1 ${ROUNDS:-2}); do
-  for L in ${LIBS:-leastereo_amd/libleastereo_hip.so}; do
+  # the library order reversed on even rounds so a first-run/second-run bias cancels
+  LL=(${LIBS:-leastereo_amd/libleastereo_hip.so}); [ $((r % 2)) -eq 0 ] && LL=($(printf '%s\n' "${LL[@]}" | tac))
+  for L in "${LL[@]}"; do
     echo "== round $r $L"
     LEASTEREO_HIP_LIB=$L timeout -k 10 ${STEP_TIMEOUT:-120} python3 ${PROG:-tools/pair_bf16_probe.py --iters 20} || exit 1
   done
