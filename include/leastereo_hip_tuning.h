@@ -26,6 +26,12 @@ int lea_conv3d_set_tile_override(int nt, int tw, int td);
  * operand from the 8 corners, no staging), 0 = always the register-staged engine. */
 int lea_conv3d_set_rs_gather(int on);
 
+/* 1 (default) = the fp32 1x1 streaming kernel ("conv1x1_kernel") gives each lane NT
+ * consecutive voxels, so its loads, residual reads and stores are NT-float vectors (when
+ * every base, batch stride and D*H*W is a multiple of NT floats), 0 = one float per lane
+ * and tile.  Bit-identical. */
+int lea_conv1x1_set_vector(int on);
+
 /* bf16 engine: force the conv tile -- th rows, td planes, mt 16-row tiles per wave
  * (th <= 0 restores the planner; tools/conv_sweep.py --bf16). */
 int lea_conv3d_bf16_set_tile_override(int th, int td, int mt);

@@ -105,6 +105,7 @@ SIGNATURES = {
     "lea_conv3d_wino2_set_pipeline": (_i, [_i]),
     "lea_conv3d_wino_set_epi_buf": (_i, [_i]),
     "lea_conv3d_set_rs_gather": (_i, [_i]),
+    "lea_conv1x1_set_vector": (_i, [_i]),
     "lea_conv3d_bf16_set_stream1x1": (_i, [_i]),
     "lea_conv3d_wino_set_small_cout": (_i, [_i]),
     "lea_conv3d_wino_set_block48": (_i, [_i]),
@@ -178,6 +179,7 @@ TUNING_ENV = {"LEASTEREO_WINO2_WALK": "lea_conv3d_wino2_set_walk",
               "LEASTEREO_WINO2_PIPE": "lea_conv3d_wino2_set_pipeline",
               "LEASTEREO_EPI_BUF": "lea_conv3d_wino_set_epi_buf",
               "LEASTEREO_RS_GATHER": "lea_conv3d_set_rs_gather",
+              "LEASTEREO_1X1_VEC": "lea_conv1x1_set_vector",
               "LEASTEREO_BF16_1X1": "lea_conv3d_bf16_set_stream1x1",
               "LEASTEREO_RESAMPLE_K": "lea_resample_bf16_set_batch",
               "LEASTEREO_RESAMPLE_COLS": "lea_resample_bf16_set_cols",

@@ -226,12 +226,17 @@ __global__ __launch_bounds__(256) void conv1x1_rs_f32_kernel(const ConvArgs a, i
 // (16 consecutive floats per 16-lane group), all CIN_B/4 k-steps of a chunk
 // issued before its MFMAs so a chunk's loads are in flight together.  Weights of
 // the chunk (32 x COPS floats) are staged in LDS.  The volume is treated as a
-// flat run of D*H*W voxels.
-template <int MT, int NT>
+// flat run of D*H*W voxels.  VEC (r05): lane n owns the NT consecutive voxels v0 + NT n + j
+// (column n of tile j) instead of v0 + 16 j + n, so its loads, residual reads and stores are
+// NT-float vectors -- 16 lanes cover 64 NT contiguous bytes per instruction instead of 64
+// (host: every base, batch stride and D*H*W a multiple of NT floats).  Each output's k-step
+// sequence is unchanged: bit-identical.
+template <int MT, int NT, bool VEC>
 __global__ __launch_bounds__(kConvThreads) void conv1x1_kernel(const ConvArgs a) {
   using P = PackCfg<1, MT>;
   constexpr int CIN_B = P::CIN_B;
   constexpr int KS = CIN_B / 4;
+  using vecf = float __attribute__((ext_vector_type(NT)));
   __shared__ __attribute__((aligned(16))) float ws[P::CHUNK];
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -243,6 +248,9 @@ __global__ __launch_bounds__(kConvThreads) void conv1x1_kernel(const ConvArgs a)
   const long long V = (long long)a.D * a.H * a.W;
   const long long v0 = ((long long)blockIdx.x * kConvWaves + wave) * NT * 16;
   const int kq = lane >> 4, n = lane & 15;
+  // voxel of (lane, tile j): VEC v0 + NT n + j, else v0 + 16 j + n
+  auto vox = [&](int j) -> long long { return VEC ? v0 + NT * n + j : v0 + j * 16 + n; };
+  const bool full = VEC && vox(NT - 1) < V;
 
   f32x4 acc[MT][NT];
 #pragma unroll
@@ -257,10 +265,16 @@ __global__ __launch_bounds__(kConvThreads) void conv1x1_kernel(const ConvArgs a)
       const int c = ch * CIN_B + 4 * s + kq;
       const float* src = (c < a.cin1) ? a.x + (long long)b * a.xbs + (long long)c * V
                                       : a.x2 + (long long)b * a.x2bs + (long long)(c - a.cin1) * V;
+      if (VEC && full && c < a.cin) {
+        const vecf t = *reinterpret_cast<const vecf*>(src + vox(0));
 #pragma unroll
-      for (int j = 0; j < NT; ++j) {
-        const long long v = v0 + j * 16 + n;
-        bv[s][j] = (c < a.cin && v < V) ? src[v] : 0.f;
+        for (int j = 0; j < NT; ++j) bv[s][j] = t[j];
+      } else {
+#pragma unroll
+        for (int j = 0; j < NT; ++j) {
+          const long long v = vox(j);
+          bv[s][j] = (c < a.cin && v < V) ? src[v] : 0.f;
+        }
       }
     }
     __syncthreads();  // previous chunk's weight reads are done
@@ -294,9 +308,25 @@ __global__ __launch_bounds__(kConvThreads) void conv1x1_kernel(const ConvArgs a)
       if (co >= a.cout) continue;
       const float sc = a.scale ? a.scale[co] : 1.f;
       const float sh = a.shift ? a.shift[co] : 0.f;
+      if (VEC && full) {
+        const long long o = (long long)co * V + vox(0);
+        vecf val;
+#pragma unroll
+        for (int j = 0; j < NT; ++j) {
+          val[j] = acc[m][j][r] * sc + sh;
+          if (relu) val[j] = fmaxf(val[j], 0.f);
+        }
+        if (resid) {
+          const vecf rv = *reinterpret_cast<const vecf*>(a.res + (long long)b * a.rbs + o);
+#pragma unroll
+          for (int j = 0; j < NT; ++j) val[j] += rv[j];
+        }
+        *reinterpret_cast<vecf*>(a.y + (long long)b * a.ybs + o) = val;
+        continue;
+      }
 #pragma unroll
       for (int j = 0; j < NT; ++j) {
-        const long long v = v0 + j * 16 + n;
+        const long long v = vox(j);
         if (v >= V) continue;
         const long long o = (long long)co * V + v;
         float val = acc[m][j][r] * sc + sh;
@@ -622,13 +652,20 @@ int run_rs(const ConvArgs& a, int tw, int B, hipStream_t st) {
   return launch(conv3d_reg_kernel<KS, MT, NT, 32, true>, a, LEA_TILE_TH(KS, MT, NT, 32), 32, B, st);
 }
 
+int g_1x1_vec = 1;  // lea_conv1x1_set_vector: the NT-float vector form of conv1x1_kernel
+
 template <int MT, int NT>
 int launch_1x1(const ConvArgs& a, int B, hipStream_t st) {
   const long long vox = (long long)a.D * a.H * a.W;
   const long long per = kConvWaves * NT * 16;
   const long long gx = (vox + per - 1) / per;
   LEA_CHECK_ARG(gx < (1LL << 31) && (long long)B * a.ncob <= 65535, "lea_conv3d: grid too large");
-  conv1x1_kernel<MT, NT><<<dim3((unsigned)gx, B * a.ncob), kConvThreads, 0, st>>>(a);
+  // the vector form needs every per-channel and per-batch base on an NT-float boundary
+  auto al = [](const void* q) { return q == nullptr || ((uintptr_t)q % (NT * 4)) == 0; };
+  const bool vec = g_1x1_vec && vox % NT == 0 && al(a.x) && al(a.x2) && al(a.y) && al(a.res) &&
+                   a.xbs % NT == 0 && a.x2bs % NT == 0 && a.ybs % NT == 0 && a.rbs % NT == 0;
+  if (vec) conv1x1_kernel<MT, NT, true><<<dim3((unsigned)gx, B * a.ncob), kConvThreads, 0, st>>>(a);
+  else conv1x1_kernel<MT, NT, false><<<dim3((unsigned)gx, B * a.ncob), kConvThreads, 0, st>>>(a);
   return launch_status("lea_conv3d");
 }
 
@@ -779,6 +816,13 @@ extern "C" int lea_conv3d_set_rs_gather(int on) {
   lea::clear_error();
   LEA_CHECK_ARG(on == 0 || on == 1, "lea_conv3d_set_rs_gather: on=%d", on);
   lea::g_rs_gather = on;
+  return 0;
+}
+
+extern "C" int lea_conv1x1_set_vector(int on) {
+  lea::clear_error();
+  LEA_CHECK_ARG(on == 0 || on == 1, "lea_conv1x1_set_vector: on=%d", on);
+  lea::g_1x1_vec = on;
   return 0;
 }
 

@@ -67,6 +67,7 @@ def test_invalid_arguments_are_rejected_before_launch():
     finally:
         lib.lea_conv3d_set_rs_gather(1)
     assert lib.lea_conv3d_kernel_name(1, 8, 32, 96, 160, 1, 0) == b"conv1x1_kernel<1, 4>"
+    assert lib.lea_conv1x1_set_vector(2) == 1001 and lib.lea_conv1x1_set_vector(1) == 0
     # unsupported dtype is reported as such
     assert lib.lea_disparity_regression(x, x, 1, 1, 1, 1, 1, 7, None) == 1002
     assert lib.lea_resample3d_trilinear(x, 0, x, 0, 1, 1, 1, 1, 1, 1, 1, 1, 1, None, None, 0, 0,

@@ -175,6 +175,46 @@ def test_conv_resampled_vs_torch(k, cin, cout, src, dst):
     np.testing.assert_allclose(y.cpu().double().numpy(), refy.numpy(), rtol=1e-4, atol=1e-4)
 
 
+@pytest.mark.parametrize("b,cin,cin2,cout,shape,resid", [
+    (2, 24, 0, 8, (8, 12, 20), False), (1, 48, 0, 16, (4, 6, 10), True),
+    (2, 32, 16, 32, (5, 7, 12), False),     # virtual concat, D*H*W % 4 == 0
+    (1, 64, 0, 48, (3, 5, 7), True),        # D*H*W odd: the vector form declines
+    (3, 96, 32, 64, (2, 9, 20), False), (1, 8, 0, 16, (1, 1, 4), True)])
+def test_conv1x1_vector_form_is_the_scalar_form(b, cin, cin2, cout, shape, resid):
+    """lea_conv1x1_set_vector(1) (lane n owns NT consecutive voxels: vector loads and
+    stores) stores exactly what the one-float-per-lane form stores, into a channel slice,
+    with the residual epilogue and a second source; both against torch in float64."""
+    lib = _lib.load()
+    g = torch.Generator(device=DEV).manual_seed(cin + cout + cin2)
+    x = torch.randn((b, cin) + shape, device=DEV, generator=g)
+    x2 = torch.randn((b, cin2) + shape, device=DEV, generator=g) if cin2 else None
+    w = torch.randn(cout, cin + cin2, 1, 1, 1, device=DEV, generator=g) / np.sqrt(cin + cin2)
+    scale = torch.rand(cout, device=DEV, generator=g) + 0.5
+    shift = torch.randn(cout, device=DEV, generator=g) * 0.1
+    res = torch.randn((b, cout) + shape, device=DEV, generator=g) if resid else None
+    base = torch.randn((b, cout + 8) + shape, device=DEV, generator=g)
+    pw = kernels.pack_conv_weight(w)
+    outs = []
+    try:
+        for on in (0, 1):
+            assert lib.lea_conv1x1_set_vector(on) == 0
+            y = base.clone()
+            kernels.conv3d_bnrelu(x, pw, cout, 1, scale, shift, relu=True, out=y[:, 4:4 + cout], x2=x2,
+                                  residual=res)
+            outs.append(y)
+    finally:
+        lib.lea_conv1x1_set_vector(1)
+    assert torch.equal(outs[0], outs[1])
+    xin = torch.cat((x, x2), 1) if cin2 else x
+    want = torch.relu(F.conv3d(xin.double(), w.double()) * scale.double().view(1, -1, 1, 1, 1)
+                      + shift.double().view(1, -1, 1, 1, 1))
+    if resid:
+        want = want + res.double()
+    np.testing.assert_allclose(outs[1][:, 4:4 + cout].cpu().double().numpy(), want.cpu().numpy(),
+                               rtol=1e-4, atol=1e-4)
+    assert torch.equal(outs[1][:, :4], base[:, :4]) and torch.equal(outs[1][:, 4 + cout:], base[:, 4 + cout:])
+
+
 @pytest.mark.parametrize("cin,cout,src,dst", [
     (32, 32, (8, 12, 20), (4, 6, 10)),      # L0 -> L1 stacked share conv
     (64, 64, (5, 9, 17), (3, 5, 9)),        # L1 -> L2 stacked, odd sizes
