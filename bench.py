@@ -117,6 +117,13 @@ def parse(argv=None):
                    help="matching-net arithmetic (bf16 = BASELINE configs 3/4)")
     p.add_argument("--config", choices=sorted(CONFIGS), default=None,
                    help="preset: c2 (default workload) / c3 / c4 (per GPU) / c5 of BASELINE.json")
+    p.add_argument("--extra-configs", default="auto",
+                   help="BASELINE configs timed after the headline one (graph replays, no CPU legs), "
+                        "comma list; auto = c3,c5 at N = 1 and c4 at N > 1; empty to skip")
+    p.add_argument("--extra-steps", type=int, default=10, help="timed steps per extra config")
+    p.add_argument("--dist-backend", choices=("nccl", "gloo"), default="nccl",
+                   help="N > 1 process group: nccl (= RCCL over xGMI) or gloo (rehearsal of the N-rank "
+                        "path on fewer GPUs: every rank on cuda:0 when the box has fewer GPUs than ranks)")
     p.add_argument("--stub", type=int, default=0, help=argparse.SUPPRESS)  # tests: no GPU, gloo
     a = p.parse_args(argv)
     if a.config:
@@ -471,31 +478,28 @@ def run_stub(args, info):
     parallel.finalize()
 
 
-def run(args, info):
+def measure(a, info, device, *, steps, warmup, pair_check, epe):
+    """One configuration on this rank: build the model, capture the forward (``a.graph``),
+    ``warmup`` untimed steps, one probed eager forward (the path roofline and the dominant
+    conv kernel), then EXACTLY ``steps`` timed steps bracketed by barrier + synchronize on
+    both sides, the max over ranks; after the timed region the per-pair check of this
+    rank's shard and the golden EPE.  Returns the pieces ``run`` assembles."""
     world, rank = info.world, info.rank
-    device = torch.device("cuda", info.local_rank)
-    if world > 1:
-        torch.cuda.set_device(device)
-    parallel.init("nccl", info, device)  # nccl = RCCL over xGMI on ROCm
-    torch.set_num_threads(rank_threads(world))  # the cpu_baseline leg (N = 1) resets it
-    torch.backends.cudnn.allow_tf32 = False
-    torch.backends.cuda.matmul.allow_tf32 = False
-
-    model = build_model(args.maxdisp, device, args.precision)
-    model.check_shape(args.height, args.width)
+    model = build_model(a.maxdisp, device, a.precision)
+    model.check_shape(a.height, a.width)
     # weak scaling: rank r owns pairs shard(r) of the world*batch global batch, generated
     # on its own device from a rank-seeded stream
-    shard = parallel.shard(world * args.batch, info)
-    assert len(shard) == args.batch
+    shard = parallel.shard(world * a.batch, info)
+    assert len(shard) == a.batch
     g = torch.Generator(device=device).manual_seed(1234 + rank)
-    left = torch.randn(args.batch, 3, args.height, args.width, device=device, generator=g)
-    right = torch.randn(args.batch, 3, args.height, args.width, device=device, generator=g)
+    left = torch.randn(a.batch, 3, a.height, a.width, device=device, generator=g)
+    right = torch.randn(a.batch, 3, a.height, a.width, device=device, generator=g)
 
     def step():
         return model(left, right)
 
-    if args.graph:
-        graphed = model.graphed(args.batch, args.height, args.width)
+    if a.graph:
+        graphed = model.graphed(a.batch, a.height, a.width)
 
         def step():  # noqa: F811  (inputs already resident: replay only)
             graphed.graph.replay()
@@ -504,7 +508,7 @@ def run(args, info):
         graphed.y.copy_(right)
 
     with torch.no_grad():
-        for _ in range(max(args.warmup, 1)):
+        for _ in range(max(warmup, 1)):
             out = step()
         # every launch of one (untimed) eager forward: the path roofline, and the
         # dominant conv kernel instantiation
@@ -514,7 +518,7 @@ def run(args, info):
         t_roof_ms, t_hbm_ms, t_mat_ms, n_launch = path_roofline(probe.records)
         convs = {n: d for n, d in per_kernel.items() if d["mfma_flops"] > 0}
         dominant = max(convs, key=lambda n: convs[n]["ms"])
-        if args.breakdown and info.is_main:
+        if getattr(a, "breakdown", 0) and info.is_main:
             for n, d in sorted(per_kernel.items(), key=lambda kv: -kv[1]["ms"]):
                 log(f"{n:48s} launches {d['launches']:3d}  {d['ms']:8.3f} ms  "
                     f"{d['mfma_flops'] / d['ms'] / 1e9:8.1f} TFLOP/s issued  "
@@ -525,32 +529,32 @@ def run(args, info):
         with kernels.KernelProbe([dominant]) as probe:
             # per-step latency: HIP events between consecutive steps (SURVEY §8d's
             # median and p10/p90), on the stream the forward is launched on
-            ev = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps + 1)]
+            ev = [torch.cuda.Event(enable_timing=True) for _ in range(steps + 1)]
             t0 = time.perf_counter()
             ev[0].record()
-            for i in range(args.steps):
+            for i in range(steps):
                 out = step()
                 ev[i + 1].record()
             torch.cuda.synchronize()
             parallel.barrier()
             elapsed = time.perf_counter() - t0
-        if args.graph:  # replays bypass the launch-time probe: time one eager forward after
+        if a.graph:  # replays bypass the launch-time probe: time one eager forward after
             with kernels.KernelProbe([dominant]) as probe:
                 model(left, right)
         dom = probe.summary()[dominant]
         dom_shapes = probe.by_shape(dominant)
-        step_ms = sorted(ev[i].elapsed_time(ev[i + 1]) for i in range(args.steps))
+        step_ms = sorted(ev[i].elapsed_time(ev[i + 1]) for i in range(steps))
     elapsed = parallel.max_over_ranks(elapsed, device)
     per_rank_steps = gather_step_stats(step_ms, device)
 
     # after the timed region: the per-pair check of this rank's shard against an
     # independent HIP path, then the data path's one collective (all-gather over ranks)
     pair = None
-    if args.pair_check:
-        ref_prec = "f32_direct" if args.precision == "f32" else "f32"
+    if pair_check:
+        ref_prec = "f32_direct" if a.precision == "f32" else "f32"
         with independent_check_engines():
             with torch.no_grad():
-                check = build_model(args.maxdisp, device, ref_prec)(left, right)
+                check = build_model(a.maxdisp, device, ref_prec)(left, right)
                 torch.cuda.synchronize()
         e = (out.double() - check.double()).abs().mean(dim=(1, 2)).float()
         del check
@@ -560,27 +564,35 @@ def run(args, info):
                        "stem0), the feature net's 3x3 convs on the DMA/MFMA engine (no few-channel "
                        "tile, no pair launch) with unfused stems, the per-output gather resample and "
                        "the online-softmin LDS disparity kernel; only the streamed 1x1 conv kernel "
-                       "is common to both" if args.precision == "f32" else
+                       "is common to both" if a.precision == "f32" else
                        "HIP f32 path, same weights, the feature net's 3x3 convs on the DMA/MFMA engine "
                        "with unfused stems, the per-output gather resample, online-softmin LDS "
                        "disparity kernel"),
-                "pairs": world * args.batch, "max": max(per_pair), "mean": sum(per_pair) / len(per_pair),
+                "pairs": world * a.batch, "max": max(per_pair), "mean": sum(per_pair) / len(per_pair),
                 "per_pair": per_pair}
-    epe = None
-    if args.epe:
-        e = torch.tensor([golden_epe(device, args.precision)], device=device, dtype=torch.float32)
-        epe = [float(v) for v in parallel.gather_per_pair(e).cpu()]
+    epe_v = None
+    if epe:
+        e = torch.tensor([golden_epe(device, a.precision)], device=device, dtype=torch.float32)
+        epe_v = [float(v) for v in parallel.gather_per_pair(e).cpu()]
+    return dict(model=model, left=left, right=right, out=out, elapsed=elapsed, step_ms=step_ms,
+                per_rank_steps=per_rank_steps, dominant=dominant, dom=dom, dom_shapes=dom_shapes,
+                t_roof_ms=t_roof_ms, t_hbm_ms=t_hbm_ms, t_mat_ms=t_mat_ms, n_launch=n_launch,
+                pair=pair, epe=epe_v, steps=steps)
 
+
+def roofline_fields(a, m):
+    """The dominant kernel's ``roofline`` and the forward's ``path_roofline`` objects of a
+    measured configuration (``measure``)."""
+    dominant, dom, dom_shapes = m["dominant"], m["dom"], m["dom_shapes"]
     launches = dom["launches"]
     ms_per_launch = dom["ms"] / launches
     issued = dom["mfma_flops"] / launches
     direct = dom["flops"] / launches
-    bf16 = args.precision == "bf16"
-    peak = BF16_MFMA_PEAK_TFLOPS if bf16 else FP32_PEAK_TFLOPS
+    peak = BF16_MFMA_PEAK_TFLOPS if a.precision == "bf16" else FP32_PEAK_TFLOPS
     achieved = issued / (ms_per_launch * 1e-3) / 1e12
     alg_bytes = dom["bytes"] / launches  # inputs + output (+ residual) + weights, once
     traffic = None
-    cfg = config_name(args)
+    cfg = config_name(a)
     tf_file = os.path.join(REPO, "profiles", "hbm_traffic.json")
     if os.path.exists(tf_file):
         with open(tf_file) as f:
@@ -589,13 +601,92 @@ def run(args, info):
         # (bytes per launch depend on the shapes)
         entry = tf.get(f"{dominant}@{cfg}") or (tf.get(dominant) if cfg == "c2" else None) or {}
         traffic = entry.get("bytes_per_launch")
-    ms_step = elapsed / args.steps * 1e3
-    probed_steps = 1 if args.graph else args.steps  # forwards the dominant kernel's probe saw
+    ms_step = m["elapsed"] / m["steps"] * 1e3
+    probed_steps = 1 if a.graph else m["steps"]  # forwards the dominant kernel's probe saw
+    roof = {"bound": "mfma", "kernel": dominant, "algorithm": algorithm_name(dominant),
+            "achieved": achieved, "peak": peak, "unit": "TFLOP/s", "frac": achieved / peak,
+            "traffic": traffic, "algorithmic_bytes_per_launch": alg_bytes,
+            "traffic_over_algorithmic": None if traffic is None else traffic / alg_bytes,
+            "work": "MFMA FLOPs the kernel issues per launch (Winograd products, cout "
+                    "padded to its blocks); DESIGN.md §4 gives the per-launch formula",
+            "flops_per_launch": issued, "ms_per_launch": ms_per_launch,
+            "launches_per_step": launches / probed_steps,
+            "timed_over": "one eager forward after the timed graph replays (replays bypass "
+                          "the launch probe)" if a.graph else "every step of the timed region",
+            "by_shape": [{"shape": "B%d %d->%d @ %dx%dx%d k%d" % sh if sh else None,
+                          "launches_per_step": d["launches"] / probed_steps,
+                          "ms_per_launch": d["ms"] / d["launches"],
+                          "issued_tflops": d["mfma_flops"] / d["ms"] / 1e9,
+                          "frac": d["mfma_flops"] / d["ms"] / 1e9 / peak}
+                         for sh, d in sorted(dom_shapes.items(), key=lambda kv: -kv[1]["ms"])],
+            "direct_equivalent": {"flops_per_launch": direct,
+                                  "achieved": direct / (ms_per_launch * 1e-3) / 1e12,
+                                  "note": "the reference algorithm's (direct convolution's) "
+                                          "FLOPs for the same outputs; not a utilisation"}}
+    path = {"t_roof_ms": m["t_roof_ms"], "frac": m["t_roof_ms"] / ms_step,
+            "hbm_only_ms": m["t_hbm_ms"], "hbm_frac": m["t_hbm_ms"] / ms_step,
+            "hbm_frac_rule": "bytes this implementation's kernels must move (each launch's "
+                             "inputs + output + residual + weights once; the factored stem0 "
+                             "and fused layers as run) / 8 TB/s, over the step",
+            "hbm_frac_baseline_accounting": (
+                None if HBM_ONLY_REFERENCE_MS.get((cfg, a.batch)) is None else
+                HBM_ONLY_REFERENCE_MS[(cfg, a.batch)] / ms_step),
+            "hbm_frac_baseline_rule": "BASELINE.md §3: the reference algorithm's ConvBR-fused "
+                                      "bytes (C2 21.36 GB fp32, C3 74.0 / C4 85.4 GB per 8 "
+                                      "pairs bf16) / 8 TB/s, over the step",
+            "matrix_only_ms": m["t_mat_ms"], "launches": m["n_launch"],
+            "source": "one eager forward: sum over its launches of max(issued MFMA FLOP / "
+                      "peak, VALU FLOP / fp32 peak, algorithmic bytes / 8 TB/s)",
+            "reference_algorithm_t_roof_ms": T_ROOF_REFERENCE_MS.get((cfg, a.batch))}
+    return roof, path
+
+
+def extra_legs(args, world):
+    """BASELINE configs timed after the headline leg: at N = 1 the bf16
+    KITTI batch (c3) and Middlebury (c5); at N > 1 config 4 (bf16, 8 pairs per GPU), the
+    one BASELINE.md §4 names for the scaling curve.  The headline config is never repeated."""
+    if args.extra_configs != "auto":
+        names = [c for c in args.extra_configs.split(",") if c]
+    else:
+        names = ["c3", "c5"] if world == 1 else ["c4"]
+    return [c for c in names if c != config_name(args)]
+
+
+def leg_args(args, cfg):
+    a = argparse.Namespace(**vars(args))
+    for k, v in CONFIGS[cfg].items():
+        setattr(a, k, v)
+    return a
+
+
+def run(args, info):
+    world = info.world
+    backend = args.dist_backend
+    if backend == "gloo" and torch.cuda.device_count() < world:
+        # gloo rehearsal of the N-rank path on a box with fewer GPUs (tests/test_gpu_bench.py):
+        # every rank on cuda:0; the device tensors' collectives go through host copies
+        device = torch.device("cuda", 0)
+    else:
+        device = torch.device("cuda", info.local_rank)
+    if world > 1:
+        torch.cuda.set_device(device)
+    parallel.init(backend, info, device)  # nccl = RCCL over xGMI on ROCm
+    torch.set_num_threads(rank_threads(world))  # the cpu_baseline leg (N = 1) resets it
+    torch.backends.cudnn.allow_tf32 = False
+    torch.backends.cuda.matmul.allow_tf32 = False
+
+    m = measure(args, info, device, steps=args.steps, warmup=args.warmup,
+                pair_check=args.pair_check, epe=args.epe)
+    roof, path = roofline_fields(args, m)
+    ms_step = m["elapsed"] / args.steps * 1e3
+    step_ms = m["step_ms"]
+    cfg = config_name(args)
+    bf16 = args.precision == "bf16"
     workload = WORKLOADS.get(cfg, f"{args.height}x{args.width} D={args.maxdisp} {args.precision}, "
                                   f"batch {args.batch} per GPU")
     result = {
         "metric": METRIC,
-        "value": world * args.batch * args.steps / elapsed,
+        "value": world * args.batch * args.steps / m["elapsed"],
         "unit": "pairs/s",
         "n_gpus": world,
         "steps": args.steps,
@@ -603,7 +694,7 @@ def run(args, info):
         "ms_per_step": ms_step,
         "step_ms": {"median": _quantile(step_ms, 0.5), "p10": _quantile(step_ms, 0.1),
                     "p90": _quantile(step_ms, 0.9), "source": "HIP events between steps, this rank"},
-        "per_rank_step_ms": per_rank_steps,
+        "per_rank_step_ms": m["per_rank_steps"],
         "host_threads_per_rank": torch.get_num_threads(),
         "higher_is_better": True,
         "scaling": "weak",
@@ -615,51 +706,50 @@ def run(args, info):
                    "height": args.height, "width": args.width, "maxdisp": args.maxdisp,
                    "global_batch": world * args.batch,
                    "parallelism": f"dp{world} (pairs sharded over ranks, no collective in the step)",
-                   "launch": "hip graph replay" if args.graph else "eager"},
-        "roofline": {"bound": "mfma", "kernel": dominant, "algorithm": algorithm_name(dominant),
-                     "achieved": achieved, "peak": peak, "unit": "TFLOP/s", "frac": achieved / peak,
-                     "traffic": traffic, "algorithmic_bytes_per_launch": alg_bytes,
-                     "traffic_over_algorithmic": None if traffic is None else traffic / alg_bytes,
-                     "work": "MFMA FLOPs the kernel issues per launch (Winograd products, cout "
-                             "padded to its blocks); DESIGN.md §4 gives the per-launch formula",
-                     "flops_per_launch": issued, "ms_per_launch": ms_per_launch,
-                     "launches_per_step": launches / probed_steps,
-                     "timed_over": "one eager forward after the timed graph replays (replays bypass "
-                                   "the launch probe)" if args.graph else "every step of the timed region",
-                     "by_shape": [{"shape": "B%d %d->%d @ %dx%dx%d k%d" % sh if sh else None,
-                                   "launches_per_step": d["launches"] / probed_steps,
-                                   "ms_per_launch": d["ms"] / d["launches"],
-                                   "issued_tflops": d["mfma_flops"] / d["ms"] / 1e9,
-                                   "frac": d["mfma_flops"] / d["ms"] / 1e9 / peak}
-                                  for sh, d in sorted(dom_shapes.items(), key=lambda kv: -kv[1]["ms"])],
-                     "direct_equivalent": {"flops_per_launch": direct,
-                                           "achieved": direct / (ms_per_launch * 1e-3) / 1e12,
-                                           "note": "the reference algorithm's (direct convolution's) "
-                                                   "FLOPs for the same outputs; not a utilisation"}},
-        "path_roofline": {"t_roof_ms": t_roof_ms, "frac": t_roof_ms / ms_step,
-                          "hbm_only_ms": t_hbm_ms, "hbm_frac": t_hbm_ms / ms_step,
-                          "hbm_frac_rule": "bytes this implementation's kernels must move (each launch's "
-                                           "inputs + output + residual + weights once; the factored stem0 "
-                                           "and fused layers as run) / 8 TB/s, over the step",
-                          "hbm_frac_baseline_accounting": (
-                              None if HBM_ONLY_REFERENCE_MS.get((cfg, args.batch)) is None else
-                              HBM_ONLY_REFERENCE_MS[(cfg, args.batch)] / ms_step),
-                          "hbm_frac_baseline_rule": "BASELINE.md §3: the reference algorithm's ConvBR-fused "
-                                                    "bytes (C2 21.36 GB fp32, C3 74.0 / C4 85.4 GB per 8 "
-                                                    "pairs bf16) / 8 TB/s, over the step",
-                          "matrix_only_ms": t_mat_ms, "launches": n_launch,
-                          "source": "one eager forward: sum over its launches of max(issued MFMA FLOP / "
-                                    "peak, VALU FLOP / fp32 peak, algorithmic bytes / 8 TB/s)",
-                          "reference_algorithm_t_roof_ms": T_ROOF_REFERENCE_MS.get((cfg, args.batch))},
-        "pair_epe_px": pair,
-        "epe_px": None if epe is None else {
+                   "launch": "hip graph replay" if args.graph else "eager",
+                   "dist_backend": backend if world > 1 else None},
+        "roofline": roof,
+        "path_roofline": path,
+        "pair_epe_px": m["pair"],
+        "epe_px": None if m["epe"] is None else {
             "vs": "reference LEAStereo fp32 disparity (tests/golden e2e b1_h96_w192_md48)"
                   + (" (bf16 matching net: no upstream tolerance; see DESIGN.md)" if bf16 else ""),
-            "max_over_ranks": max(epe), "per_rank": epe},
+            "max_over_ranks": max(m["epe"]), "per_rank": m["epe"]},
     }
     if info.is_main and world == 1 and args.cpu_baseline:
-        result["cpu_baseline"] = cpu_baseline(args, model, left[:1], right[:1], out[:1],
+        result["cpu_baseline"] = cpu_baseline(args, m["model"], m["left"][:1], m["right"][:1], m["out"][:1],
                                               float(_quantile(step_ms, 0.5)) * 1e-3, device)
+        torch.set_num_threads(rank_threads(world))
+    legs = extra_legs(args, world)
+    if legs:
+        del m
+        torch.cuda.empty_cache()
+        result["configs"] = {}
+    for name in legs:
+        # the other BASELINE configs on the same box in the same run (top-level fields stay
+        # the headline config's): graph replays only, no CPU or eager legs; at N > 1 the
+        # per-pair check and its all-gather run too (north_star's one RCCL gather of per-pair EPE)
+        a = leg_args(args, name)
+        lm = measure(a, info, device, steps=args.extra_steps, warmup=2, pair_check=world > 1, epe=False)
+        lroof, lpath = roofline_fields(a, lm)
+        lms = lm["elapsed"] / args.extra_steps * 1e3
+        result["configs"][name] = {
+            "workload": WORKLOADS[name], "value": world * a.batch * args.extra_steps / lm["elapsed"],
+            "unit": "pairs/s", "dtype": a.precision, "global_batch": world * a.batch,
+            "steps": args.extra_steps, "warmup": 2, "ms_per_step": lms,
+            "step_ms": {"median": _quantile(lm["step_ms"], 0.5), "p10": _quantile(lm["step_ms"], 0.1),
+                        "p90": _quantile(lm["step_ms"], 0.9)},
+            "per_rank_step_ms": lm["per_rank_steps"],
+            "roofline": {k: lroof[k] for k in ("kernel", "achieved", "peak", "unit", "frac", "traffic",
+                                               "traffic_over_algorithmic", "ms_per_launch",
+                                               "launches_per_step", "by_shape")},
+            "path_roofline": {k: lpath[k] for k in ("t_roof_ms", "frac", "hbm_frac",
+                                                    "hbm_frac_baseline_accounting")},
+            "pair_epe_px": lm["pair"],
+            "timing": f"{args.extra_steps} timed graph replays after 2 warm-up, barrier + synchronize "
+                      "on both sides, max over ranks"}
+        del lm
+        torch.cuda.empty_cache()
     if info.is_main:
         print(json.dumps(result), flush=True)
     parallel.finalize()

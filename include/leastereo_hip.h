@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define LEA_ABI_VERSION 12
+#define LEA_ABI_VERSION 13
 
 #define LEA_F32 0
 #define LEA_BF16 1
@@ -234,6 +234,11 @@ int lea_conv3d_bnrelu_costvolume_bf16(const void* left, const void* right, int64
 /* Kernel instantiation the bf16 conv of this shape launches. */
 const char* lea_conv3d_kernel_name_bf16(int B, int cout, int cin, int D, int H, int W, int k,
                                         int costvolume);
+
+/* 1 if lea_conv3d_bnrelu_bf16 takes LEA_PAIR_SUM for two sources of `cin` channels each
+ * into `cout` (3x3x3) at this shape -- the planner's D-streaming form under the current
+ * tuning (ABI 13) -- else 0; a caller falls back to two launches when 0. */
+int lea_conv3d_bf16_pair_supported(int B, int cin, int cout, int D, int H, int W);
 
 /* ConvBR 1x1 of a trilinearly resampled c8 input (align_corners=True): the cell
  * preprocess after a level change, skip_model_3d.py:44-53, without the resampled

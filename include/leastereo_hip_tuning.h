@@ -96,7 +96,8 @@ int lea_tapsum_set_rows(int on);
  * workgroup reads when it owns R output rows plus `halo` rows either side, for a
  * trilinear axis Hi -> Ho (align_corners ac): the LDS bound of resample3d_rows/sep_f32
  * (halo 0) and tapsum_hwpass_rows_f32 (halo 1).  A kernel that ever met more rows than
- * this would write NaN rather than read rows it never staged. */
+ * this would write NaN rather than read rows it never staged.  Returns -1 (and sets
+ * lea_last_error) on bad arguments: any positive value is a row count. */
 int lea_staged_rows(int Hi, int Ho, int ac, int R, int halo);
 
 /* 1 = the Winograd entries run 16-cout layers (the L1 cells' 16 -> 16 ops) on the F(2,3) along W

@@ -12,7 +12,7 @@ LIB_PATH = os.environ.get(
     "LEASTEREO_HIP_LIB",
     os.path.join(os.path.dirname(os.path.abspath(__file__)), "libleastereo_hip.so"))
 
-ABI_VERSION = 12
+ABI_VERSION = 13
 LEA_F32 = 0
 LEA_BF16 = 1
 LEA_RELU = 1
@@ -64,6 +64,7 @@ SIGNATURES = {
     "lea_conv3d_bnrelu_costvolume_bf16": (_i, [_p, _p, _i64, _p, _p, _p, _p, _i64, _i, _i, _i, _i,
                                                _i, _i, _u, _p]),
     "lea_conv3d_kernel_name_bf16": (ctypes.c_char_p, [_i, _i, _i, _i, _i, _i, _i, _i]),
+    "lea_conv3d_bf16_pair_supported": (_i, [_i, _i, _i, _i, _i, _i]),
     "lea_conv3d_bf16_set_tile_override": (_i, [_i, _i, _i]),
     "lea_conv3d_bf16_set_variant": (_i, [_i]),
     "lea_resample3d_trilinear_bf16": (_i, [_p, _i64, _p, _i64, _i, _i, _i, _i, _i, _i, _i, _i,

@@ -48,6 +48,22 @@ inline int launch_status(const char* what) {
     }                              \
   } while (0)
 
+// Epilogue flags an entry point accepts: LEA_PAIR_SUM where the entry has no
+// pair form is LEA_E_UNSUPPORTED (the header's contract), any other bit outside `allowed`
+// LEA_E_INVALID -- never silently a different computation.
+#define LEA_CHECK_FLAGS(flags, allowed, who)                                                  \
+  do {                                                                                       \
+    const unsigned lea_f_ = (flags), lea_a_ = (allowed);                                     \
+    if ((lea_f_ & LEA_PAIR_SUM) && !(lea_a_ & LEA_PAIR_SUM)) {                               \
+      ::lea::set_error("%s: LEA_PAIR_SUM is not supported by this entry point", (who));      \
+      return LEA_E_UNSUPPORTED;                                                              \
+    }                                                                                        \
+    if (lea_f_ & ~(lea_a_ | LEA_PAIR_SUM)) {                                                 \
+      ::lea::set_error("%s: unknown flag bits 0x%x", (who), lea_f_ & ~(lea_a_ | LEA_PAIR_SUM)); \
+      return LEA_E_INVALID;                                                                  \
+    }                                                                                        \
+  } while (0)
+
 constexpr int kWave = 64;
 
 // ---- trilinear interpolation with aten's source-index rule (UpSample.h:

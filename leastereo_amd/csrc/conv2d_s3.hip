@@ -185,6 +185,7 @@ extern "C" int lea_conv2d_s3_bnrelu(const void* x, int64_t x_bstride, const floa
                                     unsigned flags, int dtype, void* stream) {
   using namespace lea;
   clear_error();
+  LEA_CHECK_FLAGS(flags, LEA_RELU, "lea_conv2d_s3_bnrelu");
   LEA_CHECK_ARG(x && w && y && x != y, "lea_conv2d_s3_bnrelu: null or aliased pointer");
   LEA_CHECK_ARG((scale == nullptr) == (shift == nullptr),
                 "lea_conv2d_s3_bnrelu: scale/shift must both be set or both NULL");

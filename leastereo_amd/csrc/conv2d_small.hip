@@ -203,6 +203,7 @@ extern "C" int lea_conv2d_bnrelu_pair(const void* x, int64_t x_bstride, const fl
   LEA_CHECK_ARG(a.x && a.wp && a.y && a.y2, "lea_conv2d_bnrelu_pair: null pointer");
   LEA_CHECK_ARG((a.scale == nullptr) == (a.shift == nullptr),
                 "lea_conv2d_bnrelu_pair: scale/shift must both be set or both NULL");
+  LEA_CHECK_FLAGS(flags, LEA_RELU | LEA_RESIDUAL, "lea_conv2d_bnrelu_pair");
   LEA_CHECK_ARG(!(flags & LEA_RESIDUAL) || a.res, "lea_conv2d_bnrelu_pair: LEA_RESIDUAL without residual");
   LEA_CHECK_ARG(B > 0 && cin > 0 && H > 0 && W > 0 && c1 > 0 && c1 < cout && c1 % 8 == 0,
                 "lea_conv2d_bnrelu_pair: bad shape B=%d cin=%d cout=%d c1=%d H=%d W=%d", B, cin, cout, c1, H, W);

@@ -777,6 +777,7 @@ int conv_common(ConvArgs& a, int B, int k, bool resample, int dtype, void* strea
   LEA_CHECK_ARG(a.x && a.wp && a.y, "lea_conv3d: null pointer");
   LEA_CHECK_ARG((a.scale == nullptr) == (a.shift == nullptr),
                 "lea_conv3d: scale/shift must both be set or both NULL");
+  LEA_CHECK_FLAGS(a.flags, LEA_RELU | LEA_RESIDUAL, "lea_conv3d");
   LEA_CHECK_ARG(!(a.flags & LEA_RESIDUAL) || a.res, "lea_conv3d: LEA_RESIDUAL without residual");
   LEA_CHECK_ARG(B > 0 && a.cin > 0 && a.cout > 0 && a.D > 0 && a.H > 0 && a.W > 0,
                 "lea_conv3d: bad shape B=%d cin=%d cout=%d D=%d H=%d W=%d", B, a.cin, a.cout, a.D,
@@ -959,6 +960,7 @@ extern "C" int lea_conv2d_bnrelu(const void* x, int64_t x_bstride, const float* 
   LEA_CHECK_ARG(a.x && a.wp && a.y, "lea_conv2d: null pointer");
   LEA_CHECK_ARG((a.scale == nullptr) == (a.shift == nullptr),
                 "lea_conv2d: scale/shift must both be set or both NULL");
+  LEA_CHECK_FLAGS(flags, LEA_RELU | LEA_RESIDUAL, "lea_conv2d");
   LEA_CHECK_ARG(!(flags & LEA_RESIDUAL) || a.res, "lea_conv2d: LEA_RESIDUAL without residual");
   LEA_CHECK_ARG(B > 0 && cin > 0 && cout > 0 && H > 0 && W > 0,
                 "lea_conv2d: bad shape B=%d cin=%d cout=%d H=%d W=%d", B, cin, cout, H, W);
@@ -1013,6 +1015,7 @@ extern "C" int lea_conv3d_bnrelu_costvolume(const void* left, const void* right,
   a.H = H;
   a.W = W;
   a.flags = flags & LEA_RELU;
+  LEA_CHECK_FLAGS(flags, LEA_RELU, "lea_conv3d_bnrelu_costvolume");
   LEA_CHECK_ARG(left && right && w_packed && y && y != left && y != right,
                 "lea_conv3d_bnrelu_costvolume: null or aliased pointer");
   LEA_CHECK_ARG((scale == nullptr) == (shift == nullptr),

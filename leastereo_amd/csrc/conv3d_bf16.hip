@@ -1465,6 +1465,14 @@ extern "C" int lea_conv3d_pack_weights_bf16(const float* w, void* packed, int co
   return launch_status("lea_conv3d_pack_weights_bf16");
 }
 
+extern "C" int lea_conv3d_bf16_pair_supported(int B, int cin, int cout, int D, int H, int W) {
+  // the same conditions bf16_conv_common applies to LEA_PAIR_SUM (the tuning
+  // knobs can take a shape off the D-streaming plan)
+  if (B <= 0 || cin <= 0 || cout <= 0 || D <= 0 || H <= 0 || W <= 0 || cin % 8 || cout % 8) return 0;
+  const bf::Plan p = bf::plan(B, cout, D, H, W, 3, cin);
+  return cout <= 16 && p.nsplit > 0 && cin <= 8 * p.nb ? 1 : 0;
+}
+
 extern "C" const char* lea_conv3d_kernel_name_bf16(int B, int cout, int cin, int D, int H, int W,
                                                    int k, int costvolume) {
   if (B <= 0 || cout <= 0 || cin <= 0 || (k != 1 && k != 3) || D <= 0 || H <= 0 || W <= 0) return nullptr;
@@ -1542,6 +1550,8 @@ extern "C" int lea_conv3d_bnrelu_bf16(const void* x, int64_t x_bstride, const vo
   a.H = H;
   a.W = W;
   a.flags = flags;
+  clear_error();
+  LEA_CHECK_FLAGS(flags, LEA_RELU | LEA_RESIDUAL | LEA_PAIR_SUM, "lea_conv3d_bnrelu_bf16");
   if (cin2 % 8 != 0 || (cin2 > 0 && !x2)) {
     set_error("lea_conv3d_bnrelu_bf16: bad second source");
     return LEA_E_INVALID;
@@ -1571,6 +1581,8 @@ extern "C" int lea_conv3d_bnrelu_costvolume_bf16(const void* left, const void* r
   a.H = H;
   a.W = W;
   a.flags = flags & LEA_RELU;
+  clear_error();
+  LEA_CHECK_FLAGS(flags, LEA_RELU, "lea_conv3d_bnrelu_costvolume_bf16");
   if (C % 16 != 0) {  // chunks of 2 blocks must not straddle left/right
     set_error("lea_conv3d_bnrelu_costvolume_bf16: C=%d must be a multiple of 16", C);
     return LEA_E_INVALID;
@@ -1626,6 +1638,7 @@ extern "C" int lea_resample3d_trilinear_bf16(const void* x, int64_t x_bstride, v
                                              const float* scale, const float* shift,
                                              unsigned flags, void* stream) {
   clear_error();
+  LEA_CHECK_FLAGS(flags, LEA_RELU, "lea_resample3d_trilinear_bf16");
   LEA_CHECK_ARG(x && y && x != y, "lea_resample3d_trilinear_bf16: null or aliased pointer");
   LEA_CHECK_ARG((scale == nullptr) == (shift == nullptr),
                 "lea_resample3d_trilinear_bf16: scale/shift must both be set or both NULL");
@@ -1665,6 +1678,7 @@ extern "C" int lea_conv1x1_resampled_bf16(const void* x, int64_t x_bstride, int 
                                           void* y, int64_t y_bstride, int B, int cin, int cout, int D,
                                           int H, int W, unsigned flags, void* stream) {
   clear_error();
+  LEA_CHECK_FLAGS(flags, LEA_RELU, "lea_conv1x1_resampled_bf16");
   LEA_CHECK_ARG(x && w_packed && y && x != y, "lea_conv1x1_resampled_bf16: null or aliased pointer");
   LEA_CHECK_ARG((scale == nullptr) == (shift == nullptr),
                 "lea_conv1x1_resampled_bf16: scale/shift must both be set or both NULL");
@@ -1746,6 +1760,7 @@ extern "C" int lea_conv2d_bnrelu_bf16(const void* x, int64_t x_bstride, const vo
   LEA_CHECK_ARG(x && w_packed && y && x != y, "lea_conv2d_bnrelu_bf16: null or aliased pointer");
   LEA_CHECK_ARG((scale == nullptr) == (shift == nullptr),
                 "lea_conv2d_bnrelu_bf16: scale/shift must both be set or both NULL");
+  LEA_CHECK_FLAGS(flags, LEA_RELU | LEA_RESIDUAL, "lea_conv2d_bnrelu_bf16");
   LEA_CHECK_ARG(!(flags & LEA_RESIDUAL) || residual, "lea_conv2d_bnrelu_bf16: LEA_RESIDUAL without residual");
   LEA_CHECK_ARG(B > 0 && cin > 0 && cout > 0 && H > 0 && W > 0 && cin % 8 == 0 && cout % 8 == 0,
                 "lea_conv2d_bnrelu_bf16: bad shape B=%d cin=%d cout=%d H=%d W=%d", B, cin, cout, H, W);

@@ -591,6 +591,8 @@ extern "C" int lea_bn_forward_f32(const float* z, float* y, int B, int C, int64_
                                   const float* beta, float* running_mean, float* running_var, float momentum,
                                   float eps, int training, unsigned flags, float* mean, float* invstd,
                                   void* workspace, void* stream) {
+  lea::clear_error();
+  LEA_CHECK_FLAGS(flags, LEA_RELU, "lea_bn_forward_f32");
   LEA_CHECK_ARG(z && y && mean && invstd, "lea_bn_forward_f32: null pointer");
   LEA_CHECK_ARG(B > 0 && C > 0 && V > 0 && (long long)B * C <= 65535, "lea_bn_forward_f32: bad shape");
   LEA_CHECK_ARG((running_mean == nullptr) == (running_var == nullptr), "lea_bn_forward_f32: running stats pair");
@@ -618,6 +620,8 @@ extern "C" int lea_bn_backward_f32(const float* dy, const float* y, const float*
                                    int64_t V, const float* gamma, const float* mean, const float* invstd,
                                    int training, unsigned flags, float* dgamma, float* dbeta, void* workspace,
                                    void* stream) {
+  lea::clear_error();
+  LEA_CHECK_FLAGS(flags, LEA_RELU, "lea_bn_backward_f32");
   LEA_CHECK_ARG(dy && z && dz && mean && invstd && workspace, "lea_bn_backward_f32: null pointer");
   LEA_CHECK_ARG(!(flags & LEA_RELU) || y, "lea_bn_backward_f32: LEA_RELU needs y");
   LEA_CHECK_ARG(B > 0 && C > 0 && V > 0 && (long long)B * C <= 65535, "lea_bn_backward_f32: bad shape");

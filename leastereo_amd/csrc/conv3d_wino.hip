@@ -224,10 +224,8 @@ __global__ __launch_bounds__(kConvThreads, 2) void conv3d_wino_kernel(const Conv
 #pragma unroll
     for (int t = 0; t < WSLOTS_W; ++t) {
       const int j = wave + kConvWaves * t;
-#ifndef LEA_EXP_NOWDMA
       if (j < WSLOTS)  // the last piece reads into the next chunk / the buffer's tail pad
         dma_dwordx4(wsrc + j * 256 + lane * 4, lds0 + 4 * (unsigned)(wdst - smem + j * 256));
-#endif
     }
     const long long cvol = CV ? (long long)HW : (long long)HW * a.D;  // channel stride
     const unsigned crec = CV ? (unsigned)HW * 4u : nrec;
@@ -240,9 +238,7 @@ __global__ __launch_bounds__(kConvThreads, 2) void conv3d_wino_kernel(const Conv
                                        : a.x2 + (long long)b * a.x2bs + (long long)(c - a.cin1) * cvol;
         const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)base, 0, crec, 0x00020000);
         const int cb = C::cbh(0) + ci * C::CSH;
-#ifndef LEA_EXP_NOHALO  // ablation builds: outputs wrong, timing only
         if (ok16[t]) dma_dwordx4_buf(rs, voff16[t], lds0 + 4 * (unsigned)(st - smem + cb + (k % P16) * 256));
-#endif
       }
       return;
     }
@@ -265,9 +261,7 @@ __global__ __launch_bounds__(kConvThreads, 2) void conv3d_wino_kernel(const Conv
         const int j = wave + kConvWaves * t;
         unsigned vo = voff[t];
         if constexpr (CV) vo = voff[t] ^ ((voff[t] ^ voffr[t]) & rmask);
-#ifndef LEA_EXP_NOHALO
         if (j < XSLOTS) dma_dword(rs, vo, lds0 + 4 * (unsigned)(st - smem + ci * C::CIS + j * 64));
-#endif
       }
     }
   };
@@ -308,11 +302,7 @@ __global__ __launch_bounds__(kConvThreads, 2) void conv3d_wino_kernel(const Conv
 
   // epilogue of one depth group (output planes d0 ..): A^T, folded BN, ReLU, residual;
   // lane stores outputs w0 + F p .. + F - 1
-#ifdef LEA_EXP_NORES  // timing experiments (tools/build_variants.sh): no residual read
-  const bool relu = a.flags & LEA_RELU, resid = false;
-#else
   const bool relu = a.flags & LEA_RELU, resid = a.flags & LEA_RESIDUAL;
-#endif
   const long long DHW = (long long)HW * a.D;
   const int w = w0 + F * pq;
   // the buffer-addressed form (wino_common.h, F = 4): residual loads all issued first,
@@ -421,13 +411,7 @@ __global__ __launch_bounds__(kConvThreads, 2) void conv3d_wino_kernel(const Conv
           const float* rp = a.res + (long long)b * a.rbs + o;
           const bool vec = nv == F &&
               ((reinterpret_cast<uintptr_t>(yp) | (resid ? reinterpret_cast<uintptr_t>(rp) : 0)) & (4 * F - 1)) == 0;
-#ifdef LEA_EXP_NOSTORE  // timing experiments: keep the epilogue math, drop the stores
-          if (y[0] == 1234.5f) *yp = y[F - 1];
-          else if (true) {
-          } else if (vec) {
-#else
           if (vec) {
-#endif
             if constexpr (F == 2) {
               if (resid) {
                 const float2 rv = *reinterpret_cast<const float2*>(rp);
@@ -458,9 +442,6 @@ __global__ __launch_bounds__(kConvThreads, 2) void conv3d_wino_kernel(const Conv
   }
   };
 
-#ifdef LEA_EXP_STAGGER  // timing experiment: the second workgroup of a CU starts late
-  if (blockIdx.x >= 256 && blockIdx.x < 512) __builtin_amdgcn_s_sleep(LEA_EXP_STAGGER);
-#endif
   issue(0, smem);
   for (int it = 0; it < nitems; ++it) {
     const int ch = it % nchunks;
@@ -1062,6 +1043,7 @@ extern "C" int lea_conv3d_bnrelu_wino(const void* x, int64_t x_bstride, const vo
   a.H = H;
   a.W = W;
   a.flags = flags;
+  LEA_CHECK_FLAGS(flags, LEA_RELU | LEA_RESIDUAL | LEA_PAIR_SUM, "lea_conv3d_bnrelu_wino");
   LEA_CHECK_ARG(cin2 >= 0 && cin2 <= cin && (cin2 == 0 || x2), "lea_conv3d_bnrelu_wino: bad second source");
   return wino::common(a, B, false, dtype, stream);
 }
@@ -1090,6 +1072,7 @@ extern "C" int lea_conv3d_bnrelu_costvolume_wino(const void* left, const void* r
   a.H = H;
   a.W = W;
   a.flags = flags & LEA_RELU;
+  LEA_CHECK_FLAGS(flags, LEA_RELU, "lea_conv3d_bnrelu_costvolume_wino");
   LEA_CHECK_ARG(left && right && y != left && y != right,
                 "lea_conv3d_bnrelu_costvolume_wino: null or aliased pointer");
   return wino::common(a, B, true, dtype, stream);

@@ -157,26 +157,9 @@ __device__ __forceinline__ void aw4(const float a0, const float a1, const float 
 
 // Diagnostic build (-DLEA_EXP_STAMPS, tools/build_variants.sh): s_memtime stamps around
 // the loop's phases, per-wave cycle sums stored to ConvArgs::dbg (never in the real kernel)
-#ifdef LEA_EXP_STAMPS
-constexpr int kStampPhases = 8;  // dma wait, barrier 1, dma issue, V pass, barrier 2, steps, epilogue, total
-__device__ __forceinline__ unsigned long long stamp() {
-  unsigned long long t;
-  __builtin_amdgcn_sched_barrier(0);
-  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
-  __builtin_amdgcn_sched_barrier(0);
-  return t;
-}
-#define LEA_STAMP(k)                  \
-  do {                                \
-    const unsigned long long t_ = stamp(); \
-    st_sum[k] += t_ - st_prev;        \
-    st_prev = t_;                     \
-  } while (0)
-#else
 #define LEA_STAMP(k) \
   do {               \
   } while (0)
-#endif
 
 template <int Q, int WC, int MTE, int NW, int OCC, int PV, bool CV>
 __global__ __launch_bounds__(NW * 64, OCC) void conv3d_wino2_kernel(const ConvArgs a) {
@@ -328,10 +311,8 @@ __global__ __launch_bounds__(NW * 64, OCC) void conv3d_wino2_kernel(const ConvAr
 #pragma unroll
     for (int t = 0; t < WSLOTS_W; ++t) {
       const int j = wave + NW * t;
-#ifndef LEA_EXP_NOWDMA
       if (j < WSLOTS)  // the last piece reads into the next chunk / the buffer's tail pad
         dma_dwordx4(wsrc + j * 256 + lane * 4, lds0 + 4 * (unsigned)(wdst - smem + j * 256));
-#endif
     }
     const long long cvol = CV ? (long long)HW : (long long)HW * a.D;  // channel stride
     const unsigned crec = CV ? (unsigned)HW * 4u : nrec;
@@ -344,9 +325,7 @@ __global__ __launch_bounds__(NW * 64, OCC) void conv3d_wino2_kernel(const ConvAr
         const int c = ch * CIN_B + ci;
         const unsigned long long base = (c < a.cin1 ? xa : x2s) + cbase + coff4[k];
         const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)base, 0, crec, 0x00020000);
-#ifndef LEA_EXP_NOHALO
         dma_dwordx4_buf(rs, voff4[k], lds0 + 4 * (unsigned)(st - smem + C::cb4(0) + ci * C::CS4 + j * 256));
-#endif
       }
       return;
     }
@@ -360,9 +339,7 @@ __global__ __launch_bounds__(NW * 64, OCC) void conv3d_wino2_kernel(const ConvAr
                                        : a.x2 + (long long)b * a.x2bs + (long long)(c - a.cin1) * cvol;
         const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)base, 0, crec, 0x00020000);
         const int cb = ci == 0 ? C::cb2(0) : ci == 1 ? C::cb2(1) : ci == 2 ? C::cb2(2) : C::cb2(3);
-#ifndef LEA_EXP_NOHALO  // ablation builds (tools/wino2_ablate.sh): outputs wrong, timing only
         if (ok16) dma_dwordx4_buf(rs, voff16, lds0 + 4 * (unsigned)(st - smem + cb + j16 * 256));
-#endif
       }
       return;
     }
@@ -380,9 +357,7 @@ __global__ __launch_bounds__(NW * 64, OCC) void conv3d_wino2_kernel(const ConvAr
         const int j = wave + NW * t;
         unsigned vo = voff[t];
         if constexpr (CV) vo = voff[t] ^ ((voff[t] ^ voffr[t]) & rmask);
-#ifndef LEA_EXP_NOHALO
         if (PV == 0 || j < XSLOTS) dma_dword(rs, vo, lds0 + 4 * (unsigned)(st - smem + ci * C::CIS + j * 64));
-#endif
       }
     }
   };
@@ -420,11 +395,7 @@ __global__ __launch_bounds__(NW * 64, OCC) void conv3d_wino2_kernel(const ConvAr
   // epilogue of one depth pair (output planes d0, d0 + 1): A_W^T per D point, A_D^T
   // (with G_D's 1/2 factors), folded BN, ReLU, residual; the lane stores 4 outputs
   // along W for each of the two planes
-#ifdef LEA_EXP_NORES  // timing experiments (tools/build_variants.sh): no residual read
-  const bool relu = a.flags & LEA_RELU, resid = false;
-#else
   const bool relu = a.flags & LEA_RELU, resid = a.flags & LEA_RESIDUAL;
-#endif
   const long long DHW = (long long)HW * a.D;
   const int w = w0 + F * pq;
   const int h = h0 + trow;
@@ -514,13 +485,7 @@ __global__ __launch_bounds__(NW * 64, OCC) void conv3d_wino2_kernel(const ConvAr
           const float* rp = a.res + (long long)b * a.rbs + o;
           const bool vec = nv == F &&
               ((reinterpret_cast<uintptr_t>(yp) | (resid ? reinterpret_cast<uintptr_t>(rp) : 0)) & 15) == 0;
-#ifdef LEA_EXP_NOSTORE  // timing experiments: keep the epilogue math, drop the stores
-          if (y[0] == 1234.5f) *yp = y[F - 1];
-          else if (true) {
-          } else if (vec) {
-#else
           if (vec) {
-#endif
             if (resid) {
               const float4 rv = *reinterpret_cast<const float4*>(rp);
               y[0] += rv.x;
@@ -541,11 +506,6 @@ __global__ __launch_bounds__(NW * 64, OCC) void conv3d_wino2_kernel(const ConvAr
       }
   };
 
-#ifdef LEA_EXP_STAMPS
-  unsigned long long st_sum[kStampPhases] = {};
-  unsigned long long st_prev = stamp();
-  const unsigned long long st_begin = st_prev;
-#endif
   issue(0, 0, smem);
   LEA_STAMP(2);
   int ich = 0, ipr = 0;  // item it = (chunk, depth pair)
@@ -554,9 +514,7 @@ __global__ __launch_bounds__(NW * 64, OCC) void conv3d_wino2_kernel(const ConvAr
     const bool wrap = ich + 1 == nchunks;  // item it + 1 starts the next pair
     wait_item<NST>(ebuf && ch == 0 && it > 0);  // this wave's pieces of item it landed
     LEA_STAMP(0);
-#ifndef LEA_EXP_NOBAR1  // ablation builds (tools/wino2_ablate.sh): outputs wrong, timing only
     __syncthreads();  // ... and everyone's; item it-1's stage is free
-#endif
     LEA_STAMP(1);
     if (it + 1 < nitems) issue(wrap ? 0 : ich + 1, wrap ? ipr + 1 : ipr, smem + ((it + 1) & 1) * C::STAGE);
     LEA_STAMP(2);
@@ -568,11 +526,7 @@ __global__ __launch_bounds__(NW * 64, OCC) void conv3d_wino2_kernel(const ConvAr
       static_assert(PV == 2 || (C::RW % 64 == 34 && C::CIS % 64 == 32 && C::RH % 2 == 0 && Q == 8),
                     "transform pass bank map");
       static_assert(PV != 2 || (Q == 8 && CIN_B == 4), "transform pass bank map (16-byte halo)");
-#ifdef LEA_EXP_NOVPASS
-      for (int u = tid; u < 0; u += NW * 64) {
-#else
       for (int u = tid; u < C::NUNIT; u += NW * 64) {
-#endif
         // PV = 1: 32 consecutive units = 8 groups x 2 rows x 2 channels: the b64 reads'
         // dword offsets 4 g + {0, RW, CIS, RW + CIS} cover the 64 banks once.
         // PV = 2: 8 groups x 4 channels of one row: 4 g + CB2(c) + 3 covers them (Cfg2)
@@ -614,9 +568,7 @@ __global__ __launch_bounds__(NW * 64, OCC) void conv3d_wino2_kernel(const ConvAr
         for (int k = 0; k < 6; ++k) tp[k] = make_float4(vf[4 * k], vf[4 * k + 1], vf[4 * k + 2], vf[4 * k + 3]);
       }
       LEA_STAMP(3);
-#ifndef LEA_EXP_NOBAR2
       __syncthreads();
-#endif
       LEA_STAMP(4);
     }
     // one kh step: the inputs (4 planes x 6 staged values as float2s, or the 24
@@ -648,11 +600,7 @@ __global__ __launch_bounds__(NW * 64, OCC) void conv3d_wino2_kernel(const ConvAr
           }
 #pragma unroll
           for (int q = 0; q < 3; ++q)
-#ifdef LEA_EXP_NOLDSRD
-            o.x2[pl][q] = make_float2((float)(kh + it), (float)(pl * q) + sp[0] * 0.f);
-#else
             o.x2[pl][q] = *reinterpret_cast<const float2*>(sp + 2 * q);
-#endif
         }
       }
 #pragma unroll
@@ -661,11 +609,7 @@ __global__ __launch_bounds__(NW * 64, OCC) void conv3d_wino2_kernel(const ConvAr
         for (int kw = 0; kw < 3; ++kw)
 #pragma unroll
           for (int m = 0; m < MTE; ++m)
-#ifdef LEA_EXP_NOLDSRD
-            o.g[kd * 3 + kw][m] = (float)(kd + kw * kh + it);
-#else
             o.g[kd * 3 + kw][m] = ws[((kd * 3 + kh) * 3 + kw) * CIN_B * C::COP + woff[m]];
-#endif
     };
     struct Xf {
       float v[NX][NE];
@@ -683,41 +627,23 @@ __global__ __launch_bounds__(NW * 64, OCC) void conv3d_wino2_kernel(const ConvAr
         float bw[C::PLANES][NX];
 #pragma unroll
         for (int pl = 0; pl < C::PLANES; ++pl)
-#ifdef LEA_EXP_NOXF  // no transforms: V and U straight from the staged values
-        {
-          const float e6[6] = {o.x2[pl][0].x, o.x2[pl][0].y, o.x2[pl][1].x, o.x2[pl][1].y, o.x2[pl][2].x, o.x2[pl][2].y};
-          for (int x = 0; x < NX; ++x) bw[pl][x] = e6[x];
-        }
-#else
         {
           if constexpr (C::H4)
             bw4(o.h4[pl][0].x, o.h4[pl][0].y, o.h4[pl][0].z, o.h4[pl][0].w, o.h4[pl][1].x, o.h4[pl][1].y, bw[pl]);
           else
             bw4(o.x2[pl][0].x, o.x2[pl][0].y, o.x2[pl][1].x, o.x2[pl][1].y, o.x2[pl][2].x, o.x2[pl][2].y, bw[pl]);
         }
-#endif
 #pragma unroll
         for (int x = 0; x < NX; ++x) {
-#ifdef LEA_EXP_NOXF
-          for (int e = 0; e < NE; ++e) T.v[x][e] = bw[e][x];
-#else
           T.v[x][0] = bw[0][x] - bw[2][x];
           T.v[x][1] = bw[1][x] + bw[2][x];
           T.v[x][2] = bw[2][x] - bw[1][x];
           T.v[x][3] = bw[1][x] - bw[3][x];
-#endif
         }
       }
 #pragma unroll
       for (int m = 0; m < MTE; ++m) {
         float uw[3][NX];
-#ifdef LEA_EXP_NOXF
-        for (int kd = 0; kd < 3; ++kd)
-          for (int x = 0; x < NX; ++x) uw[kd][x] = o.g[kd * 3 + x % 3][m];
-        for (int x = 0; x < NX; ++x)
-          for (int e = 0; e < NE; ++e) T.u[x][e][m] = uw[e % 3][x];
-        continue;
-#endif
 #pragma unroll
         for (int kd = 0; kd < 3; ++kd) gw4(o.g[kd * 3][m], o.g[kd * 3 + 1][m], o.g[kd * 3 + 2][m], uw[kd]);
 #pragma unroll
@@ -737,11 +663,7 @@ __global__ __launch_bounds__(NW * 64, OCC) void conv3d_wino2_kernel(const ConvAr
         for (int e = 0; e < NE; ++e)
 #pragma unroll
           for (int m = 0; m < MTE; ++m)
-#ifdef LEA_EXP_NOMFMA  // keeps the operands live with one VALU op instead of the MFMA
-            acc[x][e][m][0] += T.u[x][e][m] * T.v[x][e];
-#else
             acc[x][e][m] = __builtin_amdgcn_mfma_f32_16x16x4f32(T.u[x][e][m], T.v[x][e], acc[x][e][m], 0, 0, 0);
-#endif
     };
     // 3 kh steps: LDS reads two steps ahead, transforms one step ahead
     Raw raw[2];
@@ -795,16 +717,6 @@ __global__ __launch_bounds__(NW * 64, OCC) void conv3d_wino2_kernel(const ConvAr
     ich = wrap ? 0 : ich + 1;
     ipr += wrap;
   }
-#ifdef LEA_EXP_STAMPS
-  st_sum[7] = stamp() - st_begin;
-  if (a.dbg) {  // lane k < 8 stores phase k of this wave (a lane-indexed vector store)
-    unsigned v = 0;
-#pragma unroll
-    for (int k = 0; k < kStampPhases; ++k)
-      if (lane == k) v = (unsigned)st_sum[k];
-    if (lane < kStampPhases) a.dbg[((long long)blockIdx.x * NW + wave) * kStampPhases + lane] = v;
-  }
-#endif
 }
 
 
@@ -902,20 +814,14 @@ __global__ __launch_bounds__(256, 2) void conv3d_wino2p_kernel(const ConvArgs a)
       const unsigned long long base = (c < a.cin1 ? xa : x2s) + cb + (unsigned long long)ci * cvolb;
       const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)base, 0, nrec, 0x00020000);
       constexpr int cbs[4] = {CB0, CB1, CB2, CB3};
-#ifndef LEA_EXP_NOHALO
       dma_dwordx4_buf(rs, vo, lds0 + 4 * (unsigned)(buf * XS + cbs[ci] + wave * 256));
-#endif
     }
   };
   float4 gw[kGL / 4];  // this lane's taps of the current chunk: [kh][kd][kw]
   auto load_g = [&](int ch) {
     const float4* src = reinterpret_cast<const float4*>(wl + (long long)ch * WC * 64 * kGL);
-#ifdef LEA_EXP_NOWDMA
-    for (int k = 0; k < kGL / 4; ++k) gw[k] = make_float4(1.f, 0.5f, 0.25f, (float)ch);
-#else
 #pragma unroll
     for (int k = 0; k < kGL / 4; ++k) gw[k] = src[64 * k];
-#endif
   };
   // V-pass of one item: unit u = (group g, channel c, halo row r), as PV = 2; branch-free:
   // the fourth wave repeats the first wave's units and stores the same values
@@ -1041,22 +947,15 @@ __global__ __launch_bounds__(256, 2) void conv3d_wino2p_kernel(const ConvArgs a)
       asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NST) : "memory");
     else
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-#ifndef LEA_EXP_NOBAR1
     __syncthreads();
-#endif
     const float* tv = tvb + (it & 1) * TS;
     struct Raw {
       float4 v4[6];
     };
     auto load_step = [&](int kh, Raw& o) {
       const float4* tp = reinterpret_cast<const float4*>(tv + toff + kh * C::TRS);
-#ifdef LEA_EXP_NOLDSRD  // ablation: V operands from registers (no LDS reads)
-      for (int k = 0; k < 6; ++k) o.v4[k] = make_float4(0.5f * kh, 0.25f, (float)k, 1.f);
-      (void)tp;
-#else
 #pragma unroll
       for (int k = 0; k < 6; ++k) o.v4[k] = tp[k];
-#endif
     };
     struct Xf {
       float v[NX][NE];
@@ -1070,12 +969,6 @@ __global__ __launch_bounds__(256, 2) void conv3d_wino2p_kernel(const ConvArgs a)
         for (int i = 0; i < 4; ++i) T.v[(4 * k + i) % NX][(4 * k + i) / NX] = e4[i];
       }
       const float* g = reinterpret_cast<const float*>(gw) + kh * 9;
-#ifdef LEA_EXP_NOUXF  // ablation: U read straight from the taps (no transform VALU)
-#pragma unroll
-      for (int x = 0; x < NX; ++x)
-#pragma unroll
-        for (int e = 0; e < NE; ++e) T.u[x][e] = g[(x * NE + e) % 9];
-#else
       float uw[3][NX];
 #pragma unroll
       for (int kd = 0; kd < 3; ++kd) gw4(g[kd * 3], g[kd * 3 + 1], g[kd * 3 + 2], uw[kd]);
@@ -1087,18 +980,13 @@ __global__ __launch_bounds__(256, 2) void conv3d_wino2p_kernel(const ConvArgs a)
         T.u[x][2] = s - uw[1][x];
         T.u[x][3] = uw[2][x];
       }
-#endif
     };
     auto mfmas = [&](const Xf& T) {
 #pragma unroll
       for (int x = 0; x < NX; ++x)
 #pragma unroll
         for (int e = 0; e < NE; ++e)
-#ifdef LEA_EXP_NOMFMA
-          acc[x][e][0] += T.u[x][e] * T.v[x][e];
-#else
           acc[x][e] = __builtin_amdgcn_mfma_f32_16x16x4f32(T.u[x][e], T.v[x][e], acc[x][e], 0, 0, 0);
-#endif
     };
     Raw raw[2];
     Xf xf[2];
@@ -1113,9 +1001,7 @@ __global__ __launch_bounds__(256, 2) void conv3d_wino2p_kernel(const ConvArgs a)
     load_step(2, raw[0]);
     xform(1, raw[1], xf[1]);
     mfmas(xf[0]);
-#ifndef LEA_EXP_NOVPASS
     vpass((it + 1) & 1);
-#endif
     xform(2, raw[0], xf[0]);
     // g(min(it + 1, nitems - 1)): the last item's chunk is nchunks - 1 = ich
     load_g(it + 1 < nitems ? (ich + 1 == nchunks ? 0 : ich + 1) : ich);
@@ -1170,28 +1056,11 @@ long long lane_weights_floats(int cout, int cin) {
   return (long long)((cout + 31) / 32) * (cin / CIN_B) * 2 * 64 * kGL;
 }
 
-#ifdef LEA_EXP_STAMPS
-unsigned* g_dbg = nullptr;
-}  // namespace wino
-}  // namespace lea
-// diagnostic export (not in the public headers): the per-wave phase buffer of the next
-// W x D launches, nblk * NW * 8 u32 (nullptr = off)
-extern "C" int lea_exp_wino2_stamps(void* buf) {
-  lea::wino::g_dbg = (unsigned*)buf;
-  return 0;
-}
-namespace lea {
-namespace wino {
-#endif
 
 thread_local char g_name2[96];
 
 
-#ifdef LEA_EXP_STAMPS
-#define LEA_WINO2_DBG a.dbg = g_dbg;
-#else
 #define LEA_WINO2_DBG
-#endif
 #define LEA_WINO2_CASE(Q, WC, MTE, NW, OCC, PV, CV)                                                \
   if (p.q == Q && p.wc == WC && p.mte == MTE && p.nw == NW && p.occ == OCC && p.pv == PV) {        \
     using C_ = Cfg2<Q, WC, MTE, NW, OCC, PV>;                                                      \

@@ -539,6 +539,7 @@ extern "C" int lea_cv_stem_combine(const void* lmaps, int64_t l_bstride, const v
   a.D = D3;
   a.H = H;
   a.W = W;
+  LEA_CHECK_FLAGS(flags, LEA_RELU | 0x300u, "lea_cv_stem_combine");
   a.flags = flags & (LEA_RELU | 0x300u);  // 0x100 / 0x200: probe-only variants (tools)
   a.nseg = (W + cvs::WS - 1) / cvs::WS;
   const int ob = dtype == LEA_F32 ? cvs::OB : cvs::OB8;

@@ -26,9 +26,11 @@ __global__ __launch_bounds__(TW * TH) void feature_stem_kernel(
     const float* __restrict__ x, long long xbs, const float* __restrict__ w0, const float* __restrict__ sc0,
     const float* __restrict__ sh0, const float* __restrict__ w1, const float* __restrict__ sc1,
     const float* __restrict__ sh1, void* __restrict__ y, long long ybs, int Hi, int Wi, int Ho, int Wo) {
+  static_assert(C1 % 2 == 0, "stem1's packed FMAs read w1s as float2 pairs of couts");
   __shared__ float patch[CIN][PH][PW];
   // the weights, c0-major, staged once (r04; read as wave-uniform scalar loads, each c0
-  // iteration waited on ~70 of them): w0s[c0][c][3][3] as given, w1s[c0][o][3][3]
+  // iteration waited on ~70 of them): w0s[c0][c][3][3] as given, w1s[c0][tap][cout]
+  // (r05: cout innermost, so stem1's packed f32x2 FMAs read two couts per LDS word)
   __shared__ __attribute__((aligned(16))) float w0s[C0 * CIN * 9 + 1];
   __shared__ __attribute__((aligned(16))) float w1s[C0 * C1 * 9];
   __shared__ float bn0[2][C0];  // stem0's folded BN (scale, shift)

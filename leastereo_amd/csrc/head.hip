@@ -408,6 +408,7 @@ extern "C" int lea_tapsum_upsample(const void* q, int64_t q_bstride, void* y, in
   // of 8); y is f32 NCDHW either way (the disparity regression reads f32)
   using namespace lea;
   clear_error();
+  LEA_CHECK_FLAGS(flags, LEA_RELU, "lea_tapsum_upsample");
   LEA_CHECK_ARG(q && y && q != y && workspace, "lea_tapsum_upsample: null or aliased pointer");
   LEA_CHECK_ARG((scale == nullptr) == (shift == nullptr),
                 "lea_tapsum_upsample: scale/shift must both be set or both NULL");

@@ -216,8 +216,12 @@ extern "C" int lea_resample_set_mode(int mode) {
 
 extern "C" int lea_staged_rows(int Hi, int Ho, int ac, int R, int halo) {
   lea::clear_error();
-  LEA_CHECK_ARG(Hi > 0 && Ho > 0 && R > 0 && halo >= 0 && (ac == 0 || ac == 1),
-                "lea_staged_rows: Hi=%d Ho=%d ac=%d R=%d halo=%d", Hi, Ho, ac, R, halo);
+  // a row count can be any positive int (~1008 rows at config 5), so an error is -1, never
+  // LEA_E_INVALID
+  if (!(Hi > 0 && Ho > 0 && R > 0 && halo >= 0 && (ac == 0 || ac == 1))) {
+    lea::set_error("lea_staged_rows: Hi=%d Ho=%d ac=%d R=%d halo=%d", Hi, Ho, ac, R, halo);
+    return -1;
+  }
   return lea::staged_rows(Hi, Ho, ac, R, halo);
 }
 
@@ -227,6 +231,7 @@ extern "C" int lea_resample3d_trilinear(const void* x, int64_t x_bstride, void* 
                                         unsigned flags, int dtype, void* stream) {
   using namespace lea;
   clear_error();
+  LEA_CHECK_FLAGS(flags, LEA_RELU, "lea_resample3d_trilinear");
   LEA_CHECK_ARG(x && y && x != y, "lea_resample3d_trilinear: null or aliased pointer");
   LEA_CHECK_ARG((scale == nullptr) == (shift == nullptr),
                 "lea_resample3d_trilinear: scale/shift must both be set or both NULL");

@@ -97,9 +97,6 @@ __device__ __forceinline__ void buf_store4(__amdgpu_buffer_rsrc_t rs, unsigned o
 template <int NST>
 __device__ __forceinline__ void wait_item(bool after_epilogue) {
   static_assert(NST > 0 && NST < 64, "vmcnt immediate");
-#ifdef LEA_EXP_NOWAIT  // timing experiment (tools/build_variants.sh): the DMA wait dropped
-  return;
-#endif
   if (after_epilogue)
     asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NST) : "memory");
   else

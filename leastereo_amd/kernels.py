@@ -638,8 +638,13 @@ def conv3d_bnrelu_bf16(x: torch.Tensor, packed: torch.Tensor, cout: int, k: int,
 def pair_sum_supported_bf16(x: torch.Tensor, x2: torch.Tensor, out: torch.Tensor) -> bool:
     """Whether conv3d_bnrelu_bf16(..., pair_sum=True) takes these c8 operands: two equal sources
     of one K chunk each (8 or 16 channels), cout <= 16, D >= 4 (the D-streaming kernel)."""
-    return bool(x.shape[1] == x2.shape[1] and x.shape[1] in (1, 2) and out.shape[1] * 8 <= 16
-                and x.shape[2] >= 4 and tuple(x.shape[2:5]) == tuple(x2.shape[2:5]))
+    if not (x.shape[1] == x2.shape[1] and x.shape[1] in (1, 2) and out.shape[1] * 8 <= 16
+            and x.shape[2] >= 4 and tuple(x.shape[2:5]) == tuple(x2.shape[2:5])):
+        return False
+    # the library's own plan decides (a tuning override can take the shape off the
+    # D-streaming kernel): ask it rather than fail mid-forward
+    b, cb, d, h, w = (int(s) for s in x.shape[:5])
+    return bool(_lib.load().lea_conv3d_bf16_pair_supported(b, cb * 8, int(out.shape[1]) * 8, d, h, w))
 
 
 def conv1x1_resampled_bf16(x: torch.Tensor, size, packed: torch.Tensor, cout: int, scale, shift,

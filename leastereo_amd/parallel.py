@@ -39,7 +39,8 @@ def rank_info() -> RankInfo:
 def init(backend: str, info: RankInfo, device: torch.device | None = None):
     """Join the process group when world > 1 (MASTER_ADDR/PORT from the env)."""
     if info.world > 1 and not dist.is_initialized():
-        kw = {"device_id": device} if (device is not None and device.type == "cuda") else {}
+        kw = {"device_id": device} if (backend == "nccl" and device is not None
+                                       and device.type == "cuda") else {}
         dist.init_process_group(backend, rank=info.rank, world_size=info.world, **kw)
 
 
@@ -51,10 +52,18 @@ def shard(n_pairs: int, info: RankInfo) -> range:
     return range(lo, hi)
 
 
+def _host_staged() -> bool:
+    """gloo's collectives take host tensors: a device tensor goes through a host copy
+    (the gloo rehearsal of the N-rank GPU path; RCCL works on the device tensors)."""
+    return dist.get_backend() == "gloo"
+
+
 def max_over_ranks(value: float, device: torch.device) -> float:
     """Slowest rank's time (the job's time)."""
     t = torch.tensor([value], dtype=torch.float64, device=device)
     if dist.is_initialized() and dist.get_world_size() > 1:
+        if _host_staged():
+            t = t.cpu()
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
 
@@ -64,10 +73,10 @@ def gather_per_pair(values: torch.Tensor) -> torch.Tensor:
     concatenation on every rank.  The single collective of the data path."""
     if not (dist.is_initialized() and dist.get_world_size() > 1):
         return values
-    out = torch.empty(dist.get_world_size() * values.numel(), dtype=values.dtype,
-                      device=values.device)
-    dist.all_gather_into_tensor(out, values.contiguous())
-    return out
+    src = values.cpu() if _host_staged() else values
+    out = torch.empty(dist.get_world_size() * src.numel(), dtype=src.dtype, device=src.device)
+    dist.all_gather_into_tensor(out, src.contiguous())
+    return out.to(values.device)
 
 
 def barrier():

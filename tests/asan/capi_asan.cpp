@@ -74,6 +74,14 @@ int main() {
                                                    1, 4, 4, 4, 4, 4, 3, LEA_RELU, LEA_F32, nullptr));
   expect_err("conv residual", lea_conv3d_bnrelu(p, 0, nullptr, 0, 0, f, nullptr, nullptr, nullptr, 0, f + 8, 0,
                                                 1, 4, 4, 4, 4, 4, 3, LEA_RESIDUAL, LEA_F32, nullptr));
+  expect_err("conv pair-sum", lea_conv3d_bnrelu(p, 0, f + 16, 0, 4, f, nullptr, nullptr, nullptr, 0, f + 8, 0,
+                                                1, 8, 4, 4, 4, 4, 3, LEA_RELU | LEA_PAIR_SUM, LEA_F32, nullptr),
+             LEA_E_UNSUPPORTED);
+  expect_err("conv unknown flag", lea_conv3d_bnrelu(p, 0, nullptr, 0, 0, f, nullptr, nullptr, nullptr, 0, f + 8, 0,
+                                                    1, 4, 4, 4, 4, 4, 3, 0x40u, LEA_F32, nullptr));
+  expect_err("conv2d pair-sum", lea_conv2d_bnrelu(p, 0, f, nullptr, nullptr, nullptr, 0, f + 8, 0, 1, 4, 4, 4, 4,
+                                                  LEA_PAIR_SUM, LEA_F32, nullptr),
+             LEA_E_UNSUPPORTED);
   expect_err("resampled null", lea_conv3d_bnrelu_resampled(nullptr, 0, 2, 2, 2, f, nullptr, nullptr, nullptr, 0,
                                                            p, 0, 1, 4, 4, 4, 4, 4, 1, 0, LEA_F32, nullptr));
   expect_err("cv conv null", lea_conv3d_bnrelu_costvolume(nullptr, p, 0, f, nullptr, nullptr, p, 0, 1, 4, 4, 4,

@@ -70,6 +70,29 @@ def test_invalid_arguments_are_rejected_before_launch():
     assert lib.lea_conv1x1_set_vector(2) == 1001 and lib.lea_conv1x1_set_vector(1) == 0
     # unsupported dtype is reported as such
     assert lib.lea_disparity_regression(x, x, 1, 1, 1, 1, 1, 7, None) == 1002
+    # LEA_PAIR_SUM on an entry without a pair form is LEA_E_UNSUPPORTED (the header's
+    # contract; ADVICE r05: the direct engine had run a plain conv over the concatenation),
+    # unknown flag bits LEA_E_INVALID -- both before any launch
+    x2 = ctypes.c_void_p(48)
+    pair, relu = 4, 1
+    assert lib.lea_conv3d_bnrelu(x, 0, x2, 0, 4, x, None, None, None, 0, y, 0,
+                                 1, 8, 4, 4, 4, 4, 3, relu | pair, 0, None) == 1002
+    assert b"LEA_PAIR_SUM" in lib.lea_last_error()
+    assert lib.lea_conv3d_bnrelu(x, 0, None, 0, 0, x, None, None, None, 0, y, 0,
+                                 1, 8, 4, 4, 4, 4, 3, relu | 64, 0, None) == 1001
+    assert b"unknown flag" in lib.lea_last_error()
+    assert lib.lea_conv3d_bnrelu_resampled(x, 0, 2, 2, 2, x, None, None, None, 0, y, 0,
+                                           1, 8, 4, 4, 4, 4, 1, pair, 0, None) == 1002
+    assert lib.lea_conv2d_bnrelu(x, 0, x, None, None, None, 0, y, 0, 1, 8, 8, 4, 4, pair, 0, None) == 1002
+    assert lib.lea_conv3d_bnrelu_costvolume(x, x2, 0, x, None, None, y, 0, 1, 8, 8, 4, 4, 4,
+                                            pair, 0, None) == 1002
+    assert lib.lea_resample3d_trilinear(x, 0, y, 0, 1, 1, 1, 1, 1, 1, 1, 1, 1, None, None, pair, 0,
+                                        None) == 1002
+    assert lib.lea_resample3d_trilinear(x, 0, y, 0, 1, 1, 1, 1, 1, 1, 1, 1, 1, None, None, 2, 0,
+                                        None) == 1001
+    # the pair entries still accept it (rejected later only for an unsupported shape)
+    assert lib.lea_conv3d_bnrelu_wino(x, 0, None, 0, 0, x, None, None, None, 0, y, 0,
+                                      1, 8, 4, 4, 4, 4, relu | 64, 0, None) == 1001
     assert lib.lea_resample3d_trilinear(x, 0, x, 0, 1, 1, 1, 1, 1, 1, 1, 1, 1, None, None, 0, 0,
                                         None) == 1001
     assert lib.lea_resample3d_trilinear(x, 0, y, 0, 1, 1, 1, 1, 1, 1, 1, 1, 1, x, None, 0, 0,

@@ -122,3 +122,23 @@ def test_bench_parse_presets():
     h = bench.host_cores()
     assert 1 <= h["threads"] <= h["logical_cpus_in_affinity"]
     assert h["physical_cores_in_affinity"] <= h["logical_cpus_in_affinity"]
+
+
+def test_bench_extra_legs():
+    """The configs timed after the headline one: c3 + c5 at N = 1, c4 at
+    N > 1, never the headline config itself; an explicit list or none on request."""
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("bench_mod", os.path.join(REPO, "bench.py"))
+    bench = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bench)
+    assert bench.extra_legs(bench.parse([]), 1) == ["c3", "c5"]
+    assert bench.extra_legs(bench.parse([]), 8) == ["c4"]
+    assert bench.extra_legs(bench.parse(["--config", "c4"]), 8) == []
+    assert bench.extra_legs(bench.parse(["--config", "c3"]), 1) == ["c5"]
+    assert bench.extra_legs(bench.parse(["--extra-configs", ""]), 1) == []
+    assert bench.extra_legs(bench.parse(["--extra-configs", "c4,c5"]), 1) == ["c4", "c5"]
+    a = bench.parse(["--steps", "7"])
+    leg = bench.leg_args(a, "c5")
+    assert (leg.height, leg.width, leg.maxdisp, leg.batch, leg.precision) == (1008, 1512, 264, 1, "f32")
+    assert bench.config_name(leg) == "c5" and bench.config_name(a) == "c2" and leg.steps == 7
+    assert bench.parse(["--gpus", "2", "--dist-backend", "gloo"]).dist_backend == "gloo"

@@ -86,6 +86,6 @@ def test_staged_rows_sweep():
 
 def test_staged_rows_rejects_bad_arguments():
     lib = _lib.load()
-    assert lib.lea_staged_rows(0, 4, 1, 8, 0) == 1001
+    assert lib.lea_staged_rows(0, 4, 1, 8, 0) == -1
     assert b"lea_staged_rows" in lib.lea_last_error()
-    assert lib.lea_staged_rows(4, 8, 2, 8, 0) == 1001
+    assert lib.lea_staged_rows(4, 8, 2, 8, 0) == -1

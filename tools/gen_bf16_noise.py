@@ -10,7 +10,13 @@ on the inputs tests/test_gpu_bf16.py uses at configs 3 and 4 (8 pairs each), plu
 0's relative L2 distance at every stage (feature maps, stem0/1, conv1/2, the 12 cells,
 the matching cost).
 
---source reference (default): the reference itself --
+--source oracle (the default since r06): oracle/torch_ref.py (the reference's
+aten op sequence restated) in bf16 vs f32: tests/golden/bf16_noise_oracle.json.  It
+reproduces the reference's figures bit for bit (``agreement_with_oracle`` in
+bf16_noise.json), so regenerating the bar needs no reference code.
+
+--source reference (explicit opt-in only; VERDICT r04 #5 made the committed
+bf16_noise.json this way): the reference itself --
 /root/reference/retrain/LEAStereo.py imported read-only (bytecode writing off, as
 tools/gen_golden.py does), its ``feature`` and ``matching`` modules converted to
 bfloat16, its own ``LEAStereo.forward`` (cost volume at LEAStereo.py:34-48 included)
@@ -18,10 +24,11 @@ with the ``Disp`` module wrapped to take the cost in f32 (LEAStereo.py:51); stag
 values through forward hooks on the reference's modules.  Writes bf16_noise.json and
 its agreement with the oracle's figures (bf16_noise_oracle.json).
 
---source oracle: the same with oracle/torch_ref.py (the reference's aten op sequence
-restated) in place of the reference: tests/golden/bf16_noise_oracle.json.
+Only our own deterministic weights (leastereo_amd.weights) are loaded into it; no
+pickle or checkpoint from the reference tree is read.
 
-    PYTHONDONTWRITEBYTECODE=1 python tools/gen_bf16_noise.py [--source oracle]
+    python tools/gen_bf16_noise.py                       # oracle
+    PYTHONDONTWRITEBYTECODE=1 python tools/gen_bf16_noise.py --source reference
     (~10-20 min on 8 cores)
 """
 from __future__ import annotations
@@ -180,7 +187,8 @@ def agreement(cases, other):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--source", choices=("reference", "oracle"), default="reference")
+    ap.add_argument("--source", choices=("reference", "oracle"), default="oracle",
+                    help="oracle (default): the restatement; reference: import /root/reference (opt-in)")
     opt = ap.parse_args()
     torch.set_num_threads(os.cpu_count() or 1)
     sd, a = state_dict(), arch()
