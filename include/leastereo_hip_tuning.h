@@ -144,6 +144,12 @@ int lea_conv3d_wino_set_fence(int on);
  * tile (PV = 2).  Same packed weights. */
 int lea_conv3d_wino2_set_pipeline(int on);
 
+/* 1 = the pipelined W x D kernel reads the per-lane weights with G_W already applied by the
+ * packer (54 floats per cout and channel; the step forms only the D part of U: half the
+ * transform VALU, bit-identical outputs), 0 = the raw taps (r06 experiment).  Both copies
+ * are always packed. */
+int lea_conv3d_wino2p_set_wpre(int on);
+
 /* 1 (default) = the Winograd engines' buffer-addressed epilogue where the shape allows
  * it (W % 4 == 0, 16-B aligned output / residual; residual loads issued together, the
  * next chunk's DMA waited for without the stores), 0 = the per-group epilogue. */

@@ -104,6 +104,7 @@ SIGNATURES = {
     "lea_conv2d_bnrelu_pair": (_i, [_p, _i64, _p, _p, _p, _p, _i64, _p, _i64, _p, _i64, _i, _i, _i, _i, _i,
                                     _i, _u, _p]),
     "lea_conv3d_wino2_set_pipeline": (_i, [_i]),
+    "lea_conv3d_wino2p_set_wpre": (_i, [_i]),
     "lea_conv3d_wino_set_epi_buf": (_i, [_i]),
     "lea_conv3d_set_rs_gather": (_i, [_i]),
     "lea_conv1x1_set_vector": (_i, [_i]),
@@ -178,6 +179,7 @@ TUNING_ENV = {"LEASTEREO_WINO2_WALK": "lea_conv3d_wino2_set_walk",
               "LEASTEREO_RESAMPLE_MODE": "lea_resample_set_mode",
               "LEASTEREO_CONV2D_SMALL": "lea_conv2d_set_small",
               "LEASTEREO_WINO2_PIPE": "lea_conv3d_wino2_set_pipeline",
+              "LEASTEREO_WINO2P_WPRE": "lea_conv3d_wino2p_set_wpre",
               "LEASTEREO_EPI_BUF": "lea_conv3d_wino_set_epi_buf",
               "LEASTEREO_RS_GATHER": "lea_conv3d_set_rs_gather",
               "LEASTEREO_1X1_VEC": "lea_conv1x1_set_vector",

@@ -656,6 +656,7 @@ int g_block48 = 1;
 int g_epibuf = 1;  // lea_conv3d_wino_set_epi_buf
 int g_halo16 = 1;  // lea_conv3d_wino2_set_halo16
 int g_pipe = 1;    // lea_conv3d_wino2_set_pipeline
+int g_wpre = 0;    // lea_conv3d_wino2p_set_wpre
 int g_fence = 1;   // lea_conv3d_wino_set_fence: the depth-paired 16-byte-halo tile's fenced schedule (r04 default)
 int g_lane16 = 2;  // lea_conv3d_wino2_set_lane_halo16 (2: the fenced step schedule, PV = 5; r04 default)
 // lea_conv3d_wino_set_w22: layers on the F(2,3) x F(2,3) tile (conv3d_wino22.hip): 0 none (LEA_PAIR_SUM
@@ -908,10 +909,13 @@ extern "C" int lea_conv3d_wino_pack_weights(const float* w, float* packed, int c
     case 1: wino::pack_wino_kernel<1><<<grid, 256, 0, st>>>(w, packed, cout, cin, cin / wino::CIN_B, staged); break;
     case 3: wino::pack_wino_kernel<3><<<grid, 256, 0, st>>>(w, packed, cout, cin, cin / wino::CIN_B, staged); break;
     default: {
-      const long long lane = uoff - staged;
+      const long long lane = wino::lane_raw_floats(cout, cin), lanew = uoff - staged - lane;
       wino::pack_wino_kernel<2><<<grid, 256, 0, st>>>(w, packed, cout, cin, cin / wino::CIN_B, staged);
       const int g2 = (int)std::min<long long>((lane + 255) / 256, 4096);
       wino::pack_wino_lane_kernel<<<g2, 256, 0, st>>>(w, packed + staged, cout, cin, cin / wino::CIN_B, lane);
+      const int g3 = (int)std::min<long long>((lanew + 255) / 256, 4096);
+      wino::pack_wino_lane_wpre_kernel<<<g3, 256, 0, st>>>(w, packed + staged + lane, cout, cin,
+                                                           cin / wino::CIN_B, lanew);
     }
   }
   if (wino::has_u22(cout)) {  // the F(2,3) x F(2,3) tile's U
@@ -972,6 +976,13 @@ extern "C" int lea_conv3d_wino2_set_pipeline(int on) {
   clear_error();
   LEA_CHECK_ARG(on == 0 || on == 1, "lea_conv3d_wino2_set_pipeline: on=%d", on);
   wino::g_pipe = on;
+  return 0;
+}
+
+extern "C" int lea_conv3d_wino2p_set_wpre(int on) {
+  clear_error();
+  LEA_CHECK_ARG(on == 0 || on == 1, "lea_conv3d_wino2p_set_wpre: on=%d", on);
+  wino::g_wpre = on;
   return 0;
 }
 

@@ -735,8 +735,14 @@ __global__ __launch_bounds__(NW * 64, OCC) void conv3d_wino2_kernel(const ConvAr
 // from the per-lane copy (16-byte slices) lea_conv3d_wino_pack_weights appends for 32-cout blocks.
 // Ablations of the two-barrier tile (tools/wino2_ablate.sh, conv1/2: 858 us) put its
 // V-pass at 118 us and the weight DMA at 49 us, serialised with the MFMAs.
-constexpr int kGL = 28;  // floats per lane and chunk in the per-lane weights (27 taps + pad)
+constexpr int kGL = 28;   // floats per lane and chunk in the per-lane weights (27 taps + pad)
+constexpr int kGLW = 56;  // the same with G_W applied by the packer (r06): [kh][kd][6 W points] + pad
 
+// WPRE (r06, lea_conv3d_wino2p_set_wpre): the per-lane weights arrive with the W transform
+// already applied (G_W g per kernel row, the packer's gw4 -- the same fp32 operations, so the
+// same bits), 54 floats per (cout, channel) instead of 27 raw taps: the step transform is the
+// D part alone (18 VALU instead of 36), for 7 more 16-byte loads per lane and item
+template <bool WPRE>
 __global__ __launch_bounds__(256, 2) void conv3d_wino2p_kernel(const ConvArgs a) {
   using C = Cfg2<8, 2, 1, 4, 2, 2>;  // the PV = 2 tile's geometry and maps (tv, V-pass banks)
   constexpr int Q = 8, WC = 2, F = 4, NX = 6, NE = 4, TD = 2;
@@ -777,9 +783,12 @@ __global__ __launch_bounds__(256, 2) void conv3d_wino2p_kernel(const ConvArgs a)
   const int HW = a.H * a.W;
   const unsigned nrec = (unsigned)(HW * a.D) * 4u;
   const long long cvol = (long long)HW * a.D;
-  // per-lane weights (slice-major, see pack_wino_lane_kernel): after the staged copy (ncob * nchunks * WS floats + 256 pad)
+  // per-lane weights (slice-major, see pack_wino_lane_kernel): after the staged copy (ncob * nchunks * WS floats + 256 pad);
+  // the W-transformed copy (WPRE) after the raw one
+  constexpr int GL = WPRE ? kGLW : kGL;
   const float* wl = a.wp + (long long)a.ncob * nchunks * C::WS + 256 +
-                    ((long long)cob * nchunks * WC + wc) * 64 * kGL + lane * 4;
+                    (WPRE ? (long long)a.ncob * nchunks * WC * 64 * kGL : 0LL) +
+                    ((long long)cob * nchunks * WC + wc) * 64 * GL + lane * 4;
 
   // 16-byte halo pieces: block slot j16 = wave of every channel (4 per wave per item);
   // lanes past the halo (e16 >= BLK16) read out of range: zeros into the channel's pad
@@ -817,11 +826,11 @@ __global__ __launch_bounds__(256, 2) void conv3d_wino2p_kernel(const ConvArgs a)
       dma_dwordx4_buf(rs, vo, lds0 + 4 * (unsigned)(buf * XS + cbs[ci] + wave * 256));
     }
   };
-  float4 gw[kGL / 4];  // this lane's taps of the current chunk: [kh][kd][kw]
+  float4 gw[GL / 4];  // this lane's taps of the current chunk: [kh][kd][kw] (WPRE: [kh][kd][W point])
   auto load_g = [&](int ch) {
-    const float4* src = reinterpret_cast<const float4*>(wl + (long long)ch * WC * 64 * kGL);
+    const float4* src = reinterpret_cast<const float4*>(wl + (long long)ch * WC * 64 * GL);
 #pragma unroll
-    for (int k = 0; k < kGL / 4; ++k) gw[k] = src[64 * k];
+    for (int k = 0; k < GL / 4; ++k) gw[k] = src[64 * k];
   };
   // V-pass of one item: unit u = (group g, channel c, halo row r), as PV = 2; branch-free:
   // the fourth wave repeats the first wave's units and stores the same values
@@ -968,10 +977,18 @@ __global__ __launch_bounds__(256, 2) void conv3d_wino2p_kernel(const ConvArgs a)
 #pragma unroll
         for (int i = 0; i < 4; ++i) T.v[(4 * k + i) % NX][(4 * k + i) / NX] = e4[i];
       }
-      const float* g = reinterpret_cast<const float*>(gw) + kh * 9;
       float uw[3][NX];
+      if constexpr (WPRE) {
+        const float* g = reinterpret_cast<const float*>(gw) + kh * 18;
 #pragma unroll
-      for (int kd = 0; kd < 3; ++kd) gw4(g[kd * 3], g[kd * 3 + 1], g[kd * 3 + 2], uw[kd]);
+        for (int kd = 0; kd < 3; ++kd)
+#pragma unroll
+          for (int x = 0; x < NX; ++x) uw[kd][x] = g[kd * 6 + x];
+      } else {
+        const float* g = reinterpret_cast<const float*>(gw) + kh * 9;
+#pragma unroll
+        for (int kd = 0; kd < 3; ++kd) gw4(g[kd * 3], g[kd * 3 + 1], g[kd * 3 + 2], uw[kd]);
+      }
 #pragma unroll
       for (int x = 0; x < NX; ++x) {
         const float s = uw[0][x] + uw[2][x];
@@ -1052,8 +1069,35 @@ __global__ void pack_wino_lane_kernel(const float* __restrict__ w, float* __rest
   }
 }
 
+// the W-transformed copy (WPRE), after the raw one: slice s holds entries 4 s .. 4 s + 3 of
+// [kh][kd][W point] (G_W g of each kernel row, gw4's operations: the kernel's own bits), then two zeros
+__global__ void pack_wino_lane_wpre_kernel(const float* __restrict__ w, float* __restrict__ out, int cout, int cin,
+                                           int nchunks, long long total) {
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
+       i += (long long)gridDim.x * blockDim.x) {
+    long long q = i;
+    const int e = (int)(q % (64 * kGLW)); q /= 64 * kGLW;
+    const int k = (e / 256) * 4 + (e & 3), ln = (e & 255) >> 2;
+    const int wc = (int)(q % 2); q /= 2;
+    const int ch = (int)(q % nchunks);
+    const int cb = (int)(q / nchunks);
+    const int co = cb * 32 + 16 * wc + (ln & 15), c = ch * CIN_B + (ln >> 4);
+    float v = 0.f;
+    if (k < 54 && co < cout && c < cin) {
+      const int kh = k / 18, kd = (k % 18) / 6, x = k % 6;
+      const float* g = w + (((long long)co * cin + c) * 9 + kd * 3 + kh) * 3;
+      float u[6];
+      gw4(g[0], g[1], g[2], u);
+      v = u[x];
+    }
+    out[i] = v;
+  }
+}
+
+long long lane_raw_floats(int cout, int cin) { return (long long)((cout + 31) / 32) * (cin / CIN_B) * 2 * 64 * kGL; }
+
 long long lane_weights_floats(int cout, int cin) {
-  return (long long)((cout + 31) / 32) * (cin / CIN_B) * 2 * 64 * kGL;
+  return lane_raw_floats(cout, cin) + (long long)((cout + 31) / 32) * (cin / CIN_B) * 2 * 64 * kGLW;
 }
 
 
@@ -1101,7 +1145,10 @@ int run2(const Plan2& p, ConvArgs a, int B, hipStream_t st, bool cv) {
       const long long n_ = (long long)a.ntiles * ((a.ndz + a.spw - 1) / a.spw) * B * a.ncob;
       LEA_CHECK_ARG(n_ < (1LL << 31), "lea_conv3d(wino2): grid too large");
       a.nblk = (int)n_;
-      conv3d_wino2p_kernel<<<dim3((unsigned)n_), 256, 0, st>>>(a);
+      if (g_wpre)
+        conv3d_wino2p_kernel<true><<<dim3((unsigned)n_), 256, 0, st>>>(a);
+      else
+        conv3d_wino2p_kernel<false><<<dim3((unsigned)n_), 256, 0, st>>>(a);
       return launch_status("lea_conv3d(wino2p)");
     }
   }

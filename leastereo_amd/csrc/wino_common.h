@@ -140,8 +140,12 @@ int run2(const Plan2& p, ConvArgs a, int B, hipStream_t st, bool cv);
 // the PV = 3 tile's per-lane weight copy (16-byte slices) (appended to the packed weights of 32-cout
 // blocks by lea_conv3d_wino_pack_weights), in floats, and its packer
 long long lane_weights_floats(int cout, int cin);
+long long lane_raw_floats(int cout, int cin);  // the raw-tap part of it (the W-transformed copy follows)
 __global__ void pack_wino_lane_kernel(const float* __restrict__ w, float* __restrict__ out, int cout, int cin,
                                       int nchunks, long long total);
+__global__ void pack_wino_lane_wpre_kernel(const float* __restrict__ w, float* __restrict__ out, int cout, int cin,
+                                           int nchunks, long long total);
+extern int g_wpre;  // lea_conv3d_wino2p_set_wpre
 const char* name2(const Plan2& p, bool cv);
 
 // F(2,3) x F(2,3) tile for the 16-cout layers (conv3d_wino22.hip): the U section the packer

@@ -4,6 +4,8 @@ against float64 torch, with the tolerance of the direct fp32 engine
 roundings per product, far inside it -- and against the direct engine itself.
 End to end the model runs on this engine by default, so test_gpu_parity.py's
 e2e / config-1 / full-size cases cover it at EPE <= 1e-3 px."""
+import os
+
 import numpy as np
 import pytest
 import torch
@@ -13,6 +15,7 @@ from leastereo_amd import _lib, kernels
 
 pytestmark = pytest.mark.gpu
 DEV = "cuda"
+WPRE_DEFAULT = 0  # lea_conv3d_wino2p_set_wpre's library default (csrc/conv3d_wino.hip g_wpre)
 
 
 def _ref(x, w, scale, shift, relu, res=None):
@@ -417,9 +420,10 @@ def test_wd_halo16_is_bit_identical_to_dword_pieces(b, cin, c1, cout, shape, mod
     x1, x2 = (xs[:, :c1].contiguous(), xs[:, c1:].contiguous()) if c1 < cin else (xs, None)
     pw = kernels.pack_conv_weight_wino(w.to(DEV))
     outs = {}
-    for on, pipe, fence in ((1, 1, 1), (1, 0, 1), (0, 1, 1), (1, 1, 0)):
+    # (halo16, pipeline, fence, W-transformed per-lane weights: r06 lea_conv3d_wino2p_set_wpre)
+    for on, pipe, fence, wpre in ((1, 1, 1, 0), (1, 0, 1, 0), (0, 1, 1, 0), (1, 1, 0, 0), (1, 1, 1, 1)):
         assert lib.lea_conv3d_wino2_set_halo16(on) == 0 and lib.lea_conv3d_wino2_set_pipeline(pipe) == 0
-        assert lib.lea_conv3d_wino_set_fence(fence) == 0
+        assert lib.lea_conv3d_wino_set_fence(fence) == 0 and lib.lea_conv3d_wino2p_set_wpre(wpre) == 0
         try:
             name = kernels.wino_kernel_name(b, cout, *shape, cin=cin)
             if cout <= 8:
@@ -431,16 +435,17 @@ def test_wd_halo16_is_bit_identical_to_dword_pieces(b, cin, c1, cout, shape, mod
             else:
                 assert name.startswith("conv3d_wino2_kernel<8, 2, 1, 4, 2, %d," % (2 if on else 1)), name
             out = r.to(DEV).clone() if mode == "acc" else None
-            outs[(on, pipe, fence)] = kernels.conv3d_bnrelu_wino(
+            outs[(on, pipe, fence, wpre)] = kernels.conv3d_bnrelu_wino(
                 x1, pw, cout, scale.to(DEV), shift.to(DEV), relu=True, out=out, accumulate=mode == "acc", x2=x2,
                 residual=r.to(DEV) if mode == "res" else None)
         finally:
             lib.lea_conv3d_wino2_set_halo16(1)
             lib.lea_conv3d_wino2_set_pipeline(1)
             lib.lea_conv3d_wino_set_fence(1)
-    base = outs[(0, 1, 1)]
-    assert all(torch.equal(o, base) for o in outs.values())
-    np.testing.assert_allclose(outs[(1, 1, 1)].cpu().double().numpy(), want.numpy(), rtol=1e-4, atol=1e-4)
+            lib.lea_conv3d_wino2p_set_wpre(int(os.environ.get("LEASTEREO_WINO2P_WPRE") or WPRE_DEFAULT))
+    base = outs[(0, 1, 1, 0)]
+    assert all(torch.equal(o, base) for o in outs.values()), [k for k, o in outs.items() if not torch.equal(o, base)]
+    np.testing.assert_allclose(outs[(1, 1, 1, 0)].cpu().double().numpy(), want.numpy(), rtol=1e-4, atol=1e-4)
 
 
 @pytest.mark.parametrize("b,cin,c1,cout,shape,mode", [
