@@ -144,10 +144,11 @@ int lea_conv3d_wino_set_fence(int on);
  * tile (PV = 2).  Same packed weights. */
 int lea_conv3d_wino2_set_pipeline(int on);
 
-/* 1 = the pipelined W x D kernel reads the per-lane weights with G_W already applied by the
- * packer (54 floats per cout and channel; the step forms only the D part of U: half the
- * transform VALU, bit-identical outputs), 0 = the raw taps (r06 experiment).  Both copies
- * are always packed. */
+/* 1 (default since r06) = the pipelined W x D kernel reads the per-lane weights with G_W
+ * already applied by the packer (54 floats per cout and channel; the step forms only the D
+ * part of U: 197 -> 147 VALU per item, bit-identical outputs; -0.7 % per forward on the
+ * kernel's layers, profiles/r06_wpre_ab.txt), 0 = the raw taps.  Both copies are always
+ * packed. */
 int lea_conv3d_wino2p_set_wpre(int on);
 
 /* 1 (default) = the Winograd engines' buffer-addressed epilogue where the shape allows

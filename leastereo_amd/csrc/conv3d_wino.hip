@@ -656,7 +656,7 @@ int g_block48 = 1;
 int g_epibuf = 1;  // lea_conv3d_wino_set_epi_buf
 int g_halo16 = 1;  // lea_conv3d_wino2_set_halo16
 int g_pipe = 1;    // lea_conv3d_wino2_set_pipeline
-int g_wpre = 0;    // lea_conv3d_wino2p_set_wpre
+int g_wpre = 1;    // lea_conv3d_wino2p_set_wpre (r06: -0.7 % on the kernel, bit-identical)
 int g_fence = 1;   // lea_conv3d_wino_set_fence: the depth-paired 16-byte-halo tile's fenced schedule (r04 default)
 int g_lane16 = 2;  // lea_conv3d_wino2_set_lane_halo16 (2: the fenced step schedule, PV = 5; r04 default)
 // lea_conv3d_wino_set_w22: layers on the F(2,3) x F(2,3) tile (conv3d_wino22.hip): 0 none (LEA_PAIR_SUM

@@ -28,6 +28,17 @@ from . import kernels
 from .arch import scale_dimension
 
 
+def _stacked(fl: torch.Tensor, fr: torch.Tensor) -> torch.Tensor:
+    """[fl; fr] along the batch: a view when fr directly follows fl in one buffer (the
+    forward's stacked feature batch, LEAStereo.forward), else a copy (torch.cat) -- the
+    r05 C4 forward's two copyBuffer launches were this cat of adjacent views."""
+    if (fl.is_contiguous() and fr.is_contiguous() and fl.shape == fr.shape and fl.dtype == fr.dtype
+            and fl.device == fr.device
+            and fr.data_ptr() == fl.data_ptr() + fl.numel() * fl.element_size()):
+        return fl.as_strided((2 * fl.shape[0],) + tuple(fl.shape[1:]), fl.stride())
+    return torch.cat((fl, fr), 0)
+
+
 @dataclass
 class ConvParams:
     packed: torch.Tensor      # packed weights ("s3": the raw [cout, cin, 3, 3] weight)
@@ -756,9 +767,9 @@ class MatchingExecutorBF16(_C8Layout, MatchingExecutor):
         if cf * 2 != p.cin:
             raise ValueError(f"stem0 expects {p.cin} cost-volume channels, got 2*{cf}")
         if fl.dtype == torch.bfloat16:  # the bf16 feature net already hands over c8 maps
-            f8, b = torch.cat((fl, fr), 0), fl.shape[0]
+            f8, b = _stacked(fl, fr), fl.shape[0]
         else:
-            f8 = kernels.to_c8(torch.cat((fl, fr), 0))  # [2B, C/8, 1, H, W, 8]
+            f8 = kernels.to_c8(_stacked(fl, fr))  # [2B, C/8, 1, H, W, 8]
             b = fl.shape[0]
         d3 = int(maxdisp / 3)
         if self.cv is not None and kernels.cv_stem_supported(p.cout, d3, f8.shape[4], True):

@@ -15,7 +15,7 @@ from leastereo_amd import _lib, kernels
 
 pytestmark = pytest.mark.gpu
 DEV = "cuda"
-WPRE_DEFAULT = 0  # lea_conv3d_wino2p_set_wpre's library default (csrc/conv3d_wino.hip g_wpre)
+WPRE_DEFAULT = 1  # lea_conv3d_wino2p_set_wpre's library default (csrc/conv3d_wino.hip g_wpre)
 
 
 def _ref(x, w, scale, shift, relu, res=None):
