@@ -249,16 +249,101 @@ __global__ __launch_bounds__(kDispThreads, 4) void disparity_rows_f32(const floa
   disp[((long long)b * Ho + oh) * Wo + ow] = over ? __builtin_nanf("") : t / s;
 }
 
+// Three-row form (r06): output rows 3k, 3k + 1, 3k + 2 read source rows
+// k - 1, k, k + 1 only (x3 up-sampling, align_corners=False), so one workgroup of 3 x 256
+// threads owns 256 columns of all three: every raw source value is loaded ONCE (three loads
+// per staged element, for three H-lerped rows) instead of twice by each of three row
+// workgroups (six), and the row-position arithmetic is paid once per element.  Each output
+// row's LDS row is ah.l0 * row(ah.i0) + ah.l1 * row(ah.i1) with that row's own weights -- the
+// two-row kernel's expression, so every output is bit-identical to disparity_rows_f32; the
+// per-pixel phase is that kernel's.  LDS 3 * D3 * kDispCols floats (74 KB at D3 = 64: two
+// workgroups, 24 waves per CU).
+constexpr int kDisp3Threads = 3 * kDispThreads;
+
+template <int D3, int MD, bool FAST>
+__global__ __launch_bounds__(kDisp3Threads) void disparity_rows3_f32(const float* __restrict__ cost,
+                                                                   float* __restrict__ disp, int H3, int W3,
+                                                                   float rh, float rw) {
+#pragma clang fp contract(off)
+  __shared__ float hl[3][D3 * kDispCols];
+  const int Ho = 3 * H3, Wo = 3 * W3;
+  const int ow0 = blockIdx.x * kDispThreads;
+  const int k = blockIdx.y;  // source row k: output rows 3k .. 3k + 2
+  const int b = blockIdx.z;
+  const AxisW a0 = src_axis(rh, 3 * k, H3, Ho), a1 = src_axis(rh, 3 * k + 1, H3, Ho),
+              a2 = src_axis(rh, 3 * k + 2, H3, Ho);
+  // the staged raw rows: lo = min of the three rows' i0 (k - 1, or 0 at the top), lo + 1, lo + 2
+  // clamped to the map; every i0 / i1 of the three rows lies in [lo, lo + 2] (x3: k - 1 .. k + 1)
+  const int lo = min(a0.i0, min(a1.i0, a2.i0));
+  const int r1 = min(lo + 1, H3 - 1), r2 = min(lo + 2, H3 - 1);
+  const int c_lo = src_axis(rw, ow0, W3, Wo).i0;
+  const int c_hi = src_axis(rw, min(ow0 + kDispThreads - 1, Wo - 1), W3, Wo).i1;
+  const bool over = c_hi - c_lo + 1 > kDispCols ||
+                    max(a0.i1, max(a1.i1, a2.i1)) > lo + 2;  // host-checked; NaN rather than a wrong row
+  const int ncol = min(c_hi - c_lo + 1, kDispCols);
+  const long long HW = (long long)H3 * W3;
+  const float* base = cost + (long long)b * D3 * HW + c_lo;
+  const float* p0 = base + (long long)lo * W3;
+  const float* p1 = base + (long long)r1 * W3;
+  const float* p2 = base + (long long)r2 * W3;
+  // row i of the map as one of the three staged values (workgroup-uniform selects)
+  auto pick = [&](int i, float v0, float v1, float v2) { return i == lo ? v0 : (i == lo + 1 ? v1 : v2); };
+  for (int e = threadIdx.x; e < D3 * ncol; e += kDisp3Threads) {
+    const int dd = e / ncol, c = e - dd * ncol;
+    const long long o = (long long)dd * HW + c;
+    const float v0 = p0[o], v1 = p1[o], v2 = p2[o];
+    const int s = dd * kDispCols + c;
+    hl[0][s] = a0.l0 * pick(a0.i0, v0, v1, v2) + a0.l1 * pick(a0.i1, v0, v1, v2);
+    hl[1][s] = a1.l0 * pick(a1.i0, v0, v1, v2) + a1.l1 * pick(a1.i1, v0, v1, v2);
+    hl[2][s] = a2.l0 * pick(a2.i0, v0, v1, v2) + a2.l1 * pick(a2.i1, v0, v1, v2);
+  }
+  __syncthreads();
+  const int row = __builtin_amdgcn_readfirstlane(threadIdx.x / kDispThreads);  // wave-uniform
+  const int ow = ow0 + (int)threadIdx.x % kDispThreads;
+  const int oh = 3 * k + row;
+  if (ow >= Wo) return;  // no barrier below
+  const float* h = hl[row];
+  const AxisW aw = src_axis(rw, ow, W3, Wo);
+  const int j0 = min(aw.i0 - c_lo, kDispCols - 1), j1 = min(aw.i1 - c_lo, kDispCols - 1);
+  auto plane = [&](int dd) { return aw.l0 * h[dd * kDispCols + j0] + aw.l1 * h[dd * kDispCols + j1]; };
+  float m = plane(0);
+#pragma unroll
+  for (int dd = 1; dd < D3; ++dd) {
+    m = fminf(m, plane(dd));
+    if (dd % 8 == 7) __builtin_amdgcn_sched_barrier(0);
+  }
+  constexpr float rd = (float)D3 / (float)MD;
+  float s = 0.f, t = 0.f;
+  float vlo = plane(0), vhi = plane(D3 > 1 ? 1 : 0);
+  int kk = 0;  // vlo = plane kk, vhi = plane min(kk + 1, D3 - 1): constants after unrolling
+#pragma clang loop unroll(full)
+  for (int od = 0; od < MD; ++od) {
+    const AxisW ad = src_axis(rd, od, D3, MD);  // constants after unrolling
+    while (kk < ad.i0) {
+      ++kk;
+      vlo = vhi;
+      vhi = plane(kk + 1 < D3 ? kk + 1 : D3 - 1);
+    }
+    const float v1 = ad.i1 == kk ? vlo : vhi;
+    const float u = ad.l0 * vlo + ad.l1 * v1;
+    const float e = FAST ? dexp<true>(m - u) : exp_noovf(m - u);
+    s += e;
+    t += (float)od * e;
+    if (od % 12 == 11) __builtin_amdgcn_sched_barrier(0);
+  }
+  disp[((long long)b * Ho + oh) * Wo + ow] = over ? __builtin_nanf("") : t / s;
+}
+
 }  // namespace lea
 
-// lea_disparity_set_register_form: 2 (default, r05) = the row-staged kernel for the configured
+// lea_disparity_set_register_form: 3 = the three-row staged kernel (r06), 2 (default, r05) = the row-staged kernel for the configured
 // (D3, maxdisp), 1 = the register kernel for them, 0 = the online-softmin kernel everywhere
 // (A/B and tests)
 static int g_disp_reg = 2;
 extern "C" int lea_disparity_set_register_form(int on) {
   using namespace lea;
   clear_error();
-  LEA_CHECK_ARG(on >= 0 && on <= 2, "lea_disparity_set_register_form: %d", on);
+  LEA_CHECK_ARG(on >= 0 && on <= 3, "lea_disparity_set_register_form: %d", on);
   g_disp_reg = on;
   return 0;
 }
@@ -289,8 +374,21 @@ extern "C" int lea_disparity_regression(const void* cost, float* disp, int B, in
     k_<<<grid, block, 0, as_stream(stream)>>>((const float*)cost, disp, H3, W3, rh, rw);                 \
     return launch_status("lea_disparity_regression");                                                  \
   }
-  // the row-staged form: 256 outputs of a row read <= kDispCols source columns (Wo = 3 W3)
-  const bool rows_ok = g_disp_reg == 2 && (256LL * W3 + Wo - 1) / Wo + 2 <= kDispCols;
+  // the row-staged forms: 256 outputs of a row read <= kDispCols source columns (Wo = 3 W3)
+  const bool cols_ok = (256LL * W3 + Wo - 1) / Wo + 2 <= kDispCols;
+#define LEA_DISP_ROWS3(D3_, MD_)                                                                        \
+  if (D3 == D3_ && maxdisp == MD_) {                                                                   \
+    auto k_ = fast ? disparity_rows3_f32<D3_, MD_, true> : disparity_rows3_f32<D3_, MD_, false>;        \
+    k_<<<dim3((Wo + kDispThreads - 1) / kDispThreads, H3, B), kDisp3Threads, 0, as_stream(stream)>>>(   \
+        (const float*)cost, disp, H3, W3, rh, rw);                                                     \
+    return launch_status("lea_disparity_regression");                                                  \
+  }
+  if (g_disp_reg == 3 && cols_ok) {
+    LEA_DISP_ROWS3(4, 12) LEA_DISP_ROWS3(8, 24) LEA_DISP_ROWS3(16, 48) LEA_DISP_ROWS3(32, 96)
+    LEA_DISP_ROWS3(64, 192) LEA_DISP_ROWS3(88, 264)
+  }
+#undef LEA_DISP_ROWS3
+  const bool rows_ok = g_disp_reg >= 2 && cols_ok;
 #define LEA_DISP_ROWS(D3_, MD_)                                                                         \
   if (D3 == D3_ && maxdisp == MD_) {                                                                   \
     auto k_ = fast ? disparity_rows_f32<D3_, MD_, true> : disparity_rows_f32<D3_, MD_, false>;          \

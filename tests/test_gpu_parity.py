@@ -390,7 +390,7 @@ def test_disparity_vs_oracle_sizes():
 
 
 @pytest.mark.parametrize("shape,md", [((1, 1, 64, 12, 20), 192), ((2, 1, 32, 9, 13), 96), ((1, 1, 16, 7, 4), 48),
-                                      ((1, 1, 8, 5, 6), 24)])
+                                      ((1, 1, 8, 5, 6), 24), ((1, 1, 88, 4, 90), 264), ((2, 1, 4, 1, 3), 12)])
 def test_disparity_register_form_matches_the_lds_form(shape, md):
     """The row-staged disparity kernel (the default: source rows H-lerped into LDS, two passes
     over the planes), the register kernel (D3 plane values in registers, compile-time depth
@@ -403,7 +403,7 @@ def test_disparity_register_form_matches_the_lds_form(shape, md):
     refd = ref.disp_forward(x.double(), md).numpy()
     for fast in (False, True):
         out = {}
-        for on in (2, 1, 0):
+        for on in (3, 2, 1, 0):
             assert lib.lea_disparity_set_register_form(on) == 0
             try:
                 out[on] = kernels.disparity_regression(x.to(DEV), md, fast).cpu().double().numpy()
@@ -412,6 +412,8 @@ def test_disparity_register_form_matches_the_lds_form(shape, md):
             err = np.abs(out[on] - refd)
             assert err.max() < 2e-3 and err.mean() < 1e-4, (fast, on, err.max(), err.mean())
         assert np.abs(out[1] - out[0]).max() < 1e-3 and np.abs(out[2] - out[1]).max() < 1e-3
+        # the three-row staging (r06) forms the two-row kernel's LDS values: same bits
+        assert np.array_equal(out[3], out[2]), np.abs(out[3] - out[2]).max()
 
 
 @pytest.mark.parametrize("b,c,cout,maxdisp,hw", [(2, 32, 32, 48, (12, 40)), (1, 4, 16, 27, (5, 7)),

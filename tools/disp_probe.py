@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """The disparity regression at the bench shapes, every form (lea_disparity_set_register_form
-2 / 1 / 0), f32 and fast exp: HIP-event microseconds and the largest difference from form 1.
+3 / 2 / 1 / 0), f32 and fast exp: HIP-event microseconds and the largest difference from form 1.
 
   python tools/disp_probe.py [--iters 20]
 """
@@ -27,7 +27,7 @@ def main():
         x = torch.randn(b, 1, d3, h3, w3, device="cuda", generator=g) * 3
         for fast in (False, True):
             out = {}
-            for form in (1, 2, 0):
+            for form in (1, 2, 3, 0):
                 _lib.check(lib.lea_disparity_set_register_form(form), "form")
                 out[form] = kernels.disparity_regression(x, md, fast)
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -38,7 +38,9 @@ def main():
                 torch.cuda.synchronize()
                 us = e0.elapsed_time(e1) / a.iters * 1e3
                 print(f"{name} fast={int(fast)} form={form} {us:8.1f} us  max|d - form1| "
-                      f"{float((out[form] - out.get(1, out[form])).abs().max()):.2e}", flush=True)
+                      f"{float((out[form] - out.get(1, out[form])).abs().max()):.2e}"
+                      + (f"  form 3 == form 2: {bool(torch.equal(out[3], out[2]))}" if form == 3 else ""),
+                      flush=True)
     _lib.check(lib.lea_disparity_set_register_form(2), "form")
 
 
