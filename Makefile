@@ -12,7 +12,7 @@ all: $(LIB)
 
 # the Winograd engines: SLP-packed f32 VALU (v_pk_*) beside MFMAs costs more issue
 # cycles than the scalar pairs it replaces (MI355X_MICROARCH.md, filler prices)
-build/obj/conv3d_wino.o build/obj/conv3d_wino2.o: HIPFLAGS += -fno-slp-vectorize
+build/obj/conv3d_wino.o build/obj/conv3d_wino2.o build/obj/conv3d_wino44.o: HIPFLAGS += -fno-slp-vectorize
 
 build/obj/%.o: leastereo_amd/csrc/%.hip $(wildcard leastereo_amd/csrc/*.h) include/leastereo_hip.h include/leastereo_hip_tuning.h
 	@mkdir -p build/obj

@@ -413,6 +413,8 @@ def _eager_modes(ref, sd_dev, arch, l, r, md, hip_s, hip_out, modes, timed, warm
 # ------------------------------------------------------------------------ roofline
 def algorithm_name(kernel: str) -> str:
     """The convolution algorithm a conv kernel instantiation runs."""
+    if kernel.startswith("conv3d_wino44"):
+        return "winograd F(4,3) along W x F(4,3) along D"
     if kernel.startswith("conv3d_wino2"):
         return "winograd F(4,3) along W x F(2,3) along D"
     if kernel.startswith("conv3d_wino_kernel<"):

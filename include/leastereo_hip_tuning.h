@@ -151,6 +151,12 @@ int lea_conv3d_wino2_set_pipeline(int on);
  * packed. */
 int lea_conv3d_wino2p_set_wpre(int on);
 
+/* 1 = the layers of the pipelined W x D kernel run on the F(4,3) x F(4,3) tile instead
+ * ("conv3d_wino44_kernel", r06: 36 MFMA products per 4 x 4 outputs and kernel row instead of
+ * 48; the W points split over two waves that swap accumulators in the epilogue), 0 = the
+ * pipelined F(4,3) x F(2,3) kernel.  Same packed weights (both per-lane copies are packed). */
+int lea_conv3d_wino44_set(int on);
+
 /* 1 (default) = the Winograd engines' buffer-addressed epilogue where the shape allows
  * it (W % 4 == 0, 16-B aligned output / residual; residual loads issued together, the
  * next chunk's DMA waited for without the stores), 0 = the per-group epilogue. */

@@ -909,13 +909,17 @@ extern "C" int lea_conv3d_wino_pack_weights(const float* w, float* packed, int c
     case 1: wino::pack_wino_kernel<1><<<grid, 256, 0, st>>>(w, packed, cout, cin, cin / wino::CIN_B, staged); break;
     case 3: wino::pack_wino_kernel<3><<<grid, 256, 0, st>>>(w, packed, cout, cin, cin / wino::CIN_B, staged); break;
     default: {
-      const long long lane = wino::lane_raw_floats(cout, cin), lanew = uoff - staged - lane;
+      const long long lane = wino::lane_raw_floats(cout, cin), lane44 = wino::lane44_floats(cout, cin),
+                      lanew = uoff - staged - lane - lane44;
       wino::pack_wino_kernel<2><<<grid, 256, 0, st>>>(w, packed, cout, cin, cin / wino::CIN_B, staged);
       const int g2 = (int)std::min<long long>((lane + 255) / 256, 4096);
       wino::pack_wino_lane_kernel<<<g2, 256, 0, st>>>(w, packed + staged, cout, cin, cin / wino::CIN_B, lane);
       const int g3 = (int)std::min<long long>((lanew + 255) / 256, 4096);
       wino::pack_wino_lane_wpre_kernel<<<g3, 256, 0, st>>>(w, packed + staged + lane, cout, cin,
                                                            cin / wino::CIN_B, lanew);
+      const int g4 = (int)std::min<long long>((lane44 + 255) / 256, 4096);
+      wino::pack_wino44_lane_kernel<<<g4, 256, 0, st>>>(w, packed + staged + lane + lanew, cout, cin,
+                                                        cin / wino::CIN_B, lane44);
     }
   }
   if (wino::has_u22(cout)) {  // the F(2,3) x F(2,3) tile's U
@@ -976,6 +980,13 @@ extern "C" int lea_conv3d_wino2_set_pipeline(int on) {
   clear_error();
   LEA_CHECK_ARG(on == 0 || on == 1, "lea_conv3d_wino2_set_pipeline: on=%d", on);
   wino::g_pipe = on;
+  return 0;
+}
+
+extern "C" int lea_conv3d_wino44_set(int on) {
+  clear_error();
+  LEA_CHECK_ARG(on == 0 || on == 1, "lea_conv3d_wino44_set: on=%d", on);
+  wino::g_w44 = on;
   return 0;
 }
 

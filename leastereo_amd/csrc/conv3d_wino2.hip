@@ -1097,7 +1097,8 @@ __global__ void pack_wino_lane_wpre_kernel(const float* __restrict__ w, float* _
 long long lane_raw_floats(int cout, int cin) { return (long long)((cout + 31) / 32) * (cin / CIN_B) * 2 * 64 * kGL; }
 
 long long lane_weights_floats(int cout, int cin) {
-  return lane_raw_floats(cout, cin) + (long long)((cout + 31) / 32) * (cin / CIN_B) * 2 * 64 * kGLW;
+  return lane_raw_floats(cout, cin) + (long long)((cout + 31) / 32) * (cin / CIN_B) * 2 * 64 * kGLW +
+         lane44_floats(cout, cin);  // + the F(4,3) x F(4,3) kernel's copy (conv3d_wino44.hip)
 }
 
 
@@ -1136,6 +1137,7 @@ int run2(const Plan2& p, ConvArgs a, int B, hipStream_t st, bool cv) {
     LEA_WINO2_CASE(8, 1, 1, 4, 2, 4, false)
     LEA_WINO2_CASE(8, 1, 1, 4, 2, 5, false)
     if (p.q == 8 && p.wc == 2 && p.mte == 1 && p.nw == 4 && p.occ == 2 && p.pv == 3) {
+      if (g_w44) return run44(a, B, p.spw, st);  // F(4,3) x F(4,3) on the same layers (r06)
       using C_ = Cfg2<8, 2, 1, 4, 2, 2>;
       a.ncob = (a.cout + C_::COP - 1) / C_::COP;
       a.tiles_w = (a.W + C_::TW - 1) / C_::TW;
@@ -1158,7 +1160,7 @@ int run2(const Plan2& p, ConvArgs a, int B, hipStream_t st, bool cv) {
 }
 
 const char* name2(const Plan2& p, bool cv) {
-  if (p.pv == 3 && !cv) return "conv3d_wino2p_kernel";
+  if (p.pv == 3 && !cv) return g_w44 ? "conv3d_wino44_kernel" : "conv3d_wino2p_kernel";
   snprintf(g_name2, sizeof(g_name2), "conv3d_wino2_kernel<%d, %d, %d, %d, %d, %d, %s>", p.q, p.wc, p.mte,
            p.nw, p.occ, p.pv, cv ? "true" : "false");
   return g_name2;

@@ -146,6 +146,13 @@ __global__ void pack_wino_lane_kernel(const float* __restrict__ w, float* __rest
 __global__ void pack_wino_lane_wpre_kernel(const float* __restrict__ w, float* __restrict__ out, int cout, int cin,
                                            int nchunks, long long total);
 extern int g_wpre;  // lea_conv3d_wino2p_set_wpre
+// F(4,3) x F(4,3) tile (conv3d_wino44.hip, r06): the layers of the pipelined W x D kernel when
+// g_w44 (lea_conv3d_wino44_set); its per-lane weight section (the last of lane_weights_floats)
+extern int g_w44;
+long long lane44_floats(int cout, int cin);
+__global__ void pack_wino44_lane_kernel(const float* __restrict__ w, float* __restrict__ out, int cout, int cin,
+                                        int nchunks, long long total);
+int run44(ConvArgs a, int B, int spw, hipStream_t st);
 const char* name2(const Plan2& p, bool cv);
 
 // F(2,3) x F(2,3) tile for the 16-cout layers (conv3d_wino22.hip): the U section the packer

@@ -969,6 +969,8 @@ def wino_mfma_scale(cout: int, name: str) -> float:
         return (-(-cout // 16) * 16) / cout * 4.0 / 9.0
     if name.startswith("conv3d_wino2p_kernel"):  # the one-barrier W x D tile: 32-cout blocks
         return (-(-cout // 32) * 32) / cout / 3.0
+    if name.startswith("conv3d_wino44_kernel"):  # F(4,3) x F(4,3): 36 per (4 x 4 outputs x 9 taps)
+        return (-(-cout // 32) * 32) / cout / 4.0
     if name.startswith("conv3d_wino2_kernel<"):
         _, wc, mte = (int(t) for t in name.split("<", 1)[1].split(",")[:3])
         cop = 16 * wc * mte

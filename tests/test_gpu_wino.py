@@ -16,6 +16,7 @@ from leastereo_amd import _lib, kernels
 pytestmark = pytest.mark.gpu
 DEV = "cuda"
 WPRE_DEFAULT = 1  # lea_conv3d_wino2p_set_wpre's library default (csrc/conv3d_wino.hip g_wpre)
+W44_DEFAULT = 0  # lea_conv3d_wino44_set's library default (csrc/conv3d_wino44.hip g_w44)
 
 
 def _ref(x, w, scale, shift, relu, res=None):
@@ -543,3 +544,42 @@ def test_wino22_writes_only_its_channel_slice():
     want = F.conv3d(x.double(), w.double(), None, 1, 1)
     np.testing.assert_allclose(big[:, 16:32].cpu().double().numpy(), want.cpu().numpy(), rtol=1e-4, atol=1e-4)
     assert bool((big[:, :16] == 3.0).all()) and bool((big[:, 32:] == 3.0).all())
+
+
+@pytest.mark.parametrize("b,cin,c1,cout,shape,mode", [
+    (1, 32, 32, 32, (5, 9, 320), "acc"), (2, 128, 64, 64, (5, 9, 40), "res"), (1, 64, 64, 32, (4, 7, 36), None),
+    (1, 32, 32, 96, (3, 6, 20), "res"), (2, 16, 8, 32, (7, 13, 4), None), (1, 32, 32, 32, (1, 1, 4), None),
+    (1, 16, 16, 32, (8, 12, 32), "acc"), (1, 128, 64, 64, (16, 10, 96), None), (1, 32, 32, 32, (6, 5, 68), "res"),
+    (2, 12, 12, 40, (9, 3, 12), "acc")])
+def test_wino44_vs_float64(b, cin, c1, cout, shape, mode):
+    """The F(4,3) x F(4,3) tile (r06, lea_conv3d_wino44_set: the pipelined W x D kernel's layers;
+    the W points split over two waves that swap accumulators in the epilogue) against float64
+    torch at the engine bar (|d| <= 1e-4 + 1e-4 |ref|) and against the F(4,3) x F(2,3) kernel:
+    ragged D (not a multiple of 4: masked planes), H (odd), W (partial 32-wide tiles), a single
+    item, two sources, couts padded to the 32-cout block (40, 96), every epilogue."""
+    lib = _lib.load()
+    g = torch.Generator().manual_seed(cin + 3 * cout + shape[2])
+    x = torch.randn((b, cin) + shape, generator=g)
+    w = torch.randn(cout, cin, 3, 3, 3, generator=g) / np.sqrt(cin * 27)
+    scale = torch.rand(cout, generator=g) + 0.5
+    shift = torch.randn(cout, generator=g) * 0.1
+    r = torch.randn((b, cout) + shape, generator=g)
+    want = _ref(x, w, scale, shift, True, r if mode else None)
+    xs = x.to(DEV)
+    x1, x2 = (xs[:, :c1].contiguous(), xs[:, c1:].contiguous()) if c1 < cin else (xs, None)
+    pw = kernels.pack_conv_weight_wino(w.to(DEV))
+    outs = {}
+    for on in (0, 1):
+        assert lib.lea_conv3d_wino44_set(on) == 0
+        try:
+            name = kernels.wino_kernel_name(b, cout, *shape, cin=cin)
+            if cin > 8:
+                assert name == ("conv3d_wino44_kernel" if on else "conv3d_wino2p_kernel"), name
+            out = r.to(DEV).clone() if mode == "acc" else None
+            outs[on] = kernels.conv3d_bnrelu_wino(
+                x1, pw, cout, scale.to(DEV), shift.to(DEV), relu=True, out=out, accumulate=mode == "acc", x2=x2,
+                residual=r.to(DEV) if mode == "res" else None).cpu().double()
+        finally:
+            lib.lea_conv3d_wino44_set(int(os.environ.get("LEASTEREO_WINO44") or W44_DEFAULT))
+    np.testing.assert_allclose(outs[1].numpy(), want.numpy(), rtol=1e-4, atol=1e-4)
+    np.testing.assert_allclose(outs[1].numpy(), outs[0].numpy(), rtol=1e-4, atol=1e-4)
