@@ -170,7 +170,7 @@ def independent_check_engines():
     fe = executor.FeatureExecutor
     saved = (fe.FUSED_STEM, fe.PAIR_S0)
     env = lambda var, default: int(os.environ.get(var) or default)  # noqa: E731
-    switches = (("lea_disparity_set_register_form", 0, "LEASTEREO_DISP_REG", 2),
+    switches = (("lea_disparity_set_register_form", 0, "LEASTEREO_DISP_REG", 3),
                 ("lea_conv2d_set_small", 0, "LEASTEREO_CONV2D_SMALL", 1),
                 ("lea_resample_set_mode", 2, "LEASTEREO_RESAMPLE_MODE", 0),
                 ("lea_tapsum_set_rows", 0, "LEASTEREO_TAPSUM_ROWS", 2))

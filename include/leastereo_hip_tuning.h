@@ -78,7 +78,9 @@ int lea_conv2d_set_small(int on);
 /* lea_conv2d_kernel_name with the input channel count (the few-channel tile depends on it). */
 const char* lea_conv2d_kernel_name_cin(int B, int cin, int cout, int H, int W);
 
-/* Disparity regression: 2 (default, r05) = the row-staged kernel (a workgroup's two source
+/* Disparity regression: 3 (default, r06) = the three-row staged kernel (one workgroup of 768
+ * threads per three output rows: each raw source value loaded once; bit-identical to 2; D3 = 88
+ * stays on 2); 2 (r05) = the row-staged kernel (a workgroup's two source
  * rows of every plane H-lerped into LDS, two passes over the planes, compile-time depth axis,
  * no rescaling softmin) for the configured (D3, maxdisp) pairs (4, 12), (8, 24), (16, 48),
  * (32, 96), (64, 192); 1 = the register kernel (D3 plane values in registers) for them; 0 = the
@@ -151,10 +153,11 @@ int lea_conv3d_wino2_set_pipeline(int on);
  * packed. */
 int lea_conv3d_wino2p_set_wpre(int on);
 
-/* 1 = the layers of the pipelined W x D kernel run on the F(4,3) x F(4,3) tile instead
- * ("conv3d_wino44_kernel", r06: 36 MFMA products per 4 x 4 outputs and kernel row instead of
- * 48; the W points split over two waves that swap accumulators in the epilogue), 0 = the
- * pipelined F(4,3) x F(2,3) kernel.  Same packed weights (both per-lane copies are packed). */
+/* 1 (default since r06) = the layers of the pipelined W x D kernel run on the F(4,3) x F(4,3)
+ * tile instead ("conv3d_wino44_kernel": 36 MFMA products per 4 x 4 outputs and kernel row
+ * instead of 48; the W points split over two waves that swap accumulators in the epilogue;
+ * -9.5 % on those layers, profiles/r06_w44_ab.txt), 0 = the pipelined F(4,3) x F(2,3)
+ * kernel.  Same packed weights (every per-lane copy is packed). */
 int lea_conv3d_wino44_set(int on);
 
 /* 1 (default) = the Winograd engines' buffer-addressed epilogue where the shape allows

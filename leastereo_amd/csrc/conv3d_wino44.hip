@@ -455,7 +455,7 @@ __global__ __launch_bounds__(256, 2) void conv3d_wino44_kernel(const ConvArgs a)
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
-int g_w44 = 0;  // lea_conv3d_wino44_set
+int g_w44 = 1;  // lea_conv3d_wino44_set (r06 default: -9.5 % on its layers, profiles/r06_w44_ab.txt)
 
 int run44(ConvArgs a, int B, int spw, hipStream_t st) {
   a.ncob = (a.cout + 31) / 32;

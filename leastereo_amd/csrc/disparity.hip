@@ -336,10 +336,11 @@ __global__ __launch_bounds__(kDisp3Threads) void disparity_rows3_f32(const float
 
 }  // namespace lea
 
-// lea_disparity_set_register_form: 3 = the three-row staged kernel (r06), 2 (default, r05) = the row-staged kernel for the configured
+// lea_disparity_set_register_form: 3 (default, r06) = the three-row staged kernel (C2 69.5 -> 68.3,
+// C4 275.6 -> 266.4 us; not at D3 = 88), 2 (r05) = the row-staged kernel for the configured
 // (D3, maxdisp), 1 = the register kernel for them, 0 = the online-softmin kernel everywhere
 // (A/B and tests)
-static int g_disp_reg = 2;
+static int g_disp_reg = 3;
 extern "C" int lea_disparity_set_register_form(int on) {
   using namespace lea;
   clear_error();
@@ -383,9 +384,11 @@ extern "C" int lea_disparity_regression(const void* cost, float* disp, int B, in
         (const float*)cost, disp, H3, W3, rh, rw);                                                     \
     return launch_status("lea_disparity_regression");                                                  \
   }
+  // (88, 264) -- config 5 -- keeps the two-row kernel: three rows' LDS (101 KB) leave one
+  // workgroup per CU there (213 -> 260 us, profiles/r06_disp_probe.txt)
   if (g_disp_reg == 3 && cols_ok) {
     LEA_DISP_ROWS3(4, 12) LEA_DISP_ROWS3(8, 24) LEA_DISP_ROWS3(16, 48) LEA_DISP_ROWS3(32, 96)
-    LEA_DISP_ROWS3(64, 192) LEA_DISP_ROWS3(88, 264)
+    LEA_DISP_ROWS3(64, 192)
   }
 #undef LEA_DISP_ROWS3
   const bool rows_ok = g_disp_reg >= 2 && cols_ok;

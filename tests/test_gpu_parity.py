@@ -408,7 +408,7 @@ def test_disparity_register_form_matches_the_lds_form(shape, md):
             try:
                 out[on] = kernels.disparity_regression(x.to(DEV), md, fast).cpu().double().numpy()
             finally:
-                lib.lea_disparity_set_register_form(2)
+                lib.lea_disparity_set_register_form(3)
             err = np.abs(out[on] - refd)
             assert err.max() < 2e-3 and err.mean() < 1e-4, (fast, on, err.max(), err.mean())
         assert np.abs(out[1] - out[0]).max() < 1e-3 and np.abs(out[2] - out[1]).max() < 1e-3

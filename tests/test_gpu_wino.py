@@ -16,7 +16,7 @@ from leastereo_amd import _lib, kernels
 pytestmark = pytest.mark.gpu
 DEV = "cuda"
 WPRE_DEFAULT = 1  # lea_conv3d_wino2p_set_wpre's library default (csrc/conv3d_wino.hip g_wpre)
-W44_DEFAULT = 0  # lea_conv3d_wino44_set's library default (csrc/conv3d_wino44.hip g_w44)
+W44_DEFAULT = 1  # lea_conv3d_wino44_set's library default (csrc/conv3d_wino44.hip g_w44)
 
 
 def _ref(x, w, scale, shift, relu, res=None):
@@ -421,6 +421,7 @@ def test_wd_halo16_is_bit_identical_to_dword_pieces(b, cin, c1, cout, shape, mod
     x1, x2 = (xs[:, :c1].contiguous(), xs[:, c1:].contiguous()) if c1 < cin else (xs, None)
     pw = kernels.pack_conv_weight_wino(w.to(DEV))
     outs = {}
+    assert lib.lea_conv3d_wino44_set(0) == 0  # this test is the F(4,3) x F(2,3) kernel's
     # (halo16, pipeline, fence, W-transformed per-lane weights: r06 lea_conv3d_wino2p_set_wpre)
     for on, pipe, fence, wpre in ((1, 1, 1, 0), (1, 0, 1, 0), (0, 1, 1, 0), (1, 1, 0, 0), (1, 1, 1, 1)):
         assert lib.lea_conv3d_wino2_set_halo16(on) == 0 and lib.lea_conv3d_wino2_set_pipeline(pipe) == 0
@@ -444,6 +445,7 @@ def test_wd_halo16_is_bit_identical_to_dword_pieces(b, cin, c1, cout, shape, mod
             lib.lea_conv3d_wino2_set_pipeline(1)
             lib.lea_conv3d_wino_set_fence(1)
             lib.lea_conv3d_wino2p_set_wpre(int(os.environ.get("LEASTEREO_WINO2P_WPRE") or WPRE_DEFAULT))
+    lib.lea_conv3d_wino44_set(int(os.environ.get("LEASTEREO_WINO44") or W44_DEFAULT))
     base = outs[(0, 1, 1, 0)]
     assert all(torch.equal(o, base) for o in outs.values()), [k for k, o in outs.items() if not torch.equal(o, base)]
     np.testing.assert_allclose(outs[(1, 1, 1, 0)].cpu().double().numpy(), want.numpy(), rtol=1e-4, atol=1e-4)

@@ -41,7 +41,7 @@ def main():
                       f"{float((out[form] - out.get(1, out[form])).abs().max()):.2e}"
                       + (f"  form 3 == form 2: {bool(torch.equal(out[3], out[2]))}" if form == 3 else ""),
                       flush=True)
-    _lib.check(lib.lea_disparity_set_register_form(2), "form")
+    _lib.check(lib.lea_disparity_set_register_form(3), "form")
 
 
 if __name__ == "__main__":
