@@ -198,7 +198,8 @@ __global__ __launch_bounds__(256, 2) void conv3d_wino44_kernel(const ConvArgs a)
   const int vxh = __builtin_amdgcn_readfirstlane(tid >> 7);
   const int vxo = (vc == 0 ? CB0 : vc == 1 ? CB1 : vc == 2 ? CB2 : CB3) + vr * RWA + 3 + F * vg;
   const int vto = vc * TCS + vr * TRS + GS * vg + XHS * vxh;
-  auto vpass = [&](int buf) {
+  auto vpass = [&](auto XHC, int buf) {
+    constexpr int VXH = decltype(XHC)::value;  // == vxh (wave-uniform): a compile-time branch
     const float* sp0 = halo + buf * XS + vxo;
     float bw[PLANES][3];
 #pragma unroll
@@ -207,7 +208,7 @@ __global__ __launch_bounds__(256, 2) void conv3d_wino44_kernel(const ConvArgs a)
       const float2 a0 = *reinterpret_cast<const float2*>(sp);
       const float2 a1 = *reinterpret_cast<const float2*>(sp + 2);
       const float2 a2 = *reinterpret_cast<const float2*>(sp + 4);
-      if (vxh == 0) {  // W points 0, 1, 2 (bt6's first three rows)
+      if constexpr (VXH == 0) {  // W points 0, 1, 2 (bt6's first three rows)
         const float pa = fmaf(-4.f, a1.x, a2.x), pb = fmaf(-4.f, a0.y, a1.y);
         bw[pl][0] = fmaf(4.f, a0.x, fmaf(-5.f, a1.x, a2.x));
         bw[pl][1] = pa + pb;
@@ -347,111 +348,111 @@ __global__ __launch_bounds__(256, 2) void conv3d_wino44_kernel(const ConvArgs a)
       }
     }
   };
-  auto epilogue = [&](int d0, float* xch) {
-    if (xh == 0)
-      epilogue_xh(std::integral_constant<int, 0>{}, d0, xch);
-    else
-      epilogue_xh(std::integral_constant<int, 1>{}, d0, xch);
-  };
-
-  // prologue: halo(0), g(0), halo(1); V(0)
-  issue_halo(0, 0, 0);
-  load_g(0);
-  if (nitems > 1) {
-    issue_halo(1 % nchunks, 1 / nchunks, 1);
-    asm volatile("s_waitcnt vmcnt(4)" ::: "memory");  // all but halo(1)'s four pieces
-  } else {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  }
-  __syncthreads();
-  vpass(0);
-  bool after_epi = false;
-  int ich = 0, iqd = 0;  // item it = (chunk, depth quad)
-  int hch = min(2, nitems - 1) % nchunks, hqd = min(2, nitems - 1) / nchunks;
-  for (int it = 0; it < nitems; ++it) {
-    if (after_epi)
-      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NST) : "memory");
-    else
+  // the prologue and the item loop, specialised per x-half (wave-uniform): no branch in the body
+  auto run = [&](auto XHC) {
+    // prologue: halo(0), g(0), halo(1); V(0)
+    issue_halo(0, 0, 0);
+    load_g(0);
+    if (nitems > 1) {
+      issue_halo(1 % nchunks, 1 / nchunks, 1);
+      asm volatile("s_waitcnt vmcnt(4)" ::: "memory");  // all but halo(1)'s four pieces
+    } else {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
     __syncthreads();
-    const float* tv = tvb + (it & 1) * TS;
-    struct Raw {
-      float4 v4[4];
-      float2 v2;
-    };
-    auto load_step = [&](int kh, Raw& o) {
-      const float* tp = tv + toff + kh * TRS;
-#pragma unroll
-      for (int k = 0; k < 4; ++k) o.v4[k] = reinterpret_cast<const float4*>(tp)[k];
-      o.v2 = *reinterpret_cast<const float2*>(tp + 16);
-    };
-    struct Xf {
-      float v[NX][NE];
-      float u[NX][NE];
-    };
-    auto xform = [&](int kh, const Raw& o, Xf& T) {
-      const float e18[18] = {o.v4[0].x, o.v4[0].y, o.v4[0].z, o.v4[0].w, o.v4[1].x, o.v4[1].y,
-                             o.v4[1].z, o.v4[1].w, o.v4[2].x, o.v4[2].y, o.v4[2].z, o.v4[2].w,
-                             o.v4[3].x, o.v4[3].y, o.v4[3].z, o.v4[3].w, o.v2.x, o.v2.y};
-#pragma unroll
-      for (int x = 0; x < NX; ++x)
-#pragma unroll
-        for (int e = 0; e < NE; ++e) T.v[x][e] = e18[x * 6 + e];
-      const float* g = reinterpret_cast<const float*>(gw) + kh * 9;
-#pragma unroll
-      for (int x = 0; x < NX; ++x) {  // G_D' along the kernel depth (gw4)
-        const float g0 = g[x], g1 = g[3 + x], g2 = g[6 + x];
-        const float s = g0 + g2, s4 = fmaf(4.f, g2, g0);
-        T.u[x][0] = g0;
-        T.u[x][1] = s + g1;
-        T.u[x][2] = s - g1;
-        T.u[x][3] = fmaf(2.f, g1, s4);
-        T.u[x][4] = fmaf(-2.f, g1, s4);
-        T.u[x][5] = g2;
+    vpass(XHC, 0);
+    bool after_epi = false;
+    int ich = 0, iqd = 0;  // item it = (chunk, depth quad)
+    int hch = min(2, nitems - 1) % nchunks, hqd = min(2, nitems - 1) / nchunks;
+    for (int it = 0; it < nitems; ++it) {
+      if (after_epi)
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NST) : "memory");
+      else
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      const float* tv = tvb + (it & 1) * TS;
+      struct Raw {
+        float4 v4[4];
+        float2 v2;
+      };
+      auto load_step = [&](int kh, Raw& o) {
+        const float* tp = tv + toff + kh * TRS;
+  #pragma unroll
+        for (int k = 0; k < 4; ++k) o.v4[k] = reinterpret_cast<const float4*>(tp)[k];
+        o.v2 = *reinterpret_cast<const float2*>(tp + 16);
+      };
+      struct Xf {
+        float v[NX][NE];
+        float u[NX][NE];
+      };
+      auto xform = [&](int kh, const Raw& o, Xf& T) {
+        const float e18[18] = {o.v4[0].x, o.v4[0].y, o.v4[0].z, o.v4[0].w, o.v4[1].x, o.v4[1].y,
+                               o.v4[1].z, o.v4[1].w, o.v4[2].x, o.v4[2].y, o.v4[2].z, o.v4[2].w,
+                               o.v4[3].x, o.v4[3].y, o.v4[3].z, o.v4[3].w, o.v2.x, o.v2.y};
+  #pragma unroll
+        for (int x = 0; x < NX; ++x)
+  #pragma unroll
+          for (int e = 0; e < NE; ++e) T.v[x][e] = e18[x * 6 + e];
+        const float* g = reinterpret_cast<const float*>(gw) + kh * 9;
+  #pragma unroll
+        for (int x = 0; x < NX; ++x) {  // G_D' along the kernel depth (gw4)
+          const float g0 = g[x], g1 = g[3 + x], g2 = g[6 + x];
+          const float s = g0 + g2, s4 = fmaf(4.f, g2, g0);
+          T.u[x][0] = g0;
+          T.u[x][1] = s + g1;
+          T.u[x][2] = s - g1;
+          T.u[x][3] = fmaf(2.f, g1, s4);
+          T.u[x][4] = fmaf(-2.f, g1, s4);
+          T.u[x][5] = g2;
+        }
+      };
+      auto mfmas = [&](const Xf& T) {
+  #pragma unroll
+        for (int x = 0; x < NX; ++x)
+  #pragma unroll
+          for (int e = 0; e < NE; ++e)
+            acc[x][e] = __builtin_amdgcn_mfma_f32_16x16x4f32(T.u[x][e], T.v[x][e], acc[x][e], 0, 0, 0);
+      };
+      Raw raw[2];
+      Xf xf[2];
+      __builtin_amdgcn_iglp_opt(0);
+      load_step(0, raw[0]);
+      load_step(1, raw[1]);
+      xform(0, raw[0], xf[0]);
+      // halo(it + 2) into the buffer V-pass(it) read; past the last item the DMA / V-pass /
+      // loads repeat the last one (nothing reads them): one basic block
+      issue_halo(hch, hqd, it & 1);
+      load_step(2, raw[0]);
+      xform(1, raw[1], xf[1]);
+      mfmas(xf[0]);
+      vpass(XHC, (it + 1) & 1);
+      xform(2, raw[0], xf[0]);
+      load_g(it + 1 < nitems ? (ich + 1 == nchunks ? 0 : ich + 1) : ich);
+      mfmas(xf[1]);
+      mfmas(xf[0]);
+      after_epi = false;
+      if (ich == nchunks - 1) {
+        epilogue_xh(XHC, (pz0 + iqd) * TD, tvb + (it & 1) * TS);
+        after_epi = true;
+  #pragma unroll
+        for (int x = 0; x < NX; ++x)
+  #pragma unroll
+          for (int e = 0; e < NE; ++e) acc[x][e] = f32x4{0.f, 0.f, 0.f, 0.f};
       }
-    };
-    auto mfmas = [&](const Xf& T) {
-#pragma unroll
-      for (int x = 0; x < NX; ++x)
-#pragma unroll
-        for (int e = 0; e < NE; ++e)
-          acc[x][e] = __builtin_amdgcn_mfma_f32_16x16x4f32(T.u[x][e], T.v[x][e], acc[x][e], 0, 0, 0);
-    };
-    Raw raw[2];
-    Xf xf[2];
-    __builtin_amdgcn_iglp_opt(0);
-    load_step(0, raw[0]);
-    load_step(1, raw[1]);
-    xform(0, raw[0], xf[0]);
-    // halo(it + 2) into the buffer V-pass(it) read; past the last item the DMA / V-pass /
-    // loads repeat the last one (nothing reads them): one basic block
-    issue_halo(hch, hqd, it & 1);
-    load_step(2, raw[0]);
-    xform(1, raw[1], xf[1]);
-    mfmas(xf[0]);
-    vpass((it + 1) & 1);
-    xform(2, raw[0], xf[0]);
-    load_g(it + 1 < nitems ? (ich + 1 == nchunks ? 0 : ich + 1) : ich);
-    mfmas(xf[1]);
-    mfmas(xf[0]);
-    after_epi = false;
-    if (ich == nchunks - 1) {
-      epilogue((pz0 + iqd) * TD, tvb + (it & 1) * TS);
-      after_epi = true;
-#pragma unroll
-      for (int x = 0; x < NX; ++x)
-#pragma unroll
-        for (int e = 0; e < NE; ++e) acc[x][e] = f32x4{0.f, 0.f, 0.f, 0.f};
+      if (++ich == nchunks) {
+        ich = 0;
+        ++iqd;
+      }
+      if (it + 3 < nitems && ++hch == nchunks) {
+        hch = 0;
+        ++hqd;
+      }
     }
-    if (++ich == nchunks) {
-      ich = 0;
-      ++iqd;
-    }
-    if (it + 3 < nitems && ++hch == nchunks) {
-      hch = 0;
-      ++hqd;
-    }
-  }
+  };
+  if (xh == 0)
+    run(std::integral_constant<int, 0>{});
+  else
+    run(std::integral_constant<int, 1>{});
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
