@@ -774,7 +774,9 @@ inline void plan_halo16(Plan& p, bool cv, int W, const ConvArgs* a, int cin = 0)
     // the one-barrier pipeline uses the buffer-addressed epilogue only
     // (layers of one or two chunks per depth pair stay on the two-barrier tile: L0 8->24
     // ran 286 us there, 296-301 us pipelined -- r03 sweeps)
-    const bool pipe = g_pipe && g_epibuf && (a == nullptr || epi_buf_ok(*a)) && (cin == 0 || cin > 2 * CIN_B);
+    // (g_w44 == 2: the two-chunk layers -- L0 8 -> 24 -- on the F(4,3) x F(4,3) tile too)
+    const bool pipe = g_pipe && g_epibuf && (a == nullptr || epi_buf_ok(*a)) &&
+                      (cin == 0 || cin > 2 * CIN_B || (g_w44 == 2 && cin > CIN_B));
     if (p.p2.pv == 1 && p.p2.nw == 4 && p.p2.mte == 1) p.p2.pv = pipe ? 3 : 2;
     // the per-lane 16-cout tile (the L1 cells): 16-byte pieces, interleaved row sets (r04)
     if (g_lane16 && p.p2.pv == 0 && p.p2.q == 8 && p.p2.wc == 1 && p.p2.mte == 1 && p.p2.nw == 4 &&
@@ -985,7 +987,7 @@ extern "C" int lea_conv3d_wino2_set_pipeline(int on) {
 
 extern "C" int lea_conv3d_wino44_set(int on) {
   clear_error();
-  LEA_CHECK_ARG(on == 0 || on == 1, "lea_conv3d_wino44_set: on=%d", on);
+  LEA_CHECK_ARG(on >= 0 && on <= 2, "lea_conv3d_wino44_set: on=%d", on);
   wino::g_w44 = on;
   return 0;
 }
