@@ -158,7 +158,8 @@ int lea_conv3d_wino2p_set_wpre(int on);
  * instead of 48; the W points split over two waves that swap accumulators in the epilogue;
  * -9.5 % on those layers, profiles/r06_w44_ab.txt), 0 = the pipelined F(4,3) x F(2,3)
  * kernel, 2 = as 1 and also the two-chunk layers (cin 8: the L0 8 -> 24 sibling group) that
- * otherwise stay on the two-barrier tile.  Same packed weights (every per-lane copy is packed). */
+ * otherwise stay on the two-barrier tile, 3 = as 2 and the 16-cout layers as half-empty 32-cout
+ * blocks.  Same packed weights (every per-lane copy is packed). */
 int lea_conv3d_wino44_set(int on);
 
 /* 1 (default) = the Winograd engines' buffer-addressed epilogue where the shape allows

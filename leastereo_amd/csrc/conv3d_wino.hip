@@ -673,11 +673,16 @@ inline long long staged_floats(int cout, int cin) {
   const int mt = host_mt(cout), cop = cop_of(mt), nstep = mt == 0 ? 12 : 9;
   return (long long)((cout + cop - 1) / cop) * (cin / CIN_B) * nstep * 3 * CIN_B * cop + 256;
 }
-// couts <= 32 also carry the F(2,3) x F(2,3) tile's U, after the staged rows and (32-cout
-// blocks) the per-lane copy
+// packed layout: the staged rows; (32-cout blocks) the pipelined F(4,3) x F(2,3) tile's per-lane
+// copies; (16- and 32-cout blocks) the F(4,3) x F(4,3) tile's per-lane copy, in 32-cout blocks
+// (conv3d_wino44.hip, r06); (couts <= 32) the F(2,3) x F(2,3) tile's U
 inline bool has_u22(int cout) { return cout <= 32; }
-inline long long u22_offset(int cout, int cin) {
+inline bool has_l44(int cout) { return host_mt(cout) == 1 || host_mt(cout) == 2; }
+inline long long l44_offset(int cout, int cin) {
   return staged_floats(cout, cin) + (host_mt(cout) == 2 ? lane_weights_floats(cout, cin) : 0);
+}
+inline long long u22_offset(int cout, int cin) {
+  return l44_offset(cout, cin) + (has_l44(cout) ? lane44_floats(cout, cin) : 0);
 }
 
 // W x D engine tile for variant v (2..4), or nullptr-equivalent (q = 0) when the
@@ -776,12 +781,18 @@ inline void plan_halo16(Plan& p, bool cv, int W, const ConvArgs* a, int cin = 0)
     // ran 286 us there, 296-301 us pipelined -- r03 sweeps)
     // (g_w44 == 2: the two-chunk layers -- L0 8 -> 24 -- on the F(4,3) x F(4,3) tile too)
     const bool pipe = g_pipe && g_epibuf && (a == nullptr || epi_buf_ok(*a)) &&
-                      (cin == 0 || cin > 2 * CIN_B || (g_w44 == 2 && cin > CIN_B));
+                      (cin == 0 || cin > 2 * CIN_B || (g_w44 >= 2 && cin > CIN_B));
     if (p.p2.pv == 1 && p.p2.nw == 4 && p.p2.mte == 1) p.p2.pv = pipe ? 3 : 2;
     // the per-lane 16-cout tile (the L1 cells): 16-byte pieces, interleaved row sets (r04)
     if (g_lane16 && p.p2.pv == 0 && p.p2.q == 8 && p.p2.wc == 1 && p.p2.mte == 1 && p.p2.nw == 4 &&
         p.p2.occ == 2)
       p.p2.pv = g_lane16 == 2 ? 5 : 4;
+    // g_w44 == 3 (r06 experiment): the 16-cout layers on the F(4,3) x F(4,3) tile as half-empty
+    // 32-cout blocks (the pipelined tile's plan: pv 3 with two cout tiles)
+    if (g_w44 == 3 && pipe && p.mt == 1 && (p.p2.pv == 4 || p.p2.pv == 5)) {
+      p.p2.pv = 3;
+      p.p2.wc = 2;
+    }
   } else if (p.mt == 0 && p.f == 4 && p.q == 16 && p.np == 1 && p.td == 2) {
     p.h16 = true;  // the depth-paired 64-wide tile (the L0 8-channel cell ops)
   }
@@ -881,6 +892,7 @@ int common(ConvArgs& a, int B, bool cv, int dtype, void* stream) {
   }
   plan_halo16(p, cv, a.W, &a);
   if (g_epibuf && epi_buf_ok(a)) a.flags |= kEpiBuf;
+  if (has_l44(a.cout)) a.uoff = l44_offset(a.cout, a.cin);  // (the F(4,3) x F(4,3) tile's section)
   return run(p, a, B, as_stream(stream), cv);
 }
 
@@ -905,24 +917,26 @@ extern "C" int lea_conv3d_wino_pack_weights(const float* w, float* packed, int c
   const long long total = (long long)lea_conv3d_wino_packed_floats(cout, cin);
   const int grid = (int)std::min<long long>((total + 255) / 256, 4096);
   hipStream_t st = as_stream(stream);
-  const long long staged = wino::staged_floats(cout, cin), uoff = wino::u22_offset(cout, cin);
+  const long long staged = wino::staged_floats(cout, cin), uoff = wino::u22_offset(cout, cin),
+                  l44 = wino::l44_offset(cout, cin);
   switch (wino::host_mt(cout)) {
     case 0: wino::pack_wino_dp_kernel<<<grid, 256, 0, st>>>(w, packed, cout, cin, cin / wino::CIN_B, staged); break;
     case 1: wino::pack_wino_kernel<1><<<grid, 256, 0, st>>>(w, packed, cout, cin, cin / wino::CIN_B, staged); break;
     case 3: wino::pack_wino_kernel<3><<<grid, 256, 0, st>>>(w, packed, cout, cin, cin / wino::CIN_B, staged); break;
     default: {
-      const long long lane = wino::lane_raw_floats(cout, cin), lane44 = wino::lane44_floats(cout, cin),
-                      lanew = uoff - staged - lane - lane44;
+      const long long lane = wino::lane_raw_floats(cout, cin), lanew = l44 - staged - lane;
       wino::pack_wino_kernel<2><<<grid, 256, 0, st>>>(w, packed, cout, cin, cin / wino::CIN_B, staged);
       const int g2 = (int)std::min<long long>((lane + 255) / 256, 4096);
       wino::pack_wino_lane_kernel<<<g2, 256, 0, st>>>(w, packed + staged, cout, cin, cin / wino::CIN_B, lane);
       const int g3 = (int)std::min<long long>((lanew + 255) / 256, 4096);
       wino::pack_wino_lane_wpre_kernel<<<g3, 256, 0, st>>>(w, packed + staged + lane, cout, cin,
                                                            cin / wino::CIN_B, lanew);
-      const int g4 = (int)std::min<long long>((lane44 + 255) / 256, 4096);
-      wino::pack_wino44_lane_kernel<<<g4, 256, 0, st>>>(w, packed + staged + lane + lanew, cout, cin,
-                                                        cin / wino::CIN_B, lane44);
     }
+  }
+  if (wino::has_l44(cout)) {  // the F(4,3) x F(4,3) tile's per-lane copy
+    const long long n44 = wino::lane44_floats(cout, cin);
+    const int g4 = (int)std::min<long long>((n44 + 255) / 256, 4096);
+    wino::pack_wino44_lane_kernel<<<g4, 256, 0, st>>>(w, packed + l44, cout, cin, cin / wino::CIN_B, n44);
   }
   if (wino::has_u22(cout)) {  // the F(2,3) x F(2,3) tile's U
     const long long u = total - uoff;
@@ -987,7 +1001,7 @@ extern "C" int lea_conv3d_wino2_set_pipeline(int on) {
 
 extern "C" int lea_conv3d_wino44_set(int on) {
   clear_error();
-  LEA_CHECK_ARG(on >= 0 && on <= 2, "lea_conv3d_wino44_set: on=%d", on);
+  LEA_CHECK_ARG(on >= 0 && on <= 3, "lea_conv3d_wino44_set: on=%d", on);
   wino::g_w44 = on;
   return 0;
 }

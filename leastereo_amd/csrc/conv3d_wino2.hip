@@ -1097,8 +1097,7 @@ __global__ void pack_wino_lane_wpre_kernel(const float* __restrict__ w, float* _
 long long lane_raw_floats(int cout, int cin) { return (long long)((cout + 31) / 32) * (cin / CIN_B) * 2 * 64 * kGL; }
 
 long long lane_weights_floats(int cout, int cin) {
-  return lane_raw_floats(cout, cin) + (long long)((cout + 31) / 32) * (cin / CIN_B) * 2 * 64 * kGLW +
-         lane44_floats(cout, cin);  // + the F(4,3) x F(4,3) kernel's copy (conv3d_wino44.hip)
+  return lane_raw_floats(cout, cin) + (long long)((cout + 31) / 32) * (cin / CIN_B) * 2 * 64 * kGLW;
 }
 
 

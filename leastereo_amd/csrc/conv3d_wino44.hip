@@ -148,11 +148,8 @@ __global__ __launch_bounds__(256, 2) void conv3d_wino44_kernel(const ConvArgs a)
   const int HW = a.H * a.W;
   const unsigned nrec = (unsigned)(HW * a.D) * 4u;
   const long long cvol = (long long)HW * a.D;
-  // per-lane weights: after the staged copy, the pipelined tile's raw and W-transformed per-lane
-  // copies (conv3d_wino2.hip lane_weights_floats) -- this kernel's section last
-  const long long staged = (long long)a.ncob * nchunks * (27 * CIN_B * 32) + 256;
-  const long long lanes2p = (long long)a.ncob * nchunks * 2 * 64 * (28 + 56);
-  const float* wl = a.wp + staged + lanes2p + ((long long)(cob * nchunks) * 4 + wc * 2 + xh) * 64 * KGL + lane * 4;
+  // per-lane weights: this kernel's section of the packed weights at a.uoff (the host's l44_offset)
+  const float* wl = a.wp + a.uoff + ((long long)(cob * nchunks) * 4 + wc * 2 + xh) * 64 * KGL + lane * 4;
 
   // 16-byte halo pieces: piece = wave of every channel; block e16 = (plane, row, 16-byte column)
   const int e16 = 64 * wave + lane;

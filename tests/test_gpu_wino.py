@@ -585,3 +585,30 @@ def test_wino44_vs_float64(b, cin, c1, cout, shape, mode):
             lib.lea_conv3d_wino44_set(int(os.environ.get("LEASTEREO_WINO44") or W44_DEFAULT))
     np.testing.assert_allclose(outs[1].numpy(), want.numpy(), rtol=1e-4, atol=1e-4)
     np.testing.assert_allclose(outs[1].numpy(), outs[0].numpy(), rtol=1e-4, atol=1e-4)
+
+
+@pytest.mark.parametrize("mode,b,cin,cout,shape,res", [
+    (2, 1, 8, 24, (9, 8, 68), "acc"), (2, 2, 8, 32, (5, 6, 40), None),
+    (3, 1, 16, 16, (11, 20, 40), "acc"), (3, 2, 16, 16, (5, 9, 36), "res"), (3, 1, 32, 16, (4, 13, 68), None),
+    (3, 1, 16, 12, (6, 10, 44), "acc")])
+def test_wino44_modes_vs_float64(mode, b, cin, cout, shape, res):
+    """lea_conv3d_wino44_set modes 2 (the two-chunk layers on the F(4,3) x F(4,3) tile) and 3
+    (also the 16-cout layers, as half-empty 32-cout blocks) against float64 torch."""
+    lib = _lib.load()
+    g = torch.Generator().manual_seed(cin + 5 * cout + shape[2])
+    x = torch.randn((b, cin) + shape, generator=g)
+    w = torch.randn(cout, cin, 3, 3, 3, generator=g) / np.sqrt(cin * 27)
+    scale = torch.rand(cout, generator=g) + 0.5
+    shift = torch.randn(cout, generator=g) * 0.1
+    r = torch.randn((b, cout) + shape, generator=g)
+    want = _ref(x, w, scale, shift, True, r if res else None)
+    pw = kernels.pack_conv_weight_wino(w.to(DEV))
+    assert lib.lea_conv3d_wino44_set(mode) == 0
+    try:
+        assert kernels.wino_kernel_name(b, cout, *shape, cin=cin) == "conv3d_wino44_kernel"
+        out = r.to(DEV).clone() if res == "acc" else None
+        y = kernels.conv3d_bnrelu_wino(x.to(DEV), pw, cout, scale.to(DEV), shift.to(DEV), relu=True, out=out,
+                                       accumulate=res == "acc", residual=r.to(DEV) if res == "res" else None)
+    finally:
+        lib.lea_conv3d_wino44_set(int(os.environ.get("LEASTEREO_WINO44") or W44_DEFAULT))
+    np.testing.assert_allclose(y.cpu().double().numpy(), want.numpy(), rtol=1e-4, atol=1e-4)
