@@ -7,6 +7,7 @@ tensor or a missing library raises.
 """
 from __future__ import annotations
 
+import contextlib
 import os
 
 import torch
@@ -980,6 +981,23 @@ def wino_mfma_scale(cout: int, name: str) -> float:
         return (f + 2) / (3.0 * f) * 12 / 9 * 8 / cout
     cop = 16 if cout <= 16 else (48 if cout % 32 != 0 and cout % 48 == 0 else 32)
     return (f + 2) / (3.0 * f) * (-(-cout // cop) * cop) / cout
+
+
+@contextlib.contextmanager
+def wino_depth_f2():
+    """Run the enclosed Winograd convs of the pipelined kernel's layers on the F(4,3) x F(2,3)
+    tile (lea_conv3d_wino44_set(0)) instead of the F(4,3) x F(4,3) one, then restore the
+    process setting (LEASTEREO_WINO44, default 1).  The training path uses it: its gradient
+    bars (tests/test_gpu_training.py) were calibrated on the F(2,3)-along-D numerics, and
+    F(4,3) along D adds fp32 roundings that the backward chain amplifies (r06: a feature-net
+    BN-weight gradient at 2.9e-3 of its scale against the 2e-3 bar).  Process-wide, like
+    every tuning setter: not for concurrent use from several threads."""
+    lib = _lib.load()
+    check(lib.lea_conv3d_wino44_set(0), "lea_conv3d_wino44_set")
+    try:
+        yield
+    finally:
+        check(lib.lea_conv3d_wino44_set(int(os.environ.get("LEASTEREO_WINO44") or 1)), "lea_conv3d_wino44_set")
 
 
 def wino_kernel_name(b, cout, d, h, w, costvolume=False, cin=0):

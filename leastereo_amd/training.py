@@ -80,7 +80,8 @@ def _conv(x: torch.Tensor, w: torch.Tensor, relu: bool = False) -> torch.Tensor:
     cout, cin, k = w.shape[0], w.shape[1], w.shape[-1]
     b, _, d, h, wd = x.shape
     if kernels.wino_eligible(cout, cin, k) and kernels.wino_preferred(b, cout, cin, d, h, wd):
-        return kernels.conv3d_bnrelu_wino(x, kernels.pack_conv_weight_wino(w), cout, None, None, relu=relu)
+        with kernels.wino_depth_f2():  # the training bars' numerics (kernels.wino_depth_f2)
+            return kernels.conv3d_bnrelu_wino(x, kernels.pack_conv_weight_wino(w), cout, None, None, relu=relu)
     return kernels.conv3d_bnrelu(x, kernels.pack_conv_weight(w), cout, k, None, None, relu=relu)
 
 
