@@ -26,7 +26,7 @@
 // its three points on each of the 6 input planes, then the D transform (B^T of F(4,3) along
 // the planes) -- 18 floats [x][e], exactly what the consuming wave reads.
 // Epilogue (the quad's last chunk): the two x-halves of a cout tile swap accumulators through
-// LDS (the just-consumed V buffer, two rounds) so each holds all 36 points of two of the
+// LDS (the just-consumed V and halo buffers, one exchange) so each holds all 36 points of two of the
 // four couts its lanes carry, then A_W^T and A_D^T (with G's factors), BN, ReLU, residual,
 // buffer-addressed float4 stores.
 //
@@ -57,7 +57,7 @@ static_assert(CB1 % 64 == 3 && CB2 % 64 == 33 && CB3 % 64 == 35, "V-pass bank ma
 static_assert(BLK16 <= 4 * 64 && 4 * 256 <= CB1 - CB0, "whole pieces per channel region");
 static_assert(TRS % 64 == 0 && TCS % 8 == 4 && GS % 8 == 0 && XHS % 4 == 0 && TRS >= Q * GS && TCS >= RH * TRS,
               "V bank map");
-static_assert(4 * 64 * 18 <= TS, "epilogue exchange round fits the V buffer");
+static_assert(4 * 64 * 20 <= TS && 4 * 64 * 16 <= XS, "epilogue exchange fits a V and a halo buffer");
 static_assert((2 * XS + 2 * TS) * 4 * 2 <= 160 * 1024, "two workgroups per CU");
 }  // namespace w44
 
@@ -255,11 +255,11 @@ __global__ __launch_bounds__(256, 2) void conv3d_wino44_kernel(const ConvArgs a)
   const __amdgpu_buffer_rsrc_t rrs =
       block_rsrc((resid ? a.res : a.y) + (long long)b * (resid ? a.rbs : a.ybs) + (long long)co0 * DHW, nco * DHW * 4);
   // the epilogue body for x-half XH (a compile-time constant: every register index static)
-  auto epilogue_xh = [&](auto XHC, int d0, float* xch) {
+  auto epilogue_xh = [&](auto XHC, int d0, float* xch0, float* xch1) {
     constexpr int XH = decltype(XHC)::value;
     constexpr int RS = 2 * (1 - XH);  // the element pair of the f32x4 the partner finalizes
-    // swap accumulators with the other x-half of this cout tile (wave ^ 2): two rounds of three
-    // D points, 18 floats per lane as [wave][4 float4 + 1 float2][lane]
+    // swap accumulators with the other x-half of this cout tile (wave ^ 2) in one exchange through
+    // xch0 (the V buffer just consumed) and xch1 (the halo buffer V-pass(it + 1) consumed)
     float mine[2][6][NE];  // [r][x 0..5][e]: all 36 points of this wave's two couts
 #pragma unroll
     for (int x = 0; x < NX; ++x)
@@ -268,44 +268,39 @@ __global__ __launch_bounds__(256, 2) void conv3d_wino44_kernel(const ConvArgs a)
         mine[0][3 * XH + x][e] = acc[x][e][2 * XH];
         mine[1][3 * XH + x][e] = acc[x][e][2 * XH + 1];
       }
+    // the 36 values this wave sends, [x][e][r]: 20 through xch0, 16 through xch1 (float4s, lanes contiguous)
+    float snd[36];
 #pragma unroll
-    for (int round = 0; round < 2; ++round) {
-      float s[18];
+    for (int x = 0; x < NX; ++x)
 #pragma unroll
-      for (int x = 0; x < NX; ++x)
-#pragma unroll
-        for (int e3 = 0; e3 < 3; ++e3) {
-          s[x * 6 + e3 * 2] = acc[x][3 * round + e3][RS];
-          s[x * 6 + e3 * 2 + 1] = acc[x][3 * round + e3][RS + 1];
-        }
-      __syncthreads();  // round 0: every wave done reading the V buffer; round 1: round 0's reads done
-      float* wr = xch + wave * (18 * 64);
-#pragma unroll
-      for (int k = 0; k < 4; ++k)
-        reinterpret_cast<float4*>(wr + k * 256)[lane] = make_float4(s[4 * k], s[4 * k + 1], s[4 * k + 2], s[4 * k + 3]);
-      reinterpret_cast<float2*>(wr + 1024)[lane] = make_float2(s[16], s[17]);
-      __syncthreads();
-      const float* rd = xch + (wave ^ 2) * (18 * 64);
-      float g[18];
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        const float4 t = reinterpret_cast<const float4*>(rd + k * 256)[lane];
-        g[4 * k] = t.x;
-        g[4 * k + 1] = t.y;
-        g[4 * k + 2] = t.z;
-        g[4 * k + 3] = t.w;
+      for (int e = 0; e < NE; ++e) {
+        snd[(x * 6 + e) * 2] = acc[x][e][RS];
+        snd[(x * 6 + e) * 2 + 1] = acc[x][e][RS + 1];
       }
-      const float2 t2 = reinterpret_cast<const float2*>(rd + 1024)[lane];
-      g[16] = t2.x;
-      g[17] = t2.y;
+    __syncthreads();  // every wave done reading both buffers (the steps' V, the V-pass's halo)
 #pragma unroll
-      for (int x = 0; x < NX; ++x)
-#pragma unroll
-        for (int e3 = 0; e3 < 3; ++e3) {
-          mine[0][3 * (1 - XH) + x][3 * round + e3] = g[x * 6 + e3 * 2];
-          mine[1][3 * (1 - XH) + x][3 * round + e3] = g[x * 6 + e3 * 2 + 1];
-        }
+    for (int k = 0; k < 9; ++k) {
+      float* wr = k < 5 ? xch0 + wave * (20 * 64) + k * 256 : xch1 + wave * (16 * 64) + (k - 5) * 256;
+      reinterpret_cast<float4*>(wr)[lane] = make_float4(snd[4 * k], snd[4 * k + 1], snd[4 * k + 2], snd[4 * k + 3]);
     }
+    __syncthreads();
+    float rcv[36];
+#pragma unroll
+    for (int k = 0; k < 9; ++k) {
+      const float* rd = k < 5 ? xch0 + (wave ^ 2) * (20 * 64) + k * 256 : xch1 + (wave ^ 2) * (16 * 64) + (k - 5) * 256;
+      const float4 t = reinterpret_cast<const float4*>(rd)[lane];
+      rcv[4 * k] = t.x;
+      rcv[4 * k + 1] = t.y;
+      rcv[4 * k + 2] = t.z;
+      rcv[4 * k + 3] = t.w;
+    }
+#pragma unroll
+    for (int x = 0; x < NX; ++x)
+#pragma unroll
+      for (int e = 0; e < NE; ++e) {
+        mine[0][3 * (1 - XH) + x][e] = rcv[(x * 6 + e) * 2];
+        mine[1][3 * (1 - XH) + x][e] = rcv[(x * 6 + e) * 2 + 1];
+      }
     const bool lv = h < a.H && w < a.W;
     unsigned off[2][TD];
 #pragma unroll
@@ -429,7 +424,7 @@ __global__ __launch_bounds__(256, 2) void conv3d_wino44_kernel(const ConvArgs a)
       mfmas(xf[0]);
       after_epi = false;
       if (ich == nchunks - 1) {
-        epilogue_xh(XHC, (pz0 + iqd) * TD, tvb + (it & 1) * TS);
+        epilogue_xh(XHC, (pz0 + iqd) * TD, tvb + (it & 1) * TS, halo + ((it + 1) & 1) * XS);
         after_epi = true;
   #pragma unroll
         for (int x = 0; x < NX; ++x)
