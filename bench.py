@@ -623,8 +623,12 @@ def roofline_fields(a, m):
                          for sh, d in sorted(dom_shapes.items(), key=lambda kv: -kv[1]["ms"])],
             "direct_equivalent": {"flops_per_launch": direct,
                                   "achieved": direct / (ms_per_launch * 1e-3) / 1e12,
+                                  "issued_per_direct_flop": issued / direct,
                                   "note": "the reference algorithm's (direct convolution's) "
-                                          "FLOPs for the same outputs; not a utilisation"}}
+                                          "FLOPs for the same outputs; not a utilisation.  A "
+                                          "Winograd tile that issues fewer products per output "
+                                          "lowers frac at equal speed: compare kernels by time "
+                                          "or by this rate (DESIGN.md §4 Round 6)"}}
     path = {"t_roof_ms": m["t_roof_ms"], "frac": m["t_roof_ms"] / ms_step,
             "hbm_only_ms": m["t_hbm_ms"], "hbm_frac": m["t_hbm_ms"] / ms_step,
             "hbm_frac_rule": "bytes this implementation's kernels must move (each launch's "
