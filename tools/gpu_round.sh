@@ -14,7 +14,7 @@ if [ -z "${SKIP_TESTS:-}" ]; then
     > gpurun_out/pytest_gpu.log 2>&1
   rc=$?; tail -3 gpurun_out/pytest_gpu.log; [ $rc -eq 0 ] || exit $rc
 fi
-B="python3 bench.py --steps 3 --warmup 1 --cpu-baseline 0 --epe 0 --pair-check 0"
+B="python3 bench.py --steps 3 --warmup 1 --cpu-baseline 0 --epe 0 --pair-check 0 --extra-configs="
 for ctr in FETCH_SIZE WRITE_SIZE; do
   timeout -k 10 300 rocprofv3 --pmc $ctr --kernel-trace --output-format csv -d gpurun_out/traffic/c2_$ctr -o run -- $B \
     > gpurun_out/traffic/c2_$ctr.log 2>&1
@@ -26,11 +26,12 @@ CONFIGS="c3 c4 c5" bash tools/gpu_traffic_bf16.sh || exit $?
 for c in c3 c4 c5; do python3 tools/traffic_merge.py $c gpurun_out/traffic_$c.json; done
 cp profiles/hbm_traffic.json gpurun_out/traffic/hbm_traffic_merged.json
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_$TAG -o run -- \
-  python3 bench.py --steps 5 --warmup 2 --cpu-baseline 0 --epe 0 --pair-check 0 > gpurun_out/prof_$TAG.json 2> gpurun_out/prof_$TAG.err
+  python3 bench.py --steps 5 --warmup 2 --cpu-baseline 0 --epe 0 --pair-check 0 --extra-configs= > gpurun_out/prof_$TAG.json 2> gpurun_out/prof_$TAG.err
 rc=$?; echo "prof rc=$rc"; [ $rc -eq 0 ] || exit $rc
 python3 tools/trace_report.py gpurun_out/prof_$TAG > gpurun_out/prof_${TAG}_forward.txt; head -8 gpurun_out/prof_${TAG}_forward.txt
 for c in c2 c3 c4 c5; do
   timeout -k 10 500 python3 bench.py --config $c --steps 20 --warmup 5 --breakdown 1 --cpu-baseline $([ $c = c2 ] && echo 1 || echo 0) \
+    $([ $c = c2 ] || echo --extra-configs=) \
     > gpurun_out/bench_${TAG}_$c.json 2> gpurun_out/bench_${TAG}_$c.err
   rc=$?; echo "bench $c rc=$rc"; [ $rc -eq 0 ] || { tail -5 gpurun_out/bench_${TAG}_$c.err; exit $rc; }
   python3 -c "import json; d=json.load(open('gpurun_out/bench_${TAG}_$c.json')); r=d['roofline']; print('$c', round(d['value'],1), round(d['ms_per_step'],2), r['kernel'], round(r['frac'],3), r['traffic'], round(d['path_roofline']['frac'],3))"

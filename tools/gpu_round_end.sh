@@ -12,7 +12,7 @@ timeout -k 10 300 python3 -c "import __graft_entry__ as g; g.smoke()" > gpurun_o
 tail -1 gpurun_out/smoke_$T.log
 timeout -k 10 400 python3 bench.py > gpurun_out/bench_${T}_c2.json 2> gpurun_out/bench_${T}_c2.err || { tail -5 gpurun_out/bench_${T}_c2.err; exit 1; }
 for c in c3 c4; do
-  timeout -k 10 300 python3 bench.py --config $c --steps 20 --warmup 5 --breakdown 1 --cpu-baseline 0 > gpurun_out/bench_${T}_$c.json 2> gpurun_out/bench_${T}_$c.err || { tail -5 gpurun_out/bench_${T}_$c.err; exit 1; }
+  timeout -k 10 300 python3 bench.py --config $c --steps 20 --warmup 5 --breakdown 1 --cpu-baseline 0 --extra-configs= > gpurun_out/bench_${T}_$c.json 2> gpurun_out/bench_${T}_$c.err || { tail -5 gpurun_out/bench_${T}_$c.err; exit 1; }
 done
-timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_${T}_c2 -o run -- python3 bench.py --steps 5 --warmup 2 --cpu-baseline 0 --epe 0 --pair-check 0 > gpurun_out/prof_${T}_c2.json 2> gpurun_out/prof_${T}_c2.err || exit 1
+timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_${T}_c2 -o run -- python3 bench.py --steps 5 --warmup 2 --cpu-baseline 0 --epe 0 --pair-check 0 --extra-configs= > gpurun_out/prof_${T}_c2.json 2> gpurun_out/prof_${T}_c2.err || exit 1
 python3 tools/trace_report.py gpurun_out/prof_${T}_c2 > gpurun_out/prof_${T}_c2_forward.txt

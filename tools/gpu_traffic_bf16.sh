@@ -7,7 +7,7 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 mkdir -p gpurun_out/traffic_bf16
 for c in ${CONFIGS:-c3 c4}; do
-  B="python3 bench.py --config $c --steps 2 --warmup 1 --cpu-baseline 0 --epe 0 --pair-check 0"
+  B="python3 bench.py --config $c --steps 2 --warmup 1 --cpu-baseline 0 --epe 0 --pair-check 0 --extra-configs="
   for ctr in FETCH_SIZE WRITE_SIZE; do
     timeout -k 10 300 rocprofv3 --pmc $ctr --kernel-trace --output-format csv -d gpurun_out/traffic_bf16/${c}_$ctr -o run -- $B \
       > gpurun_out/traffic_bf16/${c}_$ctr.log 2>&1
