@@ -162,6 +162,11 @@ int lea_conv3d_wino2p_set_wpre(int on);
  * blocks.  Same packed weights (every per-lane copy is packed). */
 int lea_conv3d_wino44_set(int on);
 
+/* 1 = the F(4,3) x F(4,3) tile reads U itself from its per-lane copy (the packer applies both
+ * G factors' matrices: 54 floats per cout, channel and x-half; the steps form no U), 0 = the
+ * G_W' g copy with G_D' applied per step.  Bit-identical; both copies are always packed. */
+int lea_conv3d_wino44_set_upre(int on);
+
 /* 1 (default) = the Winograd engines' buffer-addressed epilogue where the shape allows
  * it (W % 4 == 0, 16-B aligned output / residual; residual loads issued together, the
  * next chunk's DMA waited for without the stores), 0 = the per-group epilogue. */

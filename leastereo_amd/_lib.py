@@ -106,6 +106,7 @@ SIGNATURES = {
     "lea_conv3d_wino2_set_pipeline": (_i, [_i]),
     "lea_conv3d_wino2p_set_wpre": (_i, [_i]),
     "lea_conv3d_wino44_set": (_i, [_i]),
+    "lea_conv3d_wino44_set_upre": (_i, [_i]),
     "lea_conv3d_wino_set_epi_buf": (_i, [_i]),
     "lea_conv3d_set_rs_gather": (_i, [_i]),
     "lea_conv1x1_set_vector": (_i, [_i]),
@@ -182,6 +183,7 @@ TUNING_ENV = {"LEASTEREO_WINO2_WALK": "lea_conv3d_wino2_set_walk",
               "LEASTEREO_WINO2_PIPE": "lea_conv3d_wino2_set_pipeline",
               "LEASTEREO_WINO2P_WPRE": "lea_conv3d_wino2p_set_wpre",
               "LEASTEREO_WINO44": "lea_conv3d_wino44_set",
+              "LEASTEREO_WINO44_UPRE": "lea_conv3d_wino44_set_upre",
               "LEASTEREO_EPI_BUF": "lea_conv3d_wino_set_epi_buf",
               "LEASTEREO_RS_GATHER": "lea_conv3d_set_rs_gather",
               "LEASTEREO_1X1_VEC": "lea_conv1x1_set_vector",

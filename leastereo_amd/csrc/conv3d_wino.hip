@@ -933,10 +933,12 @@ extern "C" int lea_conv3d_wino_pack_weights(const float* w, float* packed, int c
                                                            cin / wino::CIN_B, lanew);
     }
   }
-  if (wino::has_l44(cout)) {  // the F(4,3) x F(4,3) tile's per-lane copy
-    const long long n44 = wino::lane44_floats(cout, cin);
+  if (wino::has_l44(cout)) {  // the F(4,3) x F(4,3) tile's per-lane copies (G_W' g, then U)
+    const long long n44 = wino::lane44_g_floats(cout, cin), n44u = wino::lane44_floats(cout, cin) - n44;
     const int g4 = (int)std::min<long long>((n44 + 255) / 256, 4096);
     wino::pack_wino44_lane_kernel<<<g4, 256, 0, st>>>(w, packed + l44, cout, cin, cin / wino::CIN_B, n44);
+    const int g5 = (int)std::min<long long>((n44u + 255) / 256, 4096);
+    wino::pack_wino44_lane_u_kernel<<<g5, 256, 0, st>>>(w, packed + l44 + n44, cout, cin, cin / wino::CIN_B, n44u);
   }
   if (wino::has_u22(cout)) {  // the F(2,3) x F(2,3) tile's U
     const long long u = total - uoff;
@@ -1003,6 +1005,13 @@ extern "C" int lea_conv3d_wino44_set(int on) {
   clear_error();
   LEA_CHECK_ARG(on >= 0 && on <= 3, "lea_conv3d_wino44_set: on=%d", on);
   wino::g_w44 = on;
+  return 0;
+}
+
+extern "C" int lea_conv3d_wino44_set_upre(int on) {
+  clear_error();
+  LEA_CHECK_ARG(on == 0 || on == 1, "lea_conv3d_wino44_set_upre: on=%d", on);
+  wino::g_w44u = on;
   return 0;
 }
 

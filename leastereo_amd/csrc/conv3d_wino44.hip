@@ -52,6 +52,7 @@ constexpr int CB0 = 1, CB1 = CB0 + 1024 + 2, CB2 = CB1 + 1024 + 30, CB3 = CB2 + 
 constexpr int XS = (CB3 + 1024 + 3) / 4 * 4;   // floats per halo buffer
 constexpr int GS = 40, XHS = 20, TRS = 320, TCS = 1284, TS = 4 * TCS;
 constexpr int KGL = 28;                        // per-lane weights per (cout, channel): [kh][kd][x 3] + pad
+constexpr int KGU = 56;                        // UPRE: U = G_D' G_W' g, [kh][x 3][e 6] + pad
 constexpr int NST = 8;                         // buffer stores per epilogue and lane
 static_assert(CB1 % 64 == 3 && CB2 % 64 == 33 && CB3 % 64 == 35, "V-pass bank map");
 static_assert(BLK16 <= 4 * 64 && 4 * 256 <= CB1 - CB0, "whole pieces per channel region");
@@ -88,7 +89,43 @@ __global__ void pack_wino44_lane_kernel(const float* __restrict__ w, float* __re
   }
 }
 
-long long lane44_floats(int cout, int cin) { return (long long)((cout + 31) / 32) * (cin / CIN_B) * 4 * 64 * w44::KGL; }
+// the UPRE copy (r06): entry k = kh * 18 + x3 * 6 + e of U = G_D' (G_W' g) -- the kernel's own
+// transform (gw4 along W, then along D), so the same bits -- after the G_W' g copy
+__global__ void pack_wino44_lane_u_kernel(const float* __restrict__ w, float* __restrict__ out, int cout, int cin,
+                                          int nchunks, long long total) {
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
+       i += (long long)gridDim.x * blockDim.x) {
+    long long q = i;
+    const int e = (int)(q % (64 * w44::KGU)); q /= 64 * w44::KGU;
+    const int k = (e / 256) * 4 + (e & 3), ln = (e & 255) >> 2;
+    const int xh = (int)(q % 2); q /= 2;
+    const int wc = (int)(q % 2); q /= 2;
+    const int ch = (int)(q % nchunks);
+    const int cb = (int)(q / nchunks);
+    const int co = cb * 32 + 16 * wc + (ln & 15), c = ch * CIN_B + (ln >> 4);
+    float v = 0.f;
+    if (k < 54 && co < cout && c < cin) {
+      const int kh = k / 18, x = 3 * xh + (k % 18) / 6, ed = k % 6;
+      float gwx[3];
+      for (int kd = 0; kd < 3; ++kd) {
+        const float* g = w + (((long long)co * cin + c) * 9 + kd * 3 + kh) * 3;
+        const float s = g[0] + g[2], s4 = fmaf(4.f, g[2], g[0]);
+        const float u[6] = {g[0], s + g[1], s - g[1], fmaf(2.f, g[1], s4), fmaf(-2.f, g[1], s4), g[2]};
+        gwx[kd] = u[x];
+      }
+      const float g0 = gwx[0], g1 = gwx[1], g2 = gwx[2];
+      const float s = g0 + g2, s4 = fmaf(4.f, g2, g0);
+      const float u[6] = {g0, s + g1, s - g1, fmaf(2.f, g1, s4), fmaf(-2.f, g1, s4), g2};
+      v = u[ed];
+    }
+    out[i] = v;
+  }
+}
+
+long long lane44_g_floats(int cout, int cin) { return (long long)((cout + 31) / 32) * (cin / CIN_B) * 4 * 64 * w44::KGL; }
+long long lane44_floats(int cout, int cin) {
+  return lane44_g_floats(cout, cin) + (long long)((cout + 31) / 32) * (cin / CIN_B) * 4 * 64 * w44::KGU;
+}
 
 namespace {
 // F(4,3): B^T x (6 -> 6), G' g (3 -> 6, no row factors), A^T with the factors (6 -> 4)
@@ -116,6 +153,9 @@ __device__ __forceinline__ void at6(const float a0, const float a1, const float 
 }
 }  // namespace
 
+// UPRE (lea_conv3d_wino44_set_upre): the per-lane weights are U itself (the packer's second
+// copy), so the step forms no U: 54 fewer VALU per item, 7 more 16-byte loads, 28 more VGPRs
+template <bool UPRE>
 __global__ __launch_bounds__(256, 2) void conv3d_wino44_kernel(const ConvArgs a) {
   using namespace w44;
   constexpr int NX = 3, NE = 6;  // this wave's W points x the D points
@@ -149,7 +189,9 @@ __global__ __launch_bounds__(256, 2) void conv3d_wino44_kernel(const ConvArgs a)
   const unsigned nrec = (unsigned)(HW * a.D) * 4u;
   const long long cvol = (long long)HW * a.D;
   // per-lane weights: this kernel's section of the packed weights at a.uoff (the host's l44_offset)
-  const float* wl = a.wp + a.uoff + ((long long)(cob * nchunks) * 4 + wc * 2 + xh) * 64 * KGL + lane * 4;
+  constexpr int GL = UPRE ? KGU : KGL;
+  const float* wl = a.wp + a.uoff + (UPRE ? (long long)a.ncob * nchunks * 4 * 64 * KGL : 0LL) +
+                    ((long long)(cob * nchunks) * 4 + wc * 2 + xh) * 64 * GL + lane * 4;
 
   // 16-byte halo pieces: piece = wave of every channel; block e16 = (plane, row, 16-byte column)
   const int e16 = 64 * wave + lane;
@@ -182,11 +224,11 @@ __global__ __launch_bounds__(256, 2) void conv3d_wino44_kernel(const ConvArgs a)
       dma_dwordx4_buf(rs, vo, lds0 + 4 * (unsigned)(buf * XS + cbs[ci] + wave * 256));
     }
   };
-  float4 gw[KGL / 4];  // this lane's G_W' g of the current chunk: [kh][kd][x 3]
+  float4 gw[GL / 4];  // this lane's G_W' g of the current chunk: [kh][kd][x 3] (UPRE: U, [kh][x 3][e 6])
   auto load_g = [&](int ch) {
-    const float4* src = reinterpret_cast<const float4*>(wl + (long long)ch * 4 * 64 * KGL);
+    const float4* src = reinterpret_cast<const float4*>(wl + (long long)ch * 4 * 64 * GL);
 #pragma unroll
-    for (int k = 0; k < KGL / 4; ++k) gw[k] = src[64 * k];
+    for (int k = 0; k < GL / 4; ++k) gw[k] = src[64 * k];
   };
   // V-pass unit of thread t: W group vg, channel vc, halo row vr, x-half vxh (wave-uniform)
   const int vg = (tid & 3) | (((tid >> 3) & 1) << 2);
@@ -385,17 +427,25 @@ __global__ __launch_bounds__(256, 2) void conv3d_wino44_kernel(const ConvArgs a)
         for (int x = 0; x < NX; ++x)
   #pragma unroll
           for (int e = 0; e < NE; ++e) T.v[x][e] = e18[x * 6 + e];
-        const float* g = reinterpret_cast<const float*>(gw) + kh * 9;
+        if constexpr (UPRE) {
+          const float* u = reinterpret_cast<const float*>(gw) + kh * 18;
   #pragma unroll
-        for (int x = 0; x < NX; ++x) {  // G_D' along the kernel depth (gw4)
-          const float g0 = g[x], g1 = g[3 + x], g2 = g[6 + x];
-          const float s = g0 + g2, s4 = fmaf(4.f, g2, g0);
-          T.u[x][0] = g0;
-          T.u[x][1] = s + g1;
-          T.u[x][2] = s - g1;
-          T.u[x][3] = fmaf(2.f, g1, s4);
-          T.u[x][4] = fmaf(-2.f, g1, s4);
-          T.u[x][5] = g2;
+          for (int x = 0; x < NX; ++x)
+  #pragma unroll
+            for (int e = 0; e < NE; ++e) T.u[x][e] = u[x * 6 + e];
+        } else {
+          const float* g = reinterpret_cast<const float*>(gw) + kh * 9;
+  #pragma unroll
+          for (int x = 0; x < NX; ++x) {  // G_D' along the kernel depth (gw4)
+            const float g0 = g[x], g1 = g[3 + x], g2 = g[6 + x];
+            const float s = g0 + g2, s4 = fmaf(4.f, g2, g0);
+            T.u[x][0] = g0;
+            T.u[x][1] = s + g1;
+            T.u[x][2] = s - g1;
+            T.u[x][3] = fmaf(2.f, g1, s4);
+            T.u[x][4] = fmaf(-2.f, g1, s4);
+            T.u[x][5] = g2;
+          }
         }
       };
       auto mfmas = [&](const Xf& T) {
@@ -449,6 +499,7 @@ __global__ __launch_bounds__(256, 2) void conv3d_wino44_kernel(const ConvArgs a)
 }
 
 int g_w44 = 1;  // lea_conv3d_wino44_set (r06 default: -9.5 % on its layers, profiles/r06_w44_ab.txt)
+int g_w44u = 0;  // lea_conv3d_wino44_set_upre
 
 int run44(ConvArgs a, int B, int spw, hipStream_t st) {
   a.ncob = (a.cout + 31) / 32;
@@ -459,7 +510,10 @@ int run44(ConvArgs a, int B, int spw, hipStream_t st) {
   const long long n_ = (long long)a.ntiles * ((a.ndz + a.spw - 1) / a.spw) * B * a.ncob;
   LEA_CHECK_ARG(n_ < (1LL << 31), "lea_conv3d(wino44): grid too large");
   a.nblk = (int)n_;
-  conv3d_wino44_kernel<<<dim3((unsigned)n_), 256, 0, st>>>(a);
+  if (g_w44u)
+    conv3d_wino44_kernel<true><<<dim3((unsigned)n_), 256, 0, st>>>(a);
+  else
+    conv3d_wino44_kernel<false><<<dim3((unsigned)n_), 256, 0, st>>>(a);
   return launch_status("lea_conv3d(wino44)");
 }
 

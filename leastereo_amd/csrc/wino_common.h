@@ -149,9 +149,13 @@ extern int g_wpre;  // lea_conv3d_wino2p_set_wpre
 // F(4,3) x F(4,3) tile (conv3d_wino44.hip, r06): the layers of the pipelined W x D kernel when
 // g_w44 (lea_conv3d_wino44_set); its per-lane weight section (the last of lane_weights_floats)
 extern int g_w44;
+extern int g_w44u;  // lea_conv3d_wino44_set_upre
 long long lane44_floats(int cout, int cin);
+long long lane44_g_floats(int cout, int cin);  // the G_W' g part (the U copy follows)
 __global__ void pack_wino44_lane_kernel(const float* __restrict__ w, float* __restrict__ out, int cout, int cin,
                                         int nchunks, long long total);
+__global__ void pack_wino44_lane_u_kernel(const float* __restrict__ w, float* __restrict__ out, int cout, int cin,
+                                          int nchunks, long long total);
 int run44(ConvArgs a, int B, int spw, hipStream_t st);
 const char* name2(const Plan2& p, bool cv);
 

@@ -32,7 +32,9 @@ def short(n):
     """Our kernel name (lea_*_kernel_name) of a rocprof name: 'fn<args>' or plain 'fn'."""
     m = re.search(r"lea::(?:\w+::)*(\w+)<([^>]*)>", n)
     if m:
-        return f"{m.group(1)}<{m.group(2)}>"
+        # a bool-only template (conv3d_wino2p_kernel<true>, conv3d_wino44_kernel<false>: code
+        # variants of one kernel the library names without arguments)
+        return m.group(1) if m.group(2) in ("true", "false") else f"{m.group(1)}<{m.group(2)}>"
     m = re.search(r"lea::(?:\w+::)*(\w+)\(", n)
     return m.group(1) if m else None
 
