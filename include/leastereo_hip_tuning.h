@@ -167,6 +167,11 @@ int lea_conv3d_wino44_set(int on);
  * G_W' g copy with G_D' applied per step.  Bit-identical; both copies are always packed. */
 int lea_conv3d_wino44_set_upre(int on);
 
+/* Item-body schedule of the F(4,3) x F(4,3) tile (r06 A/B): 0 = the default (V-pass after the
+ * first step's MFMAs, iglp_opt(0)), 1 = the V-pass issued first, 2 = 0 without iglp_opt,
+ * 3 = 1 with an explicit one-MFMA / three-VALU interleave.  Bit-identical. */
+int lea_conv3d_wino44_set_sched(int s);
+
 /* 1 (default) = the Winograd engines' buffer-addressed epilogue where the shape allows
  * it (W % 4 == 0, 16-B aligned output / residual; residual loads issued together, the
  * next chunk's DMA waited for without the stores), 0 = the per-group epilogue. */

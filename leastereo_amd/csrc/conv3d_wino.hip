@@ -1008,6 +1008,13 @@ extern "C" int lea_conv3d_wino44_set(int on) {
   return 0;
 }
 
+extern "C" int lea_conv3d_wino44_set_sched(int s) {
+  clear_error();
+  LEA_CHECK_ARG(s >= 0 && s <= 3, "lea_conv3d_wino44_set_sched: %d", s);
+  wino::g_w44s = s;
+  return 0;
+}
+
 extern "C" int lea_conv3d_wino44_set_upre(int on) {
   clear_error();
   LEA_CHECK_ARG(on == 0 || on == 1, "lea_conv3d_wino44_set_upre: on=%d", on);

@@ -155,7 +155,11 @@ __device__ __forceinline__ void at6(const float a0, const float a1, const float 
 
 // UPRE (lea_conv3d_wino44_set_upre): the per-lane weights are U itself (the packer's second
 // copy), so the step forms no U: 54 fewer VALU per item, 7 more 16-byte loads, 28 more VGPRs
-template <bool UPRE>
+// SCHED (lea_conv3d_wino44_set_sched, r06 A/B): 0 = the body below under iglp_opt(0); 1 = the
+// V-pass issued first (its LDS reads at the item head, its VALU free to spread over all three
+// steps); 2 = as 0 without iglp_opt; 3 = as 1 with an explicit interleave (sched_group_barrier:
+// one MFMA, three VALU, repeated)
+template <bool UPRE, int SCHED>
 __global__ __launch_bounds__(256, 2) void conv3d_wino44_kernel(const ConvArgs a) {
   using namespace w44;
   constexpr int NX = 3, NE = 6;  // this wave's W points x the D points
@@ -457,7 +461,8 @@ __global__ __launch_bounds__(256, 2) void conv3d_wino44_kernel(const ConvArgs a)
       };
       Raw raw[2];
       Xf xf[2];
-      __builtin_amdgcn_iglp_opt(0);
+      if constexpr (SCHED == 0 || SCHED == 1) __builtin_amdgcn_iglp_opt(0);
+      if constexpr (SCHED == 1 || SCHED == 3) vpass(XHC, (it + 1) & 1);
       load_step(0, raw[0]);
       load_step(1, raw[1]);
       xform(0, raw[0], xf[0]);
@@ -467,11 +472,18 @@ __global__ __launch_bounds__(256, 2) void conv3d_wino44_kernel(const ConvArgs a)
       load_step(2, raw[0]);
       xform(1, raw[1], xf[1]);
       mfmas(xf[0]);
-      vpass(XHC, (it + 1) & 1);
+      if constexpr (SCHED == 0 || SCHED == 2) vpass(XHC, (it + 1) & 1);
       xform(2, raw[0], xf[0]);
       load_g(it + 1 < nitems ? (ich + 1 == nchunks ? 0 : ich + 1) : ich);
       mfmas(xf[1]);
       mfmas(xf[0]);
+      if constexpr (SCHED == 3) {
+#pragma unroll
+        for (int k = 0; k < 54; ++k) {
+          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // one MFMA
+          __builtin_amdgcn_sched_group_barrier(0x002, 3, 0);  // three VALU
+        }
+      }
       after_epi = false;
       if (ich == nchunks - 1) {
         epilogue_xh(XHC, (pz0 + iqd) * TD, tvb + (it & 1) * TS, halo + ((it + 1) & 1) * XS);
@@ -500,6 +512,7 @@ __global__ __launch_bounds__(256, 2) void conv3d_wino44_kernel(const ConvArgs a)
 
 int g_w44 = 1;  // lea_conv3d_wino44_set (r06 default: -9.5 % on its layers, profiles/r06_w44_ab.txt)
 int g_w44u = 0;  // lea_conv3d_wino44_set_upre
+int g_w44s = 0;  // lea_conv3d_wino44_set_sched
 
 int run44(ConvArgs a, int B, int spw, hipStream_t st) {
   a.ncob = (a.cout + 31) / 32;
@@ -510,10 +523,17 @@ int run44(ConvArgs a, int B, int spw, hipStream_t st) {
   const long long n_ = (long long)a.ntiles * ((a.ndz + a.spw - 1) / a.spw) * B * a.ncob;
   LEA_CHECK_ARG(n_ < (1LL << 31), "lea_conv3d(wino44): grid too large");
   a.nblk = (int)n_;
+  const dim3 grid((unsigned)n_);
   if (g_w44u)
-    conv3d_wino44_kernel<true><<<dim3((unsigned)n_), 256, 0, st>>>(a);
+    conv3d_wino44_kernel<true, 0><<<grid, 256, 0, st>>>(a);
+  else if (g_w44s == 1)
+    conv3d_wino44_kernel<false, 1><<<grid, 256, 0, st>>>(a);
+  else if (g_w44s == 2)
+    conv3d_wino44_kernel<false, 2><<<grid, 256, 0, st>>>(a);
+  else if (g_w44s == 3)
+    conv3d_wino44_kernel<false, 3><<<grid, 256, 0, st>>>(a);
   else
-    conv3d_wino44_kernel<false><<<dim3((unsigned)n_), 256, 0, st>>>(a);
+    conv3d_wino44_kernel<false, 0><<<grid, 256, 0, st>>>(a);
   return launch_status("lea_conv3d(wino44)");
 }
 

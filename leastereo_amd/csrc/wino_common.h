@@ -150,6 +150,7 @@ extern int g_wpre;  // lea_conv3d_wino2p_set_wpre
 // g_w44 (lea_conv3d_wino44_set); its per-lane weight section (the last of lane_weights_floats)
 extern int g_w44;
 extern int g_w44u;  // lea_conv3d_wino44_set_upre
+extern int g_w44s;  // lea_conv3d_wino44_set_sched
 long long lane44_floats(int cout, int cin);
 long long lane44_g_floats(int cout, int cin);  // the G_W' g part (the U copy follows)
 __global__ void pack_wino44_lane_kernel(const float* __restrict__ w, float* __restrict__ out, int cout, int cin,

@@ -28,13 +28,19 @@ def load(d, counter):
     return per, names
 
 
+# kernels the library names without their (code-variant) template arguments
+PLAIN = {"conv3d_wino44_kernel", "conv3d_wino2p_kernel"}
+
+
 def short(n):
     """Our kernel name (lea_*_kernel_name) of a rocprof name: 'fn<args>' or plain 'fn'."""
     m = re.search(r"lea::(?:\w+::)*(\w+)<([^>]*)>", n)
     if m:
         # a bool-only template (conv3d_wino2p_kernel<true>, conv3d_wino44_kernel<false>: code
         # variants of one kernel the library names without arguments)
-        return m.group(1) if m.group(2) in ("true", "false") else f"{m.group(1)}<{m.group(2)}>"
+        if m.group(1) in PLAIN or m.group(2) in ("true", "false"):
+            return m.group(1)
+        return f"{m.group(1)}<{m.group(2)}>"
     m = re.search(r"lea::(?:\w+::)*(\w+)\(", n)
     return m.group(1) if m else None
 
