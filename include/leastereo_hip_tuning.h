@@ -168,8 +168,8 @@ int lea_conv3d_wino44_set(int on);
 int lea_conv3d_wino44_set_upre(int on);
 
 /* Item-body schedule of the F(4,3) x F(4,3) tile (r06 A/B): 0 = the default (V-pass after the
- * first step's MFMAs, iglp_opt(0)), 1 = the V-pass issued first, 2 = 0 without iglp_opt,
- * 3 = 1 with an explicit one-MFMA / three-VALU interleave.  Bit-identical. */
+ * first step's MFMAs, iglp_opt(0)), 1 = the V-pass after the second step's MFMAs, 2 = 0 without
+ * iglp_opt, 3 = the V-pass after all MFMAs.  Bit-identical. */
 int lea_conv3d_wino44_set_sched(int s);
 
 /* 1 (default) = the Winograd engines' buffer-addressed epilogue where the shape allows

@@ -155,10 +155,11 @@ __device__ __forceinline__ void at6(const float a0, const float a1, const float 
 
 // UPRE (lea_conv3d_wino44_set_upre): the per-lane weights are U itself (the packer's second
 // copy), so the step forms no U: 54 fewer VALU per item, 7 more 16-byte loads, 28 more VGPRs
-// SCHED (lea_conv3d_wino44_set_sched, r06 A/B): 0 = the body below under iglp_opt(0); 1 = the
-// V-pass issued first (its LDS reads at the item head, its VALU free to spread over all three
-// steps); 2 = as 0 without iglp_opt; 3 = as 1 with an explicit interleave (sched_group_barrier:
-// one MFMA, three VALU, repeated)
+// SCHED (lea_conv3d_wino44_set_sched, r06 A/B, profiles/r06_w44_sched_ab*.txt): 0 = the body
+// below under iglp_opt(0) (the V-pass after the first step's MFMAs); 1 = the V-pass after the
+// second step's MFMAs; 2 = as 0 without iglp_opt; 3 = the V-pass after all MFMAs.  (Measured
+// and dropped: the V-pass issued first, +4 %; an explicit one-MFMA / three-VALU
+// sched_group_barrier interleave, +10 %.)
 template <bool UPRE, int SCHED>
 __global__ __launch_bounds__(256, 2) void conv3d_wino44_kernel(const ConvArgs a) {
   using namespace w44;
@@ -461,8 +462,7 @@ __global__ __launch_bounds__(256, 2) void conv3d_wino44_kernel(const ConvArgs a)
       };
       Raw raw[2];
       Xf xf[2];
-      if constexpr (SCHED == 0 || SCHED == 1) __builtin_amdgcn_iglp_opt(0);
-      if constexpr (SCHED == 1 || SCHED == 3) vpass(XHC, (it + 1) & 1);
+      if constexpr (SCHED != 2) __builtin_amdgcn_iglp_opt(0);
       load_step(0, raw[0]);
       load_step(1, raw[1]);
       xform(0, raw[0], xf[0]);
@@ -476,14 +476,9 @@ __global__ __launch_bounds__(256, 2) void conv3d_wino44_kernel(const ConvArgs a)
       xform(2, raw[0], xf[0]);
       load_g(it + 1 < nitems ? (ich + 1 == nchunks ? 0 : ich + 1) : ich);
       mfmas(xf[1]);
+      if constexpr (SCHED == 1) vpass(XHC, (it + 1) & 1);
       mfmas(xf[0]);
-      if constexpr (SCHED == 3) {
-#pragma unroll
-        for (int k = 0; k < 54; ++k) {
-          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // one MFMA
-          __builtin_amdgcn_sched_group_barrier(0x002, 3, 0);  // three VALU
-        }
-      }
+      if constexpr (SCHED == 3) vpass(XHC, (it + 1) & 1);
       after_epi = false;
       if (ich == nchunks - 1) {
         epilogue_xh(XHC, (pz0 + iqd) * TD, tvb + (it & 1) * TS, halo + ((it + 1) & 1) * XS);
