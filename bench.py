@@ -170,7 +170,7 @@ def independent_check_engines():
     fe = executor.FeatureExecutor
     saved = (fe.FUSED_STEM, fe.PAIR_S0)
     env = lambda var, default: int(os.environ.get(var) or default)  # noqa: E731
-    switches = (("lea_disparity_set_register_form", 0, "LEASTEREO_DISP_REG", 3),
+    switches = (("lea_disparity_set_register_form", 0, "LEASTEREO_DISP_REG", 4),
                 ("lea_conv2d_set_small", 0, "LEASTEREO_CONV2D_SMALL", 1),
                 ("lea_resample_set_mode", 2, "LEASTEREO_RESAMPLE_MODE", 0),
                 ("lea_tapsum_set_rows", 0, "LEASTEREO_TAPSUM_ROWS", 2))
@@ -463,7 +463,7 @@ def run_stub(args, info):
     for _ in range(args.steps):
         ts = time.perf_counter()
         torch.zeros(args.batch, 8, 8).add_(1.0)
-        step_ms.append((time.perf_counter() - ts) * 1e3 + info.rank)  # rank-tagged: order check
+        step_ms.append((time.perf_counter() - ts) * 1e3 + 10.0 * info.rank)  # rank-tagged: order check
     parallel.barrier()
     elapsed = parallel.max_over_ranks(time.perf_counter() - t0, torch.device("cpu"))
     per_rank = gather_step_stats(sorted(step_ms), torch.device("cpu"))

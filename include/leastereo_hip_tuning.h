@@ -78,7 +78,9 @@ int lea_conv2d_set_small(int on);
 /* lea_conv2d_kernel_name with the input channel count (the few-channel tile depends on it). */
 const char* lea_conv2d_kernel_name_cin(int B, int cin, int cout, int H, int W);
 
-/* Disparity regression: 3 (default, r06) = the three-row staged kernel (one workgroup of 768
+/* Disparity regression: 4 (default, r06) = form 3 (form 2 at D3 = 88) with D3 exponentials per
+ * pixel instead of maxdisp (x3 depth up-sampling: exp(m - u) as products of exp((m - v_k) / 3);
+ * within a few ulp per term of form 3, not bit-identical); 3 = the three-row staged kernel (one workgroup of 768
  * threads per three output rows: each raw source value loaded once; bit-identical to 2; D3 = 88
  * stays on 2); 2 (r05) = the row-staged kernel (a workgroup's two source
  * rows of every plane H-lerped into LDS, two passes over the planes, compile-time depth axis,
@@ -171,6 +173,12 @@ int lea_conv3d_wino44_set_upre(int on);
  * first step's MFMAs, iglp_opt(0)), 1 = the V-pass after the second step's MFMAs, 2 = 0 without
  * iglp_opt, 3 = the V-pass after all MFMAs.  Bit-identical. */
 int lea_conv3d_wino44_set_sched(int s);
+
+/* The F(4,3) x F(4,3) tile's workgroup order: 0 = linear (cout block, depth group, tile),
+ * g in 1..16 = groups of g x g tiles x max(1, 64 / (cout blocks g^2)) depth groups,
+ * consecutive per XCD (L2 sharing of the halo), -1 (default) = 16 on grids of >= 8192
+ * workgroups, else 0.  Bit-identical. */
+int lea_conv3d_wino44_set_group(int g);
 
 /* 1 (default) = the Winograd engines' buffer-addressed epilogue where the shape allows
  * it (W % 4 == 0, 16-B aligned output / residual; residual loads issued together, the

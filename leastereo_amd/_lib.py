@@ -108,6 +108,7 @@ SIGNATURES = {
     "lea_conv3d_wino44_set": (_i, [_i]),
     "lea_conv3d_wino44_set_upre": (_i, [_i]),
     "lea_conv3d_wino44_set_sched": (_i, [_i]),
+    "lea_conv3d_wino44_set_group": (_i, [_i]),
     "lea_conv3d_wino_set_epi_buf": (_i, [_i]),
     "lea_conv3d_set_rs_gather": (_i, [_i]),
     "lea_conv1x1_set_vector": (_i, [_i]),

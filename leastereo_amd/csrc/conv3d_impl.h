@@ -81,6 +81,7 @@ struct ConvArgs {
   long long y2bs;
   int csplit;
   long long uoff;          // F(2,3) x F(2,3) tile (conv3d_wino22.hip): U section of the packed weights
+  int grp;                 // F(4,3) x F(4,3) tile: block order (0 = linear; g = groups of g x g tiles)
 };
 
 // KD = kernel depth: KS for the 3D convs, 1 for the feature net's 2D 3x3 convs

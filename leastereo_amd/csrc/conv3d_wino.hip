@@ -1008,6 +1008,13 @@ extern "C" int lea_conv3d_wino44_set(int on) {
   return 0;
 }
 
+extern "C" int lea_conv3d_wino44_set_group(int g) {
+  clear_error();
+  LEA_CHECK_ARG(g >= -1 && g <= 16, "lea_conv3d_wino44_set_group: %d", g);
+  wino::g_w44g = g;
+  return 0;
+}
+
 extern "C" int lea_conv3d_wino44_set_sched(int s) {
   clear_error();
   LEA_CHECK_ARG(s >= 0 && s <= 3, "lea_conv3d_wino44_set_sched: %d", s);

@@ -179,13 +179,46 @@ __global__ __launch_bounds__(256, 2) void conv3d_wino44_kernel(const ConvArgs a)
   const int lin = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + idx;
   const int spw = a.spw > 0 ? a.spw : 1;
   const int ngz = (a.ndz + spw - 1) / spw;
-  const int cob = lin % a.ncob;
-  const int rest = lin / a.ncob;
-  const int gz = rest % ngz;
-  const int tile = (rest / ngz) % a.ntiles;
-  const int b = rest / (ngz * a.ntiles);
-  const int h0 = (tile / a.tiles_w) * TH;
-  const int w0 = (tile % a.tiles_w) * TW;
+  int cob, gz, th, tw, b;
+  if (a.grp == 0) {  // linear: cout block fastest, then depth group, then tile
+    cob = lin % a.ncob;
+    const int rest = lin / a.ncob;
+    gz = rest % ngz;
+    const int tile = (rest / ngz) % a.ntiles;
+    b = rest / (ngz * a.ntiles);
+    th = tile / a.tiles_w;
+    tw = tile % a.tiles_w;
+  } else {
+    // grouped: the ~64 workgroups an XCD holds at once (consecutive `lin`) cover a box of
+    // GZ depth groups x G tile rows x G tile columns x every cout block, so the halo rows,
+    // planes and columns neighbouring tiles share are fetched once into that XCD's L2.
+    // Edge groups are partial; all divisions are scalar.
+    const int G = a.grp, nth = a.ntiles / a.tiles_w, ntw = a.tiles_w;
+    const int GZ = max(1, 64 / (a.ncob * G * G));
+    const int per_b = a.ncob * ngz * a.ntiles;
+    b = lin / per_b;
+    int r = lin - b * per_b;
+    const int slab = a.ncob * GZ * a.ntiles;
+    const int i = r / slab;
+    r -= i * slab;
+    const int cz = min(GZ, ngz - i * GZ);
+    const int rowg = a.ncob * cz * G * ntw;
+    const int j = r / rowg;
+    r -= j * rowg;
+    const int ch = min(G, nth - j * G);
+    const int cellg = a.ncob * cz * ch * G;
+    const int k = r / cellg;
+    r -= k * cellg;
+    const int cw = min(G, ntw - k * G);
+    cob = r % a.ncob;
+    r /= a.ncob;
+    tw = k * G + r % cw;
+    r /= cw;
+    th = j * G + r % ch;
+    gz = i * GZ + r / ch;
+  }
+  const int h0 = th * TH;
+  const int w0 = tw * TW;
   const int pz0 = gz * spw, nquads = min(spw, a.ndz - pz0);
   const int co0 = cob * 32;
   const int nchunks = a.cin / CIN_B;
@@ -508,6 +541,7 @@ __global__ __launch_bounds__(256, 2) void conv3d_wino44_kernel(const ConvArgs a)
 int g_w44 = 1;  // lea_conv3d_wino44_set (r06 default: -9.5 % on its layers, profiles/r06_w44_ab.txt)
 int g_w44u = 0;  // lea_conv3d_wino44_set_upre
 int g_w44s = 0;  // lea_conv3d_wino44_set_sched
+int g_w44g = -1;  // lea_conv3d_wino44_set_group (-1: auto)
 
 int run44(ConvArgs a, int B, int spw, hipStream_t st) {
   a.ncob = (a.cout + 31) / 32;
@@ -518,6 +552,10 @@ int run44(ConvArgs a, int B, int spw, hipStream_t st) {
   const long long n_ = (long long)a.ntiles * ((a.ndz + a.spw - 1) / a.spw) * B * a.ncob;
   LEA_CHECK_ARG(n_ < (1LL << 31), "lea_conv3d(wino44): grid too large");
   a.nblk = (int)n_;
+  // auto: 16 x 16-tile groups on the large grids (conv1/2, stem1: HBM traffic -37 / -33 %, time
+  // unchanged, profiles/r06_w44_group_traffic.txt), linear on the small ones (whose whole grid
+  // fits the L2s; grouped +1-2 %, r06_w44_group_ab.txt)
+  a.grp = g_w44g >= 0 ? g_w44g : (n_ >= 8192 ? 16 : 0);
   const dim3 grid((unsigned)n_);
   if (g_w44u)
     conv3d_wino44_kernel<true, 0><<<grid, 256, 0, st>>>(a);

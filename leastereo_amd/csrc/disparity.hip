@@ -188,7 +188,54 @@ __global__ __launch_bounds__(kDispThreads) void disparity_reg_f32(const float* _
 // depth axis and softmin are the register form's.
 constexpr int kDispCols = 96;  // >= the source columns of 256 outputs at x3 (88), + slack
 
-template <int D3, int MD, bool FAST>
+// FACT (r06, form 4): the per-pixel phase with D3 exponentials instead of MD.  x3 up-sampling
+// along D with align_corners=False puts od = 3k + 1 on plane k and od = 3k, 3k + 2 a third of
+// the way towards planes k - 1, k + 1 (clamped at the ends), so with F_k = exp((m - v_k) / 3):
+// exp(m - u) = F_{k-1} F_k^2,  F_k^3,  F_k^2 F_{k+1}, summed in the same od order.  The kernel
+// is VALU-bound on the exponentials; rolled loops keep it at 32-49 VGPRs.  Not bit-identical
+// to the per-od exponentials (a few ulp per term; the oracle bars).
+template <int D3, int MD, bool FAST, class Plane>
+__device__ __forceinline__ float softmin_fact(const Plane& plane) {
+#pragma clang fp contract(off)
+  static_assert(MD == 3 * D3, "x3 depth up-sampling");
+  // a plain select (no NaN in the planes): fminf's NaN rule let the vectoriser split this loop
+  // into per-pair NaN tests and divergent branches
+  float m = plane(0);
+#pragma unroll 8
+  for (int dd = 1; dd < D3; ++dd) {
+    const float v = plane(dd);
+    m = v < m ? v : m;
+  }
+  auto fk = [&](int dd) {
+    if constexpr (FAST)  // __expf's exp2(x log2 e) with the 1/3 folded into its multiplier
+      return __builtin_amdgcn_exp2f((m - plane(dd)) * (0x1.715476p+0f / 3.f));
+    else
+      return exp_noovf((m - plane(dd)) * 0x1.555556p-2f);
+  };
+  float s = 0.f, t = 0.f;
+  float fp = fk(0), fc = fp;  // F_{k-1}, F_k
+  float od = 0.f;             // 3k (exact in float)
+#pragma unroll 4
+  for (int k = 0; k < D3; ++k) {
+    const float fn = k + 1 < D3 ? fk(k + 1) : fc;
+    const float f2 = fc * fc;
+    const float e1 = f2 * fc;
+    const float e0 = k == 0 ? e1 : fp * f2;
+    const float e2 = k + 1 < D3 ? f2 * fn : e1;
+    s += e0;
+    t += od * e0;
+    s += e1;
+    t += (od + 1.f) * e1;
+    s += e2;
+    t += (od + 2.f) * e2;
+    od += 3.f;
+    fp = fc;
+    fc = fn;
+  }
+  return t / s;
+}
+
+template <int D3, int MD, bool FAST, bool FACT>
 __global__ __launch_bounds__(kDispThreads, 4) void disparity_rows_f32(const float* __restrict__ cost,
                                                                    float* __restrict__ disp, int H3, int W3,
                                                                    float rh, float rw) {
@@ -219,6 +266,11 @@ __global__ __launch_bounds__(kDispThreads, 4) void disparity_rows_f32(const floa
   const AxisW aw = src_axis(rw, ow, W3, Wo);
   const int j0 = min(aw.i0 - c_lo, kDispCols - 1), j1 = min(aw.i1 - c_lo, kDispCols - 1);
   auto plane = [&](int dd) { return aw.l0 * hl[dd * kDispCols + j0] + aw.l1 * hl[dd * kDispCols + j1]; };
+  if constexpr (FACT) {
+    const float r = softmin_fact<D3, MD, FAST>(plane);
+    disp[((long long)b * Ho + oh) * Wo + ow] = over ? __builtin_nanf("") : r;
+    return;
+  }
   // pass 1: the smallest plane value; pass 2 forms the planes again from LDS in depth order
   // (the register form kept all D3 of them live: two waves per SIMD)
   float m = plane(0);
@@ -260,7 +312,7 @@ __global__ __launch_bounds__(kDispThreads, 4) void disparity_rows_f32(const floa
 // workgroups, 24 waves per CU).
 constexpr int kDisp3Threads = 3 * kDispThreads;
 
-template <int D3, int MD, bool FAST>
+template <int D3, int MD, bool FAST, bool FACT>
 __global__ __launch_bounds__(kDisp3Threads) void disparity_rows3_f32(const float* __restrict__ cost,
                                                                    float* __restrict__ disp, int H3, int W3,
                                                                    float rh, float rw) {
@@ -306,6 +358,11 @@ __global__ __launch_bounds__(kDisp3Threads) void disparity_rows3_f32(const float
   const AxisW aw = src_axis(rw, ow, W3, Wo);
   const int j0 = min(aw.i0 - c_lo, kDispCols - 1), j1 = min(aw.i1 - c_lo, kDispCols - 1);
   auto plane = [&](int dd) { return aw.l0 * h[dd * kDispCols + j0] + aw.l1 * h[dd * kDispCols + j1]; };
+  if constexpr (FACT) {
+    const float r = softmin_fact<D3, MD, FAST>(plane);
+    disp[((long long)b * Ho + oh) * Wo + ow] = over ? __builtin_nanf("") : r;
+    return;
+  }
   float m = plane(0);
 #pragma unroll
   for (int dd = 1; dd < D3; ++dd) {
@@ -336,15 +393,16 @@ __global__ __launch_bounds__(kDisp3Threads) void disparity_rows3_f32(const float
 
 }  // namespace lea
 
-// lea_disparity_set_register_form: 3 (default, r06) = the three-row staged kernel (C2 69.5 -> 68.3,
+// lea_disparity_set_register_form: 4 (default, r06) = form 3 with D3 exponentials per pixel
+// instead of maxdisp (softmin_mean's FACT; the two-row kernel at D3 = 88 likewise), 3 = the three-row staged kernel (C2 69.5 -> 68.3,
 // C4 275.6 -> 266.4 us; not at D3 = 88), 2 (r05) = the row-staged kernel for the configured
 // (D3, maxdisp), 1 = the register kernel for them, 0 = the online-softmin kernel everywhere
 // (A/B and tests)
-static int g_disp_reg = 3;
+static int g_disp_reg = 4;
 extern "C" int lea_disparity_set_register_form(int on) {
   using namespace lea;
   clear_error();
-  LEA_CHECK_ARG(on >= 0 && on <= 3, "lea_disparity_set_register_form: %d", on);
+  LEA_CHECK_ARG(on >= 0 && on <= 4, "lea_disparity_set_register_form: %d", on);
   g_disp_reg = on;
   return 0;
 }
@@ -379,14 +437,16 @@ extern "C" int lea_disparity_regression(const void* cost, float* disp, int B, in
   const bool cols_ok = (256LL * W3 + Wo - 1) / Wo + 2 <= kDispCols;
 #define LEA_DISP_ROWS3(D3_, MD_)                                                                        \
   if (D3 == D3_ && maxdisp == MD_) {                                                                   \
-    auto k_ = fast ? disparity_rows3_f32<D3_, MD_, true> : disparity_rows3_f32<D3_, MD_, false>;        \
+    auto k_ = fact ? (fast ? disparity_rows3_f32<D3_, MD_, true, true> : disparity_rows3_f32<D3_, MD_, false, true>)   \
+                   : (fast ? disparity_rows3_f32<D3_, MD_, true, false> : disparity_rows3_f32<D3_, MD_, false, false>); \
     k_<<<dim3((Wo + kDispThreads - 1) / kDispThreads, H3, B), kDisp3Threads, 0, as_stream(stream)>>>(   \
         (const float*)cost, disp, H3, W3, rh, rw);                                                     \
     return launch_status("lea_disparity_regression");                                                  \
   }
   // (88, 264) -- config 5 -- keeps the two-row kernel: three rows' LDS (101 KB) leave one
   // workgroup per CU there (213 -> 260 us, profiles/r06_disp_probe.txt)
-  if (g_disp_reg == 3 && cols_ok) {
+  const bool fact = g_disp_reg == 4;
+  if (g_disp_reg >= 3 && cols_ok) {
     LEA_DISP_ROWS3(4, 12) LEA_DISP_ROWS3(8, 24) LEA_DISP_ROWS3(16, 48) LEA_DISP_ROWS3(32, 96)
     LEA_DISP_ROWS3(64, 192)
   }
@@ -394,7 +454,8 @@ extern "C" int lea_disparity_regression(const void* cost, float* disp, int B, in
   const bool rows_ok = g_disp_reg >= 2 && cols_ok;
 #define LEA_DISP_ROWS(D3_, MD_)                                                                         \
   if (D3 == D3_ && maxdisp == MD_) {                                                                   \
-    auto k_ = fast ? disparity_rows_f32<D3_, MD_, true> : disparity_rows_f32<D3_, MD_, false>;          \
+    auto k_ = fact ? (fast ? disparity_rows_f32<D3_, MD_, true, true> : disparity_rows_f32<D3_, MD_, false, true>)   \
+                   : (fast ? disparity_rows_f32<D3_, MD_, true, false> : disparity_rows_f32<D3_, MD_, false, false>); \
     k_<<<grid, block, 0, as_stream(stream)>>>((const float*)cost, disp, H3, W3, rh, rw);                 \
     return launch_status("lea_disparity_regression");                                                  \
   }

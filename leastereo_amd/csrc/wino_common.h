@@ -151,6 +151,7 @@ extern int g_wpre;  // lea_conv3d_wino2p_set_wpre
 extern int g_w44;
 extern int g_w44u;  // lea_conv3d_wino44_set_upre
 extern int g_w44s;  // lea_conv3d_wino44_set_sched
+extern int g_w44g;  // lea_conv3d_wino44_set_group
 long long lane44_floats(int cout, int cin);
 long long lane44_g_floats(int cout, int cin);  // the G_W' g part (the U copy follows)
 __global__ void pack_wino44_lane_kernel(const float* __restrict__ w, float* __restrict__ out, int cout, int cin,

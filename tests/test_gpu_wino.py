@@ -17,6 +17,7 @@ pytestmark = pytest.mark.gpu
 DEV = "cuda"
 WPRE_DEFAULT = 1  # lea_conv3d_wino2p_set_wpre's library default (csrc/conv3d_wino.hip g_wpre)
 W44U_DEFAULT = 0  # lea_conv3d_wino44_set_upre's library default (csrc/conv3d_wino44.hip g_w44u)
+W44G_DEFAULT = -1  # lea_conv3d_wino44_set_group's library default (g_w44g: auto)
 W44_DEFAULT = 1  # lea_conv3d_wino44_set's library default (csrc/conv3d_wino44.hip g_w44)
 
 
@@ -577,23 +578,27 @@ def test_wino44_vs_float64(b, cin, c1, cout, shape, mode):
     x1, x2 = (xs[:, :c1].contiguous(), xs[:, c1:].contiguous()) if c1 < cin else (xs, None)
     pw = kernels.pack_conv_weight_wino(w.to(DEV))
     outs = {}
-    for on, upre in ((0, 0), (1, 0), (1, 1)):
+    for on, upre, grp in ((0, 0, 0), (1, 0, 0), (1, 1, 0), (1, 0, 2), (1, 0, 3), (1, 0, 16)):
         assert lib.lea_conv3d_wino44_set(on) == 0 and lib.lea_conv3d_wino44_set_upre(upre) == 0
+        assert lib.lea_conv3d_wino44_set_group(grp) == 0
         try:
             name = kernels.wino_kernel_name(b, cout, *shape, cin=cin)
             if cin > 8:
                 assert name == ("conv3d_wino44_kernel" if on else "conv3d_wino2p_kernel"), name
             out = r.to(DEV).clone() if mode == "acc" else None
-            outs[(on, upre)] = kernels.conv3d_bnrelu_wino(
+            outs[(on, upre, grp)] = kernels.conv3d_bnrelu_wino(
                 x1, pw, cout, scale.to(DEV), shift.to(DEV), relu=True, out=out, accumulate=mode == "acc", x2=x2,
                 residual=r.to(DEV) if mode == "res" else None).cpu().double()
         finally:
             lib.lea_conv3d_wino44_set(int(os.environ.get("LEASTEREO_WINO44") or W44_DEFAULT))
             lib.lea_conv3d_wino44_set_upre(int(os.environ.get("LEASTEREO_WINO44_UPRE") or W44U_DEFAULT))
-    np.testing.assert_allclose(outs[(1, 0)].numpy(), want.numpy(), rtol=1e-4, atol=1e-4)
-    np.testing.assert_allclose(outs[(1, 0)].numpy(), outs[(0, 0)].numpy(), rtol=1e-4, atol=1e-4)
+            lib.lea_conv3d_wino44_set_group(W44G_DEFAULT)
+    np.testing.assert_allclose(outs[(1, 0, 0)].numpy(), want.numpy(), rtol=1e-4, atol=1e-4)
+    np.testing.assert_allclose(outs[(1, 0, 0)].numpy(), outs[(0, 0, 0)].numpy(), rtol=1e-4, atol=1e-4)
     # U precomputed by the packer (lea_conv3d_wino44_set_upre): the kernel's own operations, same bits
-    assert torch.equal(outs[(1, 1)], outs[(1, 0)])
+    assert torch.equal(outs[(1, 1, 0)], outs[(1, 0, 0)])
+    # grouped workgroup orders (lea_conv3d_wino44_set_group; 3: partial edge groups): same bits
+    assert all(torch.equal(outs[(1, 0, g)], outs[(1, 0, 0)]) for g in (2, 3, 16))
 
 
 @pytest.mark.parametrize("mode,b,cin,cout,shape,res", [

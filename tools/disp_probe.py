@@ -27,7 +27,7 @@ def main():
         x = torch.randn(b, 1, d3, h3, w3, device="cuda", generator=g) * 3
         for fast in (False, True):
             out = {}
-            for form in (1, 2, 3, 0):
+            for form in (1, 2, 3, 4, 0):
                 _lib.check(lib.lea_disparity_set_register_form(form), "form")
                 out[form] = kernels.disparity_regression(x, md, fast)
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -41,7 +41,7 @@ def main():
                       f"{float((out[form] - out.get(1, out[form])).abs().max()):.2e}"
                       + (f"  form 3 == form 2: {bool(torch.equal(out[3], out[2]))}" if form == 3 else ""),
                       flush=True)
-    _lib.check(lib.lea_disparity_set_register_form(3), "form")
+    _lib.check(lib.lea_disparity_set_register_form(4), "form")
 
 
 if __name__ == "__main__":
