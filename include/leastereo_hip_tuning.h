@@ -176,7 +176,7 @@ int lea_conv3d_wino44_set_sched(int s);
 
 /* The F(4,3) x F(4,3) tile's workgroup order: 0 = linear (cout block, depth group, tile),
  * g in 1..16 = groups of g x g tiles x max(1, 64 / (cout blocks g^2)) depth groups,
- * consecutive per XCD (L2 sharing of the halo), -1 (default) = 16 on grids of >= 8192
+ * consecutive per XCD (L2 sharing of the halo), -1 (default) = 16 on grids of >= 2048
  * workgroups, else 0.  Bit-identical. */
 int lea_conv3d_wino44_set_group(int g);
 

@@ -552,10 +552,11 @@ int run44(ConvArgs a, int B, int spw, hipStream_t st) {
   const long long n_ = (long long)a.ntiles * ((a.ndz + a.spw - 1) / a.spw) * B * a.ncob;
   LEA_CHECK_ARG(n_ < (1LL << 31), "lea_conv3d(wino44): grid too large");
   a.nblk = (int)n_;
-  // auto: 16 x 16-tile groups on the large grids (conv1/2, stem1: HBM traffic -37 / -33 %, time
-  // unchanged, profiles/r06_w44_group_traffic.txt), linear on the small ones (whose whole grid
-  // fits the L2s; grouped +1-2 %, r06_w44_group_ab.txt)
-  a.grp = g_w44g >= 0 ? g_w44g : (n_ >= 8192 ? 16 : 0);
+  // auto: 16 x 16-tile groups on the large grids (C2: conv1/2 and stem1, 3840 workgroups; HBM
+  // traffic -42 / -44 %, time unchanged, profiles/r06_w44_group_traffic2.txt), linear on the
+  // small ones (<= 864 workgroups, whose whole grid fits the L2s; grouped +1-2 %,
+  // r06_w44_group_ab.txt)
+  a.grp = g_w44g >= 0 ? g_w44g : (n_ >= 2048 ? 16 : 0);
   const dim3 grid((unsigned)n_);
   if (g_w44u)
     conv3d_wino44_kernel<true, 0><<<grid, 256, 0, st>>>(a);

@@ -20,16 +20,20 @@ for ctr in FETCH_SIZE WRITE_SIZE; do
     > gpurun_out/traffic/c2_$ctr.log 2>&1
   rc=$?; echo "c2 $ctr rc=$rc"; [ $rc -eq 0 ] || exit $rc
 done
-python3 tools/traffic_report.py gpurun_out/traffic/c2_FETCH_SIZE gpurun_out/traffic/c2_WRITE_SIZE gpurun_out/traffic/c2.json | head -6
+python3 tools/traffic_report.py gpurun_out/traffic/c2_FETCH_SIZE gpurun_out/traffic/c2_WRITE_SIZE gpurun_out/traffic/c2.json > gpurun_out/traffic/c2.txt
+head -6 gpurun_out/traffic/c2.txt
 python3 -c "import json; o=json.load(open('profiles/hbm_traffic.json')); n=json.load(open('gpurun_out/traffic/c2.json')); o={k: v for k, v in o.items() if '@' in k}; o.update(n); json.dump(o, open('profiles/hbm_traffic.json', 'w'), indent=1, sort_keys=True)"
-CONFIGS="c3 c4 c5" bash tools/gpu_traffic_bf16.sh || exit $?
-for c in c3 c4 c5; do python3 tools/traffic_merge.py $c gpurun_out/traffic_$c.json; done
+TC=${TRAFFIC_CONFIGS:-c3 c4 c5}
+if [ -n "$TC" ]; then
+  CONFIGS="$TC" bash tools/gpu_traffic_bf16.sh || exit $?
+  for c in $TC; do python3 tools/traffic_merge.py $c gpurun_out/traffic_$c.json; done
+fi
 cp profiles/hbm_traffic.json gpurun_out/traffic/hbm_traffic_merged.json
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_$TAG -o run -- \
   python3 bench.py --steps 5 --warmup 2 --cpu-baseline 0 --epe 0 --pair-check 0 --extra-configs= > gpurun_out/prof_$TAG.json 2> gpurun_out/prof_$TAG.err
 rc=$?; echo "prof rc=$rc"; [ $rc -eq 0 ] || exit $rc
 python3 tools/trace_report.py gpurun_out/prof_$TAG > gpurun_out/prof_${TAG}_forward.txt; head -8 gpurun_out/prof_${TAG}_forward.txt
-for c in c2 c3 c4 c5; do
+for c in ${BENCH_CONFIGS:-c2 c3 c4 c5}; do
   timeout -k 10 500 python3 bench.py --config $c --steps 20 --warmup 5 --breakdown 1 --cpu-baseline $([ $c = c2 ] && echo 1 || echo 0) \
     $([ $c = c2 ] || echo --extra-configs=) \
     > gpurun_out/bench_${TAG}_$c.json 2> gpurun_out/bench_${TAG}_$c.err
