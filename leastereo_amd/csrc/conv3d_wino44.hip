@@ -282,9 +282,14 @@ __global__ __launch_bounds__(256, 2) void conv3d_wino44_kernel(const ConvArgs a)
 #pragma unroll
     for (int pl = 0; pl < PLANES; ++pl) {
       const float* sp = sp0 + pl * PLANEA;
-      const float2 a0 = *reinterpret_cast<const float2*>(sp);
-      const float2 a1 = *reinterpret_cast<const float2*>(sp + 2);
-      const float2 a2 = *reinterpret_cast<const float2*>(sp + 4);
+      // native 8-byte vectors, kept whole: HIP's float2 struct loaded as two dwords (and the
+      // unused half of a2 dropped) became ds_read2_b32 / ds_read_b32, banked on 32 banks, where
+      // the channel bases (1, 3, 33, 35 mod 64) collide two-way; as ds_read_b64 they are
+      // conflict-free (tools/w44_banks.py)
+      f32x2 a0 = *reinterpret_cast<const f32x2*>(sp);
+      f32x2 a1 = *reinterpret_cast<const f32x2*>(sp + 2);
+      f32x2 a2 = *reinterpret_cast<const f32x2*>(sp + 4);
+      asm volatile("" : "+v"(a0), "+v"(a1), "+v"(a2));
       if constexpr (VXH == 0) {  // W points 0, 1, 2 (bt6's first three rows)
         const float pa = fmaf(-4.f, a1.x, a2.x), pb = fmaf(-4.f, a0.y, a1.y);
         bw[pl][0] = fmaf(4.f, a0.x, fmaf(-5.f, a1.x, a2.x));

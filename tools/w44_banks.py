@@ -1,9 +1,11 @@
 #!/usr/bin/env python3
-"""Exhaustive LDS bank check of the F(4,3) x F(4,3) tile's maps (csrc/conv3d_wino44.hip):
-the V-pass's ds_read_b64 of the halo (two 32-lane groups, 64 banks), its ds_write_b128 of V
-(8 groups of 8 lanes, 32 banks), and the steps' ds_read_b128 of V (4 lane groups of 16 lanes
-per MI355X_MICROARCH.md's LDS table, 64 banks) -- every kh, x-half, read offset and plane.
-Prints the extra cycles per instruction (0 = conflict-free)."""
+"""Exhaustive LDS bank check of the F(4,3) x F(4,3) tile's maps (csrc/conv3d_wino44.hip), per
+MI355X_MICROARCH.md's LDS table: the V-pass's halo reads as ds_read_b64 (two 32-lane groups,
+64 banks) and as the ds_read2_b64 the compiler pairs them into (16-lane groups, 32 banks) --
+and, for the record, as the ds_read2_b32 they compiled to while loaded through HIP's float2
+struct (32-lane groups, 32 banks: the round-6 PMC's 30 M conflict cycles per launch) -- its
+ds_write_b128 / ds_write_b64 of V, and the steps' ds_read_b128 / ds_read_b64 of V, every kh,
+x-half, read offset and plane.  Prints the extra cycles per instruction (0 = conflict-free)."""
 CB = [1, 1027, 2081, 3107]
 RWA, PLANEA = 40, 160
 GS, XHS, TRS, TCS = 40, 20, 320, 1284
@@ -42,18 +44,38 @@ def main():
                 assert all(a % 2 == 0 for a in addr.values()), "b64 alignment"
                 e = conflicts([[addr[l] for l in range(0, 32)], [addr[l] for l in range(32, 64)]], 2, 64)
                 worst = max(worst, e)
-        for m in range(5):  # the V-pass's writes (4 x b128 + 1 x b64)
+        for m in range(4):  # the V-pass's b128 writes
             addr = {}
             for t in lanes:
                 g, c, r, xh = vpass_unit(t)
                 addr[t % 64] = c * TCS + r * TRS + g * GS + xh * XHS + 4 * m
             e = conflicts([[addr[l] for l in range(8 * k, 8 * k + 8)] for k in range(8)], 4, 32)
             worst = max(worst, e)
-    print("V-pass halo reads + V writes: extra cycles", worst)
+    print("V-pass halo reads (ds_read_b64) + V b128 writes: extra cycles", worst)
+    w2, w32, wb64 = 0, 0, 0
+    for wave in range(4):
+        lanes = range(64 * wave, 64 * wave + 64)
+        for pl in range(6):
+            for j in range(3):
+                addr = {}
+                for t in lanes:
+                    g, c, r, _ = vpass_unit(t)
+                    addr[t % 64] = CB[c] + pl * PLANEA + r * RWA + 3 + 4 * g + 2 * j
+                w2 = max(w2, conflicts([[addr[l] for l in range(16 * k, 16 * k + 16)] for k in range(4)], 2, 32))
+                for k in range(2):  # each dword alone, as ds_read_b32 / one half of ds_read2_b32
+                    w32 = max(w32, conflicts([[addr[l] + k for l in range(0, 32)], [addr[l] + k for l in range(32, 64)]], 1, 32))
+        addr = {}
+        for t in lanes:
+            g, c, r, xh = vpass_unit(t)
+            addr[t % 64] = c * TCS + r * TRS + g * GS + xh * XHS + 16
+        wb64 = max(wb64, conflicts([[addr[l] for l in range(16 * k, 16 * k + 16)] for k in range(4)], 2, 32))
+    print("V-pass halo reads as ds_read2_b64: extra cycles", w2)
+    print("V-pass halo reads as ds_read_b32 / ds_read2_b32 (the pre-fix code): extra cycles per access", w32)
+    print("V-pass V b64 write: extra cycles", wb64)
     worst = 0
     for xh in range(2):
         for kh in range(3):
-            for m in range(5):
+            for m in range(4):
                 addr = {}
                 for l in range(64):
                     ci, p = l >> 4, l & 15
@@ -61,6 +83,12 @@ def main():
                     assert addr[l] % 4 == 0
                 worst = max(worst, conflicts([[addr[l] for l in g] for g in B128_GROUPS], 4, 64))
     print("step V reads (ds_read_b128): extra cycles", worst)
+    worst = 0
+    for xh in range(2):
+        for kh in range(3):
+            addr = {l: (l >> 4) * TCS + ((l & 15) // 8 + kh) * TRS + GS * ((l & 15) % 8) + XHS * xh + 16 for l in range(64)}
+            worst = max(worst, conflicts([[addr[l] for l in range(0, 32)], [addr[l] for l in range(32, 64)]], 2, 64))
+    print("step V read (ds_read_b64): extra cycles", worst)
 
 
 if __name__ == "__main__":
