@@ -310,7 +310,9 @@ __global__ __launch_bounds__(256, 2) void conv3d_wino44_kernel(const ConvArgs a)
 #pragma unroll
     for (int k = 0; k < 4; ++k)
       *reinterpret_cast<float4*>(tp + 4 * k) = make_float4(vf[4 * k], vf[4 * k + 1], vf[4 * k + 2], vf[4 * k + 3]);
-    *reinterpret_cast<float2*>(tp + 16) = make_float2(vf[16], vf[17]);
+    // floats 16, 17 as a 16-byte store into the unit's 20-float slot (the last two are padding): as
+    // ds_write_b64 they met two-way on 32 banks (tools/w44_banks.py)
+    *reinterpret_cast<f32x4*>(tp + 16) = f32x4{vf[16], vf[17], vf[16], vf[17]};
   };
 
   const int ci = lane >> 4, p = lane & 15;
@@ -450,13 +452,16 @@ __global__ __launch_bounds__(256, 2) void conv3d_wino44_kernel(const ConvArgs a)
       const float* tv = tvb + (it & 1) * TS;
       struct Raw {
         float4 v4[4];
-        float2 v2;
+        f32x4 v2;  // floats 16, 17 (and the slot's two padding floats)
       };
       auto load_step = [&](int kh, Raw& o) {
         const float* tp = tv + toff + kh * TRS;
   #pragma unroll
         for (int k = 0; k < 4; ++k) o.v4[k] = reinterpret_cast<const float4*>(tp)[k];
-        o.v2 = *reinterpret_cast<const float2*>(tp + 16);
+        // read whole (ds_read_b128: conflict-free): as a b64 the compiler paired two kh rows into
+        // a ds_read2_b64, four-way on 32 banks
+        o.v2 = *reinterpret_cast<const f32x4*>(tp + 16);
+        asm volatile("" : "+v"(o.v2));
       };
       struct Xf {
         float v[NX][NE];
@@ -465,7 +470,7 @@ __global__ __launch_bounds__(256, 2) void conv3d_wino44_kernel(const ConvArgs a)
       auto xform = [&](int kh, const Raw& o, Xf& T) {
         const float e18[18] = {o.v4[0].x, o.v4[0].y, o.v4[0].z, o.v4[0].w, o.v4[1].x, o.v4[1].y,
                                o.v4[1].z, o.v4[1].w, o.v4[2].x, o.v4[2].y, o.v4[2].z, o.v4[2].w,
-                               o.v4[3].x, o.v4[3].y, o.v4[3].z, o.v4[3].w, o.v2.x, o.v2.y};
+                               o.v4[3].x, o.v4[3].y, o.v4[3].z, o.v4[3].w, o.v2[0], o.v2[1]};
   #pragma unroll
         for (int x = 0; x < NX; ++x)
   #pragma unroll

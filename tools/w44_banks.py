@@ -44,7 +44,7 @@ def main():
                 assert all(a % 2 == 0 for a in addr.values()), "b64 alignment"
                 e = conflicts([[addr[l] for l in range(0, 32)], [addr[l] for l in range(32, 64)]], 2, 64)
                 worst = max(worst, e)
-        for m in range(4):  # the V-pass's b128 writes
+        for m in range(5):  # the V-pass's b128 writes (the fifth: floats 16, 17 + slot padding)
             addr = {}
             for t in lanes:
                 g, c, r, xh = vpass_unit(t)
@@ -71,11 +71,11 @@ def main():
         wb64 = max(wb64, conflicts([[addr[l] for l in range(16 * k, 16 * k + 16)] for k in range(4)], 2, 32))
     print("V-pass halo reads as ds_read2_b64: extra cycles", w2)
     print("V-pass halo reads as ds_read_b32 / ds_read2_b32 (the pre-fix code): extra cycles per access", w32)
-    print("V-pass V b64 write: extra cycles", wb64)
+    print("V-pass V b64 write (the pre-fix tail store): extra cycles", wb64)
     worst = 0
     for xh in range(2):
         for kh in range(3):
-            for m in range(4):
+            for m in range(5):
                 addr = {}
                 for l in range(64):
                     ci, p = l >> 4, l & 15
@@ -88,7 +88,13 @@ def main():
         for kh in range(3):
             addr = {l: (l >> 4) * TCS + ((l & 15) // 8 + kh) * TRS + GS * ((l & 15) % 8) + XHS * xh + 16 for l in range(64)}
             worst = max(worst, conflicts([[addr[l] for l in range(0, 32)], [addr[l] for l in range(32, 64)]], 2, 64))
-    print("step V read (ds_read_b64): extra cycles", worst)
+    print("step V tail read as ds_read_b64 (pre-fix): extra cycles", worst)
+    worst = 0
+    for xh in range(2):
+        for kh in range(2):  # two kh rows paired into one ds_read2_b64 (16-lane groups, 32 banks)
+            addr = {l: (l >> 4) * TCS + ((l & 15) // 8 + kh) * TRS + GS * ((l & 15) % 8) + XHS * xh + 16 for l in range(64)}
+            worst = max(worst, 2 * conflicts([[addr[l] for l in range(16 * k, 16 * k + 16)] for k in range(4)], 2, 32))
+    print("step V tail reads as ds_read2_b64 (pre-fix, both accesses): extra cycles", worst)
 
 
 if __name__ == "__main__":
