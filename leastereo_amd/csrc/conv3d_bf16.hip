@@ -69,7 +69,12 @@ struct Cfg {
   static constexpr int RH = TH + KS - 1, RW = 16 + KS - 1;
   static constexpr int PLANE = RH * RW;
   static constexpr int IMG = PLANES * PLANE;  // 16-B voxel-blocks per channel block
-  static constexpr int STAGE = NB * IMG;      // 16-B slots per stage
+  // channel-block stride in LDS: a multiple of 16 slots, so the two blocks a ds_read_b128 lane
+  // group reads (k-groups 2m, 2m + 1: NB = 2) sit on the same banks modulo their column and the
+  // group's 16 columns stay on distinct ones (r06: IMG = 180 for the 2D tiles put them two-way,
+  // half the LDS cycles of those launches were conflict cycles)
+  static constexpr int IMGS = (IMG + 15) / 16 * 16;
+  static constexpr int STAGE = NB * IMGS;     // 16-B slots per stage
   static constexpr int PIECES = (IMG + 63) / 64;
   static constexpr int PIECES_W = (PIECES + 3) / 4;
 };
@@ -151,7 +156,7 @@ __global__ __launch_bounds__(kThreads, 2) void conv_bf16_kernel(const Args a) {
         unsigned vo = voff[t];
         if constexpr (CV) vo = voff[t] ^ ((voff[t] ^ voffr[t]) & rmask);
         if (j < C::PIECES && j * 64 + lane < C::IMG)
-          __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void*)(st + k * C::IMG + j * 64), 16, vo, 0, 0, 0);
+          __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void*)(st + k * C::IMGS + j * 64), 16, vo, 0, 0, 0);
       }
     }
   };
@@ -162,7 +167,7 @@ __global__ __launch_bounds__(kThreads, 2) void conv_bf16_kernel(const Args a) {
     const int tap = min(slot / NB, C::T - 1);  // slots past the last tap carry zero weights
     const int blk = slot % NB;
     const int kd = tap / (KS * KS), kh = (tap / KS) % KS, kw = tap % KS;
-    return blk * C::IMG + kd * C::PLANE + kh * C::RW + kw;
+    return blk * C::IMGS + kd * C::PLANE + kh * C::RW + kw;
   };
   int vrow[C::NV];  // staged-halo slot of this wave's rows (output plane t, row r), column n
 #pragma unroll
@@ -1074,8 +1079,11 @@ __global__ __launch_bounds__(512, 2) void conv_bf16_pair_kernel(const Args a, in
 #pragma unroll
   for (int ks = 0; ks < C::S; ++ks) {
     const int slot = 4 * ks + g;
-    if (PP) {  // slot = (input plane 2s-1 + j) x (kh, kw)
-      const int j = slot / 9, t2 = slot % 9;
+    if (PP) {  // k-step ks = tap (kh, kw), lane group g = input plane 2s-1 + g (r06): the lane groups a
+      // ds_read_b128 serves together (k-groups 0 / 1, 2 / 3) then read the same tap of planes whose ring
+      // slots are 0 mod 16 apart -- conflict-free; the former order (slot = plane x 9 + tap) paired
+      // neighbouring taps, two-way on 22 % of the LDS cycles
+      const int j = g, t2 = ks;
       kdv[ks] = j;
       koff[ks] = part * C::PLANEP + (t2 / 3) * C::RW + t2 % 3;
     } else {
@@ -1093,7 +1101,7 @@ __global__ __launch_bounds__(512, 2) void conv_bf16_pair_kernel(const Args a, in
     if (PP) {
       // row n: cout n % 8 of output plane 2s + n / 8, whose kd for input plane 2s-1 + j is j - n / 8;
       // its 8 channels of tap (kd, kh, kw) are word (tap / 4, tap % 4, cout) of the packing
-      const int slot = 4 * ks + g, j = slot / 9, t2 = slot % 9;
+      const int j = g, t2 = ks;
       const int kd = j - n / 8, co = n % 8, tap = kd * 9 + t2;
       const bool ok = kd >= 0 && kd <= 2 && co < a.cout;
       av[ks] = ok ? wpv[((long long)part * C::S0 + tap / 4) * 64 + (tap % 4) * 16 + co] : bf16x8{};
