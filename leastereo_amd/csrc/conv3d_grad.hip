@@ -46,13 +46,16 @@ struct WCfg {
   static constexpr int XC = SEG + KS - 1;        // staged columns per halo row
   static constexpr int XR = KD * KS;             // staged (kd, kh) rows per channel
   static constexpr int XS = CI * XR * XC;        // staged halo values per segment
-  // LDS strides (floats): a row of 70 and a channel of 630 (k = 3), 210 (2D 3x3), a
-  // channel of 68 (k = 1) put the 64 lanes of every B read on 64 distinct banks
-  // (exhaustive check over the N tiles and 16 K steps); the dz tile's rows are 68 apart
+  // LDS strides (floats) for the A / B reads, each a ds_read_b32: two groups of 32 lanes on
+  // 32 banks (MI355X_MICROARCH.md, LDS).  A row of 70 and a channel of 632 (k = 3), 216 (2D
+  // 3x3), a channel of 66 (k = 1), and dz rows 66 apart put every read's 32-lane groups on 32
+  // distinct banks (tools/wgrad_banks.py, exhaustive over the N tiles, waves and K steps).
+  // r06: the strides had been chosen for 64 banks (630 / 210 / 68, dz rows 68 apart): two-way
+  // on every read, 43 % of conv1's LDS cycles were conflict cycles
   static constexpr int XRS = KS == 3 ? 70 : SEG;
-  static constexpr int CIS = KS == 3 ? XR * 70 : 68;
+  static constexpr int CIS = KS == 3 ? (KD == 3 ? 632 : 216) : 66;
   static constexpr int XLDS = CI * CIS;
-  static constexpr int GRS = 68;
+  static constexpr int GRS = 66;
   static constexpr int PX = (XS + 255) / 256;    // prefetched halo values per thread
 };
 
