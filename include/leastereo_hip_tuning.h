@@ -155,13 +155,14 @@ int lea_conv3d_wino2_set_pipeline(int on);
  * packed. */
 int lea_conv3d_wino2p_set_wpre(int on);
 
-/* 1 (default since r06) = the layers of the pipelined W x D kernel run on the F(4,3) x F(4,3)
+/* 2 (default since r06 v45) = as 1 and also the two-chunk layers (cin 8: the L0 8 -> 24 sibling
+ * group; 275.6 -> 259.7 us, profiles/r06_w44_modes_ab.txt), 1 = the layers of the pipelined W x D
+ * kernel run on the F(4,3) x F(4,3)
  * tile instead ("conv3d_wino44_kernel": 36 MFMA products per 4 x 4 outputs and kernel row
  * instead of 48; the W points split over two waves that swap accumulators in the epilogue;
  * -9.5 % on those layers, profiles/r06_w44_ab.txt), 0 = the pipelined F(4,3) x F(2,3)
- * kernel, 2 = as 1 and also the two-chunk layers (cin 8: the L0 8 -> 24 sibling group) that
- * otherwise stay on the two-barrier tile, 3 = as 2 and the 16-cout layers as half-empty 32-cout
- * blocks.  Same packed weights (every per-lane copy is packed). */
+ * kernel (the two-chunk layers then on the two-barrier tile), 3 = as 2 and the 16-cout layers as
+ * half-empty 32-cout blocks.  Same packed weights (every per-lane copy is packed). */
 int lea_conv3d_wino44_set(int on);
 
 /* 1 = the F(4,3) x F(4,3) tile reads U itself from its per-lane copy (the packer applies both

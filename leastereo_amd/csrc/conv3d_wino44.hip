@@ -548,7 +548,9 @@ __global__ __launch_bounds__(256, 2) void conv3d_wino44_kernel(const ConvArgs a)
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
-int g_w44 = 1;  // lea_conv3d_wino44_set (r06 default: -9.5 % on its layers, profiles/r06_w44_ab.txt)
+// lea_conv3d_wino44_set (r06 default 1: -9.5 % on its layers, profiles/r06_w44_ab.txt; 2 since v45,
+// after the LDS-conflict fixes: the L0 8 -> 24 group 275.6 -> 259.7 us, profiles/r06_w44_modes_ab.txt)
+int g_w44 = 2;
 int g_w44u = 0;  // lea_conv3d_wino44_set_upre
 int g_w44s = 0;  // lea_conv3d_wino44_set_sched
 int g_w44g = -1;  // lea_conv3d_wino44_set_group (-1: auto)

@@ -987,7 +987,7 @@ def wino_mfma_scale(cout: int, name: str) -> float:
 def wino_depth_f2():
     """Run the enclosed Winograd convs of the pipelined kernel's layers on the F(4,3) x F(2,3)
     tile (lea_conv3d_wino44_set(0)) instead of the F(4,3) x F(4,3) one, then restore the
-    process setting (LEASTEREO_WINO44, default 1).  The training path uses it: its gradient
+    process setting (LEASTEREO_WINO44, default 2).  The training path uses it: its gradient
     bars (tests/test_gpu_training.py) were calibrated on the F(2,3)-along-D numerics, and
     F(4,3) along D adds fp32 roundings that the backward chain amplifies (r06: a feature-net
     BN-weight gradient at 2.9e-3 of its scale against the 2e-3 bar).  Process-wide, like
@@ -997,7 +997,7 @@ def wino_depth_f2():
     try:
         yield
     finally:
-        check(lib.lea_conv3d_wino44_set(int(os.environ.get("LEASTEREO_WINO44") or 1)), "lea_conv3d_wino44_set")
+        check(lib.lea_conv3d_wino44_set(int(os.environ.get("LEASTEREO_WINO44") or 2)), "lea_conv3d_wino44_set")
 
 
 def wino_kernel_name(b, cout, d, h, w, costvolume=False, cin=0):

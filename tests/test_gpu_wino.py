@@ -18,7 +18,7 @@ DEV = "cuda"
 WPRE_DEFAULT = 1  # lea_conv3d_wino2p_set_wpre's library default (csrc/conv3d_wino.hip g_wpre)
 W44U_DEFAULT = 0  # lea_conv3d_wino44_set_upre's library default (csrc/conv3d_wino44.hip g_w44u)
 W44G_DEFAULT = -1  # lea_conv3d_wino44_set_group's library default (g_w44g: auto)
-W44_DEFAULT = 1  # lea_conv3d_wino44_set's library default (csrc/conv3d_wino44.hip g_w44)
+W44_DEFAULT = 2  # lea_conv3d_wino44_set's library default (csrc/conv3d_wino44.hip g_w44)
 
 
 def _ref(x, w, scale, shift, relu, res=None):
@@ -368,8 +368,11 @@ def test_depth_walk_is_bit_identical(b, cin, cout, shape, small):
 def test_buffer_epilogue_is_bit_identical(b, cin, cout, shape, small, variant):
     """The buffer-addressed epilogue (out-of-range lanes dropped, residual loads issued
     together; lea_conv3d_wino_set_epi_buf) stores exactly what the per-group epilogue
-    stores, into a channel slice of a larger buffer, with and without the residual."""
+    stores, into a channel slice of a larger buffer, with and without the residual.  (The
+    two-chunk 8 -> 24 shape runs on the F(4,3) x F(4,3) tile by default, which has the
+    buffer epilogue only: this test keeps it on the W x D engine it is about, mode 1.)"""
     lib = _lib.load()
+    assert lib.lea_conv3d_wino44_set(1) == 0
     g = torch.Generator(device=DEV).manual_seed(cin * 5 + cout + shape[2])
     x = torch.randn((b, cin) + shape, device=DEV, generator=g)
     w = torch.randn(cout, cin, 3, 3, 3, device=DEV, generator=g) / np.sqrt(cin * 27)
@@ -391,6 +394,7 @@ def test_buffer_epilogue_is_bit_identical(b, cin, cout, shape, small, variant):
         lib.lea_conv3d_wino_set_epi_buf(1)
         lib.lea_conv3d_wino_set_variant(0)
         lib.lea_conv3d_wino_set_small_cout(0)
+        lib.lea_conv3d_wino44_set(int(os.environ.get("LEASTEREO_WINO44") or W44_DEFAULT))
     assert torch.equal(outs[0], outs[2]) and torch.equal(outs[1], outs[3])
     assert torch.equal(outs[3][:, :4], r[:, :4]) and torch.equal(outs[3][:, 4 + cout:], r[:, 4 + cout:])
     want = F.conv3d(x.double(), w.double(), None, 1, 1)
