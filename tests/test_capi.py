@@ -115,3 +115,17 @@ def test_packed_sizes(cout, cin, k):
     else:
         assert n == -(-cout // (mt * 16)) * -(-cin // cin_b) * k ** 3 * cin_b * cops
     assert _lib.load().lea_conv3d_packed_floats(16, 8, 5) == 0
+
+
+def test_tuning_setters_reject_out_of_range_values():
+    """The round-6 tuning setters (include/leastereo_hip_tuning.h) take their documented ranges
+    and refuse the rest with LEA_E_INVALID, leaving the setting as it was (CPU: no launch)."""
+    lib = _lib.load()
+    cases = [("lea_conv3d_wino44_set", (0, 3), 2), ("lea_conv3d_wino44_set_group", (-1, 16), -1),
+             ("lea_conv3d_wino44_set_sched", (0, 3), 0), ("lea_conv3d_wino44_set_upre", (0, 1), 0),
+             ("lea_conv3d_wino2p_set_wpre", (0, 1), 1), ("lea_disparity_set_register_form", (0, 4), 4)]
+    for name, (lo, hi), default in cases:
+        fn = getattr(lib, name)
+        assert fn(lo - 1) == 1001 and fn(hi + 1) == 1001, name
+        assert name.encode() in lib.lea_last_error(), lib.lea_last_error()
+        assert fn(lo) == 0 and fn(hi) == 0 and fn(default) == 0, name
