@@ -630,3 +630,38 @@ def test_wino44_modes_vs_float64(mode, b, cin, cout, shape, res):
     finally:
         lib.lea_conv3d_wino44_set(int(os.environ.get("LEASTEREO_WINO44") or W44_DEFAULT))
     np.testing.assert_allclose(y.cpu().double().numpy(), want.numpy(), rtol=1e-4, atol=1e-4)
+
+
+@pytest.mark.parametrize("cin,cout,shape", [(32, 32, (64, 192, 320)), (128, 64, (32, 96, 160)),
+                                            (128, 32, (34, 98, 156))])
+def test_wino44_grouped_order_on_large_grids(cin, cout, shape):
+    """The grouped workgroup order the F(4,3) x F(4,3) tile takes by itself on grids of >= 2048
+    workgroups (lea_conv3d_wino44_set_group(-1): stem1 and conv1/2 at C2, 3840 workgroups; the
+    third shape, 2205 workgroups, ragged in every axis: partial boxes at every edge) writes the linear order's
+    bits, and every output is written (against float64 on a sampled window)."""
+    lib = _lib.load()
+    g = torch.Generator(device=DEV).manual_seed(cin + cout)
+    x = torch.randn((1, cin) + shape, device=DEV, generator=g)
+    w = torch.randn(cout, cin, 3, 3, 3, device=DEV, generator=g) / np.sqrt(cin * 27)
+    scale = torch.rand(cout, device=DEV, generator=g) + 0.5
+    shift = torch.randn(cout, device=DEV, generator=g) * 0.1
+    pw = kernels.pack_conv_weight_wino(w)
+    outs = []
+    try:
+        for grp in (0, -1, 16):
+            assert lib.lea_conv3d_wino44_set_group(grp) == 0
+            y = torch.full((1, cout) + shape, float("nan"), device=DEV)
+            kernels.conv3d_bnrelu_wino(x, pw, cout, scale, shift, True, y)
+            outs.append(y)
+    finally:
+        lib.lea_conv3d_wino44_set_group(W44G_DEFAULT)
+    assert kernels.wino_kernel_name(1, cout, *shape, cin=cin) == "conv3d_wino44_kernel"
+    assert torch.isfinite(outs[0]).all()
+    assert torch.equal(outs[1], outs[0]) and torch.equal(outs[2], outs[0])
+    # a window at the far corner (the last, partial box) against float64
+    d0, h0, w0 = shape[0] - 6, shape[1] - 7, shape[2] - 40
+    xs = x[:, :, d0 - 1:, h0 - 1:, w0 - 1:].double().cpu()
+    want = F.conv3d(F.pad(xs, (0, 1, 0, 1, 0, 1)), w.double().cpu())
+    want = torch.relu(want * scale.double().cpu().view(1, -1, 1, 1, 1) + shift.double().cpu().view(1, -1, 1, 1, 1))
+    np.testing.assert_allclose(outs[0][:, :, d0:, h0:, w0:].double().cpu().numpy(), want.numpy(),
+                               rtol=1e-4, atol=1e-4)
